@@ -1,0 +1,249 @@
+"""Benchmark of the MI355X planner hot path (BASELINE.json metric:
+"states-checked/sec + plan wall-time, 7-DOF arm/10 blocks, 1/2/4/8 GPU").
+
+  python bench.py [--gpus N --steps K --warmup W]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+Step = one launch of the state-validity kernel (Franka FK + capsule vs plane / box /
+self collision) over a batch of synthetic 9-D states resident in HBM, on the
+goal3_tallest 10-box scene (code/scenes.py:150-223; BASELINE config C3). Per-GPU
+batch is fixed (weak scaling); no collective is on this path. After the timed
+steps every rank also runs the C3 plan workload (21 RRT-Connect queries replaying
+goal3_tallest's pick/stack call sites) with the rank group sharding each iteration
+(RCCL all-gather), and rank 0 times the CPU oracle beside it (N=1 only).
+Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from rbe550_final_project_amd import _abi, model, scenes  # noqa: E402
+from rbe550_final_project_amd.native import Context  # noqa: E402
+
+METRIC = "states-checked/sec + plan wall-time, 7-DOF arm/10 blocks, 1/2/4/8 GPU"
+VALU_PEAK_TFLOPS = 157.3     # MI355X FP32 vector peak (MI355X_MICROARCH.md chip table)
+HBM_PEAK_GBPS = 8000.0       # spec
+BYTES_PER_STATE = 9 * 4 + 1  # 9 x fp32 in, 1 B flag out
+
+
+def flops_per_state(n_boxes):
+    """Algorithmic FP32 work of one full (collision-free) state check in
+    rp_math.h, counted from the source: FK 818 (7 x [sincos 26 +
+    Rz 18], 10 frame shifts x 6, hand Rz 18, 24 capsule endpoints x 18); capsule
+    AABBs + plane 12 x 13 = 156; box broad phase 6 compares per capsule-box pair;
+    self broad phase 6 compares x 35 pairs = 210. Narrow phases (only for
+    overlapping AABBs) are not counted."""
+    return 818 + 156 + 72 * n_boxes + 210
+
+
+def load_workload(name):
+    with open(os.path.join(ROOT, "tests", "golden", "workloads", name + ".json")) as f:
+        return json.load(f)
+
+
+def pmc_traffic(n_states):
+    """HBM bytes per validity launch from the committed rocprofv3 --pmc summary
+    (profiles/), corrected per MI355X_MICROARCH.md §HBM; None if absent."""
+    path = os.path.join(ROOT, "profiles", "pmc_validity.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        if int(d.get("states_per_launch", -1)) != int(n_states):
+            return None
+        return float(d["hbm_bytes_per_launch"])
+    except Exception:
+        return None
+
+
+def run_plans(ctx, wl, batch, seed, group):
+    """Wall time of every query of a workload (ms), plus aggregate states checked."""
+    times, states, statuses = [], 0, []
+    for i, q in enumerate(wl["queries"]):
+        sc = scenes.Scene.from_json(q["scene"])
+        ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+        ctx.set_attached(q["attached"])
+        p = _abi.make_params(seed=seed + i, batch=batch, n_waypoints=150, timeout_s=10.0)
+        if group is not None:
+            dist.barrier()
+        t0 = time.perf_counter()
+        path, st = ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+        times.append(1e3 * (time.perf_counter() - t0))
+        states += ctx.stats()["states_checked"]
+        statuses.append(st)
+    return times, states, statuses
+
+
+def cpu_baseline(scene, n_states, threads):
+    """CPU oracle (test infrastructure, the cpu_baseline leg only): OpenMP validity
+    over `threads` host cores on a bounded sample of the same workload."""
+    from oracle.oracle import OracleScene
+    o = OracleScene()
+    o.set_scene(scene.boxes, scene.plane_z, scene.base)
+    rng = np.random.default_rng(123)
+    q = (model.Q_LO + (model.Q_HI - model.Q_LO) * rng.random((n_states, 9))).astype(np.float32)
+    o.check_states(q[:4096], threads=threads)
+    t0 = time.perf_counter()
+    o.check_states(q, threads=threads)
+    dt = time.perf_counter() - t0
+    return n_states / dt, dt
+
+
+def cpu_plan_baseline(wl, seed):
+    from oracle.oracle import OracleScene
+    o = OracleScene()
+    times = []
+    for i, q in enumerate(wl["queries"]):
+        sc = scenes.Scene.from_json(q["scene"])
+        o.set_scene(sc.boxes, sc.plane_z, sc.base)
+        o.set_attached(q["attached"])
+        p = _abi.make_params(seed=seed + i, batch=1, n_waypoints=150, timeout_s=10.0)
+        t0 = time.perf_counter()
+        o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+        times.append(1e3 * (time.perf_counter() - t0))
+    return times
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--states", type=int, default=1 << 22, help="states per GPU per step")
+    ap.add_argument("--plan-batch", type=int, default=4096, help="RRT-Connect samples per iteration (global)")
+    ap.add_argument("--no-plan", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world > 1
+    if distributed:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    wl = load_workload("goal3_tallest_10box")
+    scene = scenes.goal3_tallest()           # 10 boxes, initial layout
+    ctx = Context(device=local, robot=model.robot_desc())
+    ctx.set_scene(scene.boxes, scene.plane_z, scene.base)
+
+    # synthetic states in HBM (per-rank stream of uniform samples, float32 bounds)
+    n = args.states
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    lo = torch.tensor(model.Q_LO, dtype=torch.float32, device=dev)
+    hi = torch.tensor(model.Q_HI, dtype=torch.float32, device=dev)
+    q = lo + (hi - lo) * torch.rand((n, 9), generator=g, device=dev, dtype=torch.float32)
+    q = q.contiguous()
+    flags = torch.empty(n, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        ctx.check_states_device(q.data_ptr(), n, flags.data_ptr(), stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    kernel_ms = e0.elapsed_time(e1) / args.steps      # only the validity kernel is on this stream
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if distributed:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max = float(t.item())
+    valid_frac = float(flags.float().mean().item())
+
+    total_states = n * world * args.steps
+    value = total_states / wall_max
+    ms_per_step = 1e3 * wall_max / args.steps
+
+    # ---- plan wall-time on the C3 workload (group-sharded when N > 1)
+    plan = None
+    if not args.no_plan:
+        group = None
+        try:
+            if distributed:
+                from rbe550_final_project_amd.distributed import Group
+                group = Group(ctx, args.plan_batch, local)
+            run_plans(ctx, {"queries": wl["queries"][:2]}, args.plan_batch, 100, group)   # warm-up
+            times, pstates, st = run_plans(ctx, wl, args.plan_batch, 0, group)
+            tt = torch.tensor([sum(times)], dtype=torch.float64, device=dev)
+            if distributed:
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            plan = {"queries": len(times), "batch": args.plan_batch,
+                    "total_ms": round(float(tt.item()), 3), "median_ms": round(float(np.median(times)), 3),
+                    "max_ms": round(float(np.max(times)), 3),
+                    "solved": int(sum(s in (_abi.STATUS_EXACT, _abi.STATUS_APPROXIMATE) for s in st)),
+                    "states_checked": int(pstates),
+                    "states_per_sec_in_plan": round(pstates / (sum(times) / 1e3), 1)}
+        except Exception as ex:  # report, keep the primary metric
+            plan = {"error": repr(ex)[:300]}
+
+    flop = flops_per_state(len(scene.boxes))
+    achieved_tflops = n * flop / (kernel_ms * 1e-3) / 1e12
+    traffic = pmc_traffic(n)
+    roofline = {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": VALU_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(achieved_tflops / VALU_PEAK_TFLOPS, 4), "traffic": traffic,
+                "kernel": "k_validity", "kernel_ms": round(kernel_ms, 5), "flop_per_state": flop,
+                "hbm": {"achieved": round(n * BYTES_PER_STATE / (kernel_ms * 1e-3) / 1e9, 2),
+                        "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                        "frac": round(n * BYTES_PER_STATE / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5),
+                        "bytes_per_state": BYTES_PER_STATE}}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        try:
+            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            sample = 1 << 23
+            rate, dt = cpu_baseline(scene, sample, threads)
+            ptimes = cpu_plan_baseline(wl, 0)
+            cpu = {"value": round(rate, 1), "unit": "states/s", "cores": threads, "kind": "port",
+                   "sample": f"{sample} uniform states, goal3 10-box scene, OpenMP CPU oracle ({dt:.1f} s)",
+                   "plan_total_ms": round(sum(ptimes), 3), "plan_median_ms": round(float(np.median(ptimes)), 3),
+                   "plan_sample": "21 goal3 queries, sequential RRT-Connect (batch 1), 1 core"}
+        except Exception as ex:
+            cpu = {"error": repr(ex)[:300]}
+
+    if rank == 0:
+        out = {"metric": METRIC, "value": round(value, 1), "unit": "states/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+               "data": "synthetic: uniform 9-D Franka states in the float32 joint bounds (HBM resident); "
+                       "goal3 10-box scene; plan queries from tests/golden/workloads",
+               "config": {"workload": "C3 goal3_tallest 10-block scene: validity batch per GPU + 21-query plan",
+                          "states_per_gpu": n, "global_batch": n * world, "parallelism": f"dp{world}",
+                          "valid_fraction": round(valid_frac, 4)},
+               "plan_wall": plan, "roofline": roofline, "cpu_baseline": cpu}
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if distributed:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

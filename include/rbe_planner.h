@@ -1,0 +1,213 @@
+/*
+ * rbe_planner.h — C-ABI of librbe_mi355x.so, the MI355X-native replacement for the
+ * state-validity / plan path of sgajera12/RBE550_final_project.
+ *
+ * What each entry point replaces in the reference (paths relative to /root/reference):
+ *
+ *   rp_create / rp_destroy      PlannerInterface.__init__ + _ensure_adapter      code/planning.py:14-30
+ *   rp_set_scene                the Genesis scene the collider sees (plane, boxes,
+ *                               raised robot base)                                code/scenes.py:29-34,49-85
+ *   rp_set_attached             self.attached_object + the exemption of
+ *                               collision_with_attached_object                    code/planning.py:153,221-230
+ *   rp_check_states(_device)    _is_ompl_state_valid: set_qpos (FK) +
+ *                               detect_collision + pair filter, for N states      code/planning.py:209-219,238-242
+ *   rp_state_contacts           diagnose_valid_violation (which links collide)    code/planning.py:43-57
+ *   rp_check_edges(_device)     OMPL DiscreteMotionValidator::checkMotion, run
+ *                               inside ss.solve / simplifySolution                code/planning.py:190,196
+ *   rp_plan                     plan_path body from the space setup to the
+ *                               interpolated path: RealVectorStateSpace bounds,
+ *                               RRTConnect solve, simplifySolution,
+ *                               path.interpolate(num_waypoints)                   code/planning.py:139-200
+ *   rp_group_*                  (new) data-parallel sharding of each RRT-Connect
+ *                               iteration across ranks with an all-gather;
+ *                               the reference is single-process                   code/planning.py:121-122
+ *   rp_get_stats / rp_last_error counters and error text (the reference prints /
+ *                               logs: planning.py:199, 202)
+ *
+ * ABI rules: plain C types only; 0 = ok, <0 = error (text via rp_last_error);
+ * no C++ exception crosses the boundary; every output buffer is caller-allocated;
+ * one host thread per context at a time. There is NO CPU execution path in this
+ * library: rp_create fails if no MI355X (gfx950) device is present.
+ *
+ * State layout: the 9-D Franka qpos (7 arm joints, 2 fingers) in the order of
+ * robot.n_qs (code/planning.py:143-150). Batched states are row-major N x 9.
+ */
+#ifndef RBE_PLANNER_H
+#define RBE_PLANNER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RP_NQ 9                 /* planning dimension: 7 revolute + 2 prismatic  */
+#define RP_MAX_CAPSULES 32
+#define RP_MAX_SELF_PAIRS 64
+#define RP_MAX_BOXES 64
+
+/* Link indices of the Franka chain; names match the Genesis/MJCF links the
+ * reference looks up (planning.py:222). */
+enum {
+    RP_LINK0 = 0, RP_LINK1, RP_LINK2, RP_LINK3, RP_LINK4, RP_LINK5, RP_LINK6, RP_LINK7,
+    RP_HAND = 8, RP_LEFT_FINGER = 9, RP_RIGHT_FINGER = 10, RP_NUM_LINKS = 11
+};
+
+/* Return codes */
+enum {
+    RP_OK = 0,
+    RP_ERR_ARG = -1,        /* bad argument (null pointer, size out of range)       */
+    RP_ERR_DEVICE = -2,     /* no gfx950 device / HIP runtime error                 */
+    RP_ERR_STATE = -3,      /* call out of order (e.g. rp_plan before rp_set_scene) */
+    RP_ERR_CAPACITY = -4,   /* tree / path capacity exceeded                        */
+    RP_ERR_EXCHANGE = -5    /* group all-gather callback failed                     */
+};
+
+/* Plan status (OMPL PlannerStatus analogue; planning.py:190-202 treats EXACT and
+ * APPROXIMATE as "solved"). */
+enum {
+    RP_STATUS_NONE = 0,
+    RP_STATUS_EXACT = 1,
+    RP_STATUS_APPROXIMATE = 2,
+    RP_STATUS_TIMEOUT = 3,        /* no solution and no approximate path            */
+    RP_STATUS_INVALID_START = 4,  /* start out of bounds or in collision            */
+    RP_STATUS_INVALID_GOAL = 5    /* goal out of bounds or in collision             */
+};
+
+/* One collision capsule rigidly attached to a link: segment a-b in the link frame. */
+typedef struct rp_capsule {
+    int32_t link;        /* RP_LINK*                                  */
+    float a[3];
+    float b[3];
+    float radius;
+} rp_capsule;
+
+/* Robot collision model (kinematics are the fixed Franka Panda chain). */
+typedef struct rp_robot_desc {
+    int32_t n_capsules;                        /* <= RP_MAX_CAPSULES          */
+    rp_capsule capsules[RP_MAX_CAPSULES];
+    int32_t n_self_pairs;                      /* <= RP_MAX_SELF_PAIRS        */
+    int32_t self_pairs[RP_MAX_SELF_PAIRS][2];  /* capsule index pairs         */
+} rp_robot_desc;
+
+/* Box obstacle: centre, half extents, rotation about world z (yaw, radians).
+ * Genesis gs.morphs.Box(size=s, pos=c) has half = s/2 (scenes.py:59-62). */
+typedef struct rp_box {
+    float center[3];
+    float half[3];
+    float yaw;
+} rp_box;
+
+/* rp_plan parameters. Zero / negative fields take the default shown. */
+typedef struct rp_plan_params {
+    uint64_t seed;          /* Philox key; the reference is unseeded (scenes.py:9)          */
+    int64_t batch;          /* samples per RRT-Connect iteration (global over ranks), 4096  */
+    double range;           /* steering distance, default 0.2 * maxExtent (OMPL RRTConnect) */
+    double resolution;      /* edge resolution, default 0.01 * maxExtent (OMPL default)     */
+    double timeout_s;       /* wall-clock budget of the solve, default 5.0 (planning.py:63) */
+    int64_t max_iters;      /* iteration cap (deterministic tests), default unlimited        */
+    int32_t n_waypoints;    /* path.interpolate(n) (planning.py:198), default 100; 0 = none */
+    int32_t simplify;       /* 1 = simplify the solution (smooth_path, planning.py:195)     */
+    int64_t tree_capacity;  /* nodes per tree, default 1<<22                                */
+} rp_plan_params;
+
+/* Counters of the last call (per rank). */
+typedef struct rp_stats {
+    int64_t states_checked;     /* validity evaluations actually executed             */
+    int64_t edges_checked;
+    int64_t samples;            /* samples drawn (global)                             */
+    int64_t iterations;
+    int64_t start_tree_size;
+    int64_t goal_tree_size;
+    int64_t path_states_raw;    /* before simplify / interpolate                     */
+    int64_t path_states_simplified;
+    double solve_ms;            /* wall time of the solve loop                       */
+    double simplify_ms;
+    double total_ms;            /* wall time of the whole rp_plan call               */
+    double exchange_ms;         /* time inside the group all-gather callback         */
+} rp_stats;
+
+typedef struct rp_ctx rp_ctx;
+
+/* All-gather callback used by a rank group: gather `bytes_per_rank` bytes from
+ * every rank's send buffer into recv (rank-major). Buffers are the ones registered
+ * with rp_group_init (device memory). Return 0 on success. */
+typedef int (*rp_allgather_fn)(void* user, int64_t bytes_per_rank);
+
+/* Library identity: returns a static string ("librbe_mi355x <version> gfx950"). */
+const char* rp_version(void);
+
+/* Fill `out` with the built-in Franka Panda capsule model (spec/franka_capsules.json). */
+int rp_default_robot(rp_robot_desc* out);
+
+/* Create a context on HIP device `device` (>= 0). `robot` may be NULL (default model). */
+int rp_create(rp_ctx** out, int device, const rp_robot_desc* robot);
+void rp_destroy(rp_ctx* ctx);
+
+/* Obstacles: boxes + ground plane at z = plane_z; robot base translation (the
+ * reference raises it by 1 cm, scenes.py:29-34). Replaces any previous scene and
+ * clears the attached box. */
+int rp_set_scene(rp_ctx* ctx, const rp_box* boxes, int32_t n_boxes, float plane_z,
+                 const float base_pos[3]);
+
+/* Attached object (planning.py:221-230): contacts between box `box_index` and the
+ * links set in `exempt_link_mask` (bit = 1 << RP_LINK*) are ignored.
+ * box_index = -1 clears. The reference exempts hand | left_finger | right_finger. */
+int rp_set_attached(rp_ctx* ctx, int32_t box_index, uint32_t exempt_link_mask);
+
+/* Validity of N states (row-major N x 9 float32, host memory). flags_out[i] = 1 if
+ * valid (collision free), 0 otherwise. */
+int rp_check_states(rp_ctx* ctx, const float* q, int64_t n, uint8_t* flags_out);
+
+/* Same on device-resident buffers (e.g. torch tensors' data_ptr) on the context's
+ * stream; if `stream` is non-NULL it is a hipStream_t the caller orders against. */
+int rp_check_states_device(rp_ctx* ctx, const float* q_dev, int64_t n, uint8_t* flags_dev,
+                           void* stream);
+
+/* Motion validity of N edges qa[i] -> qb[i] (row-major N x 9 float64), with OMPL's
+ * DiscreteMotionValidator semantics: qb and the interior states
+ * qa + (qb - qa) * j / nd, j = 1..nd-1, nd = ceil(|qb - qa| / resolution) are checked
+ * (qa is assumed valid). out[i] = 1 if the motion is valid. */
+int rp_check_edges(rp_ctx* ctx, const double* qa, const double* qb, int64_t n,
+                   double resolution, uint8_t* out);
+int rp_check_edges_device(rp_ctx* ctx, const double* qa_dev, const double* qb_dev, int64_t n,
+                          double resolution, uint8_t* out_dev, void* stream);
+
+/* Collision report for one state (diagnostics, planning.py:43-57): up to `cap`
+ * (link, obstacle) pairs; obstacle >= 0 is a box index, -1 the plane, -2 - k a
+ * self contact with link k. Returns the number of pairs found (may exceed cap). */
+int rp_state_contacts(rp_ctx* ctx, const double q[RP_NQ], int32_t* pairs_out, int32_t cap);
+
+/* Full query: bounds + start/goal checks, batched RRT-Connect, simplification and
+ * interpolation. path_out receives *n_out states (row-major, float64). */
+int rp_plan(rp_ctx* ctx, const double start[RP_NQ], const double goal[RP_NQ],
+            const double lo[RP_NQ], const double hi[RP_NQ], const rp_plan_params* params,
+            double* path_out, int32_t path_cap, int32_t* n_out, int32_t* status_out);
+
+/* Data-parallel rank group. Each rank (one process per GPU) owns one context; the
+ * caller allocates `send`/`recv` device buffers of `cap_bytes` and cap_bytes*world
+ * bytes and supplies an all-gather over them (torch.distributed over RCCL). After
+ * this call rp_plan shards every iteration's samples and connect targets across the
+ * group; the plan result is identical for every world size. world = 1 disables. */
+int rp_group_init(rp_ctx* ctx, int32_t rank, int32_t world, void* send_dev, void* recv_dev,
+                  int64_t cap_bytes, rp_allgather_fn fn, void* user);
+
+int rp_get_stats(rp_ctx* ctx, rp_stats* out);
+
+/* Last error text for this context (or for a failed rp_create when ctx is NULL). */
+const char* rp_last_error(rp_ctx* ctx);
+
+/* Kernel-level timing of the last rp_check_states_device call: average duration of
+ * the validity kernel measured with HIP events on the context's stream (ms). */
+int rp_last_kernel_ms(rp_ctx* ctx, double* ms);
+
+/* Numerics self-test (used by the parity tests): device sqrt(|x|), 0.13037 / x,
+ * ceil(7x) and (double)(float)x for each x[i] -> out[4*i .. 4*i+3]. The planner's
+ * steering and segment counts rely on these being IEEE correctly rounded. */
+int rp_selftest_f64(rp_ctx* ctx, const double* x, int64_t n, double* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RBE_PLANNER_H */

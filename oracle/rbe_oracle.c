@@ -1,0 +1,898 @@
+/*
+ * rbe_oracle.c — CPU ORACLE (test infrastructure only; see rbe_oracle.h).
+ *
+ * Plain C restatement of the hot path, written to the numerics contract of
+ * float32 collision arithmetic and float64 planner arithmetic, every
+ * operation in a fixed order, built with -ffp-contract=off, so that the HIP
+ * kernels of librbe_mi355x.so (which follow the same contract) must produce
+ * bit-identical validity flags, trees and paths. Reference anchors per function.
+ */
+#include "rbe_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define NQ RP_NQ
+#define NCAPMAX RP_MAX_CAPSULES
+
+typedef struct { float x, y, z; } v3;
+
+struct ro_scene {
+    int ncap;
+    int cap_link[NCAPMAX];
+    float cap_a[NCAPMAX][3], cap_b[NCAPMAX][3], cap_r[NCAPMAX];
+    int npair;
+    int pair[RP_MAX_SELF_PAIRS][2];
+    int nbox;
+    float box_c[RP_MAX_BOXES][3], box_h[RP_MAX_BOXES][3], box_cs[RP_MAX_BOXES], box_sn[RP_MAX_BOXES];
+    float box_lo[RP_MAX_BOXES][3], box_hi[RP_MAX_BOXES][3];
+    uint32_t box_exempt[RP_MAX_BOXES];   /* capsule bits */
+    float plane_z;
+    float base[3];
+};
+
+/* ------------------------------------------------------------------------- */
+/* scene                                                                     */
+/* ------------------------------------------------------------------------- */
+
+ro_scene* ro_scene_create(const rp_robot_desc* r) {
+    if (!r || r->n_capsules <= 0 || r->n_capsules > NCAPMAX || r->n_self_pairs < 0 ||
+        r->n_self_pairs > RP_MAX_SELF_PAIRS)
+        return NULL;
+    ro_scene* s = (ro_scene*)calloc(1, sizeof(ro_scene));
+    s->ncap = r->n_capsules;
+    for (int c = 0; c < s->ncap; ++c) {
+        s->cap_link[c] = r->capsules[c].link;
+        for (int k = 0; k < 3; ++k) {
+            s->cap_a[c][k] = r->capsules[c].a[k];
+            s->cap_b[c][k] = r->capsules[c].b[k];
+        }
+        s->cap_r[c] = r->capsules[c].radius;
+    }
+    s->npair = r->n_self_pairs;
+    for (int i = 0; i < s->npair; ++i) {
+        s->pair[i][0] = r->self_pairs[i][0];
+        s->pair[i][1] = r->self_pairs[i][1];
+    }
+    s->base[2] = 0.01f;
+    return s;
+}
+
+void ro_scene_destroy(ro_scene* s) { free(s); }
+
+int ro_scene_set(ro_scene* s, const rp_box* boxes, int32_t n, float plane_z, const float base[3]) {
+    if (!s || n < 0 || n > RP_MAX_BOXES || (n > 0 && !boxes)) return RP_ERR_ARG;
+    s->nbox = n;
+    for (int j = 0; j < n; ++j) {
+        const rp_box* b = &boxes[j];
+        /* yaw -> cos/sin once, in double, rounded to float (same as the product host) */
+        const float cs = (float)cos((double)b->yaw);
+        const float sn = (float)sin((double)b->yaw);
+        const float acs = cs < 0.0f ? -cs : cs, asn = sn < 0.0f ? -sn : sn;
+        float ext[3];
+        ext[0] = acs * b->half[0] + asn * b->half[1];
+        ext[1] = asn * b->half[0] + acs * b->half[1];
+        ext[2] = b->half[2];
+        for (int k = 0; k < 3; ++k) {
+            s->box_c[j][k] = b->center[k];
+            s->box_h[j][k] = b->half[k];
+            s->box_lo[j][k] = b->center[k] - ext[k];
+            s->box_hi[j][k] = b->center[k] + ext[k];
+        }
+        s->box_cs[j] = cs;
+        s->box_sn[j] = sn;
+        s->box_exempt[j] = 0;
+    }
+    s->plane_z = plane_z;
+    if (base) {
+        s->base[0] = base[0];
+        s->base[1] = base[1];
+        s->base[2] = base[2];
+    }
+    return RP_OK;
+}
+
+int ro_scene_set_attached(ro_scene* s, int32_t box, uint32_t link_mask) {
+    if (!s || box >= s->nbox) return RP_ERR_ARG;
+    for (int j = 0; j < s->nbox; ++j) s->box_exempt[j] = 0;
+    if (box < 0) return RP_OK;
+    uint32_t bits = 0;
+    for (int c = 0; c < s->ncap; ++c)
+        if ((link_mask >> s->cap_link[c]) & 1u) bits |= 1u << c;
+    s->box_exempt[box] = bits;
+    return RP_OK;
+}
+
+/* ------------------------------------------------------------------------- */
+/* float32 kinematics + collision (planning.py:209-230 restated)             */
+/* ------------------------------------------------------------------------- */
+
+static float mn(float a, float b) { return a < b ? a : b; }
+static float mx(float a, float b) { return a > b ? a : b; }
+static float c01(float x) { return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x); }
+static float dot(v3 u, v3 v) { return (u.x * v.x + u.y * v.y) + u.z * v.z; }
+
+void ro_sincos(float x, float* sn, float* cs) {
+    float t = x * 0.636619772f;
+    float k = floorf(t + 0.5f);
+    float r = x - k * 1.5703125f;
+    r = r - k * 4.837512969970703125e-4f;
+    r = r - k * 7.54978995489188216e-8f;
+    float z = r * r;
+    float ps = -1.9515295891e-4f;
+    ps = ps * z;
+    ps = ps + 8.3321608736e-3f;
+    ps = ps * z;
+    ps = ps + -1.6666654611e-1f;
+    float sr = r + (r * z) * ps;
+    float pc = 2.443315711809948e-5f;
+    pc = pc * z;
+    pc = pc + -1.388731625493765e-3f;
+    pc = pc * z;
+    pc = pc + 4.166664568298827e-2f;
+    float cr = (1.0f - 0.5f * z) + (z * z) * pc;
+    switch (((int)k) & 3) {
+        case 0: *sn = sr; *cs = cr; break;
+        case 1: *sn = cr; *cs = -sr; break;
+        case 2: *sn = -sr; *cs = -cr; break;
+        default: *sn = -cr; *cs = sr; break;
+    }
+}
+
+/* rotation columns R[0..2] (each a 3-vector) and origin P */
+typedef struct { float R[3][3]; float P[3]; } frame;
+
+static void f_rz(frame* f, float q) {
+    float s, c, n0[3], n1[3];
+    ro_sincos(q, &s, &c);
+    for (int k = 0; k < 3; ++k) {
+        n0[k] = c * f->R[0][k] + s * f->R[1][k];
+        n1[k] = c * f->R[1][k] - s * f->R[0][k];
+    }
+    for (int k = 0; k < 3; ++k) { f->R[0][k] = n0[k]; f->R[1][k] = n1[k]; }
+}
+/* R * Rx(+90) = [c0, c2, -c1]; R * Rx(-90) = [c0, -c2, c1] */
+static void f_rx(frame* f, int plus) {
+    float c1[3], c2[3];
+    for (int k = 0; k < 3; ++k) { c1[k] = f->R[1][k]; c2[k] = f->R[2][k]; }
+    for (int k = 0; k < 3; ++k) {
+        if (plus) { f->R[1][k] = c2[k]; f->R[2][k] = -c1[k]; }
+        else { f->R[1][k] = -c2[k]; f->R[2][k] = c1[k]; }
+    }
+}
+static void f_shift(float P[3], float k, const float col[3]) {
+    for (int i = 0; i < 3; ++i) P[i] = P[i] + k * col[i];
+}
+
+/* world frames of the 11 links (panda.xml, scenes.py:85) */
+static void link_frames(const ro_scene* s, const float q[NQ], frame F[RP_NUM_LINKS]) {
+    frame f;
+    memset(&f, 0, sizeof f);
+    f.R[0][0] = 1.0f; f.R[1][1] = 1.0f; f.R[2][2] = 1.0f;
+    f.P[0] = s->base[0]; f.P[1] = s->base[1]; f.P[2] = s->base[2];
+    F[0] = f;
+    f_shift(f.P, 0.333f, f.R[2]); f_rz(&f, q[0]); F[1] = f;
+    f_rx(&f, 0); f_rz(&f, q[1]); F[2] = f;
+    f_shift(f.P, -0.316f, f.R[1]); f_rx(&f, 1); f_rz(&f, q[2]); F[3] = f;
+    f_shift(f.P, 0.0825f, f.R[0]); f_rx(&f, 1); f_rz(&f, q[3]); F[4] = f;
+    f_shift(f.P, -0.0825f, f.R[0]); f_shift(f.P, 0.384f, f.R[1]); f_rx(&f, 0); f_rz(&f, q[4]); F[5] = f;
+    f_rx(&f, 1); f_rz(&f, q[5]); F[6] = f;
+    f_shift(f.P, 0.088f, f.R[0]); f_rx(&f, 1); f_rz(&f, q[6]); F[7] = f;
+    /* hand: flange +0.107 z, Rz(-45deg) with the rounded constants */
+    f_shift(f.P, 0.107f, f.R[2]);
+    {
+        const float c = 0.70710677f, sn = -0.70710677f;
+        float n0[3], n1[3];
+        for (int k = 0; k < 3; ++k) {
+            n0[k] = c * f.R[0][k] + sn * f.R[1][k];
+            n1[k] = c * f.R[1][k] - sn * f.R[0][k];
+        }
+        for (int k = 0; k < 3; ++k) { f.R[0][k] = n0[k]; f.R[1][k] = n1[k]; }
+    }
+    F[8] = f;
+    f_shift(f.P, 0.0584f, f.R[2]);
+    frame l = f;
+    f_shift(l.P, q[7], f.R[1]);
+    F[9] = l;
+    frame r = f;
+    f_shift(r.P, -q[8], f.R[1]);
+    for (int k = 0; k < 3; ++k) { r.R[0][k] = -f.R[0][k]; r.R[1][k] = -f.R[1][k]; }
+    F[10] = r;
+}
+
+static v3 to_world(const frame* f, const float a[3]) {
+    v3 w;
+    w.x = ((f->P[0] + a[0] * f->R[0][0]) + a[1] * f->R[1][0]) + a[2] * f->R[2][0];
+    w.y = ((f->P[1] + a[0] * f->R[0][1]) + a[1] * f->R[1][1]) + a[2] * f->R[2][1];
+    w.z = ((f->P[2] + a[0] * f->R[0][2]) + a[1] * f->R[1][2]) + a[2] * f->R[2][2];
+    return w;
+}
+
+static void capsules_world(const ro_scene* s, const float q[NQ], v3* A, v3* B) {
+    frame F[RP_NUM_LINKS];
+    link_frames(s, q, F);
+    for (int c = 0; c < s->ncap; ++c) {
+        A[c] = to_world(&F[s->cap_link[c]], s->cap_a[c]);
+        B[c] = to_world(&F[s->cap_link[c]], s->cap_b[c]);
+    }
+}
+
+void ro_fk_capsules(const ro_scene* s, const float q[NQ], float* out) {
+    v3 A[NCAPMAX], B[NCAPMAX];
+    capsules_world(s, q, A, B);
+    for (int c = 0; c < s->ncap; ++c) {
+        out[6 * c + 0] = A[c].x; out[6 * c + 1] = A[c].y; out[6 * c + 2] = A[c].z;
+        out[6 * c + 3] = B[c].x; out[6 * c + 4] = B[c].y; out[6 * c + 5] = B[c].z;
+    }
+}
+
+typedef struct { float lo[3], hi[3]; } aabb;
+
+static aabb cap_box(v3 a, v3 b, float r) {
+    aabb o;
+    o.lo[0] = mn(a.x, b.x) - r; o.hi[0] = mx(a.x, b.x) + r;
+    o.lo[1] = mn(a.y, b.y) - r; o.hi[1] = mx(a.y, b.y) + r;
+    o.lo[2] = mn(a.z, b.z) - r; o.hi[2] = mx(a.z, b.z) + r;
+    return o;
+}
+static int disjoint(const aabb* u, const float lo[3], const float hi[3]) {
+    for (int k = 0; k < 3; ++k)
+        if (u->lo[k] > hi[k] || u->hi[k] < lo[k]) return 1;
+    return 0;
+}
+
+/* derivative g(t) = q(t).d of the squared excess; writes |q(t)|^2 */
+static float g_of(const float a[3], const float d[3], const float h[3], float t, float* f2) {
+    float qv[3];
+    for (int k = 0; k < 3; ++k) {
+        float p = a[k] + t * d[k];
+        float cl = p < -h[k] ? -h[k] : (p > h[k] ? h[k] : p);
+        qv[k] = p - cl;
+    }
+    *f2 = (qv[0] * qv[0] + qv[1] * qv[1]) + qv[2] * qv[2];
+    return (qv[0] * d[0] + qv[1] * d[1]) + qv[2] * d[2];
+}
+
+/* squared distance segment a-b to box [-h,h] (box frame); DESIGN.md §3.3 */
+static float seg_box_d2(const float a[3], const float b[3], const float h[3]) {
+    float d[3], T[6];
+    for (int k = 0; k < 3; ++k) d[k] = b[k] - a[k];
+    for (int k = 0; k < 3; ++k) {
+        float u = 0.0f, v = 0.0f;
+        if (d[k] != 0.0f) {
+            float inv = 1.0f / d[k];
+            u = (-h[k] - a[k]) * inv;
+            v = (h[k] - a[k]) * inv;
+        }
+        T[2 * k] = c01(u);
+        T[2 * k + 1] = c01(v);
+    }
+    /* insertion sort: the sorted multiset is what matters */
+    for (int i = 1; i < 6; ++i) {
+        float x = T[i];
+        int j = i - 1;
+        while (j >= 0 && T[j] > x) { T[j + 1] = T[j]; --j; }
+        T[j + 1] = x;
+    }
+    float f2, f2e;
+    float g0 = g_of(a, d, h, 0.0f, &f2);
+    if (g0 >= 0.0f) return f2;
+    float g7 = g_of(a, d, h, 1.0f, &f2e);
+    if (g7 <= 0.0f) return f2e;
+    float tl = 0.0f, gl = g0, tk = 1.0f, gk = g7;
+    for (int i = 0; i < 6; ++i) {
+        float fi, gi = g_of(a, d, h, T[i], &fi);
+        if (gi >= 0.0f) { tk = T[i]; gk = gi; break; }
+        tl = T[i];
+        gl = gi;
+    }
+    float ts = tl + (tk - tl) * ((-gl) / (gk - gl));
+    g_of(a, d, h, ts, &f2);
+    return f2;
+}
+
+static float seg_seg_d2(v3 a1, v3 b1, v3 a2, v3 b2) {
+    v3 d1 = {b1.x - a1.x, b1.y - a1.y, b1.z - a1.z};
+    v3 d2 = {b2.x - a2.x, b2.y - a2.y, b2.z - a2.z};
+    v3 w = {a1.x - a2.x, a1.y - a2.y, a1.z - a2.z};
+    float A = dot(d1, d1), E = dot(d2, d2), F = dot(d2, w);
+    float s, t;
+    if (A <= 1e-12f) {
+        s = 0.0f;
+        t = (E <= 1e-12f) ? 0.0f : c01(F / E);
+    } else {
+        float C = dot(d1, w);
+        if (E <= 1e-12f) {
+            t = 0.0f;
+            s = c01(-C / A);
+        } else {
+            float Bd = dot(d1, d2);
+            float den = A * E - Bd * Bd;
+            s = den > 0.0f ? c01((Bd * F - C * E) / den) : 0.0f;
+            float tn = Bd * s + F;
+            if (tn < 0.0f) { t = 0.0f; s = c01(-C / A); }
+            else if (tn > E) { t = 1.0f; s = c01((Bd - C) / A); }
+            else t = tn / E;
+        }
+    }
+    v3 p1 = {a1.x + d1.x * s, a1.y + d1.y * s, a1.z + d1.z * s};
+    v3 p2 = {a2.x + d2.x * t, a2.y + d2.y * t, a2.z + d2.z * t};
+    v3 dd = {p1.x - p2.x, p1.y - p2.y, p1.z - p2.z};
+    return dot(dd, dd);
+}
+
+static int cap_vs_box(const ro_scene* s, int c, v3 A, v3 B, const aabb* u, int j) {
+    if ((s->box_exempt[j] >> c) & 1u) return 0;
+    if (disjoint(u, s->box_lo[j], s->box_hi[j])) return 0;
+    const float cs = s->box_cs[j], sn = s->box_sn[j];
+    float pa[3], pb[3];
+    float dx = A.x - s->box_c[j][0], dy = A.y - s->box_c[j][1], dz = A.z - s->box_c[j][2];
+    pa[0] = cs * dx + sn * dy; pa[1] = cs * dy - sn * dx; pa[2] = dz;
+    dx = B.x - s->box_c[j][0]; dy = B.y - s->box_c[j][1]; dz = B.z - s->box_c[j][2];
+    pb[0] = cs * dx + sn * dy; pb[1] = cs * dy - sn * dx; pb[2] = dz;
+    const float r = s->cap_r[c];
+    return seg_box_d2(pa, pb, s->box_h[j]) <= r * r;
+}
+
+static int pair_hit(const ro_scene* s, int p, const v3* A, const v3* B) {
+    int i = s->pair[p][0], j = s->pair[p][1];
+    aabb u = cap_box(A[i], B[i], s->cap_r[i]);
+    aabb v = cap_box(A[j], B[j], s->cap_r[j]);
+    if (disjoint(&u, v.lo, v.hi)) return 0;
+    float rr = s->cap_r[i] + s->cap_r[j];
+    return seg_seg_d2(A[i], B[i], A[j], B[j]) <= rr * rr;
+}
+
+int ro_state_valid(const ro_scene* s, const float q[NQ]) {
+    v3 A[NCAPMAX], B[NCAPMAX];
+    capsules_world(s, q, A, B);
+    for (int c = 0; c < s->ncap; ++c) {
+        aabb u = cap_box(A[c], B[c], s->cap_r[c]);
+        if (u.lo[2] <= s->plane_z) return 0;
+        for (int j = 0; j < s->nbox; ++j)
+            if (cap_vs_box(s, c, A[c], B[c], &u, j)) return 0;
+    }
+    for (int p = 0; p < s->npair; ++p)
+        if (pair_hit(s, p, A, B)) return 0;
+    return 1;
+}
+
+int ro_state_contacts(const ro_scene* s, const double qd[NQ], int32_t* out, int32_t cap) {
+    float q[NQ];
+    for (int i = 0; i < NQ; ++i) q[i] = (float)qd[i];
+    v3 A[NCAPMAX], B[NCAPMAX];
+    capsules_world(s, q, A, B);
+    int n = 0;
+#define PUSH(l, o) do { if (n < cap && out) { out[2 * n] = (l); out[2 * n + 1] = (o); } ++n; } while (0)
+    for (int c = 0; c < s->ncap; ++c) {
+        aabb u = cap_box(A[c], B[c], s->cap_r[c]);
+        if (u.lo[2] <= s->plane_z) PUSH(s->cap_link[c], -1);
+        for (int j = 0; j < s->nbox; ++j)
+            if (cap_vs_box(s, c, A[c], B[c], &u, j)) PUSH(s->cap_link[c], j);
+    }
+    for (int p = 0; p < s->npair; ++p)
+        if (pair_hit(s, p, A, B)) PUSH(s->cap_link[s->pair[p][0]], -2 - s->cap_link[s->pair[p][1]]);
+#undef PUSH
+    return n;
+}
+
+int64_t ro_check_states(const ro_scene* s, const float* q, int64_t n, uint8_t* flags, int threads) {
+#ifdef _OPENMP
+    if (threads > 0) omp_set_num_threads(threads);
+#pragma omp parallel for schedule(static)
+#endif
+    for (int64_t i = 0; i < n; ++i) flags[i] = (uint8_t)ro_state_valid(s, q + NQ * i);
+    (void)threads;
+    return n;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Philox4x32-10 (Salmon et al. 2011; Random123)                             */
+/* ------------------------------------------------------------------------- */
+
+void ro_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3], k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; ++r) {
+        if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c1 = (uint32_t)p1;
+        c3 = (uint32_t)p0;
+        c0 = n0;
+        c2 = n2;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+#define SAMPLE_TAG 0x52425035u
+
+/* uniform sample g in [lo, hi] */
+static void sample_state(uint64_t seed, uint64_t g, const double* lo, const double* hi, double* q) {
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t u[12];
+    for (uint32_t j = 0; j < 3; ++j) {
+        uint32_t ctr[4] = {(uint32_t)g, (uint32_t)(g >> 32), j, SAMPLE_TAG};
+        ro_philox(ctr, key, u + 4 * j);
+    }
+    for (int i = 0; i < NQ; ++i) {
+        double x = (double)u[i] * 2.3283064365386962890625e-10;
+        q[i] = lo[i] + (hi[i] - lo[i]) * x;
+    }
+}
+
+/* ------------------------------------------------------------------------- */
+/* float64 state space (OMPL RealVectorStateSpace semantics)                 */
+/* ------------------------------------------------------------------------- */
+
+static double dist2(const double* a, const double* b) {
+    double s = 0.0;
+    for (int i = 0; i < NQ; ++i) {
+        double d = a[i] - b[i];
+        s = s + d * d;
+    }
+    return s;
+}
+static void interp(const double* a, const double* b, double t, double* out) {
+    for (int i = 0; i < NQ; ++i) out[i] = a[i] + (b[i] - a[i]) * t;
+}
+static int valid_d(const ro_scene* s, const double* q) {
+    float f[NQ];
+    for (int i = 0; i < NQ; ++i) f[i] = (float)q[i];
+    return ro_state_valid(s, f);
+}
+
+/* checkMotion with the endpoint chosen by mode (0: `to`, 1: `from`) — OMPL
+ * DiscreteMotionValidator::checkMotion [EXT-OMPL] visits the interior in bisection
+ * order; the validity result does not depend on the order. */
+static int edge_valid(const ro_scene* s, const double* from, const double* to, int mode, double res,
+                      int64_t* states) {
+    double d = sqrt(dist2(from, to));
+    int nd = (int)ceil(d / res);
+    ++*states;
+    if (!valid_d(s, mode ? from : to)) return 0;
+    if (nd >= 2) {
+        /* FIFO of intervals (1, nd-1) */
+        int qa[512], qb[512], head = 0, tail = 0;
+        int* big_a = NULL;
+        int* big_b = NULL;
+        int capq = 512;
+        int* A = qa;
+        int* B = qb;
+        if (nd > 500) {
+            capq = nd + 8;
+            big_a = (int*)malloc(sizeof(int) * capq);
+            big_b = (int*)malloc(sizeof(int) * capq);
+            A = big_a;
+            B = big_b;
+        }
+        A[tail] = 1; B[tail] = nd - 1; ++tail;
+        int ok = 1;
+        double st[NQ];
+        while (head < tail) {
+            int a = A[head], b = B[head];
+            ++head;
+            int mid = (a + b) / 2;
+            interp(from, to, (double)mid / (double)nd, st);
+            ++*states;
+            if (!valid_d(s, st)) { ok = 0; break; }
+            if (a < mid) { A[tail] = a; B[tail] = mid - 1; ++tail; }
+            if (mid < b) { A[tail] = mid + 1; B[tail] = b; ++tail; }
+        }
+        free(big_a);
+        free(big_b);
+        return ok;
+    }
+    return 1;
+}
+
+int ro_check_edge(const ro_scene* s, const double* qa, const double* qb, double res, int64_t* states) {
+    int64_t dummy = 0;
+    return edge_valid(s, qa, qb, 0, res, states ? states : &dummy);
+}
+
+int64_t ro_check_edges(const ro_scene* s, const double* qa, const double* qb, int64_t n, double res,
+                       uint8_t* out) {
+    int64_t states = 0;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 64) reduction(+ : states)
+#endif
+    for (int64_t i = 0; i < n; ++i) {
+        int64_t st = 0;
+        out[i] = (uint8_t)edge_valid(s, qa + NQ * i, qb + NQ * i, 0, res, &st);
+        states += st;
+    }
+    return states;
+}
+
+/* ------------------------------------------------------------------------- */
+/* trees                                                                     */
+/* ------------------------------------------------------------------------- */
+
+typedef struct {
+    double* q;
+    int32_t* parent;
+    uint8_t* cand;   /* start tree: extension node whose connect did not reach */
+    int64_t n, cap;
+} tree_t;
+
+static int tree_init(tree_t* t, int64_t cap) {
+    t->q = (double*)malloc(sizeof(double) * NQ * cap);
+    t->parent = (int32_t*)malloc(sizeof(int32_t) * cap);
+    t->cand = (uint8_t*)calloc(cap, 1);
+    t->n = 0;
+    t->cap = cap;
+    return t->q && t->parent && t->cand;
+}
+static void tree_free(tree_t* t) {
+    free(t->q);
+    free(t->parent);
+    free(t->cand);
+}
+static int64_t tree_add(tree_t* t, const double* q, int32_t parent) {
+    memcpy(t->q + NQ * t->n, q, sizeof(double) * NQ);
+    t->parent[t->n] = parent;
+    t->cand[t->n] = 0;
+    return t->n++;
+}
+/* nearest node among the first n (ties -> lowest index) */
+static int32_t nearest(const tree_t* t, int64_t n, const double* x) {
+    double best = INFINITY;
+    int32_t idx = -1;
+    for (int64_t j = 0; j < n; ++j) {
+        double d = dist2(t->q + NQ * j, x);
+        if (d < best) { best = d; idx = (int32_t)j; }
+    }
+    return idx;
+}
+
+static void steer(const double* near, const double* target, double range, double* out, int* reach) {
+    double d = sqrt(dist2(near, target));
+    if (d > range) {
+        interp(near, target, range / d, out);
+        *reach = 0;
+    } else {
+        memcpy(out, target, sizeof(double) * NQ);
+        *reach = 1;
+    }
+}
+
+/* connect chain from node state y toward x: up to cmax steps of `range`
+ * (cmax = ceil(maxExtent / range) + 1 covers any pair of in-bounds states).
+ * Returns step count m; *reach = whether step m lands on x. */
+static int build_chain(const double* y, const double* x, double range, double (*chain)[NQ], int cmax,
+                       int* reach) {
+    const double* cur = y;
+    *reach = 0;
+    for (int m = 0; m < cmax; ++m) {
+        int r;
+        steer(cur, x, range, chain[m], &r);
+        if (r) { *reach = 1; return m + 1; }
+        cur = chain[m];
+    }
+    return cmax;
+}
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static int out_of_bounds(const double* q, const double* lo, const double* hi) {
+    const double eps = 2.220446049250313e-16; /* OMPL satisfiesBounds tolerance */
+    for (int i = 0; i < NQ; ++i)
+        if (q[i] - eps > hi[i] || q[i] + eps < lo[i]) return 1;
+    return 0;
+}
+
+/* PathGeometric::interpolate(count) [EXT-OMPL, SURVEY App. B.4] */
+int ro_interpolate(const double* path, int32_t n, int32_t count, double* out, int32_t cap) {
+    if (count < n || n < 2) {
+        if (n > cap) return -1;
+        memcpy(out, path, sizeof(double) * NQ * n);
+        return n;
+    }
+    if (count > cap) return -1;
+    double remaining = 0.0;
+    for (int i = 0; i + 1 < n; ++i) remaining += sqrt(dist2(path + NQ * i, path + NQ * (i + 1)));
+    int m = 0;
+    int cnt = count;
+    const int n1 = n - 1;
+    for (int i = 0; i < n1; ++i) {
+        const double* s1 = path + NQ * i;
+        const double* s2 = path + NQ * (i + 1);
+        memcpy(out + NQ * m++, s1, sizeof(double) * NQ);
+        int maxN = cnt + i - n;
+        if (maxN > 0) {
+            double seg = sqrt(dist2(s1, s2));
+            int ns = (i + 1 == n1) ? maxN + 2 : (int)floor(0.5 + (double)cnt * seg / remaining) + 1;
+            if (ns > 2) {
+                ns -= 2;
+                if (ns > maxN) ns = maxN;
+                for (int j = 1; j <= ns; ++j) interp(s1, s2, (double)j / (double)(ns + 1), out + NQ * m++);
+            } else {
+                ns = 0;
+            }
+            cnt -= ns + 1;
+            remaining -= seg;
+        } else {
+            cnt--;
+        }
+    }
+    memcpy(out + NQ * m++, path + NQ * n1, sizeof(double) * NQ);
+    return m;
+}
+
+/* walk a tree from node to its root (inclusive) */
+static int walk(const tree_t* t, int32_t node, double* out, int cap) {
+    int n = 0;
+    while (node >= 0) {
+        if (n >= cap) return -1;
+        memcpy(out + NQ * n++, t->q + NQ * node, sizeof(double) * NQ);
+        node = t->parent[node];
+    }
+    return n;
+}
+
+#define SIMPLIFY_MAXN 1024
+
+/* greedy vertex reduction: from each kept vertex jump to the
+ * farthest later vertex with a valid straight edge. */
+static int simplify_path(const ro_scene* s, double* path, int n, double res, int64_t* states) {
+    if (n < 3 || n > SIMPLIFY_MAXN) return n;
+    double* out = (double*)malloc(sizeof(double) * NQ * n);
+    int m = 0, i = 0;
+    memcpy(out, path, sizeof(double) * NQ);
+    m = 1;
+    while (i < n - 1) {
+        int j = n - 1;
+        while (j > i + 1 && !edge_valid(s, path + NQ * i, path + NQ * j, 0, res, states)) --j;
+        memcpy(out + NQ * m++, path + NQ * j, sizeof(double) * NQ);
+        i = j;
+    }
+    memcpy(path, out, sizeof(double) * NQ * m);
+    free(out);
+    return m;
+}
+
+int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], const double lo[NQ],
+            const double hi[NQ], const rp_plan_params* pp, int32_t rank, int32_t world,
+            ro_allgather_fn fn, void* user, double* path_out, int32_t path_cap, int32_t* n_out,
+            int32_t* status_out, rp_stats* stats) {
+    const double t_begin = now_s();
+    rp_stats st;
+    memset(&st, 0, sizeof st);
+    *n_out = 0;
+    *status_out = RP_STATUS_NONE;
+    if (world < 1) world = 1;
+    if (rank < 0 || rank >= world) return RP_ERR_ARG;
+    if (world > 1 && !fn) return RP_ERR_ARG;
+
+    double ext2 = 0.0;
+    for (int i = 0; i < NQ; ++i) ext2 += (hi[i] - lo[i]) * (hi[i] - lo[i]);
+    const double max_extent = sqrt(ext2);
+    rp_plan_params p = *pp;
+    if (p.batch <= 0) p.batch = 4096;
+    if (p.range <= 0) p.range = 0.2 * max_extent;
+    if (p.resolution <= 0) p.resolution = 0.01 * max_extent;
+    if (p.timeout_s <= 0) p.timeout_s = 5.0;
+    if (p.max_iters <= 0) p.max_iters = INT64_MAX;
+    if (p.tree_capacity <= 0) p.tree_capacity = 1 << 22;
+    if (p.batch % world) return RP_ERR_ARG;
+    const int cmax = (int)ceil(max_extent / p.range) + 1;
+
+    /* PlannerInputStates: invalid start / goal are skipped -> status */
+    if (out_of_bounds(start, lo, hi) || !valid_d(s, start)) {
+        *status_out = RP_STATUS_INVALID_START;
+        st.states_checked += 1;
+        if (stats) *stats = st;
+        return RP_OK;
+    }
+    if (out_of_bounds(goal, lo, hi) || !valid_d(s, goal)) {
+        *status_out = RP_STATUS_INVALID_GOAL;
+        st.states_checked += 2;
+        if (stats) *stats = st;
+        return RP_OK;
+    }
+    st.states_checked += 2;
+
+    tree_t T[2];
+    if (!tree_init(&T[0], p.tree_capacity) || !tree_init(&T[1], p.tree_capacity)) return RP_ERR_CAPACITY;
+    tree_add(&T[0], start, -1);
+    tree_add(&T[1], goal, -1);
+
+    const int64_t B = p.batch;
+    const int64_t per = B / world;
+    int32_t* res = (int32_t*)malloc(sizeof(int32_t) * B);
+    int32_t* mine = (int32_t*)malloc(sizeof(int32_t) * (per + 1));
+    int32_t* rbuf = (int32_t*)malloc(sizeof(int32_t) * (per + 1) * world);
+    int64_t* tnode = (int64_t*)malloc(sizeof(int64_t) * B);
+    int32_t* trec = (int32_t*)malloc(sizeof(int32_t) * 2 * (B + world));
+    int32_t* tmine = (int32_t*)malloc(sizeof(int32_t) * 2 * (B + world));
+    double (*chain)[NQ] = (double(*)[NQ])malloc(sizeof(double) * NQ * cmax);
+
+    int solved = 0;
+    int32_t s_node = -1, g_node = -1; /* solution join nodes (start tree, goal tree) */
+    const double t_solve = now_s();
+    int64_t iter = 0;
+    for (; iter < p.max_iters; ++iter) {
+        /* timeout: in a group every rank votes through the first exchange so that
+         * all ranks leave the loop at the same iteration */
+        const int tflag = (now_s() - t_solve) >= p.timeout_s;
+        if (world == 1 && tflag) break;
+        const int a_start = (iter % 2) == 0;
+        tree_t* A = a_start ? &T[0] : &T[1];
+        tree_t* Bt = a_start ? &T[1] : &T[0];
+        if (A->n + B > A->cap || Bt->n + B * cmax > Bt->cap) break;
+        const int64_t TA = A->n, TB = Bt->n;
+        const uint64_t g0 = (uint64_t)iter * (uint64_t)B;
+        /* extension: my slice of the batch */
+        for (int64_t k = 0; k < per; ++k) {
+            const int64_t i = rank * per + k;
+            double qr[NQ], qn[NQ];
+            int reach;
+            sample_state(p.seed, g0 + (uint64_t)i, lo, hi, qr);
+            int32_t nn = nearest(A, TA, qr);
+            steer(A->q + NQ * nn, qr, p.range, qn, &reach);
+            int ok = a_start ? edge_valid(s, A->q + NQ * nn, qn, 0, p.resolution, &st.states_checked)
+                             : edge_valid(s, qn, A->q + NQ * nn, 1, p.resolution, &st.states_checked);
+            st.edges_checked++;
+            mine[k] = ok ? nn : -1;
+        }
+        if (world > 1) {
+            double te = now_s();
+            mine[per] = tflag;
+            if (fn(user, mine, rbuf, (int64_t)(sizeof(int32_t) * (per + 1)))) { solved = -1; break; }
+            st.exchange_ms += 1e3 * (now_s() - te);
+            int any = 0;
+            for (int r = 0; r < world; ++r) {
+                memcpy(res + r * per, rbuf + r * (per + 1), sizeof(int32_t) * per);
+                any |= rbuf[r * (per + 1) + per];
+            }
+            if (any) break;
+        } else {
+            memcpy(res, mine, sizeof(int32_t) * per);
+        }
+        /* append accepted extension nodes in global sample order */
+        int64_t nacc = 0;
+        for (int64_t i = 0; i < B; ++i) {
+            if (res[i] < 0) continue;
+            double qr[NQ], qn[NQ];
+            int reach;
+            sample_state(p.seed, g0 + (uint64_t)i, lo, hi, qr);
+            steer(A->q + NQ * res[i], qr, p.range, qn, &reach);
+            tnode[nacc++] = tree_add(A, qn, res[i]);
+        }
+        st.samples += B;
+        /* connect: my slice of the accepted targets */
+        const int64_t pt = (nacc + world - 1) / world;
+        for (int64_t k = 0; k < pt; ++k) {
+            const int64_t t = rank * pt + k;
+            tmine[2 * k] = -1;
+            tmine[2 * k + 1] = 0;
+            if (t >= nacc) continue;
+            const double* x = A->q + NQ * tnode[t];
+            int32_t y = nearest(Bt, TB, x);
+            int reach;
+            int m = build_chain(Bt->q + NQ * y, x, p.range, chain, cmax, &reach);
+            int L = 0;
+            for (int c = 0; c < m; ++c) {
+                const double* from = c == 0 ? Bt->q + NQ * y : chain[c - 1];
+                int ok = a_start ? edge_valid(s, chain[c], from, 1, p.resolution, &st.states_checked)
+                                 : edge_valid(s, from, chain[c], 0, p.resolution, &st.states_checked);
+                st.edges_checked++;
+                if (!ok) break;
+                ++L;
+            }
+            tmine[2 * k] = y;
+            tmine[2 * k + 1] = L;
+        }
+        if (world > 1) {
+            double te = now_s();
+            if (fn(user, tmine, trec, (int64_t)(sizeof(int32_t) * 2 * pt))) { solved = -1; break; }
+            st.exchange_ms += 1e3 * (now_s() - te);
+        } else {
+            memcpy(trec, tmine, sizeof(int32_t) * 2 * pt);
+        }
+        /* append connect chains in target order; first REACHED wins */
+        for (int64_t t = 0; t < nacc; ++t) {
+            const int32_t y = trec[2 * t];
+            const int L = trec[2 * t + 1];
+            const double* x = A->q + NQ * tnode[t];
+            int reach;
+            int m = build_chain(Bt->q + NQ * y, x, p.range, chain, cmax, &reach);
+            int32_t par = y;
+            for (int c = 0; c < L; ++c) par = (int32_t)tree_add(Bt, chain[c], par);
+            const int reached = (L == m) && reach;
+            if (reached && !solved) {
+                solved = 1;
+                if (a_start) {       /* x in start tree, chain end in goal tree */
+                    s_node = A->parent[tnode[t]];
+                    g_node = par;
+                } else {             /* chain end in start tree, x in goal tree */
+                    s_node = Bt->parent[par];
+                    g_node = (int32_t)tnode[t];
+                }
+            }
+            if (!reached && a_start) A->cand[tnode[t]] = 1;
+        }
+        if (solved) { ++iter; break; }
+    }
+    st.iterations = iter;
+    st.solve_ms = 1e3 * (now_s() - t_solve);
+    st.start_tree_size = T[0].n;
+    st.goal_tree_size = T[1].n;
+
+    int rc = RP_OK;
+    int64_t cap = T[0].n + T[1].n + 2;
+    double* raw = (double*)malloc(sizeof(double) * NQ * cap);
+    int n_raw = 0;
+    if (solved == 1) {
+        int ns = walk(&T[0], s_node, raw, (int)cap);
+        for (int i = 0; i < ns / 2; ++i)
+            for (int k = 0; k < NQ; ++k) {
+                double tmp = raw[NQ * i + k];
+                raw[NQ * i + k] = raw[NQ * (ns - 1 - i) + k];
+                raw[NQ * (ns - 1 - i) + k] = tmp;
+            }
+        int ng = walk(&T[1], g_node, raw + NQ * ns, (int)(cap - ns));
+        n_raw = ns + ng;
+        *status_out = RP_STATUS_EXACT;
+    } else if (solved == 0) {
+        /* approximate: start-tree extension node closest to the goal */
+        double best = INFINITY;
+        int32_t bi = -1;
+        for (int64_t j = 0; j < T[0].n; ++j) {
+            if (!T[0].cand[j]) continue;
+            double d = dist2(T[0].q + NQ * j, goal);
+            if (d < best) { best = d; bi = (int32_t)j; }
+        }
+        if (bi >= 0) {
+            int ns = walk(&T[0], bi, raw, (int)cap);
+            for (int i = 0; i < ns / 2; ++i)
+                for (int k = 0; k < NQ; ++k) {
+                    double tmp = raw[NQ * i + k];
+                    raw[NQ * i + k] = raw[NQ * (ns - 1 - i) + k];
+                    raw[NQ * (ns - 1 - i) + k] = tmp;
+                }
+            n_raw = ns;
+            *status_out = RP_STATUS_APPROXIMATE;
+        } else {
+            *status_out = RP_STATUS_TIMEOUT;
+        }
+    } else {
+        rc = RP_ERR_EXCHANGE;
+    }
+    st.path_states_raw = n_raw;
+    if (n_raw > 0) {
+        double t0 = now_s();
+        if (p.simplify) n_raw = simplify_path(s, raw, n_raw, p.resolution, &st.states_checked);
+        st.simplify_ms = 1e3 * (now_s() - t0);
+        st.path_states_simplified = n_raw;
+        int m = (p.n_waypoints > 0) ? ro_interpolate(raw, n_raw, p.n_waypoints, path_out, path_cap)
+                                    : (n_raw <= path_cap ? (memcpy(path_out, raw, sizeof(double) * NQ * n_raw), n_raw) : -1);
+        if (m < 0) rc = RP_ERR_CAPACITY;
+        else *n_out = m;
+    }
+    free(raw);
+    free(res); free(mine); free(rbuf); free(tnode); free(trec); free(tmine); free(chain);
+    tree_free(&T[0]);
+    tree_free(&T[1]);
+    st.total_ms = 1e3 * (now_s() - t_begin);
+    if (stats) *stats = st;
+    return rc;
+}
+
+/* geometry primitives exported for the unit tests */
+float ro_seg_box_d2(const float a[3], const float b[3], const float h[3]) { return seg_box_d2(a, b, h); }
+float ro_seg_seg_d2(const float a1[3], const float b1[3], const float a2[3], const float b2[3]) {
+    v3 p = {a1[0], a1[1], a1[2]}, q = {b1[0], b1[1], b1[2]}, r = {a2[0], a2[1], a2[2]}, s = {b2[0], b2[1], b2[2]};
+    return seg_seg_d2(p, q, r, s);
+}

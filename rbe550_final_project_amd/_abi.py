@@ -1,0 +1,76 @@
+"""ctypes mirrors of the C-ABI structs in include/rbe_planner.h (plain data only)."""
+import ctypes as C
+
+NQ = 9
+MAX_CAPSULES = 32
+MAX_SELF_PAIRS = 64
+MAX_BOXES = 64
+
+LINK_NAMES = ["link0", "link1", "link2", "link3", "link4", "link5", "link6", "link7",
+              "hand", "left_finger", "right_finger"]
+LINK_INDEX = {n: i for i, n in enumerate(LINK_NAMES)}
+# links whose contacts with the attached object are ignored (code/planning.py:222)
+ATTACH_EXEMPT_LINKS = ("left_finger", "right_finger", "hand")
+ATTACH_EXEMPT_MASK = sum(1 << LINK_INDEX[n] for n in ATTACH_EXEMPT_LINKS)
+
+OK = 0
+ERR_ARG, ERR_DEVICE, ERR_STATE, ERR_CAPACITY, ERR_EXCHANGE = -1, -2, -3, -4, -5
+
+STATUS_NONE, STATUS_EXACT, STATUS_APPROXIMATE, STATUS_TIMEOUT, STATUS_INVALID_START, STATUS_INVALID_GOAL = range(6)
+STATUS_NAMES = {0: "NONE", 1: "EXACT", 2: "APPROXIMATE", 3: "TIMEOUT", 4: "INVALID_START", 5: "INVALID_GOAL"}
+
+
+class Capsule(C.Structure):
+    _fields_ = [("link", C.c_int32), ("a", C.c_float * 3), ("b", C.c_float * 3), ("radius", C.c_float)]
+
+
+class RobotDesc(C.Structure):
+    _fields_ = [("n_capsules", C.c_int32), ("capsules", Capsule * MAX_CAPSULES),
+                ("n_self_pairs", C.c_int32), ("self_pairs", (C.c_int32 * 2) * MAX_SELF_PAIRS)]
+
+
+class Box(C.Structure):
+    _fields_ = [("center", C.c_float * 3), ("half", C.c_float * 3), ("yaw", C.c_float)]
+
+
+class PlanParams(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("batch", C.c_int64), ("range", C.c_double),
+                ("resolution", C.c_double), ("timeout_s", C.c_double), ("max_iters", C.c_int64),
+                ("n_waypoints", C.c_int32), ("simplify", C.c_int32), ("tree_capacity", C.c_int64)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("states_checked", C.c_int64), ("edges_checked", C.c_int64), ("samples", C.c_int64),
+                ("iterations", C.c_int64), ("start_tree_size", C.c_int64), ("goal_tree_size", C.c_int64),
+                ("path_states_raw", C.c_int64), ("path_states_simplified", C.c_int64),
+                ("solve_ms", C.c_double), ("simplify_ms", C.c_double), ("total_ms", C.c_double),
+                ("exchange_ms", C.c_double)]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+def make_boxes(boxes):
+    """boxes: iterable of (center(3), half(3), yaw) -> ctypes array."""
+    boxes = list(boxes)
+    arr = (Box * max(1, len(boxes)))()
+    for i, (c, h, yaw) in enumerate(boxes):
+        arr[i].center[:] = [float(v) for v in c]
+        arr[i].half[:] = [float(v) for v in h]
+        arr[i].yaw = float(yaw)
+    return arr, len(boxes)
+
+
+def make_params(seed=0, batch=4096, range_=0.0, resolution=0.0, timeout_s=5.0, max_iters=0,
+                n_waypoints=100, simplify=True, tree_capacity=0):
+    p = PlanParams()
+    p.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    p.batch = int(batch)
+    p.range = float(range_)
+    p.resolution = float(resolution)
+    p.timeout_s = float(timeout_s)
+    p.max_iters = int(max_iters)
+    p.n_waypoints = int(n_waypoints or 0)
+    p.simplify = 1 if simplify else 0
+    p.tree_capacity = int(tree_capacity)
+    return p

@@ -1,0 +1,444 @@
+// rp_kernels.h — HIP kernels of the planner hot path (gfx950).
+//
+//   k_validity    one lane per state: FK + plane/box/self collision    (planning.py:209-230)
+//   k_edges       one lane per (edge, interpolation slot)             (OMPL checkMotion)
+//   k_ext_nn      one lane per sample: Philox sample, brute-force NN over the
+//                 tree (LDS tiles), steering                          (RRTConnect growTree)
+//   k_conn_nn     one lane per connect target: NN + connect chain     (RRTConnect connect)
+//   k_*append     tree appends in global sample order (scan offsets)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "rp_math.h"
+#include "rp_plan_math.h"
+
+namespace rp {
+
+constexpr int VBLOCK = 256;     // validity / edge block size (4 waves)
+constexpr int NNBLOCK = 256;    // NN block size
+constexpr int NNTILE = 256;     // tree nodes per LDS tile (256 x 72 B = 18 KiB)
+
+// ---------------------------------------------------------------------------
+// state validity
+// ---------------------------------------------------------------------------
+
+// Scene access: kLds = stage the scene record in LDS once per workgroup (the
+// north-star design); otherwise wave-uniform scalar loads (s_load) from the
+// constant-cached global record. Both read identical bytes.
+template <bool kLds>
+struct SceneRef;
+
+template <>
+struct SceneRef<false> {
+    const DevScene* p;
+    __device__ SceneRef(const DevScene* g, DevScene*) : p(g) {}
+};
+template <>
+struct SceneRef<true> {
+    const DevScene* p;
+    __device__ SceneRef(const DevScene* g, DevScene* lds) : p(lds) {
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(g);
+        uint32_t* dst = reinterpret_cast<uint32_t*>(lds);
+        constexpr int W = sizeof(DevScene) / 4;
+        for (int k = threadIdx.x; k < W; k += blockDim.x) dst[k] = src[k];
+        __syncthreads();
+    }
+};
+
+template <bool kLds>
+__global__ __launch_bounds__(VBLOCK) void k_validity(const float* __restrict__ q, int64_t n,
+                                                     uint8_t* __restrict__ flags,
+                                                     const DevScene* __restrict__ gsc) {
+    __shared__ DevScene lds[kLds ? 1 : 0 + 1];
+    SceneRef<kLds> sc(gsc, lds);
+    const int64_t i = (int64_t)blockIdx.x * VBLOCK + threadIdx.x;
+    if (i >= n) return;
+    float qq[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) qq[k] = q[i * NQ + k];
+    flags[i] = state_collides(qq, sc.p) ? 0 : 1;
+}
+
+// ---------------------------------------------------------------------------
+// edge validity (DiscreteMotionValidator::checkMotion semantics)
+// ---------------------------------------------------------------------------
+// Edge e: states `from` -> `to`, nd[e] segments (nd < 0: no edge). Slot 0 is the
+// checked endpoint (mode 0: `to`, mode 1: `from`), slots 1..nd-1 the interior
+// states from + (to - from) * slot / nd. valid[e] must be 1 on entry; a colliding
+// slot clears it. Optional prefix groups (connect chains): edges are grouped
+// `group` at a time; gfail[g] = first failing edge index within the group, and
+// slots of later edges of that group are skipped.
+template <bool kLds>
+__global__ __launch_bounds__(VBLOCK) void k_edges(const double* __restrict__ from,
+                                                  const double* __restrict__ to,
+                                                  const int* __restrict__ nd, int64_t n_edges,
+                                                  int kmax, int mode, uint8_t* valid, int group,
+                                                  int* gfail, unsigned long long* counter,
+                                                  const DevScene* __restrict__ gsc) {
+    __shared__ DevScene lds[kLds ? 1 : 0 + 1];
+    SceneRef<kLds> sc(gsc, lds);
+    const int64_t idx = (int64_t)blockIdx.x * VBLOCK + threadIdx.x;
+    const int64_t e = idx / kmax;
+    const int slot = (int)(idx - e * kmax);
+    bool run = false;
+    int nde = -1;
+    if (e < n_edges) {
+        nde = nd[e];
+        const int slots = nde > 1 ? nde : 1;
+        run = nde >= 0 && slot < slots && valid[e] != 0;
+        if (run && gfail) {
+            const int g = (int)(e / group), s = (int)(e - (int64_t)g * group);
+            run = gfail[g] > s;
+        }
+    }
+    const unsigned long long ballot = __ballot(run);
+    if (counter && (threadIdx.x & 63) == 0 && ballot) atomicAdd(counter, (unsigned long long)__popcll(ballot));
+    if (!run) return;
+    double st[NQ];
+    const double* a = from + e * NQ;
+    const double* b = to + e * NQ;
+    if (slot == 0) {
+        const double* ep = mode ? a : b;
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) st[k] = ep[k];
+    } else {
+        interp(a, b, (double)slot / (double)nde, st);
+    }
+    float qq[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) qq[k] = (float)st[k];
+    if (state_collides(qq, sc.p)) {
+        valid[e] = 0;
+        if (gfail) {
+            const int g = (int)(e / group), s = (int)(e - (int64_t)g * group);
+            atomicMin(&gfail[g], s);
+        }
+    }
+}
+
+// nd for arbitrary edges (API / simplification) and the max over edges
+__global__ void k_edge_prep(const double* __restrict__ from, const double* __restrict__ to, int64_t n,
+                            double res, int* nd, uint8_t* valid, int* kmax) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n) return;
+    const int c = segment_count(from + e * NQ, to + e * NQ, res);
+    nd[e] = c;
+    valid[e] = 1;
+    atomicMax(kmax, c > 1 ? c : 1);
+}
+
+// ---------------------------------------------------------------------------
+// brute-force nearest neighbour over a tree (AoS float64, LDS tiles)
+// ---------------------------------------------------------------------------
+// Every lane scans the nodes in increasing index with a strict `<`, so ties go to
+// the lowest index — the oracle's rule. All lanes of the block must call it.
+__device__ __forceinline__ int32_t nn_tiled(const double* __restrict__ tree, int64_t T,
+                                            const double x[NQ], bool active, double* tile) {
+    double best = __builtin_inf();
+    int32_t bi = -1;
+    for (int64_t base = 0; base < T; base += NNTILE) {
+        const int cnt = (int)((T - base) < NNTILE ? (T - base) : NNTILE);
+        __syncthreads();
+        const double* src = tree + base * NQ;
+        for (int k = threadIdx.x; k < cnt * NQ; k += blockDim.x) tile[k] = src[k];
+        __syncthreads();
+        if (active) {
+            for (int j = 0; j < cnt; ++j) {
+                const double d = dist2(tile + j * NQ, x);
+                if (d < best) { best = d; bi = (int32_t)(base + j); }
+            }
+        }
+    }
+    return bi;
+}
+
+struct Bounds { double lo[NQ]; double hi[NQ]; };
+
+// Extension step for samples [i0, i0 + n): sample, nearest node of tree A, steer,
+// edge record (a_start: near -> new, mode 0; goal tree: new -> near, mode 1).
+__global__ __launch_bounds__(NNBLOCK) void k_ext_nn(const double* __restrict__ A, int64_t TA,
+                                                    uint64_t seed, uint64_t g0, int64_t i0, int64_t n,
+                                                    Bounds bd, double range, double res, int a_start,
+                                                    double* __restrict__ efrom, double* __restrict__ eto,
+                                                    int* __restrict__ nd, uint8_t* __restrict__ valid,
+                                                    int32_t* __restrict__ near_out) {
+    __shared__ double tile[NNTILE * NQ];
+    const int64_t k = (int64_t)blockIdx.x * NNBLOCK + threadIdx.x;
+    const bool active = k < n;
+    double qr[NQ];
+    sample_state(seed, g0 + (uint64_t)(i0 + (active ? k : 0)), bd.lo, bd.hi, qr);
+    const int32_t nn = nn_tiled(A, TA, qr, active, tile);
+    if (!active) return;
+    double qn[NQ];
+    const double* near = A + (int64_t)nn * NQ;
+    steer(near, qr, range, qn);
+    double* f = efrom + k * NQ;
+    double* t = eto + k * NQ;
+#pragma unroll
+    for (int d = 0; d < NQ; ++d) {
+        f[d] = a_start ? near[d] : qn[d];
+        t[d] = a_start ? qn[d] : near[d];
+    }
+    nd[k] = segment_count(f, t, res);
+    valid[k] = 1;
+    near_out[k] = nn;
+}
+
+// res[k] = near index if the extension edge is valid, else -1
+__global__ void k_ext_result(const uint8_t* __restrict__ valid, const int32_t* __restrict__ near, int64_t n,
+                             int32_t* __restrict__ res) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) res[k] = valid[k] ? near[k] : -1;
+}
+
+// unpack the gathered extension records (rank-major, `per`+1 int32 per rank)
+__global__ void k_ext_unpack(const int32_t* __restrict__ rbuf, int64_t per, int world,
+                             int32_t* __restrict__ res, int* any_flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < per * world) {
+        const int64_t r = i / per, k = i - r * per;
+        res[i] = rbuf[r * (per + 1) + k];
+    }
+    if (i < world && rbuf[i * (per + 1) + per]) atomicOr(any_flag, 1);
+}
+
+__global__ void k_flag(const int32_t* __restrict__ v, int64_t n, int32_t* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = v[i] >= 0 ? 1 : 0;
+}
+
+// append accepted extension nodes at TA + exclusive_scan position
+__global__ void k_ext_append(const int32_t* __restrict__ res, const int32_t* __restrict__ incl, int64_t B,
+                             uint64_t seed, uint64_t g0, Bounds bd, double range, double* A, int32_t* Apar,
+                             uint8_t* Acand, int64_t TA) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B) return;
+    const int32_t nn = res[i];
+    if (nn < 0) return;
+    const int64_t pos = TA + incl[i] - 1;
+    double qr[NQ], qn[NQ];
+    sample_state(seed, g0 + (uint64_t)i, bd.lo, bd.hi, qr);
+    steer(A + (int64_t)nn * NQ, qr, range, qn);
+    double* dst = A + pos * NQ;
+#pragma unroll
+    for (int d = 0; d < NQ; ++d) dst[d] = qn[d];
+    Apar[pos] = nn;
+    Acand[pos] = 0;
+}
+
+// Connect targets [t0, t0 + n): x = A[TA0 + t]; nearest node y of tree B; chain
+// of steers from y toward x (<= cmax). Edge (t, s) direction by tree: B is the
+// start tree (a_start == 0): prev -> next, mode 0; else next -> prev, mode 1.
+__global__ __launch_bounds__(NNBLOCK) void k_conn_nn(const double* __restrict__ A, int64_t TA0, int64_t t0,
+                                                     int64_t n, const double* __restrict__ Bt, int64_t TB,
+                                                     double range, double res, int cmax, int a_start,
+                                                     double* __restrict__ efrom, double* __restrict__ eto,
+                                                     int* __restrict__ nd, uint8_t* __restrict__ valid,
+                                                     int* __restrict__ gfail, int32_t* __restrict__ yout,
+                                                     int32_t* __restrict__ mout) {
+    __shared__ double tile[NNTILE * NQ];
+    const int64_t k = (int64_t)blockIdx.x * NNBLOCK + threadIdx.x;
+    const bool active = k < n;
+    double x[NQ];
+    const double* xs = A + (TA0 + t0 + (active ? k : 0)) * NQ;
+#pragma unroll
+    for (int d = 0; d < NQ; ++d) x[d] = xs[d];
+    const int32_t y = nn_tiled(Bt, TB, x, active, tile);
+    if (!active) return;
+    double cur[NQ], nxt[NQ];
+    const double* ys = Bt + (int64_t)y * NQ;
+#pragma unroll
+    for (int d = 0; d < NQ; ++d) cur[d] = ys[d];
+    int m = cmax;
+    for (int s = 0; s < cmax; ++s) {
+        const int64_t e = k * cmax + s;
+        if (m < cmax) {  // chain already reached x
+            nd[e] = -1;
+            continue;
+        }
+        const int reach = steer(cur, x, range, nxt);
+        double* f = efrom + e * NQ;
+        double* t = eto + e * NQ;
+#pragma unroll
+        for (int d = 0; d < NQ; ++d) {
+            f[d] = a_start ? nxt[d] : cur[d];
+            t[d] = a_start ? cur[d] : nxt[d];
+        }
+        nd[e] = segment_count(f, t, res);
+        valid[e] = 1;
+#pragma unroll
+        for (int d = 0; d < NQ; ++d) cur[d] = nxt[d];
+        if (reach) m = s + 1;
+    }
+    gfail[k] = cmax;
+    yout[k] = y;
+    mout[k] = m;
+}
+
+// per-target record (y, L) with L = leading valid steps
+__global__ void k_conn_record(const int32_t* __restrict__ y, const int32_t* __restrict__ m,
+                              const int* __restrict__ gfail, int64_t n, int64_t pt, int32_t* __restrict__ rec) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= pt) return;
+    if (k < n) {
+        rec[2 * k] = y[k];
+        rec[2 * k + 1] = gfail[k] < m[k] ? gfail[k] : m[k];
+    } else {
+        rec[2 * k] = -1;
+        rec[2 * k + 1] = 0;
+    }
+}
+
+__global__ void k_conn_len(const int32_t* __restrict__ rec, int64_t n, int32_t* __restrict__ L) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) L[t] = rec[2 * t + 1];
+}
+
+// rebuild every target's chain from (y, L), append its first L nodes to tree B,
+// record the first REACHED target and approximate-solution candidates.
+__global__ void k_conn_append(const int32_t* __restrict__ rec, const int32_t* __restrict__ incl, int64_t n,
+                              const double* A, int64_t TA0, double* Bt, int32_t* Bpar, uint8_t* Bcand,
+                              int64_t TB, double range, int cmax, int a_start, uint8_t* Acand,
+                              int* first_reached, int32_t* chain_end) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    const int32_t y = rec[2 * t];
+    const int L = rec[2 * t + 1];
+    const int64_t off = TB + incl[t] - L;
+    double x[NQ], cur[NQ], nxt[NQ];
+    const double* xs = A + (TA0 + t) * NQ;
+    const double* ys = Bt + (int64_t)y * NQ;
+#pragma unroll
+    for (int d = 0; d < NQ; ++d) { x[d] = xs[d]; cur[d] = ys[d]; }
+    int32_t par = y;
+    int reach = 0, m = cmax;
+    for (int s = 0; s < cmax; ++s) {
+        reach = steer(cur, x, range, nxt);
+        if (s < L) {
+            double* dst = Bt + (off + s) * NQ;
+#pragma unroll
+            for (int d = 0; d < NQ; ++d) dst[d] = nxt[d];
+            Bpar[off + s] = par;
+            Bcand[off + s] = 0;
+            par = (int32_t)(off + s);
+        }
+        if (reach) { m = s + 1; break; }
+#pragma unroll
+        for (int d = 0; d < NQ; ++d) cur[d] = nxt[d];
+    }
+    const bool reached = (L == m) && reach;
+    chain_end[t] = L > 0 ? par : -1;
+    if (reached) atomicMin(first_reached, (int)t);
+    if (!reached && a_start) Acand[TA0 + t] = 1;
+}
+
+// walk parents from `node` to the root (single lane); returns count or -1 on overflow
+__global__ void k_walk(const double* __restrict__ T, const int32_t* __restrict__ par, int32_t node,
+                       double* __restrict__ out, int cap, int* n_out) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    int n = 0;
+    while (node >= 0) {
+        if (n >= cap) { *n_out = -1; return; }
+        for (int d = 0; d < NQ; ++d) out[n * NQ + d] = T[(int64_t)node * NQ + d];
+        ++n;
+        node = par[node];
+    }
+    *n_out = n;
+}
+
+// approximate solution: argmin over candidate start-tree nodes of dist2(node, goal),
+// ties -> lowest index. Stage 1: per-block (d, idx); stage 2: one block.
+struct DI { double d; int64_t i; };
+__device__ __forceinline__ DI di_min(DI a, DI b) {
+    if (b.d < a.d || (b.d == a.d && b.i < a.i)) return b;
+    return a;
+}
+__global__ void k_argmin1(const double* __restrict__ T, const uint8_t* __restrict__ cand, int64_t n,
+                          Bounds goalb, DI* partial) {
+    __shared__ DI red[256];
+    DI best = {__builtin_inf(), -1};
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+        if (!cand[j]) continue;
+        DI c = {dist2(T + j * NQ, goalb.lo), j};
+        best = di_min(best, c);
+    }
+    red[threadIdx.x] = best;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) red[threadIdx.x] = di_min(red[threadIdx.x], red[threadIdx.x + s]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+__global__ void k_argmin2(const DI* __restrict__ partial, int n, DI* out) {
+    __shared__ DI red[256];
+    DI best = {__builtin_inf(), -1};
+    for (int j = threadIdx.x; j < n; j += blockDim.x) best = di_min(best, partial[j]);
+    red[threadIdx.x] = best;
+    __syncthreads();
+    for (int s = 128; s > 0; s >>= 1) {
+        if (threadIdx.x < s) red[threadIdx.x] = di_min(red[threadIdx.x], red[threadIdx.x + s]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *out = red[0];
+}
+
+// diagnostics: collision pairs of one state (single lane)
+template <int C>
+__device__ void contacts_caps(const Capsules& k, const DevScene* sc, int32_t* out, int cap, int& n) {
+    if constexpr (C < NCAP) {
+        const float r = sc->cap[C][6];
+        const Aabb u = capsule_aabb(k.a[C], k.b[C], r);
+        if (u.lo.z <= sc->plane_z) {
+            if (n < cap) { out[2 * n] = CAP_LINK[C]; out[2 * n + 1] = -1; }
+            ++n;
+        }
+        // one box at a time through the same per-capsule test
+        DevScene one = *sc;
+        for (int j = 0; j < sc->n_boxes; ++j) {
+            for (int w = 0; w < 16; ++w) one.box[0][w] = sc->box[j][w];
+            one.n_boxes = 1;
+            one.plane_z = -__builtin_inff();
+            if (capsule_hits_boxes<C>(k, &one)) {
+                if (n < cap) { out[2 * n] = CAP_LINK[C]; out[2 * n + 1] = j; }
+                ++n;
+            }
+        }
+        contacts_caps<C + 1>(k, sc, out, cap, n);
+    }
+}
+template <int P>
+__device__ void contacts_pairs(const Capsules& k, const DevScene* sc, int32_t* out, int cap, int& n) {
+    if constexpr (P < NPAIR) {
+        if (pair_hits<P>(k, sc)) {
+            if (n < cap) { out[2 * n] = CAP_LINK[PAIRS[P][0]]; out[2 * n + 1] = -2 - CAP_LINK[PAIRS[P][1]]; }
+            ++n;
+        }
+        contacts_pairs<P + 1>(k, sc, out, cap, n);
+    }
+}
+__global__ void k_contacts(const double* __restrict__ qd, const DevScene* __restrict__ sc, int32_t* out,
+                           int cap, int* n_out) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    float q[NQ];
+    for (int i = 0; i < NQ; ++i) q[i] = (float)qd[i];
+    Capsules k;
+    fk_capsules(q, sc, k);
+    int n = 0;
+    contacts_caps<0>(k, sc, out, cap, n);
+    contacts_pairs<0>(k, sc, out, cap, n);
+    *n_out = n;
+}
+
+// numerics self-test: f64 sqrt / division / ceil and f64->f32 rounding on device
+__global__ void k_selftest(const double* __restrict__ x, int64_t n, double* __restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const double v = x[i];
+    out[4 * i + 0] = sqrt(v < 0 ? -v : v);
+    out[4 * i + 1] = 0.13037 / (v == 0 ? 1.0 : v);
+    out[4 * i + 2] = ceil(v * 7.0);
+    out[4 * i + 3] = (double)(float)v;
+}
+
+}  // namespace rp

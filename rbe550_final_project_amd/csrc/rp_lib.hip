@@ -1,0 +1,915 @@
+// rp_lib.hip — librbe_mi355x.so: C-ABI (include/rbe_planner.h) + host side of the
+// batched RRT-Connect planner driving the gfx950 kernels of rp_kernels.h.
+//
+// Replaces code/planning.py:59-207 (plan_path) and the OMPL/Genesis work behind it.
+// There is no CPU execution path: every validity evaluation runs on the GPU.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <chrono>
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rbe_planner.h"
+#include "rp_kernels.h"
+
+using namespace rp;
+
+#ifndef RP_VERSION
+#define RP_VERSION "0.1.0"
+#endif
+
+namespace {
+
+struct HipError {
+    std::string msg;
+};
+
+#define HIP_TRY(x)                                                                            \
+    do {                                                                                      \
+        hipError_t e_ = (x);                                                                  \
+        if (e_ != hipSuccess) {                                                               \
+            char b_[512];                                                                     \
+            snprintf(b_, sizeof b_, "%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, \
+                     __LINE__);                                                               \
+            throw HipError{b_};                                                               \
+        }                                                                                     \
+    } while (0)
+
+thread_local std::string g_create_error;
+
+double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    void ensure(size_t want) {
+        if (want <= n) return;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        size_t cap = std::max(want, n * 3 / 2);
+        HIP_TRY(hipMalloc(&p, cap * sizeof(T)));
+        n = cap;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+};
+
+inline unsigned blocks_for(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+
+}  // namespace
+
+struct Tree {
+    DevBuf<double> q;
+    DevBuf<int32_t> par;
+    DevBuf<uint8_t> cand;
+    int64_t n = 0;
+    void release() { q.release(); par.release(); cand.release(); }
+};
+
+struct rp_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool use_lds = false;
+    DevScene scene{};
+    DevScene* d_scene = nullptr;
+    bool have_scene = false;
+    rp_robot_desc robot{};
+    std::string err;
+    rp_stats stats{};
+    double last_kernel_ms = 0.0;
+
+    // scratch for the host-pointer APIs
+    DevBuf<float> q32;
+    DevBuf<uint8_t> flags;
+    DevBuf<double> ea, eb;
+    DevBuf<int> end_nd;
+    DevBuf<uint8_t> eval;
+    DevBuf<int> scalar;                  // small device scalars
+    DevBuf<unsigned long long> counter;
+
+    // planner workspace
+    Tree tree[2];
+    DevBuf<double> efrom, eto;
+    DevBuf<int> nd;
+    DevBuf<uint8_t> valid;
+    DevBuf<int32_t> near_, res, acc, incl, yv, mv, rec, Lv, chain_end, mine;
+    DevBuf<int> gfail;
+    DevBuf<char> cub_tmp;
+    DevBuf<double> path;
+    DevBuf<DI> partial;
+
+    // rank group
+    int rank = 0, world = 1;
+    void* g_send = nullptr;
+    void* g_recv = nullptr;
+    int64_t g_cap = 0;
+    rp_allgather_fn g_fn = nullptr;
+    void* g_user = nullptr;
+
+    ~rp_ctx() {
+        (void)hipSetDevice(device);
+        for (auto& t : tree) t.release();
+        q32.release(); flags.release(); ea.release(); eb.release(); end_nd.release(); eval.release();
+        scalar.release(); counter.release(); efrom.release(); eto.release(); nd.release(); valid.release();
+        near_.release(); res.release(); acc.release(); incl.release(); yv.release(); mv.release();
+        rec.release(); Lv.release(); chain_end.release(); mine.release(); gfail.release();
+        cub_tmp.release(); path.release(); partial.release();
+        if (d_scene) (void)hipFree(d_scene);
+        if (ev0) (void)hipEventDestroy(ev0);
+        if (ev1) (void)hipEventDestroy(ev1);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// launch helpers
+// ---------------------------------------------------------------------------
+
+void launch_validity(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, hipStream_t s) {
+    if (n <= 0) return;
+    if (c->use_lds)
+        hipLaunchKernelGGL(k_validity<true>, dim3(blocks_for(n, VBLOCK)), dim3(VBLOCK), 0, s, q, n, flags,
+                           c->d_scene);
+    else
+        hipLaunchKernelGGL(k_validity<false>, dim3(blocks_for(n, VBLOCK)), dim3(VBLOCK), 0, s, q, n, flags,
+                           c->d_scene);
+    HIP_TRY(hipGetLastError());
+}
+
+void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd, int64_t n, int kmax,
+                  int mode, uint8_t* valid, int group, int* gfail, hipStream_t s) {
+    if (n <= 0) return;
+    const int64_t threads = n * (int64_t)kmax;
+    if (c->use_lds)
+        hipLaunchKernelGGL(k_edges<true>, dim3(blocks_for(threads, VBLOCK)), dim3(VBLOCK), 0, s, from, to, nd, n,
+                           kmax, mode, valid, group, gfail, c->counter.p, c->d_scene);
+    else
+        hipLaunchKernelGGL(k_edges<false>, dim3(blocks_for(threads, VBLOCK)), dim3(VBLOCK), 0, s, from, to, nd,
+                           n, kmax, mode, valid, group, gfail, c->counter.p, c->d_scene);
+    HIP_TRY(hipGetLastError());
+}
+
+// inclusive scan of int32 (hipCUB) on the context stream
+void scan_incl(rp_ctx* c, const int32_t* in, int32_t* out, int64_t n) {
+    if (n <= 0) return;
+    size_t bytes = 0;
+    HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, bytes, in, out, (int)n, c->stream));
+    c->cub_tmp.ensure(bytes + 16);
+    HIP_TRY(hipcub::DeviceScan::InclusiveSum(c->cub_tmp.p, bytes, in, out, (int)n, c->stream));
+}
+
+template <typename T>
+T read_scalar(rp_ctx* c, const T* dev) {
+    T v;
+    HIP_TRY(hipMemcpyAsync(&v, dev, sizeof(T), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return v;
+}
+
+// all-gather `bytes` from dev buffer src into the group's recv buffer
+void exchange(rp_ctx* c, const void* src, int64_t bytes) {
+    if (bytes > c->g_cap) throw HipError{"group exchange buffer too small"};
+    HIP_TRY(hipMemcpyAsync(c->g_send, src, bytes, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const double t0 = now_s();
+    if (c->g_fn(c->g_user, bytes) != 0) throw HipError{"group all-gather callback failed"};
+    c->stats.exchange_ms += 1e3 * (now_s() - t0);
+}
+
+void upload_scene(rp_ctx* c) {
+    HIP_TRY(hipMemcpyAsync(c->d_scene, &c->scene, sizeof(DevScene), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+}
+
+// Edge validity for arbitrary host edges (API and simplification): out[i].
+int64_t check_edges_host(rp_ctx* c, const double* qa, const double* qb, int64_t n, double res,
+                         uint8_t* out) {
+    if (n <= 0) return 0;
+    c->ea.ensure(n * NQ);
+    c->eb.ensure(n * NQ);
+    c->end_nd.ensure(n);
+    c->eval.ensure(n);
+    c->scalar.ensure(16);
+    HIP_TRY(hipMemcpyAsync(c->ea.p, qa, sizeof(double) * NQ * n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->eb.p, qb, sizeof(double) * NQ * n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(c->scalar.p, 0, sizeof(int) * 16, c->stream));
+    HIP_TRY(hipMemsetAsync(c->counter.p, 0, sizeof(unsigned long long), c->stream));
+    hipLaunchKernelGGL(k_edge_prep, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, c->ea.p, c->eb.p, n, res,
+                       c->end_nd.p, c->eval.p, c->scalar.p);
+    HIP_TRY(hipGetLastError());
+    const int kmax = read_scalar(c, c->scalar.p);
+    launch_edges(c, c->ea.p, c->eb.p, c->end_nd.p, n, kmax, 0, c->eval.p, 1, nullptr, c->stream);
+    HIP_TRY(hipMemcpyAsync(out, c->eval.p, n, hipMemcpyDeviceToHost, c->stream));
+    const unsigned long long st = read_scalar(c, c->counter.p);
+    return (int64_t)st;
+}
+
+// ---------------------------------------------------------------------------
+// host path utilities (OMPL semantics; float64, fixed op order)
+// ---------------------------------------------------------------------------
+
+double h_dist2(const double* a, const double* b) {
+    double s = 0.0;
+    for (int i = 0; i < NQ; ++i) {
+        const double d = a[i] - b[i];
+        s = s + d * d;
+    }
+    return s;
+}
+void h_interp(const double* a, const double* b, double t, double* out) {
+    for (int i = 0; i < NQ; ++i) out[i] = a[i] + (b[i] - a[i]) * t;
+}
+
+// PathGeometric::interpolate(count) [EXT-OMPL, SURVEY App. B.4]
+std::vector<double> interpolate_path(const std::vector<double>& P, int count) {
+    const int n = (int)(P.size() / NQ);
+    if (count < n || n < 2) return P;
+    double remaining = 0.0;
+    for (int i = 0; i + 1 < n; ++i) remaining += std::sqrt(h_dist2(&P[NQ * i], &P[NQ * (i + 1)]));
+    std::vector<double> out;
+    out.reserve((size_t)count * NQ);
+    int cnt = count;
+    const int n1 = n - 1;
+    double tmp[NQ];
+    for (int i = 0; i < n1; ++i) {
+        const double* s1 = &P[NQ * i];
+        const double* s2 = &P[NQ * (i + 1)];
+        out.insert(out.end(), s1, s1 + NQ);
+        const int maxN = cnt + i - n;
+        if (maxN > 0) {
+            const double seg = std::sqrt(h_dist2(s1, s2));
+            int ns = (i + 1 == n1) ? maxN + 2 : (int)std::floor(0.5 + (double)cnt * seg / remaining) + 1;
+            if (ns > 2) {
+                ns -= 2;
+                if (ns > maxN) ns = maxN;
+                for (int j = 1; j <= ns; ++j) {
+                    h_interp(s1, s2, (double)j / (double)(ns + 1), tmp);
+                    out.insert(out.end(), tmp, tmp + NQ);
+                }
+            } else {
+                ns = 0;
+            }
+            cnt -= ns + 1;
+            remaining -= seg;
+        } else {
+            cnt--;
+        }
+    }
+    out.insert(out.end(), &P[NQ * n1], &P[NQ * n1] + NQ);
+    return out;
+}
+
+constexpr int SIMPLIFY_MAXN = 1024;
+
+// Greedy vertex reduction: every candidate shortcut (i, j>i+1) is
+// checked in ONE batched edge launch; then the greedy farthest-valid walk.
+std::vector<double> simplify_path(rp_ctx* c, const std::vector<double>& P, double res) {
+    const int n = (int)(P.size() / NQ);
+    if (n < 3 || n > SIMPLIFY_MAXN) return P;
+    std::vector<double> qa, qb;
+    std::vector<int> idx(n * n, -1);
+    for (int i = 0; i < n; ++i)
+        for (int j = i + 2; j < n; ++j) {
+            idx[i * n + j] = (int)(qa.size() / NQ);
+            qa.insert(qa.end(), &P[NQ * i], &P[NQ * i] + NQ);
+            qb.insert(qb.end(), &P[NQ * j], &P[NQ * j] + NQ);
+        }
+    const int64_t ne = (int64_t)(qa.size() / NQ);
+    std::vector<uint8_t> ok(ne);
+    c->stats.states_checked += check_edges_host(c, qa.data(), qb.data(), ne, res, ok.data());
+    c->stats.edges_checked += ne;
+    std::vector<double> out(P.begin(), P.begin() + NQ);
+    int i = 0;
+    while (i < n - 1) {
+        int j = n - 1;
+        while (j > i + 1 && !ok[idx[i * n + j]]) --j;
+        out.insert(out.end(), &P[NQ * j], &P[NQ * j] + NQ);
+        i = j;
+    }
+    return out;
+}
+
+bool out_of_bounds(const double* q, const double* lo, const double* hi) {
+    const double eps = 2.220446049250313e-16;  // OMPL satisfiesBounds tolerance
+    for (int i = 0; i < NQ; ++i)
+        if (q[i] - eps > hi[i] || q[i] + eps < lo[i]) return true;
+    return false;
+}
+
+bool state_valid_host(rp_ctx* c, const double* qd) {
+    float q[NQ];
+    for (int i = 0; i < NQ; ++i) q[i] = (float)qd[i];
+    c->q32.ensure(NQ);
+    c->flags.ensure(1);
+    HIP_TRY(hipMemcpyAsync(c->q32.p, q, sizeof q, hipMemcpyHostToDevice, c->stream));
+    launch_validity(c, c->q32.p, 1, c->flags.p, c->stream);
+    return read_scalar(c, c->flags.p) != 0;
+}
+
+std::vector<double> walk_tree(rp_ctx* c, int t, int32_t node) {
+    const int cap = (int)std::min<int64_t>(c->tree[t].n, 1 << 20);
+    c->path.ensure((size_t)cap * NQ);
+    c->scalar.ensure(16);
+    hipLaunchKernelGGL(k_walk, dim3(1), dim3(64), 0, c->stream, c->tree[t].q.p, c->tree[t].par.p, node, c->path.p,
+                       cap, c->scalar.p);
+    HIP_TRY(hipGetLastError());
+    const int n = read_scalar(c, c->scalar.p);
+    if (n < 0) throw HipError{"path walk overflow"};
+    std::vector<double> out((size_t)n * NQ);
+    HIP_TRY(hipMemcpyAsync(out.data(), c->path.p, sizeof(double) * NQ * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return out;
+}
+
+void reverse_states(std::vector<double>& v) {
+    const size_t n = v.size() / NQ;
+    for (size_t i = 0; i < n / 2; ++i)
+        for (int k = 0; k < NQ; ++k) std::swap(v[NQ * i + k], v[NQ * (n - 1 - i) + k]);
+}
+
+// ---------------------------------------------------------------------------
+// the batched RRT-Connect solve
+// ---------------------------------------------------------------------------
+
+int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* lo, const double* hi,
+              const rp_plan_params* pp, double* path_out, int32_t path_cap, int32_t* n_out,
+              int32_t* status_out) {
+    const double t_begin = now_s();
+    c->stats = rp_stats{};
+    *n_out = 0;
+    *status_out = RP_STATUS_NONE;
+    if (!c->have_scene) {
+        c->err = "rp_plan before rp_set_scene";
+        return RP_ERR_STATE;
+    }
+    double ext2 = 0.0;
+    for (int i = 0; i < NQ; ++i) ext2 += (hi[i] - lo[i]) * (hi[i] - lo[i]);
+    const double max_extent = std::sqrt(ext2);
+    rp_plan_params p = *pp;
+    if (p.batch <= 0) p.batch = 4096;
+    if (p.range <= 0) p.range = 0.2 * max_extent;
+    if (p.resolution <= 0) p.resolution = 0.01 * max_extent;
+    if (p.timeout_s <= 0) p.timeout_s = 5.0;
+    if (p.max_iters <= 0) p.max_iters = INT64_MAX;
+    if (p.tree_capacity <= 0) p.tree_capacity = 1 << 22;
+    const int world = c->world, rank = c->rank;
+    if (p.batch % world) {
+        c->err = "batch must be a multiple of the group size";
+        return RP_ERR_ARG;
+    }
+    const int cmax = (int)std::ceil(max_extent / p.range) + 1;
+    const int kmax = (int)std::ceil(p.range / p.resolution) + 2;
+    const int64_t B = p.batch, per = B / world;
+
+    if (out_of_bounds(start, lo, hi) || !state_valid_host(c, start)) {
+        *status_out = RP_STATUS_INVALID_START;
+        c->stats.states_checked = 1;
+        return RP_OK;
+    }
+    if (out_of_bounds(goal, lo, hi) || !state_valid_host(c, goal)) {
+        *status_out = RP_STATUS_INVALID_GOAL;
+        c->stats.states_checked = 2;
+        return RP_OK;
+    }
+    c->stats.states_checked = 2;
+
+    // workspace
+    const int64_t cap = p.tree_capacity;
+    for (auto& t : c->tree) {
+        t.q.ensure((size_t)cap * NQ);
+        t.par.ensure(cap);
+        t.cand.ensure(cap);
+        t.n = 0;
+    }
+    const int64_t ne = std::max<int64_t>(per, ((B + world - 1) / world) * cmax);
+    c->efrom.ensure(ne * NQ);
+    c->eto.ensure(ne * NQ);
+    c->nd.ensure(ne);
+    c->valid.ensure(ne);
+    c->near_.ensure(B);
+    c->res.ensure(B);
+    c->acc.ensure(B);
+    c->incl.ensure(B);
+    c->yv.ensure(B);
+    c->mv.ensure(B);
+    c->rec.ensure(2 * (B + world));
+    c->Lv.ensure(B);
+    c->chain_end.ensure(B);
+    c->gfail.ensure(B);
+    c->mine.ensure(per + 1);
+    c->scalar.ensure(16);
+    c->counter.ensure(1);
+    HIP_TRY(hipMemsetAsync(c->counter.p, 0, sizeof(unsigned long long), c->stream));
+
+    Bounds bd;
+    for (int i = 0; i < NQ; ++i) { bd.lo[i] = lo[i]; bd.hi[i] = hi[i]; }
+    // roots
+    {
+        const int32_t m1 = -1;
+        const uint8_t z = 0;
+        HIP_TRY(hipMemcpyAsync(c->tree[0].q.p, start, sizeof(double) * NQ, hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->tree[1].q.p, goal, sizeof(double) * NQ, hipMemcpyHostToDevice, c->stream));
+        for (auto& t : c->tree) {
+            HIP_TRY(hipMemcpyAsync(t.par.p, &m1, sizeof m1, hipMemcpyHostToDevice, c->stream));
+            HIP_TRY(hipMemcpyAsync(t.cand.p, &z, 1, hipMemcpyHostToDevice, c->stream));
+            t.n = 1;
+        }
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+
+    int solved = 0;
+    int32_t s_node = -1, g_node = -1;
+    const double t_solve = now_s();
+    int64_t iter = 0;
+    for (; iter < p.max_iters; ++iter) {
+        const int tflag = (now_s() - t_solve) >= p.timeout_s;
+        if (world == 1 && tflag) break;
+        const int a_start = (iter % 2) == 0;
+        Tree& A = c->tree[a_start ? 0 : 1];
+        Tree& Bt = c->tree[a_start ? 1 : 0];
+        if (A.n + B > cap || Bt.n + B * cmax > cap) break;
+        const int64_t TA = A.n, TB = Bt.n;
+        const uint64_t g0 = (uint64_t)iter * (uint64_t)B;
+
+        // ---- extension: my slice of the samples
+        hipLaunchKernelGGL(k_ext_nn, dim3(blocks_for(per, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA, p.seed,
+                           g0, (int64_t)rank * per, per, bd, p.range, p.resolution, a_start, c->efrom.p, c->eto.p,
+                           c->nd.p, c->valid.p, c->near_.p);
+        HIP_TRY(hipGetLastError());
+        launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, per, kmax, a_start ? 0 : 1, c->valid.p, 1, nullptr,
+                     c->stream);
+        c->stats.edges_checked += per;
+        if (world > 1) {
+            hipLaunchKernelGGL(k_ext_result, dim3(blocks_for(per, 256)), dim3(256), 0, c->stream, c->valid.p,
+                               c->near_.p, per, c->mine.p);
+            HIP_TRY(hipMemcpyAsync(c->mine.p + per, &tflag, sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+            exchange(c, c->mine.p, sizeof(int32_t) * (per + 1));
+            HIP_TRY(hipMemsetAsync(c->scalar.p, 0, sizeof(int), c->stream));
+            hipLaunchKernelGGL(k_ext_unpack, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream,
+                               (const int32_t*)c->g_recv, per, world, c->res.p, c->scalar.p);
+            HIP_TRY(hipGetLastError());
+            if (read_scalar(c, c->scalar.p)) break;  // some rank timed out
+        } else {
+            hipLaunchKernelGGL(k_ext_result, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->valid.p,
+                               c->near_.p, B, c->res.p);
+            HIP_TRY(hipGetLastError());
+        }
+        hipLaunchKernelGGL(k_flag, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->res.p, B, c->acc.p);
+        scan_incl(c, c->acc.p, c->incl.p, B);
+        hipLaunchKernelGGL(k_ext_append, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->res.p, c->incl.p, B,
+                           p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA);
+        HIP_TRY(hipGetLastError());
+        const int32_t nacc = read_scalar(c, c->incl.p + (B - 1));
+        A.n = TA + nacc;
+        c->stats.samples += B;
+        if (nacc == 0) continue;
+
+        // ---- connect: my slice of the accepted targets
+        const int64_t pt = (nacc + world - 1) / world;
+        const int64_t t0 = (int64_t)rank * pt;
+        const int64_t nmine = std::max<int64_t>(0, std::min<int64_t>(pt, nacc - t0));
+        if (nmine > 0) {
+            hipLaunchKernelGGL(k_conn_nn, dim3(blocks_for(nmine, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
+                               t0, nmine, Bt.q.p, TB, p.range, p.resolution, cmax, a_start, c->efrom.p, c->eto.p,
+                               c->nd.p, c->valid.p, c->gfail.p, c->yv.p, c->mv.p);
+            HIP_TRY(hipGetLastError());
+            launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, nmine * cmax, kmax, a_start ? 1 : 0, c->valid.p, cmax,
+                         c->gfail.p, c->stream);
+        }
+        hipLaunchKernelGGL(k_conn_record, dim3(blocks_for(pt, 256)), dim3(256), 0, c->stream, c->yv.p, c->mv.p,
+                           c->gfail.p, nmine, pt, c->rec.p);
+        HIP_TRY(hipGetLastError());
+        const int32_t* rec = c->rec.p;
+        if (world > 1) {
+            exchange(c, c->rec.p, sizeof(int32_t) * 2 * pt);
+            rec = (const int32_t*)c->g_recv;
+        }
+        hipLaunchKernelGGL(k_conn_len, dim3(blocks_for(nacc, 256)), dim3(256), 0, c->stream, rec, (int64_t)nacc,
+                           c->Lv.p);
+        scan_incl(c, c->Lv.p, c->incl.p, nacc);
+        const int big = INT_MAX;
+        HIP_TRY(hipMemcpyAsync(c->scalar.p, &big, sizeof(int), hipMemcpyHostToDevice, c->stream));
+        hipLaunchKernelGGL(k_conn_append, dim3(blocks_for(nacc, 256)), dim3(256), 0, c->stream, rec, c->incl.p,
+                           (int64_t)nacc, A.q.p, TA, Bt.q.p, Bt.par.p, Bt.cand.p, TB, p.range, cmax, a_start,
+                           A.cand.p, c->scalar.p, c->chain_end.p);
+        HIP_TRY(hipGetLastError());
+        int32_t hdr[2];
+        HIP_TRY(hipMemcpyAsync(&hdr[0], c->incl.p + (nacc - 1), sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(&hdr[1], c->scalar.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        c->stats.edges_checked += nmine * cmax;
+        Bt.n = TB + hdr[0];
+        const int fr = hdr[1];
+        if (fr != INT_MAX) {
+            solved = 1;
+            const int32_t end = read_scalar(c, c->chain_end.p + fr);
+            if (a_start) {   // x in the start tree; its parent is the join on the start side
+                s_node = read_scalar(c, A.par.p + (TA + fr));
+                g_node = end;
+            } else {         // chain end in the start tree; step back one node
+                s_node = read_scalar(c, Bt.par.p + end);
+                g_node = (int32_t)(TA + fr);
+            }
+            ++iter;
+            break;
+        }
+    }
+    c->stats.iterations = iter;
+    c->stats.solve_ms = 1e3 * (now_s() - t_solve);
+    c->stats.start_tree_size = c->tree[0].n;
+    c->stats.goal_tree_size = c->tree[1].n;
+
+    std::vector<double> raw;
+    if (solved) {
+        raw = walk_tree(c, 0, s_node);
+        reverse_states(raw);
+        std::vector<double> g = walk_tree(c, 1, g_node);
+        raw.insert(raw.end(), g.begin(), g.end());
+        *status_out = RP_STATUS_EXACT;
+    } else {
+        // approximate: closest start-tree extension node to the goal
+        const int64_t n0 = c->tree[0].n;
+        const int nb = (int)std::min<int64_t>(1024, blocks_for(n0, 256));
+        c->partial.ensure(nb + 1);
+        Bounds gb;
+        for (int i = 0; i < NQ; ++i) { gb.lo[i] = goal[i]; gb.hi[i] = 0.0; }
+        hipLaunchKernelGGL(k_argmin1, dim3(nb), dim3(256), 0, c->stream, c->tree[0].q.p, c->tree[0].cand.p, n0, gb,
+                           c->partial.p);
+        hipLaunchKernelGGL(k_argmin2, dim3(1), dim3(256), 0, c->stream, c->partial.p, nb, c->partial.p + nb);
+        HIP_TRY(hipGetLastError());
+        const DI best = read_scalar(c, c->partial.p + nb);
+        if (best.i >= 0) {
+            raw = walk_tree(c, 0, (int32_t)best.i);
+            reverse_states(raw);
+            *status_out = RP_STATUS_APPROXIMATE;
+        } else {
+            *status_out = RP_STATUS_TIMEOUT;
+        }
+    }
+    c->stats.states_checked += (int64_t)read_scalar(c, c->counter.p);
+    c->stats.path_states_raw = (int64_t)(raw.size() / NQ);
+    if (!raw.empty()) {
+        const double t0 = now_s();
+        if (p.simplify) raw = simplify_path(c, raw, p.resolution);
+        c->stats.simplify_ms = 1e3 * (now_s() - t0);
+        c->stats.path_states_simplified = (int64_t)(raw.size() / NQ);
+        if (p.n_waypoints > 0) raw = interpolate_path(raw, p.n_waypoints);
+        const int m = (int)(raw.size() / NQ);
+        if (m > path_cap) {
+            c->err = "path_cap too small";
+            return RP_ERR_CAPACITY;
+        }
+        std::memcpy(path_out, raw.data(), sizeof(double) * NQ * m);
+        *n_out = m;
+    }
+    c->stats.total_ms = 1e3 * (now_s() - t_begin);
+    return RP_OK;
+}
+
+bool structure_matches(const rp_robot_desc& r) {
+    if (r.n_capsules != NCAP || r.n_self_pairs != NPAIR) return false;
+    for (int i = 0; i < NCAP; ++i)
+        if (r.capsules[i].link != CAP_LINK[i]) return false;
+    for (int i = 0; i < NPAIR; ++i)
+        if (r.self_pairs[i][0] != PAIRS[i][0] || r.self_pairs[i][1] != PAIRS[i][1]) return false;
+    return true;
+}
+
+// built-in model = spec/franka_capsules.json
+const float kCaps[NCAP][7] = {
+    {-0.09f, 0.0f, 0.06f, -0.06f, 0.0f, 0.06f, 0.06f},       // link0
+    {0.0f, 0.0f, -0.193f, 0.0f, 0.0f, -0.05f, 0.06f},        // link1
+    {0.0f, 0.0f, -0.06f, 0.0f, 0.0f, 0.06f, 0.06f},          // link2
+    {0.0f, 0.0f, -0.22f, 0.0f, 0.0f, -0.07f, 0.06f},         // link3
+    {0.0f, 0.0f, -0.06f, 0.0f, 0.0f, 0.06f, 0.06f},          // link4
+    {0.0f, 0.0f, -0.31f, 0.0f, 0.0f, -0.21f, 0.06f},         // link5a
+    {0.0f, 0.08f, -0.20f, 0.0f, 0.08f, -0.06f, 0.025f},      // link5b
+    {0.0f, 0.0f, -0.07f, 0.0f, 0.0f, 0.01f, 0.05f},          // link6
+    {0.0f, 0.0f, -0.06f, 0.0f, 0.0f, 0.08f, 0.04f},          // link7
+    {0.0f, -0.05f, 0.04f, 0.0f, 0.05f, 0.04f, 0.04f},        // hand
+    {0.0f, 0.012f, 0.012f, 0.0f, 0.012f, 0.040f, 0.010f},    // left finger
+    {0.0f, 0.012f, 0.012f, 0.0f, 0.012f, 0.040f, 0.010f},    // right finger
+};
+
+}  // namespace
+
+// ===========================================================================
+// C-ABI
+// ===========================================================================
+
+#define RP_GUARD_BEGIN try {
+#define RP_GUARD_END(c)                          \
+    }                                            \
+    catch (const HipError& e) {                  \
+        if (c) (c)->err = e.msg;                 \
+        return RP_ERR_DEVICE;                    \
+    }                                            \
+    catch (const std::exception& e) {            \
+        if (c) (c)->err = e.what();              \
+        return RP_ERR_DEVICE;                    \
+    }
+
+extern "C" {
+
+const char* rp_version(void) { return "librbe_mi355x " RP_VERSION " gfx950"; }
+
+int rp_default_robot(rp_robot_desc* out) {
+    if (!out) return RP_ERR_ARG;
+    std::memset(out, 0, sizeof *out);
+    out->n_capsules = NCAP;
+    for (int i = 0; i < NCAP; ++i) {
+        out->capsules[i].link = CAP_LINK[i];
+        for (int k = 0; k < 3; ++k) {
+            out->capsules[i].a[k] = kCaps[i][k];
+            out->capsules[i].b[k] = kCaps[i][3 + k];
+        }
+        out->capsules[i].radius = kCaps[i][6];
+    }
+    out->n_self_pairs = NPAIR;
+    for (int i = 0; i < NPAIR; ++i) {
+        out->self_pairs[i][0] = PAIRS[i][0];
+        out->self_pairs[i][1] = PAIRS[i][1];
+    }
+    return RP_OK;
+}
+
+int rp_create(rp_ctx** out, int device, const rp_robot_desc* robot) {
+    if (!out) return RP_ERR_ARG;
+    *out = nullptr;
+    g_create_error.clear();
+    rp_robot_desc def;
+    if (!robot) {
+        rp_default_robot(&def);
+        robot = &def;
+    }
+    if (!structure_matches(*robot)) {
+        g_create_error = "robot description does not match the compiled Franka capsule structure";
+        return RP_ERR_ARG;
+    }
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) {
+        g_create_error = "no HIP device (librbe_mi355x has no CPU path)";
+        return RP_ERR_DEVICE;
+    }
+    if (device < 0 || device >= ndev) {
+        g_create_error = "device index out of range (librbe_mi355x has no CPU path)";
+        return RP_ERR_DEVICE;
+    }
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess || std::strstr(prop.gcnArchName, "gfx950") == nullptr) {
+        g_create_error = std::string("device is not gfx950 (MI355X): ") + prop.gcnArchName;
+        return RP_ERR_DEVICE;
+    }
+    rp_ctx* c = new rp_ctx();
+    try {
+        c->device = device;
+        HIP_TRY(hipSetDevice(device));
+        HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        HIP_TRY(hipEventCreate(&c->ev0));
+        HIP_TRY(hipEventCreate(&c->ev1));
+        HIP_TRY(hipMalloc(&c->d_scene, sizeof(DevScene)));
+        c->robot = *robot;
+        for (int i = 0; i < NCAP; ++i) {
+            for (int k = 0; k < 3; ++k) {
+                c->scene.cap[i][k] = robot->capsules[i].a[k];
+                c->scene.cap[i][3 + k] = robot->capsules[i].b[k];
+            }
+            c->scene.cap[i][6] = robot->capsules[i].radius;
+            c->scene.cap[i][7] = 0.0f;
+        }
+        c->scene.base[0] = 0.0f;
+        c->scene.base[1] = 0.0f;
+        c->scene.base[2] = 0.01f;
+        c->scene.plane_z = 0.0f;
+        c->scene.n_boxes = 0;
+        const char* lds = std::getenv("RP_SCENE_LDS");
+        c->use_lds = lds && lds[0] == '1';
+        c->counter.ensure(1);
+        c->scalar.ensure(16);
+        upload_scene(c);
+    } catch (const HipError& e) {
+        g_create_error = e.msg;
+        delete c;
+        return RP_ERR_DEVICE;
+    }
+    *out = c;
+    return RP_OK;
+}
+
+void rp_destroy(rp_ctx* c) { delete c; }
+
+int rp_set_scene(rp_ctx* c, const rp_box* boxes, int32_t n, float plane_z, const float base[3]) {
+    if (!c || n < 0 || n > MAX_BOXES || (n > 0 && !boxes)) return RP_ERR_ARG;
+    RP_GUARD_BEGIN
+    HIP_TRY(hipSetDevice(c->device));
+    for (int j = 0; j < n; ++j) {
+        const rp_box& b = boxes[j];
+        const float cs = (float)std::cos((double)b.yaw);
+        const float sn = (float)std::sin((double)b.yaw);
+        const float acs = cs < 0.0f ? -cs : cs, asn = sn < 0.0f ? -sn : sn;
+        float ext[3];
+        ext[0] = acs * b.half[0] + asn * b.half[1];
+        ext[1] = asn * b.half[0] + acs * b.half[1];
+        ext[2] = b.half[2];
+        float* r = c->scene.box[j];
+        for (int k = 0; k < 3; ++k) {
+            r[k] = b.center[k];
+            r[3 + k] = b.half[k];
+            r[8 + k] = b.center[k] - ext[k];
+            r[11 + k] = b.center[k] + ext[k];
+        }
+        r[6] = cs;
+        r[7] = sn;
+        r[14] = 0.0f;  // exempt bits = 0
+        r[15] = 0.0f;
+    }
+    c->scene.n_boxes = n;
+    c->scene.plane_z = plane_z;
+    if (base)
+        for (int k = 0; k < 3; ++k) c->scene.base[k] = base[k];
+    upload_scene(c);
+    c->have_scene = true;
+    return RP_OK;
+    RP_GUARD_END(c)
+}
+
+int rp_set_attached(rp_ctx* c, int32_t box, uint32_t link_mask) {
+    if (!c || box >= c->scene.n_boxes) return RP_ERR_ARG;
+    RP_GUARD_BEGIN
+    HIP_TRY(hipSetDevice(c->device));
+    for (int j = 0; j < c->scene.n_boxes; ++j) c->scene.box[j][14] = 0.0f;
+    if (box >= 0) {
+        uint32_t bits = 0;
+        for (int i = 0; i < NCAP; ++i)
+            if ((link_mask >> CAP_LINK[i]) & 1u) bits |= 1u << i;
+        std::memcpy(&c->scene.box[box][14], &bits, 4);
+    }
+    upload_scene(c);
+    return RP_OK;
+    RP_GUARD_END(c)
+}
+
+int rp_check_states(rp_ctx* c, const float* q, int64_t n, uint8_t* flags_out) {
+    if (!c || n < 0 || (n > 0 && (!q || !flags_out))) return RP_ERR_ARG;
+    if (n == 0) return RP_OK;
+    RP_GUARD_BEGIN
+    HIP_TRY(hipSetDevice(c->device));
+    c->q32.ensure((size_t)n * NQ);
+    c->flags.ensure(n);
+    HIP_TRY(hipMemcpyAsync(c->q32.p, q, sizeof(float) * NQ * n, hipMemcpyHostToDevice, c->stream));
+    launch_validity(c, c->q32.p, n, c->flags.p, c->stream);
+    HIP_TRY(hipMemcpyAsync(flags_out, c->flags.p, n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->stats.states_checked = n;
+    return RP_OK;
+    RP_GUARD_END(c)
+}
+
+int rp_check_states_device(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, void* stream) {
+    if (!c || n < 0 || (n > 0 && (!q || !flags))) return RP_ERR_ARG;
+    if (n == 0) return RP_OK;
+    RP_GUARD_BEGIN
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    HIP_TRY(hipEventRecord(c->ev0, s));
+    launch_validity(c, q, n, flags, s);
+    HIP_TRY(hipEventRecord(c->ev1, s));
+    c->stats.states_checked = n;
+    return RP_OK;
+    RP_GUARD_END(c)
+}
+
+int rp_last_kernel_ms(rp_ctx* c, double* ms) {
+    if (!c || !ms) return RP_ERR_ARG;
+    RP_GUARD_BEGIN
+    HIP_TRY(hipEventSynchronize(c->ev1));
+    float v = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&v, c->ev0, c->ev1));
+    *ms = v;
+    return RP_OK;
+    RP_GUARD_END(c)
+}
+
+int rp_check_edges(rp_ctx* c, const double* qa, const double* qb, int64_t n, double res, uint8_t* out) {
+    if (!c || n < 0 || (n > 0 && (!qa || !qb || !out)) || !(res > 0)) return RP_ERR_ARG;
+    if (n == 0) return RP_OK;
+    RP_GUARD_BEGIN
+    HIP_TRY(hipSetDevice(c->device));
+    c->stats = rp_stats{};
+    c->stats.states_checked = check_edges_host(c, qa, qb, n, res, out);
+    c->stats.edges_checked = n;
+    return RP_OK;
+    RP_GUARD_END(c)
+}
+
+int rp_check_edges_device(rp_ctx* c, const double* qa, const double* qb, int64_t n, double res, uint8_t* out,
+                          void* stream) {
+    if (!c || n < 0 || (n > 0 && (!qa || !qb || !out)) || !(res > 0)) return RP_ERR_ARG;
+    if (n == 0) return RP_OK;
+    RP_GUARD_BEGIN
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    c->end_nd.ensure(n);
+    c->scalar.ensure(16);
+    HIP_TRY(hipMemsetAsync(c->scalar.p, 0, sizeof(int), s));
+    hipLaunchKernelGGL(k_edge_prep, dim3(blocks_for(n, 256)), dim3(256), 0, s, qa, qb, n, res, c->end_nd.p, out,
+                       c->scalar.p);
+    HIP_TRY(hipGetLastError());
+    int kmax = 0;
+    HIP_TRY(hipMemcpyAsync(&kmax, c->scalar.p, sizeof(int), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    launch_edges(c, qa, qb, c->end_nd.p, n, kmax, 0, out, 1, nullptr, s);
+    return RP_OK;
+    RP_GUARD_END(c)
+}
+
+int rp_state_contacts(rp_ctx* c, const double q[RP_NQ], int32_t* pairs_out, int32_t cap) {
+    if (!c || !q || cap < 0 || (cap > 0 && !pairs_out)) return RP_ERR_ARG;
+    RP_GUARD_BEGIN
+    HIP_TRY(hipSetDevice(c->device));
+    c->ea.ensure(NQ);
+    c->scalar.ensure(16);
+    DevBuf<int32_t> out;
+    out.ensure(2 * (size_t)std::max(cap, 1));
+    HIP_TRY(hipMemcpyAsync(c->ea.p, q, sizeof(double) * NQ, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(k_contacts, dim3(1), dim3(64), 0, c->stream, c->ea.p, c->d_scene, out.p, cap, c->scalar.p);
+    HIP_TRY(hipGetLastError());
+    const int n = read_scalar(c, c->scalar.p);
+    if (cap > 0) {
+        HIP_TRY(hipMemcpyAsync(pairs_out, out.p, sizeof(int32_t) * 2 * std::min(n, cap), hipMemcpyDeviceToHost,
+                               c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+    }
+    out.release();
+    return n;
+    RP_GUARD_END(c)
+}
+
+int rp_plan(rp_ctx* c, const double start[RP_NQ], const double goal[RP_NQ], const double lo[RP_NQ],
+            const double hi[RP_NQ], const rp_plan_params* params, double* path_out, int32_t path_cap,
+            int32_t* n_out, int32_t* status_out) {
+    if (!c || !start || !goal || !lo || !hi || !params || !n_out || !status_out || path_cap < 0 ||
+        (path_cap > 0 && !path_out))
+        return RP_ERR_ARG;
+    RP_GUARD_BEGIN
+    HIP_TRY(hipSetDevice(c->device));
+    return plan_impl(c, start, goal, lo, hi, params, path_out, path_cap, n_out, status_out);
+    RP_GUARD_END(c)
+}
+
+int rp_group_init(rp_ctx* c, int32_t rank, int32_t world, void* send, void* recv, int64_t cap, rp_allgather_fn fn,
+                  void* user) {
+    if (!c || world < 1 || rank < 0 || rank >= world) return RP_ERR_ARG;
+    if (world > 1 && (!send || !recv || cap <= 0 || !fn)) return RP_ERR_ARG;
+    c->rank = rank;
+    c->world = world;
+    c->g_send = send;
+    c->g_recv = recv;
+    c->g_cap = cap;
+    c->g_fn = fn;
+    c->g_user = user;
+    return RP_OK;
+}
+
+int rp_get_stats(rp_ctx* c, rp_stats* out) {
+    if (!c || !out) return RP_ERR_ARG;
+    *out = c->stats;
+    return RP_OK;
+}
+
+const char* rp_last_error(rp_ctx* c) { return c ? c->err.c_str() : g_create_error.c_str(); }
+
+// Numerics self-test (test-only entry, not in the public header's contract list):
+// device sqrt / div / ceil / f64->f32 of x[i] -> out[4*i..4*i+3].
+int rp_selftest_f64(rp_ctx* c, const double* x, int64_t n, double* out) {
+    if (!c || n <= 0 || !x || !out) return RP_ERR_ARG;
+    RP_GUARD_BEGIN
+    HIP_TRY(hipSetDevice(c->device));
+    DevBuf<double> dx, dy;
+    dx.ensure(n);
+    dy.ensure(4 * n);
+    HIP_TRY(hipMemcpyAsync(dx.p, x, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
+    hipLaunchKernelGGL(k_selftest, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, dx.p, n, dy.p);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out, dy.p, sizeof(double) * 4 * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    dx.release();
+    dy.release();
+    return RP_OK;
+    RP_GUARD_END(c)
+}
+
+}  // extern "C"

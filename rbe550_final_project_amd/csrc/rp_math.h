@@ -1,0 +1,362 @@
+// rp_math.h — device arithmetic of the state-validity hot path (gfx950).
+//
+// Replaces what one reference validity callback triggers (code/planning.py:209-230):
+//   robot.set_qpos(q)         -> Genesis FK kernel            => fk_capsules()
+//   robot.detect_collision()  -> Genesis broad+narrow phase   => state_collides()
+//   collision_with_attached_object()                          => per-box exempt bits
+//
+// Numerics contract: float32, every operation written out in a fixed
+// order, compiled with -ffp-contract=off, so the CPU oracle (oracle/rbe_oracle.c),
+// which restates the same sequence, produces bit-identical flags. sin/cos come from
+// rp_sincos() (polynomial, +,-,* only), never from the device libm.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "rp_model.h"
+
+namespace rp {
+
+struct V3 { float x, y, z; };
+
+__device__ __forceinline__ float fminr(float a, float b) { return a < b ? a : b; }
+__device__ __forceinline__ float fmaxr(float a, float b) { return a > b ? a : b; }
+__device__ __forceinline__ float clamp01(float x) { return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x); }
+__device__ __forceinline__ float dot3(V3 u, V3 v) { return (u.x * v.x + u.y * v.y) + u.z * v.z; }
+
+// sin and cos of x, |x| < ~100: quadrant reduction with a 3-part pi/2, then
+// minimax polynomials on [-pi/4, pi/4].
+__device__ __forceinline__ void rp_sincos(float x, float* sn, float* cs) {
+    const float t = x * 0.636619772f;
+    const float k = floorf(t + 0.5f);
+    float r = x - k * 1.5703125f;
+    r = r - k * 4.837512969970703125e-4f;
+    r = r - k * 7.54978995489188216e-8f;
+    const float z = r * r;
+    float ps = -1.9515295891e-4f;
+    ps = ps * z;
+    ps = ps + 8.3321608736e-3f;
+    ps = ps * z;
+    ps = ps + -1.6666654611e-1f;
+    const float sr = r + (r * z) * ps;
+    float pc = 2.443315711809948e-5f;
+    pc = pc * z;
+    pc = pc + -1.388731625493765e-3f;
+    pc = pc * z;
+    pc = pc + 4.166664568298827e-2f;
+    const float cr = (1.0f - 0.5f * z) + (z * z) * pc;
+    const int qd = ((int)k) & 3;
+    float s = sr, c = cr;
+    if (qd == 1) { s = cr; c = -sr; }
+    else if (qd == 2) { s = -sr; c = -cr; }
+    else if (qd == 3) { s = -cr; c = sr; }
+    *sn = s;
+    *cs = c;
+}
+
+// A rigid frame: rotation columns c0, c1, c2 and origin p (world).
+struct Frame { V3 c0, c1, c2, p; };
+
+// R <- R * Rz(q)
+__device__ __forceinline__ void rot_z(Frame& f, float q) {
+    float s, c;
+    rp_sincos(q, &s, &c);
+    V3 n0, n1;
+    n0.x = c * f.c0.x + s * f.c1.x;
+    n0.y = c * f.c0.y + s * f.c1.y;
+    n0.z = c * f.c0.z + s * f.c1.z;
+    n1.x = c * f.c1.x - s * f.c0.x;
+    n1.y = c * f.c1.y - s * f.c0.y;
+    n1.z = c * f.c1.z - s * f.c0.z;
+    f.c0 = n0;
+    f.c1 = n1;
+}
+// R <- R * Rx(+90deg): [c0, c2, -c1]
+__device__ __forceinline__ void rot_xp(Frame& f) {
+    V3 t = f.c1;
+    f.c1 = f.c2;
+    f.c2.x = -t.x; f.c2.y = -t.y; f.c2.z = -t.z;
+}
+// R <- R * Rx(-90deg): [c0, -c2, c1]
+__device__ __forceinline__ void rot_xm(Frame& f) {
+    V3 t = f.c2;
+    f.c2 = f.c1;
+    f.c1.x = -t.x; f.c1.y = -t.y; f.c1.z = -t.z;
+}
+// p <- p + k * col
+__device__ __forceinline__ void shift(V3& p, float k, V3 col) {
+    p.x = p.x + k * col.x;
+    p.y = p.y + k * col.y;
+    p.z = p.z + k * col.z;
+}
+// world point of link-frame point (a0, a1, a2)
+__device__ __forceinline__ V3 xform(const Frame& f, float a0, float a1, float a2) {
+    V3 w;
+    w.x = ((f.p.x + a0 * f.c0.x) + a1 * f.c1.x) + a2 * f.c2.x;
+    w.y = ((f.p.y + a0 * f.c0.y) + a1 * f.c1.y) + a2 * f.c2.y;
+    w.z = ((f.p.z + a0 * f.c0.z) + a1 * f.c1.z) + a2 * f.c2.z;
+    return w;
+}
+
+struct Capsules { V3 a[NCAP]; V3 b[NCAP]; };
+
+template <int C>
+__device__ __forceinline__ void place(Capsules& k, const Frame& f, const DevScene* __restrict__ sc) {
+    const float* g = sc->cap[C];
+    k.a[C] = xform(f, g[0], g[1], g[2]);
+    k.b[C] = xform(f, g[3], g[4], g[5]);
+}
+
+// Franka Panda forward kinematics (MJCF bodies of
+// panda.xml that Genesis loads at code/scenes.py:85) -> world capsule endpoints.
+__device__ __forceinline__ void fk_capsules(const float q[NQ], const DevScene* __restrict__ sc,
+                                            Capsules& k) {
+    Frame f;
+    f.c0 = {1.0f, 0.0f, 0.0f};
+    f.c1 = {0.0f, 1.0f, 0.0f};
+    f.c2 = {0.0f, 0.0f, 1.0f};
+    f.p = {sc->base[0], sc->base[1], sc->base[2]};
+    place<C_LINK0>(k, f, sc);
+    // link1: pos (0,0,0.333), joint 1
+    shift(f.p, 0.333f, f.c2);
+    rot_z(f, q[0]);
+    place<C_LINK1>(k, f, sc);
+    // link2: quat (1,-1,0,0) = Rx(-90), joint 2
+    rot_xm(f);
+    rot_z(f, q[1]);
+    place<C_LINK2>(k, f, sc);
+    // link3: pos (0,-0.316,0), Rx(+90), joint 3
+    shift(f.p, -0.316f, f.c1);
+    rot_xp(f);
+    rot_z(f, q[2]);
+    place<C_LINK3>(k, f, sc);
+    // link4: pos (0.0825,0,0), Rx(+90), joint 4
+    shift(f.p, 0.0825f, f.c0);
+    rot_xp(f);
+    rot_z(f, q[3]);
+    place<C_LINK4>(k, f, sc);
+    // link5: pos (-0.0825,0.384,0), Rx(-90), joint 5
+    shift(f.p, -0.0825f, f.c0);
+    shift(f.p, 0.384f, f.c1);
+    rot_xm(f);
+    rot_z(f, q[4]);
+    place<C_LINK5A>(k, f, sc);
+    place<C_LINK5B>(k, f, sc);
+    // link6: Rx(+90), joint 6
+    rot_xp(f);
+    rot_z(f, q[5]);
+    place<C_LINK6>(k, f, sc);
+    // link7: pos (0.088,0,0), Rx(+90), joint 7
+    shift(f.p, 0.088f, f.c0);
+    rot_xp(f);
+    rot_z(f, q[6]);
+    place<C_LINK7>(k, f, sc);
+    // hand: pos (0,0,0.107), quat (0.9238795,0,0,-0.3826834) = Rz(-45deg)
+    shift(f.p, 0.107f, f.c2);
+    {
+        const float c = 0.70710677f, s = -0.70710677f;
+        V3 n0, n1;
+        n0.x = c * f.c0.x + s * f.c1.x;
+        n0.y = c * f.c0.y + s * f.c1.y;
+        n0.z = c * f.c0.z + s * f.c1.z;
+        n1.x = c * f.c1.x - s * f.c0.x;
+        n1.y = c * f.c1.y - s * f.c0.y;
+        n1.z = c * f.c1.z - s * f.c0.z;
+        f.c0 = n0;
+        f.c1 = n1;
+    }
+    place<C_HAND>(k, f, sc);
+    // fingers: pos (0,0,0.0584) from the hand, prismatic along +-hand y
+    shift(f.p, 0.0584f, f.c2);
+    {
+        Frame l = f;
+        shift(l.p, q[7], f.c1);
+        place<C_LFINGER>(k, l, sc);
+        Frame r = f;
+        shift(r.p, -q[8], f.c1);
+        r.c0.x = -f.c0.x; r.c0.y = -f.c0.y; r.c0.z = -f.c0.z;  // Rz(180)
+        r.c1.x = -f.c1.x; r.c1.y = -f.c1.y; r.c1.z = -f.c1.z;
+        place<C_RFINGER>(k, r, sc);
+    }
+}
+
+// Capsule AABB expanded by its radius.
+struct Aabb { V3 lo, hi; };
+__device__ __forceinline__ Aabb capsule_aabb(V3 a, V3 b, float r) {
+    Aabb o;
+    o.lo.x = fminr(a.x, b.x) - r; o.hi.x = fmaxr(a.x, b.x) + r;
+    o.lo.y = fminr(a.y, b.y) - r; o.hi.y = fmaxr(a.y, b.y) + r;
+    o.lo.z = fminr(a.z, b.z) - r; o.hi.z = fmaxr(a.z, b.z) + r;
+    return o;
+}
+__device__ __forceinline__ bool aabb_disjoint(const Aabb& u, const float* lo, const float* hi) {
+    return (u.lo.x > hi[0]) | (u.hi.x < lo[0]) | (u.lo.y > hi[1]) | (u.hi.y < lo[1]) |
+           (u.lo.z > hi[2]) | (u.hi.z < lo[2]);
+}
+__device__ __forceinline__ bool aabb_disjoint2(const Aabb& u, const Aabb& v) {
+    return (u.lo.x > v.hi.x) | (u.hi.x < v.lo.x) | (u.lo.y > v.hi.y) | (u.hi.y < v.lo.y) |
+           (u.lo.z > v.hi.z) | (u.hi.z < v.lo.z);
+}
+
+// g(t) = q(t) . d with q the excess of a + t d over the box [-h, h]; also |q|^2.
+__device__ __forceinline__ float excess_dot(V3 a, V3 d, V3 h, float t, float* f2) {
+    float px = a.x + t * d.x, py = a.y + t * d.y, pz = a.z + t * d.z;
+    float cx = px < -h.x ? -h.x : (px > h.x ? h.x : px);
+    float cy = py < -h.y ? -h.y : (py > h.y ? h.y : py);
+    float cz = pz < -h.z ? -h.z : (pz > h.z ? h.z : pz);
+    V3 qv = {px - cx, py - cy, pz - cz};
+    *f2 = dot3(qv, qv);
+    return dot3(qv, d);
+}
+
+// Segment a-b (box frame) vs box [-h, h]: squared distance is a convex piecewise
+// quadratic in t with C^1 joins; its derivative g is piecewise linear and
+// nondecreasing with breakpoints where a coordinate crosses +-h. Locate the root of
+// g between the sorted breakpoints and interpolate linearly inside that piece.
+__device__ __forceinline__ float segment_box_dist2(V3 a, V3 b, V3 h) {
+    V3 d = {b.x - a.x, b.y - a.y, b.z - a.z};
+    float T[6];
+    {
+        float u = 0.0f, v = 0.0f;
+        if (d.x != 0.0f) { float inv = 1.0f / d.x; u = (-h.x - a.x) * inv; v = (h.x - a.x) * inv; }
+        T[0] = clamp01(u); T[1] = clamp01(v);
+        u = 0.0f; v = 0.0f;
+        if (d.y != 0.0f) { float inv = 1.0f / d.y; u = (-h.y - a.y) * inv; v = (h.y - a.y) * inv; }
+        T[2] = clamp01(u); T[3] = clamp01(v);
+        u = 0.0f; v = 0.0f;
+        if (d.z != 0.0f) { float inv = 1.0f / d.z; u = (-h.z - a.z) * inv; v = (h.z - a.z) * inv; }
+        T[4] = clamp01(u); T[5] = clamp01(v);
+    }
+    // sorting network (12 exchanges) — the sorted multiset is order independent
+#define RP_CX(i, j) { float lo_ = fminr(T[i], T[j]); float hi_ = fmaxr(T[i], T[j]); T[i] = lo_; T[j] = hi_; }
+    RP_CX(0, 1) RP_CX(2, 3) RP_CX(4, 5) RP_CX(0, 2) RP_CX(3, 5) RP_CX(1, 4)
+    RP_CX(0, 1) RP_CX(2, 3) RP_CX(4, 5) RP_CX(1, 2) RP_CX(3, 4) RP_CX(2, 3)
+#undef RP_CX
+    float f2;
+    const float g0 = excess_dot(a, d, h, 0.0f, &f2);
+    float ts;
+    if (g0 >= 0.0f) {
+        return f2;
+    }
+    float f2e;
+    const float g7 = excess_dot(a, d, h, 1.0f, &f2e);
+    if (g7 <= 0.0f) {
+        return f2e;
+    }
+    float tl = 0.0f, gl = g0, tk = 1.0f, gk = g7;
+    bool found = false;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        float fi;
+        const float gi = excess_dot(a, d, h, T[i], &fi);
+        if (!found) {
+            if (gi >= 0.0f) { found = true; tk = T[i]; gk = gi; }
+            else { tl = T[i]; gl = gi; }
+        }
+    }
+    ts = tl + (tk - tl) * ((-gl) / (gk - gl));
+    excess_dot(a, d, h, ts, &f2);
+    return f2;
+}
+
+// Closest distance^2 between segments a1-b1 and a2-b2.
+__device__ __forceinline__ float segment_segment_dist2(V3 a1, V3 b1, V3 a2, V3 b2) {
+    V3 d1 = {b1.x - a1.x, b1.y - a1.y, b1.z - a1.z};
+    V3 d2 = {b2.x - a2.x, b2.y - a2.y, b2.z - a2.z};
+    V3 w = {a1.x - a2.x, a1.y - a2.y, a1.z - a2.z};
+    const float A = dot3(d1, d1), E = dot3(d2, d2), F = dot3(d2, w);
+    float s, t;
+    if (A <= 1e-12f) {
+        s = 0.0f;
+        t = (E <= 1e-12f) ? 0.0f : clamp01(F / E);
+    } else {
+        const float C = dot3(d1, w);
+        if (E <= 1e-12f) {
+            t = 0.0f;
+            s = clamp01(-C / A);
+        } else {
+            const float B = dot3(d1, d2);
+            const float den = A * E - B * B;
+            s = den > 0.0f ? clamp01((B * F - C * E) / den) : 0.0f;
+            const float tn = B * s + F;
+            if (tn < 0.0f) { t = 0.0f; s = clamp01(-C / A); }
+            else if (tn > E) { t = 1.0f; s = clamp01((B - C) / A); }
+            else { t = tn / E; }
+        }
+    }
+    V3 p1 = {a1.x + d1.x * s, a1.y + d1.y * s, a1.z + d1.z * s};
+    V3 p2 = {a2.x + d2.x * t, a2.y + d2.y * t, a2.z + d2.z * t};
+    V3 dd = {p1.x - p2.x, p1.y - p2.y, p1.z - p2.z};
+    return dot3(dd, dd);
+}
+
+// Capsule C vs every box of the scene (skipping exempt pairs).
+template <int C>
+__device__ __forceinline__ bool capsule_hits_boxes(const Capsules& k, const DevScene* __restrict__ sc) {
+    const float r = sc->cap[C][6];
+    const Aabb u = capsule_aabb(k.a[C], k.b[C], r);
+    if (u.lo.z <= sc->plane_z) return true;  // capsule vs ground plane
+    const int nb = sc->n_boxes;
+    bool hit = false;
+    for (int j = 0; j < nb && !hit; ++j) {
+        const float* bx = sc->box[j];
+        const uint32_t ex = __float_as_uint(bx[14]);
+        if ((ex >> C) & 1u) continue;
+        if (aabb_disjoint(u, bx + 8, bx + 11)) continue;
+        // narrow phase in the box frame (rotate by -yaw about z)
+        const float cs = bx[6], sn = bx[7];
+        V3 pa, pb;
+        {
+            const float dx = k.a[C].x - bx[0], dy = k.a[C].y - bx[1], dz = k.a[C].z - bx[2];
+            pa.x = cs * dx + sn * dy; pa.y = cs * dy - sn * dx; pa.z = dz;
+        }
+        {
+            const float dx = k.b[C].x - bx[0], dy = k.b[C].y - bx[1], dz = k.b[C].z - bx[2];
+            pb.x = cs * dx + sn * dy; pb.y = cs * dy - sn * dx; pb.z = dz;
+        }
+        V3 h = {bx[3], bx[4], bx[5]};
+        if (segment_box_dist2(pa, pb, h) <= r * r) hit = true;
+    }
+    return hit;
+}
+
+template <int P>
+__device__ __forceinline__ bool pair_hits(const Capsules& k, const DevScene* __restrict__ sc) {
+    constexpr int I = PAIRS[P][0], J = PAIRS[P][1];
+    const float ri = sc->cap[I][6], rj = sc->cap[J][6];
+    const Aabb u = capsule_aabb(k.a[I], k.b[I], ri);
+    const Aabb v = capsule_aabb(k.a[J], k.b[J], rj);
+    if (aabb_disjoint2(u, v)) return false;
+    const float rr = ri + rj;
+    return segment_segment_dist2(k.a[I], k.b[I], k.a[J], k.b[J]) <= rr * rr;
+}
+
+template <int C>
+__device__ __forceinline__ bool boxes_from(const Capsules& k, const DevScene* __restrict__ sc) {
+    if constexpr (C == NCAP) {
+        return false;
+    } else {
+        if (capsule_hits_boxes<C>(k, sc)) return true;
+        return boxes_from<C + 1>(k, sc);
+    }
+}
+template <int P>
+__device__ __forceinline__ bool pairs_from(const Capsules& k, const DevScene* __restrict__ sc) {
+    if constexpr (P == NPAIR) {
+        return false;
+    } else {
+        if (pair_hits<P>(k, sc)) return true;
+        return pairs_from<P + 1>(k, sc);
+    }
+}
+
+// true if the state collides with the plane, a (non-exempt) box, or itself.
+// The result is the OR over all tests; the order only decides how early a lane
+// stops (environment first: most random samples hit the ground or a box).
+__device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene* __restrict__ sc) {
+    Capsules k;
+    fk_capsules(q, sc, k);
+    if (boxes_from<0>(k, sc)) return true;
+    return pairs_from<0>(k, sc);
+}
+
+}  // namespace rp

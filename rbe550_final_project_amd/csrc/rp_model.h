@@ -1,0 +1,53 @@
+// rp_model.h — compile-time structure of the Franka Panda collision model
+// (capsule -> link assignment and self-collision pairs). The numeric geometry
+// (endpoints, radii) is runtime data (rp_robot_desc, spec/franka_capsules.json);
+// the structure is baked into the kernels so every capsule lives in registers
+// with compile-time indices (a runtime-indexed per-thread array would go to
+// scratch memory on gfx950). rp_create rejects a descriptor whose structure
+// differs from this one.
+#pragma once
+
+namespace rp {
+
+constexpr int NQ = 9;       // 7 arm joints + 2 fingers (code/planning.py:143-150)
+constexpr int NCAP = 12;
+constexpr int NLINK = 11;
+// link of each capsule: link0..link4, link5 (x2), link6, link7, hand, fingers
+constexpr int CAP_LINK[NCAP] = {0, 1, 2, 3, 4, 5, 5, 6, 7, 8, 9, 10};
+
+enum : int {
+    C_LINK0 = 0, C_LINK1, C_LINK2, C_LINK3, C_LINK4, C_LINK5A, C_LINK5B,
+    C_LINK6, C_LINK7, C_HAND, C_LFINGER, C_RFINGER
+};
+
+constexpr int NPAIR = 35;
+constexpr int PAIRS[NPAIR][2] = {
+    {C_LINK0, C_LINK5B}, {C_LINK0, C_LINK6}, {C_LINK0, C_LINK7}, {C_LINK0, C_HAND},
+    {C_LINK0, C_LFINGER}, {C_LINK0, C_RFINGER},
+    {C_LINK1, C_LINK5A}, {C_LINK1, C_LINK5B}, {C_LINK1, C_LINK6}, {C_LINK1, C_LINK7},
+    {C_LINK1, C_HAND}, {C_LINK1, C_LFINGER}, {C_LINK1, C_RFINGER},
+    {C_LINK2, C_LINK5A}, {C_LINK2, C_LINK5B}, {C_LINK2, C_LINK6}, {C_LINK2, C_LINK7},
+    {C_LINK2, C_HAND}, {C_LINK2, C_LFINGER}, {C_LINK2, C_RFINGER},
+    {C_LINK3, C_LINK6}, {C_LINK3, C_LINK7}, {C_LINK3, C_HAND}, {C_LINK3, C_LFINGER},
+    {C_LINK3, C_RFINGER},
+    {C_LINK4, C_LINK7}, {C_LINK4, C_HAND}, {C_LINK4, C_LFINGER}, {C_LINK4, C_RFINGER},
+    {C_LINK5A, C_HAND}, {C_LINK5A, C_LFINGER}, {C_LINK5A, C_RFINGER},
+    {C_LINK5B, C_HAND}, {C_LINK5B, C_LFINGER}, {C_LINK5B, C_RFINGER},
+};
+
+constexpr int MAX_BOXES = 64;
+
+// Device scene record (one constant buffer, read by wave-uniform scalar loads).
+// Box record: 16 floats so one s_load_dwordx16 fetches it.
+//   [0..2] centre  [3..5] half extents  [6] cos(yaw) [7] sin(yaw)
+//   [8..10] world AABB lo  [11..13] world AABB hi  [14] exempt-capsule bits  [15] pad
+struct DevScene {
+    float cap[NCAP][8];          // ax ay az bx by bz radius pad (link frame)
+    float box[MAX_BOXES][16];
+    float base[4];               // robot base translation (scenes.py:29-34), pad
+    float plane_z;
+    int n_boxes;
+    int pad[2];
+};
+
+}  // namespace rp

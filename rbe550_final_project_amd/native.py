@@ -1,0 +1,189 @@
+"""Loader of librbe_mi355x.so (the HIP extension) and a thin Python handle over it.
+
+The library is built in-tree (__graft_entry__.build() / `python -m
+rbe550_final_project_amd.build`). There is no fallback: if the library or a gfx950
+device is missing, every entry point raises.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_NAME = "librbe_mi355x.so"
+LIB_PATH = os.path.join(_HERE, LIB_NAME)
+
+# every symbol include/rbe_planner.h declares
+EXPORTS = ("rp_version", "rp_default_robot", "rp_create", "rp_destroy", "rp_set_scene", "rp_set_attached",
+           "rp_check_states", "rp_check_states_device", "rp_check_edges", "rp_check_edges_device",
+           "rp_state_contacts", "rp_plan", "rp_group_init", "rp_get_stats", "rp_last_error",
+           "rp_last_kernel_ms", "rp_selftest_f64")
+
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64)
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def load():
+    """Load the HIP extension; raise loudly if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(f"{LIB_PATH} is not built; run __graft_entry__.build() "
+                          "(there is no CPU fallback for the planner)")
+    L = C.CDLL(LIB_PATH)
+    vp, i32, i64, u32, f32, f64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_float, C.c_double
+    L.rp_version.restype = C.c_char_p
+    L.rp_default_robot.argtypes = [C.POINTER(_abi.RobotDesc)]
+    L.rp_create.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(_abi.RobotDesc)]
+    L.rp_destroy.argtypes = [vp]
+    L.rp_destroy.restype = None
+    L.rp_set_scene.argtypes = [vp, C.POINTER(_abi.Box), i32, f32, C.POINTER(f32)]
+    L.rp_set_attached.argtypes = [vp, i32, u32]
+    L.rp_check_states.argtypes = [vp, vp, i64, vp]
+    L.rp_check_states_device.argtypes = [vp, vp, i64, vp, vp]
+    L.rp_check_edges.argtypes = [vp, vp, vp, i64, f64, vp]
+    L.rp_check_edges_device.argtypes = [vp, vp, vp, i64, f64, vp, vp]
+    L.rp_state_contacts.argtypes = [vp, vp, vp, i32]
+    L.rp_plan.argtypes = [vp, vp, vp, vp, vp, C.POINTER(_abi.PlanParams), vp, i32, C.POINTER(i32), C.POINTER(i32)]
+    L.rp_group_init.argtypes = [vp, i32, i32, vp, vp, i64, vp, vp]
+    L.rp_get_stats.argtypes = [vp, C.POINTER(_abi.Stats)]
+    L.rp_last_error.argtypes = [vp]
+    L.rp_last_error.restype = C.c_char_p
+    L.rp_last_kernel_ms.argtypes = [vp, C.POINTER(f64)]
+    L.rp_selftest_f64.argtypes = [vp, vp, i64, vp]
+    _lib = L
+    return L
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def default_robot():
+    d = _abi.RobotDesc()
+    load().rp_default_robot(C.byref(d))
+    return d
+
+
+class Context:
+    """One planner context on one GPU (one per rank)."""
+
+    def __init__(self, device=0, robot=None):
+        L = load()
+        self._h = C.c_void_p()
+        self.robot = robot
+        rc = L.rp_create(C.byref(self._h), int(device), C.byref(robot) if robot is not None else None)
+        if rc != 0:
+            raise NativeError(f"rp_create failed ({rc}): {L.rp_last_error(None).decode()}")
+        self.device = device
+        self._cb = None
+        self._group_bufs = None
+
+    def close(self):
+        if self._h:
+            load().rp_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc < 0:
+            raise NativeError(f"{what} failed ({rc}): {load().rp_last_error(self._h).decode()}")
+        return rc
+
+    # -- scene ---------------------------------------------------------------
+    def set_scene(self, boxes, plane_z=0.0, base=(0.0, 0.0, 0.01)):
+        arr, n = _abi.make_boxes(boxes)
+        b = (C.c_float * 3)(*[float(v) for v in base])
+        self._check(load().rp_set_scene(self._h, arr, n, float(plane_z), b), "rp_set_scene")
+
+    def set_attached(self, box_index, link_mask=_abi.ATTACH_EXEMPT_MASK):
+        self._check(load().rp_set_attached(self._h, int(box_index), int(link_mask)), "rp_set_attached")
+
+    # -- validity ------------------------------------------------------------
+    def check_states(self, q):
+        q = np.ascontiguousarray(q, dtype=np.float32).reshape(-1, _abi.NQ)
+        out = np.empty(len(q), dtype=np.uint8)
+        self._check(load().rp_check_states(self._h, _ptr(q), len(q), _ptr(out)), "rp_check_states")
+        return out
+
+    def check_states_device(self, q_ptr, n, flags_ptr, stream=None):
+        self._check(load().rp_check_states_device(self._h, C.c_void_p(q_ptr), int(n), C.c_void_p(flags_ptr),
+                                                  C.c_void_p(stream) if stream else None),
+                    "rp_check_states_device")
+
+    def last_kernel_ms(self):
+        v = C.c_double()
+        self._check(load().rp_last_kernel_ms(self._h, C.byref(v)), "rp_last_kernel_ms")
+        return v.value
+
+    def check_edges(self, qa, qb, resolution):
+        qa = np.ascontiguousarray(qa, dtype=np.float64).reshape(-1, _abi.NQ)
+        qb = np.ascontiguousarray(qb, dtype=np.float64).reshape(-1, _abi.NQ)
+        out = np.empty(len(qa), dtype=np.uint8)
+        self._check(load().rp_check_edges(self._h, _ptr(qa), _ptr(qb), len(qa), float(resolution), _ptr(out)),
+                    "rp_check_edges")
+        return out
+
+    def contacts(self, q, cap=64):
+        q = np.ascontiguousarray(q, dtype=np.float64)
+        out = np.zeros((cap, 2), dtype=np.int32)
+        n = self._check(load().rp_state_contacts(self._h, _ptr(q), _ptr(out), cap), "rp_state_contacts")
+        return [tuple(int(v) for v in x) for x in out[:min(n, cap)]]
+
+    def selftest_f64(self, x):
+        x = np.ascontiguousarray(x, dtype=np.float64)
+        out = np.zeros((len(x), 4), dtype=np.float64)
+        self._check(load().rp_selftest_f64(self._h, _ptr(x), len(x), _ptr(out)), "rp_selftest_f64")
+        return out
+
+    # -- planning ------------------------------------------------------------
+    def plan(self, start, goal, lo, hi, params, path_cap=4096):
+        start = np.ascontiguousarray(start, dtype=np.float64)
+        goal = np.ascontiguousarray(goal, dtype=np.float64)
+        lo = np.ascontiguousarray(lo, dtype=np.float64)
+        hi = np.ascontiguousarray(hi, dtype=np.float64)
+        out = np.zeros((path_cap, _abi.NQ), dtype=np.float64)
+        n = C.c_int32(0)
+        status = C.c_int32(0)
+        self._check(load().rp_plan(self._h, _ptr(start), _ptr(goal), _ptr(lo), _ptr(hi), C.byref(params),
+                                   _ptr(out), path_cap, C.byref(n), C.byref(status)), "rp_plan")
+        return out[:n.value].copy(), status.value
+
+    def stats(self):
+        st = _abi.Stats()
+        self._check(load().rp_get_stats(self._h, C.byref(st)), "rp_get_stats")
+        return st.as_dict()
+
+    # -- rank group ----------------------------------------------------------
+    def group_init(self, rank, world, send_ptr, recv_ptr, cap_bytes, allgather):
+        """allgather(bytes_per_rank) -> None; gathers send[:bytes] of every rank into recv.
+        world == 1 (allgather None) returns the context to single-rank planning."""
+        if allgather is None:
+            self._cb = None
+            self._check(load().rp_group_init(self._h, 0, 1, None, None, 0, None, None), "rp_group_init")
+            return
+
+        def _cb(_user, nbytes):
+            try:
+                allgather(int(nbytes))
+                return 0
+            except Exception:  # never let a Python exception cross into C
+                import traceback
+                traceback.print_exc()
+                return 1
+        self._cb = ALLGATHER_FN(_cb)
+        self._check(load().rp_group_init(self._h, int(rank), int(world), C.c_void_p(send_ptr), C.c_void_p(recv_ptr),
+                                         int(cap_bytes), C.cast(self._cb, C.c_void_p), None), "rp_group_init")

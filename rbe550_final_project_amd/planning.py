@@ -1,0 +1,316 @@
+"""Drop-in replacement of the reference's code/planning.py (PlannerInterface).
+
+Same class, same constructor, same plan_path signature and return contract as
+code/planning.py:24-242, so code/motion_primitives.py:38/144 and the goal*.py
+scripts run unchanged. The OMPL RRTConnect + per-state Python/Genesis callback
+(planning.py:98-219) is replaced by one call into librbe_mi355x.so: batched
+RRT-Connect whose validity checks (FK + capsule collision), edge checks and
+nearest-neighbour searches run as HIP kernels on an MI355X.
+
+Reference behaviour kept (file:line of code/planning.py):
+  * planner name / batched-env / free-joint / shape checks raise    108-135
+  * bounds = robot.q_limit, as float64 of the stored values         139-150
+  * self.attached_object set; its box exempt for hand/fingers       153, 221-230
+  * start/goal bound + validity diagnostics only warn                164-183
+  * invalid start/goal or no solution -> [] + warning               190-202
+  * EXACT and APPROXIMATE solutions are "solved"                     192
+  * simplify when smooth_path, then interpolate(num_waypoints)       195-199
+  * robot qpos restored at the end                                   205
+  * returns a list of float32 tensors of shape (n_qs,)               232-242
+    (CPU tensors: motion_primitives.py:176 calls np.array on them)
+
+Not kept: the OMPL import, and planners other than RRTConnect (they are served by
+the MI355X RRT-Connect with a warning; every reference call site uses RRTConnect).
+
+Seeding (the reference is unseeded, scenes.py:9 / motion_primitives.py:153): the
+seed is RBE_PLANNER_SEED (default 0) plus a per-process query counter, or set with
+configure(seed=...). Batch size: RBE_PLANNER_BATCH / configure(batch=...).
+"""
+from __future__ import annotations
+
+import logging
+import os
+from typing import Any
+
+import numpy as np
+import torch
+
+try:  # the real simulator, when present (the goal*.py scripts)
+    import genesis as gs  # type: ignore
+except Exception:  # pragma: no cover - Genesis is absent in CI
+    gs = None
+
+from . import _abi, model, scenes
+from .native import Context
+
+_log = logging.getLogger("rbe550_final_project_amd.planning")
+
+SUPPORTED_PLANNERS = ["PRM", "RRT", "RRTConnect", "RRTstar", "EST", "FMT", "BITstar", "ABITstar"]
+
+
+class PlanningError(Exception):
+    """Raised where the reference calls gs.raise_exception."""
+
+
+def _raise(msg):
+    if gs is not None and hasattr(gs, "raise_exception"):
+        gs.raise_exception(msg)
+    raise PlanningError(msg)
+
+
+def _logger():
+    if gs is not None and getattr(gs, "logger", None) is not None:
+        return gs.logger
+    return _log
+
+
+_CONFIG = {"seed": None, "batch": None, "device": None, "tree_capacity": None}
+_QUERY_COUNTER = [0]
+
+
+def configure(seed=None, batch=None, device=None, tree_capacity=None):
+    """Set planner options without changing plan_path's signature."""
+    if seed is not None:
+        _CONFIG["seed"] = int(seed)
+        _QUERY_COUNTER[0] = 0
+    if batch is not None:
+        _CONFIG["batch"] = int(batch)
+    if device is not None:
+        _CONFIG["device"] = int(device)
+    if tree_capacity is not None:
+        _CONFIG["tree_capacity"] = int(tree_capacity)
+
+
+def _next_seed():
+    base = _CONFIG["seed"]
+    if base is None:
+        base = int(os.environ.get("RBE_PLANNER_SEED", "0"))
+    s = base + _QUERY_COUNTER[0]
+    _QUERY_COUNTER[0] += 1
+    return s
+
+
+def _batch():
+    if _CONFIG["batch"] is not None:
+        return _CONFIG["batch"]
+    return int(os.environ.get("RBE_PLANNER_BATCH", "4096"))
+
+
+def _device():
+    if _CONFIG["device"] is not None:
+        return _CONFIG["device"]
+    if "LOCAL_RANK" in os.environ:
+        return int(os.environ["LOCAL_RANK"])
+    return 0
+
+
+def tensor_to_array(x):
+    """genesis.utils.misc.tensor_to_array equivalent (planning.py:10, 131-132)."""
+    if isinstance(x, torch.Tensor):
+        return x.detach().cpu().numpy()
+    return np.asarray(x)
+
+
+def _ensure_adapter(robot: Any, scene: Any):
+    """planning.py:14-22: wrap the raw entity in RobotAdapter if needed."""
+    try:
+        from robot_adapter import RobotAdapter  # the reference's own module (code/)
+    except Exception:
+        RobotAdapter = _Adapter
+    if isinstance(robot, (RobotAdapter, _Adapter)):
+        return robot
+    return RobotAdapter(robot, scene)
+
+
+class _Adapter:
+    """Attribute-forwarding wrapper used when the reference's robot_adapter module
+    is not on the path."""
+
+    def __init__(self, robot, scene=None):
+        self.robot = robot
+        self.scene = scene
+
+    def __getattr__(self, name):
+        return getattr(self.robot, name)
+
+    def get_qpos(self):
+        return self.robot.get_qpos()
+
+    def set_qpos(self, qpos):
+        return self.robot.set_qpos(qpos)
+
+    def detect_collision(self, *a, **k):
+        return self.robot.detect_collision(*a, **k)
+
+
+class _Bounds:
+    def __init__(self, lo, hi):
+        self.low = list(lo)
+        self.high = list(hi)
+
+
+class _SpaceInfo:
+    """Minimal stand-in for OMPL's SpaceInformation used by the diagnostics."""
+
+    def __init__(self, lo, hi):
+        self._b = _Bounds(lo, hi)
+
+    def getStateSpace(self):
+        return self
+
+    def getBounds(self):
+        return self._b
+
+
+class PlannerInterface:
+    def __init__(self, robot: Any, scene: Any):
+        self.robot = _ensure_adapter(robot, scene)
+        self.scene = scene
+        self.attached_object = None
+        self._ctx = None
+        self.last_status = None
+        self.last_stats = None
+
+    # -- GPU context -----------------------------------------------------------
+    def _context(self):
+        if self._ctx is None:
+            self._ctx = Context(device=_device(), robot=model.robot_desc())
+        return self._ctx
+
+    def _sync_scene(self):
+        """Push the current obstacle geometry (boxes at their simulated poses) and
+        the attached box to the GPU context."""
+        sc = scenes.from_genesis(self.scene, self.robot)
+        ctx = self._context()
+        ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+        idx = -1
+        att = self.attached_object
+        if att:
+            ent_idx = getattr(att, "idx", None)
+            for k, e in enumerate(sc.entity_idx):
+                if e is not None and e == ent_idx:
+                    idx = k
+                    break
+        ctx.set_attached(idx)
+        self._scene_names = sc.names
+        return sc
+
+    # -- diagnostics (planning.py:32-57) ----------------------------------------
+    def diagnose_bounds_violation(self, si, state):
+        violated = []
+        b = si.getStateSpace().getBounds()
+        for i_q in range(self.robot.n_qs):
+            val = state[i_q]
+            low, high = b.low[i_q], b.high[i_q]
+            if val < low or val > high:
+                violated.append((i_q, val, low, high))
+        _logger().warning(f"State violates bounds on joints: {violated}")
+
+    def diagnose_valid_violation(self, state):
+        pairs = self._context().contacts(np.asarray([float(state[i]) for i in range(self.robot.n_qs)]))
+        bad = set()
+        for link, obst in pairs:
+            bad.add(_abi.LINK_NAMES[link])
+            if obst == -1:
+                bad.add("plane")
+            elif obst >= 0:
+                bad.add(f"box{obst}")
+            else:
+                bad.add(_abi.LINK_NAMES[-2 - obst])
+        _logger().warning(f"State causes collisions between links: {sorted(bad)}")
+
+    # -- the query (planning.py:59-207) -----------------------------------------
+    def plan_path(self, qpos_goal, qpos_start=None, timeout=5.0, smooth_path=True, num_waypoints=100,
+                  attached_object=None, planner="RRTConnect"):
+        if planner not in SUPPORTED_PLANNERS:
+            _raise(f"Planner {planner} is not supported. Supported planners: {SUPPORTED_PLANNERS}.")
+        if planner != "RRTConnect":
+            _logger().warning(f"Planner {planner} is served by the MI355X batched RRT-Connect.")
+        solver = getattr(self.robot, "_solver", None)
+        if solver is not None and getattr(solver, "n_envs", 0) > 0:
+            _raise("Motion planning is not supported for batched envs (yet).")
+        if self.robot.n_qs != self.robot.n_dofs:
+            _raise("Motion planning is not yet supported for rigid entities with free joints.")
+
+        qpos_cur = self.robot.get_qpos()
+        if qpos_start is None:
+            qpos_start = self.robot.get_qpos()
+        qpos_start = np.asarray(tensor_to_array(qpos_start), dtype=np.float64)
+        qpos_goal = np.asarray(tensor_to_array(qpos_goal), dtype=np.float64)
+        n_qs = self.robot.n_qs
+        if qpos_start.shape != (n_qs,) or qpos_goal.shape != (n_qs,):
+            _raise("Invalid shape for `qpos_start` or `qpos_goal`.")
+        if n_qs != _abi.NQ:
+            _raise(f"The MI355X planner is built for the 9-D Franka Panda (got n_qs={n_qs}).")
+
+        lo = np.asarray(tensor_to_array(self.robot.q_limit[0]), dtype=float)
+        hi = np.asarray(tensor_to_array(self.robot.q_limit[1]), dtype=float)
+
+        self.attached_object = attached_object
+        ctx = self._context()
+        self._sync_scene()
+
+        si = _SpaceInfo(lo, hi)
+        eps = np.finfo(np.float64).eps
+        start_in = bool(np.all(qpos_start - eps <= hi) and np.all(qpos_start + eps >= lo))
+        if not start_in:
+            _logger().warning("OMPL start state out of bounds")
+            self.diagnose_bounds_violation(si, qpos_start)
+        goal_in = bool(np.all(qpos_goal - eps <= hi) and np.all(qpos_goal + eps >= lo))
+        if not goal_in:
+            _logger().warning("OMPL goal state out of bounds")
+            self.diagnose_bounds_violation(si, qpos_goal)
+        flags = ctx.check_states(np.stack([qpos_start, qpos_goal]).astype(np.float32))
+        if not flags[0]:
+            _logger().warning("OMPL start state invalid")
+            self.diagnose_valid_violation(qpos_start)
+        if not flags[1]:
+            _logger().warning("OMPL goal state invalid")
+            self.diagnose_valid_violation(qpos_goal)
+
+        params = _abi.make_params(seed=_next_seed(), batch=_batch(), timeout_s=float(timeout),
+                                  n_waypoints=int(num_waypoints) if num_waypoints else 0,
+                                  simplify=bool(smooth_path), tree_capacity=_CONFIG["tree_capacity"] or 0)
+        cap = max(4096, int(num_waypoints or 0) + 16)
+        path, status = ctx.plan(qpos_start, qpos_goal, lo, hi, params, path_cap=cap)
+        self.last_status = status
+        self.last_stats = ctx.stats()
+
+        waypoints = []
+        if status in (_abi.STATUS_EXACT, _abi.STATUS_APPROXIMATE):
+            _logger().info("Path solution found successfully.")
+            print("Number of waypoints in path:", len(path))
+            waypoints = self._states_to_tensor_list(path)
+        else:
+            _logger().warning("Path planning failed. Returning empty path.")
+
+        self.robot.set_qpos(qpos_cur)
+        return waypoints
+
+    # -- single-state validity (planning.py:209-219) ------------------------------
+    def _is_ompl_state_valid(self, state):
+        q = np.asarray([float(state[i]) for i in range(_abi.NQ)], dtype=np.float32)
+        if self._ctx is None:
+            self._sync_scene()
+        return bool(self._context().check_states(q)[0])
+
+    def collision_with_attached_object(self, collision_pairs):
+        """planning.py:221-230 on a Genesis contact-pair list (kept for callers that
+        use it directly; the GPU path applies the same rule per capsule)."""
+        finger_names = {"left_finger", "right_finger", "hand"}
+        geoms = self.scene.rigid_solver.geoms
+        for a, b in collision_pairs:
+            name_a = geoms[a].link.name
+            name_b = geoms[b].link.name
+            if (name_a in finger_names and b == self.attached_object.idx) or \
+                    (name_b in finger_names and a == self.attached_object.idx):
+                continue
+            return False
+        return True
+
+    @staticmethod
+    def _states_to_tensor_list(path):
+        return [torch.tensor(row, dtype=torch.float32) for row in np.asarray(path)]
+
+    def _ompl_state_to_tensor(self, state):
+        return torch.tensor([float(state[i]) for i in range(self.robot.n_qs)], dtype=torch.float32)

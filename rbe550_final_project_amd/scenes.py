@@ -1,0 +1,215 @@
+"""Obstacle scenes of the planning path: boxes + ground plane + robot base.
+
+Scene factories transcribe the obstacle constants of code/scenes.py (the reference
+builds Genesis scenes; here only the geometry the collider sees is kept):
+
+  goal1_scattered   create_scene_6blocks      scenes.py:41-99  (6 boxes, +-5 cm xy jitter)
+  goal3_tallest     create_scene_10blocks2ln  scenes.py:150-223 (10 boxes, no jitter)
+  goal4_pentagon    create_scene_10blocks     scenes.py:226-299 (10 boxes, no jitter)
+  clutter64         SURVEY.md §8(d) C5 synthetic clutter (64 floating boxes)
+
+Every scene adds the plane first, then the boxes, then the robot, so box k of a
+scene is Genesis entity k+1 (planning.py:226 compares attached_object.idx with geom
+indices). The robot base is raised by 1 cm (scenes.py:29-34).
+
+`from_genesis()` ingests a live Genesis scene (box entities and their current
+poses) so the drop-in planning.py sees the blocks where the simulation has them.
+"""
+from dataclasses import dataclass, field
+import json
+import math
+
+import numpy as np
+
+BLOCK = 0.04                 # gs.morphs.Box(size=(0.04, 0.04, 0.04)) (scenes.py:60)
+HALF = (BLOCK / 2, BLOCK / 2, BLOCK / 2)
+BASE = (0.0, 0.0, 0.01)
+
+
+@dataclass
+class Scene:
+    boxes: list = field(default_factory=list)     # [(center(3), half(3), yaw)]
+    names: list = field(default_factory=list)
+    plane_z: float = 0.0
+    base: tuple = BASE
+    entity_idx: list = field(default_factory=list)  # Genesis entity index per box (or None)
+
+    def copy(self):
+        return Scene([(tuple(c), tuple(h), float(y)) for c, h, y in self.boxes], list(self.names), self.plane_z,
+                     tuple(self.base), list(self.entity_idx))
+
+    def index(self, name):
+        return self.names.index(name)
+
+    def move(self, name, center, yaw=None):
+        i = self.index(name)
+        c, h, y = self.boxes[i]
+        self.boxes[i] = (tuple(float(v) for v in center), h, float(y if yaw is None else yaw))
+
+    def remove(self, name):
+        i = self.index(name)
+        del self.boxes[i]
+        del self.names[i]
+        if self.entity_idx:
+            del self.entity_idx[i]
+
+    def to_json(self):
+        return {"boxes": [{"name": n, "center": list(c), "half": list(h), "yaw": y}
+                          for n, (c, h, y) in zip(self.names, self.boxes)],
+                "plane_z": self.plane_z, "base": list(self.base)}
+
+    @staticmethod
+    def from_json(d):
+        s = Scene(plane_z=float(d.get("plane_z", 0.0)), base=tuple(d.get("base", BASE)))
+        for b in d["boxes"]:
+            s.boxes.append((tuple(b["center"]), tuple(b["half"]), float(b.get("yaw", 0.0))))
+            s.names.append(b.get("name", f"box{len(s.names)}"))
+        s.entity_idx = [i + 1 for i in range(len(s.boxes))]
+        return s
+
+
+def _mk(named_centers):
+    s = Scene()
+    for i, (n, c) in enumerate(named_centers):
+        s.boxes.append((tuple(float(v) for v in c), HALF, 0.0))
+        s.names.append(n)
+        s.entity_idx.append(i + 1)
+    return s
+
+
+def goal1_scattered(seed=0, noise=0.05):
+    """create_scene_6blocks (scenes.py:41-99) with the jitter seeded instead of
+    random.seed(time.time()) (scenes.py:9)."""
+    rng = np.random.default_rng(seed)
+    nominal = [("r", (0.65, 0.0)), ("g", (0.65, 0.2)), ("b", (0.65, 0.4)),
+               ("y", (0.45, 0.0)), ("m", (0.45, 0.2)), ("c", (0.45, 0.4))]
+    out = []
+    for n, (x, y) in nominal:
+        dx, dy = rng.uniform(-noise, noise, 2)
+        out.append((n, (x + dx, y + dy, 0.02)))
+    return _mk(out)
+
+
+def goal3_tallest():
+    """create_scene_10blocks2ln (scenes.py:150-223)."""
+    pos = [("r", (0.45, -0.40)), ("g", (0.45, -0.20)), ("b", (0.45, 0.00)), ("y", (0.45, 0.20)),
+           ("o", (0.45, 0.40)), ("r2", (0.65, -0.40)), ("g2", (0.65, -0.20)), ("b2", (0.65, 0.00)),
+           ("y2", (0.65, 0.20)), ("o2", (0.65, 0.40))]
+    return _mk([(n, (x, y, 0.02)) for n, (x, y) in pos])
+
+
+def goal4_pentagon():
+    """create_scene_10blocks (scenes.py:226-299)."""
+    pos = [(0.35, -0.40), (0.35, -0.25), (0.45, -0.30), (0.6, -0.40), (0.6, -0.25),
+           (0.35, 0.40), (0.35, 0.25), (0.45, 0.30), (0.6, 0.40), (0.6, 0.25)]
+    return _mk([(f"b{i + 1}", (x, y, 0.02)) for i, (x, y) in enumerate(pos)])
+
+
+def pentagon_slots(center=(0.50, 0.10), radius=0.06):
+    """Base and top slot poses of goal4_task1.py:66-126: (x, y, yaw_deg)."""
+    base, top = [], []
+    for i in range(5):
+        a = 0.0 + i * 72.0
+        x = center[0] + radius * math.cos(math.radians(a)) + 0.0045
+        y = center[1] + radius * math.sin(math.radians(a))
+        base.append((x, y, _wrap180(a)))
+        a = i * 72.0 + 36.0
+        x = center[0] + radius * math.cos(math.radians(a)) + 0.0053
+        y = center[1] + radius * math.sin(math.radians(a)) - 0.0005
+        top.append((x, y, _wrap180(a)))
+    return base, top
+
+
+def _wrap180(a):
+    while a < -180:
+        a += 360
+    while a > 180:
+        a -= 360
+    return a
+
+
+def clutter64(seed=0x64B0, n=64, keep_clear=None):
+    """n boxes, centres x~U[0.25,0.85], y~U[-0.6,0.6],
+    z~U[0.02,0.6], half extents U[0.01,0.05], yaw 0. `keep_clear(scene_with_one_box)`
+    returns False to reject a box (e.g. one that collides with start/goal)."""
+    rng = np.random.default_rng(seed)
+    s = Scene()
+    tries = 0
+    while len(s.boxes) < n and tries < 100 * n:
+        tries += 1
+        c = (rng.uniform(0.25, 0.85), rng.uniform(-0.6, 0.6), rng.uniform(0.02, 0.6))
+        h = tuple(rng.uniform(0.01, 0.05, 3))
+        cand = ((float(c[0]), float(c[1]), float(c[2])), tuple(float(v) for v in h), 0.0)
+        if keep_clear is not None and not keep_clear(cand):
+            continue
+        s.boxes.append(cand)
+        s.names.append(f"k{len(s.names)}")
+        s.entity_idx.append(len(s.names))
+    return s
+
+
+# ---------------------------------------------------------------------------
+# Genesis ingestion (drop-in path)
+# ---------------------------------------------------------------------------
+
+def _to_np(x):
+    if hasattr(x, "detach"):
+        x = x.detach()
+    if hasattr(x, "cpu"):
+        x = x.cpu()
+    if hasattr(x, "numpy"):
+        x = x.numpy()
+    return np.asarray(x, dtype=float).reshape(-1)
+
+
+def yaw_of_quat(q):
+    """Rotation about world z of a (w, x, y, z) quaternion (tilt is ignored)."""
+    w, x, y, z = (float(v) for v in q)
+    return math.atan2(2.0 * (w * z + x * y), 1.0 - 2.0 * (y * y + z * z))
+
+
+def from_genesis(scene, robot=None):
+    """Boxes of a Genesis scene: every entity whose morph is a Box, at its current
+    pose (entity.get_pos / get_quat). Planes are taken as the ground at z = 0."""
+    s = Scene()
+    entities = getattr(scene, "entities", None)
+    if entities is None and hasattr(scene, "sim"):
+        entities = scene.sim.entities
+    base = BASE
+    plane_z = 0.0
+    raw_robot = getattr(robot, "robot", robot)
+    for ent in entities or []:
+        morph = getattr(ent, "morph", None)
+        kind = type(morph).__name__ if morph is not None else ""
+        if ent is raw_robot or ent is robot:
+            if hasattr(ent, "get_pos"):
+                base = tuple(_to_np(ent.get_pos())[:3])
+            continue
+        if kind == "Plane":
+            plane_z = float(_to_np(getattr(morph, "pos", (0.0, 0.0, 0.0)))[2])
+            continue
+        if kind != "Box":
+            continue
+        size = getattr(morph, "size", None)
+        if size is None:
+            lo, hi = np.asarray(morph.lower, float), np.asarray(morph.upper, float)
+            size = hi - lo
+        half = tuple(float(v) / 2.0 for v in _to_np(size)[:3])
+        pos = _to_np(ent.get_pos())[:3]
+        quat = _to_np(ent.get_quat())[:4] if hasattr(ent, "get_quat") else (1.0, 0.0, 0.0, 0.0)
+        s.boxes.append((tuple(float(v) for v in pos), half, yaw_of_quat(quat)))
+        s.names.append(str(getattr(ent, "idx", len(s.names))))
+        s.entity_idx.append(getattr(ent, "idx", None))
+    if robot is not None and hasattr(robot, "get_pos"):
+        try:
+            base = tuple(_to_np(robot.get_pos())[:3])
+        except Exception:
+            pass
+    s.base = base
+    s.plane_z = plane_z
+    return s
+
+
+def load_json(path):
+    with open(path) as f:
+        return Scene.from_json(json.load(f))

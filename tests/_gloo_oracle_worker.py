@@ -1,0 +1,47 @@
+"""One rank of the 2-rank gloo test: the oracle's sharded RRT-Connect with a
+torch.distributed all-gather over CPU tensors (test helper, launched by
+tests/test_oracle_planner.py)."""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from oracle.oracle import OracleScene  # noqa: E402
+from rbe550_final_project_amd import _abi, model, scenes  # noqa: E402
+
+
+def main():
+    batch, seed, qi, out = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4]
+    dist.init_process_group("gloo", init_method="env://")
+    rank, world = dist.get_rank(), dist.get_world_size()
+    wl = json.load(open(os.path.join(ROOT, "tests", "golden", "workloads", "goal4_pentagon_10box.json")))
+    q = wl["queries"][qi]
+    o = OracleScene()
+    sc = scenes.Scene.from_json(q["scene"])
+    o.set_scene(sc.boxes, sc.plane_z, sc.base)
+    o.set_attached(q["attached"])
+
+    def allgather(_user, send, recv, nbytes):
+        src = torch.frombuffer((C.c_uint8 * nbytes).from_address(send), dtype=torch.uint8).clone()
+        parts = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(world)]
+        dist.all_gather(parts, src)
+        gathered = torch.cat(parts).numpy()      # keep alive across the memmove
+        C.memmove(recv, gathered.ctypes.data, nbytes * world)
+        return 0
+
+    p = _abi.make_params(seed=seed, batch=batch, n_waypoints=150, timeout_s=60)
+    path, st, _ = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p, rank=rank, world=world,
+                         allgather=allgather)
+    np.save(out, path)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

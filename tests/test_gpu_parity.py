@@ -1,0 +1,186 @@
+"""GPU parity: librbe_mi355x.so (HIP, gfx950) vs the CPU oracle on the same inputs.
+
+Bar (BASELINE.json north_star): integer collision flags bit-exact; waypoints within
+1e-5 rad (the implementation is bit-exact by the numerics contract, DESIGN.md §3,
+so paths are compared for exact equality and the 1e-5 tolerance is the contract).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from rbe550_final_project_amd import _abi, model, scenes
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+WAYPOINT_TOL = 1e-5
+
+
+def _wl(name):
+    return json.load(open(os.path.join(GOLD, "workloads", name + ".json")))
+
+
+def _uniform(n, seed):
+    rng = np.random.default_rng(seed)
+    return (model.Q_LO + (model.Q_HI - model.Q_LO) * rng.random((n, 9))).astype(np.float32)
+
+
+def _near(q0, n, seed, sigma=0.3):
+    rng = np.random.default_rng(seed)
+    q = np.asarray(q0)[None, :] + rng.normal(0, sigma, (n, 9))
+    return np.clip(q, model.Q_LO, model.Q_HI).astype(np.float32)
+
+
+SCENES = {
+    "empty": scenes.Scene(),
+    "goal1": scenes.goal1_scattered(0),
+    "goal3": scenes.goal3_tallest(),
+    "goal4_yawed": scenes.Scene.from_json(_wl("goal4_pentagon_10box")["queries"][14]["scene"]),
+    "clutter64": scenes.Scene.from_json(_wl("clutter64")["queries"][0]["scene"]),
+}
+
+
+def _both(gpu_ctx, oracle_lib, sc, attached=-1):
+    o = oracle_lib.OracleScene()
+    o.set_scene(sc.boxes, sc.plane_z, sc.base)
+    o.set_attached(attached)
+    gpu_ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+    gpu_ctx.set_attached(attached)
+    return o
+
+
+@pytest.mark.parametrize("name", list(SCENES))
+def test_validity_flags_bit_exact(gpu_ctx, oracle_lib, name):
+    sc = SCENES[name]
+    o = _both(gpu_ctx, oracle_lib, sc)
+    q = np.concatenate([_uniform(65536, 1), _near(model.SAFE_HOME, 65536, 2)])
+    g = gpu_ctx.check_states(q)
+    c = o.check_states(q)
+    assert g.dtype == np.uint8 and set(np.unique(g)) <= {0, 1}
+    mism = np.nonzero(g != c)[0]
+    assert mism.size == 0, f"{mism.size} mismatches, first {q[mism[:3]]}"
+    assert 0.02 < g.mean() < 0.98
+
+
+def test_validity_with_attached_box(gpu_ctx, oracle_lib):
+    wl = _wl("goal3_tallest_10box")
+    for qd in [x for x in wl["queries"] if x["attached"] >= 0][:3]:
+        sc = scenes.Scene.from_json(qd["scene"])
+        o = _both(gpu_ctx, oracle_lib, sc, qd["attached"])
+        q = _near(qd["start"], 32768, 3, 0.2)
+        assert np.array_equal(gpu_ctx.check_states(q), o.check_states(q))
+
+
+def test_golden_flag_fixtures(gpu_ctx, oracle_lib):
+    """Committed flag vectors (tests/golden/flags_*.npz, seed 0x5EED) — the GPU must
+    reproduce them exactly."""
+    files = sorted(f for f in os.listdir(GOLD) if f.startswith("flags_") and f.endswith(".npz"))
+    assert files, "no golden flag fixtures"
+    for f in files:
+        d = np.load(os.path.join(GOLD, f), allow_pickle=False)
+        sc = scenes.Scene.from_json(json.loads(str(d["scene"])))
+        gpu_ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+        gpu_ctx.set_attached(int(d["attached"]))
+        assert np.array_equal(gpu_ctx.check_states(d["q"]), d["flags"]), f
+
+
+def test_large_batch_full_size_properties(gpu_ctx, oracle_lib):
+    """4M-state batch (bench size): deterministic across launches, and a strided
+    subsample equals the oracle."""
+    sc = SCENES["goal3"]
+    o = _both(gpu_ctx, oracle_lib, sc)
+    q = _uniform(1 << 22, 7)
+    a = gpu_ctx.check_states(q)
+    b = gpu_ctx.check_states(q)
+    assert np.array_equal(a, b)
+    sub = slice(0, None, 97)
+    assert np.array_equal(a[sub], o.check_states(q[sub]))
+
+
+def test_edge_flags_bit_exact(gpu_ctx, oracle_lib):
+    sc = SCENES["goal1"]
+    o = _both(gpu_ctx, oracle_lib, sc)
+    rng = np.random.default_rng(4)
+    qa = _near(model.SAFE_HOME, 4096, 5, 0.4).astype(np.float64)
+    qb = qa + rng.normal(0, 0.6, qa.shape)
+    qb = np.clip(qb, model.Q_LO, model.Q_HI)
+    res = 0.01 * model.max_extent()
+    g = gpu_ctx.check_edges(qa, qb, res)
+    c = o.check_edges(qa, qb, res)
+    assert np.array_equal(g, c)
+    assert 0.05 < g.mean() < 0.95
+    # zero-length and very long edges
+    g2 = gpu_ctx.check_edges(qa[:8], qa[:8], res)
+    assert np.array_equal(g2, o.check_edges(qa[:8], qa[:8], res))
+
+
+def test_contacts_match_oracle(gpu_ctx, oracle_lib):
+    sc = SCENES["goal1"]
+    o = _both(gpu_ctx, oracle_lib, sc)
+    q = _near(model.SAFE_HOME, 200, 9, 0.5).astype(np.float64)
+    for x in q:
+        assert sorted(gpu_ctx.contacts(x)) == sorted(o.contacts(x))
+
+
+def test_f64_device_numerics(gpu_ctx):
+    """sqrt / div / ceil / f64->f32 on the device are IEEE correctly rounded (the
+    planner's steering and segment counts depend on it)."""
+    rng = np.random.default_rng(1)
+    x = np.concatenate([rng.random(100000) * 20.0, rng.random(1000) * 1e-6, [0.0, 1.0, 2.0, 0.13037 * 3]])
+    out = gpu_ctx.selftest_f64(x)
+    assert np.array_equal(out[:, 0], np.sqrt(np.abs(x)))
+    assert np.array_equal(out[:, 1], 0.13037 / np.where(x == 0, 1.0, x))
+    assert np.array_equal(out[:, 2], np.ceil(x * 7.0))
+    assert np.array_equal(out[:, 3], x.astype(np.float32).astype(np.float64))
+
+
+PLAN_CASES = [("single_pick_place_5box", 0), ("single_pick_place_5box", 1), ("goal3_tallest_10box", 2),
+              ("goal3_tallest_10box", 5), ("goal4_pentagon_10box", 2), ("goal4_pentagon_10box", 14),
+              ("clutter64", 0)]
+
+
+@pytest.mark.parametrize("wl,qi", PLAN_CASES)
+@pytest.mark.parametrize("batch,seed", [(1, 3), (64, 11), (4096, 5)])
+def test_plan_parity(gpu_ctx, oracle_lib, wl, qi, batch, seed):
+    q = _wl(wl)["queries"][qi]
+    sc = scenes.Scene.from_json(q["scene"])
+    o = _both(gpu_ctx, oracle_lib, sc, q["attached"])
+    p = _abi.make_params(seed=seed, batch=batch, n_waypoints=150, timeout_s=60)
+    ref, st_ref, stats_ref = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+    path, st = gpu_ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+    gst = gpu_ctx.stats()
+    assert st == st_ref == _abi.STATUS_EXACT
+    assert path.shape == ref.shape == (150, 9)
+    assert np.max(np.abs(path - ref)) <= WAYPOINT_TOL
+    assert np.array_equal(path, ref)
+    assert (gst["start_tree_size"], gst["goal_tree_size"], gst["iterations"]) == \
+        (stats_ref["start_tree_size"], stats_ref["goal_tree_size"], stats_ref["iterations"])
+
+
+def test_plan_parity_hard_iterations(gpu_ctx, oracle_lib):
+    """Many iterations, no simplification/interpolation: raw tree path equality on a
+    tight pentagon query with a small range (more nodes, more NN work)."""
+    q = _wl("goal4_pentagon_10box")["queries"][8]
+    sc = scenes.Scene.from_json(q["scene"])
+    o = _both(gpu_ctx, oracle_lib, sc, q["attached"])
+    p = _abi.make_params(seed=21, batch=256, range_=0.3, n_waypoints=0, simplify=False, timeout_s=120)
+    ref, st_ref, s_ref = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+    path, st = gpu_ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+    assert st == st_ref
+    assert np.array_equal(path, ref)
+    assert gpu_ctx.stats()["start_tree_size"] == s_ref["start_tree_size"]
+
+
+def test_plan_invalid_start_goal(gpu_ctx, oracle_lib):
+    gpu_ctx.set_scene([])
+    gpu_ctx.set_attached(-1)
+    p = _abi.make_params(seed=0, batch=64, max_iters=3)
+    bad = model.SAFE_HOME.copy()
+    bad[7:] = 0.04
+    _, st = gpu_ctx.plan(bad, model.SAFE_HOME, model.Q_LO, model.Q_HI, p)
+    assert st == _abi.STATUS_INVALID_START
+    ok = model.SAFE_HOME.copy()
+    ok[7:] = np.float32(0.04)
+    _, st = gpu_ctx.plan(ok, bad, model.Q_LO, model.Q_HI, p)
+    assert st == _abi.STATUS_INVALID_GOAL

@@ -1,0 +1,104 @@
+"""The drop-in planning.PlannerInterface (code/planning.py:24-242 contract) driven
+through a Genesis-free mock robot/scene."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from rbe550_final_project_amd import model, planning, scenes
+from rbe550_final_project_amd.native import NativeError
+import mock_genesis as M
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+REF = json.load(open(os.path.join(GOLD, "reference_fixtures.json")))
+
+
+def _mk(boxes=()):
+    sc = M.Scene(list(boxes))
+    return planning.PlannerInterface(sc.robot, sc), sc
+
+
+def test_bad_planner_raises_like_reference():
+    pi, _ = _mk()
+    with pytest.raises(planning.PlanningError) as e:
+        pi.plan_path(model.SAFE_HOME, planner="Foo")
+    assert str(e.value) == REF["errors"]["bad_planner"]
+
+
+def test_bad_shape_raises_like_reference():
+    pi, _ = _mk()
+    with pytest.raises(planning.PlanningError) as e:
+        pi.plan_path(model.SAFE_HOME[:7])
+    assert str(e.value) == REF["errors"]["bad_shape"]
+
+
+def test_batched_envs_and_free_joints_raise():
+    sc = M.Scene([], n_envs=2)
+    with pytest.raises(planning.PlanningError, match="batched envs"):
+        planning.PlannerInterface(sc.robot, sc).plan_path(model.SAFE_HOME)
+    sc = M.Scene([], n_dofs=7)
+    with pytest.raises(planning.PlanningError, match="free joints"):
+        planning.PlannerInterface(sc.robot, sc).plan_path(model.SAFE_HOME)
+
+
+def test_genesis_scene_ingestion():
+    boxes = [((0.65, 0.0, 0.02), (0.02, 0.02, 0.02), 0.0), ((0.5, 0.1, 0.02), (0.02, 0.02, 0.02), 0.7)]
+    sc = M.Scene(boxes)
+    s = scenes.from_genesis(sc, sc.robot)
+    assert len(s.boxes) == 2 and s.entity_idx == [1, 2]
+    assert np.allclose(s.boxes[1][0], (0.5, 0.1, 0.02)) and abs(s.boxes[1][2] - 0.7) < 1e-6
+    assert np.allclose(s.boxes[0][1], (0.02, 0.02, 0.02))
+    assert np.allclose(s.base, model.BASE_POS)
+
+
+def test_no_silent_cpu_fallback():
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    pi, _ = _mk()
+    with pytest.raises(NativeError):
+        pi.plan_path(model.SAFE_HOME)
+
+
+@pytest.mark.gpu
+def test_plan_path_contract_on_gpu():
+    wl = json.load(open(os.path.join(GOLD, "workloads", "goal3_tallest_10box.json")))
+    q = wl["queries"][0]
+    s = scenes.Scene.from_json(q["scene"])
+    sc = M.Scene(s.boxes)
+    sc.robot.q = torch.tensor(q["start"], dtype=torch.float32)
+    pi = planning.PlannerInterface(sc.robot, sc)
+    planning.configure(seed=0)
+    wps = pi.plan_path(qpos_goal=np.array(q["goal"]), num_waypoints=150, timeout=10.0)
+    c = REF["return_contract"]
+    assert len(wps) == c["n"] == 150
+    assert all(isinstance(w, torch.Tensor) and w.dtype == torch.float32 and list(w.shape) == c["shape"]
+               and w.device.type == "cpu" for w in wps)
+    assert np.allclose(wps[0].numpy(), np.float32(q["start"]), atol=1e-6)
+    assert np.allclose(wps[-1].numpy(), np.float32(q["goal"]), atol=1e-6)
+    # consumer contract (motion_primitives.py:163-178)
+    arr = np.array(wps[-1], dtype=float, copy=True)
+    assert arr.shape == (9,)
+    # the robot's qpos is restored at the end (planning.py:205)
+    assert torch.equal(sc.robot.set_calls[-1], torch.tensor(q["start"], dtype=torch.float32))
+
+
+@pytest.mark.gpu
+def test_plan_path_attached_object_and_failure():
+    wl = json.load(open(os.path.join(GOLD, "workloads", "goal3_tallest_10box.json")))
+    q = [x for x in wl["queries"] if x["attached"] >= 0][0]
+    s = scenes.Scene.from_json(q["scene"])
+    sc = M.Scene(s.boxes)
+    sc.robot.q = torch.tensor(q["start"], dtype=torch.float32)
+    pi = planning.PlannerInterface(sc.robot, sc)
+    held = sc.entities[1 + q["attached"]]
+    wps = pi.plan_path(qpos_goal=np.array(q["goal"]), num_waypoints=150, attached_object=held, timeout=10.0)
+    assert len(wps) == 150 and pi.attached_object is held
+    # the held box must not be exempt for the arm links: without exemption the
+    # start (fingers around the block) is invalid when the fingers are closed on it
+    assert pi._is_ompl_state_valid(q["start"]) is True
+    # float64 0.04 fingers are out of float32 bounds -> [] (README.md:101-111)
+    bad = np.array(q["start"])
+    bad[7:] = 0.04
+    assert pi.plan_path(qpos_goal=np.array(q["goal"]), qpos_start=bad, num_waypoints=150) == []

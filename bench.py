@@ -148,7 +148,11 @@ def main():
     q = lo + (hi - lo) * torch.rand((n, 9), generator=g, device=dev, dtype=torch.float32)
     q = q.contiguous()
     flags = torch.empty(n, dtype=torch.uint8, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated stream: the kernel is launched on it and the HIP events are
+    # recorded on it (the legacy default stream has handle 0, which the C-ABI
+    # reads as "the context's own stream")
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.synchronize(dev)
 
     def step():
         ctx.check_states_device(q.data_ptr(), n, flags.data_ptr(), stream.cuda_stream)

@@ -160,8 +160,10 @@ int rp_set_attached(rp_ctx* ctx, int32_t box_index, uint32_t exempt_link_mask);
  * valid (collision free), 0 otherwise. */
 int rp_check_states(rp_ctx* ctx, const float* q, int64_t n, uint8_t* flags_out);
 
-/* Same on device-resident buffers (e.g. torch tensors' data_ptr) on the context's
- * stream; if `stream` is non-NULL it is a hipStream_t the caller orders against. */
+/* Same on device-resident buffers (e.g. torch tensors' data_ptr), asynchronous: the
+ * kernel is launched on `stream` (a hipStream_t) or, when `stream` is NULL, on the
+ * context's own non-blocking stream. NULL therefore does NOT mean the legacy
+ * default stream; pass an explicit stream to order against other work. */
 int rp_check_states_device(rp_ctx* ctx, const float* q_dev, int64_t n, uint8_t* flags_dev,
                            void* stream);
 

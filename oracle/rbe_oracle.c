@@ -115,27 +115,18 @@ int ro_scene_set_attached(ro_scene* s, int32_t box, uint32_t link_mask) {
 static float mn(float a, float b) { return a < b ? a : b; }
 static float mx(float a, float b) { return a > b ? a : b; }
 static float c01(float x) { return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x); }
-static float dot(v3 u, v3 v) { return (u.x * v.x + u.y * v.y) + u.z * v.z; }
+static float dot(v3 u, v3 v) { return fmaf(u.z, v.z, fmaf(u.y, v.y, u.x * v.x)); }
 
 void ro_sincos(float x, float* sn, float* cs) {
-    float t = x * 0.636619772f;
-    float k = floorf(t + 0.5f);
-    float r = x - k * 1.5703125f;
-    r = r - k * 4.837512969970703125e-4f;
-    r = r - k * 7.54978995489188216e-8f;
+    float k = floorf(x * 0.636619772f + 0.5f);
+    float r = fmaf(-k, 1.5703125f, x);
+    r = fmaf(-k, 4.837512969970703125e-4f, r);
+    r = fmaf(-k, 7.54978995489188216e-8f, r);
     float z = r * r;
-    float ps = -1.9515295891e-4f;
-    ps = ps * z;
-    ps = ps + 8.3321608736e-3f;
-    ps = ps * z;
-    ps = ps + -1.6666654611e-1f;
-    float sr = r + (r * z) * ps;
-    float pc = 2.443315711809948e-5f;
-    pc = pc * z;
-    pc = pc + -1.388731625493765e-3f;
-    pc = pc * z;
-    pc = pc + 4.166664568298827e-2f;
-    float cr = (1.0f - 0.5f * z) + (z * z) * pc;
+    float ps = fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f);
+    float sr = fmaf(r * z, ps, r);
+    float pc = fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f);
+    float cr = fmaf(z * z, pc, fmaf(-0.5f, z, 1.0f));
     switch (((int)k) & 3) {
         case 0: *sn = sr; *cs = cr; break;
         case 1: *sn = cr; *cs = -sr; break;
@@ -147,14 +138,19 @@ void ro_sincos(float x, float* sn, float* cs) {
 /* rotation columns R[0..2] (each a 3-vector) and origin P */
 typedef struct { float R[3][3]; float P[3]; } frame;
 
-static void f_rz(frame* f, float q) {
-    float s, c, n0[3], n1[3];
-    ro_sincos(q, &s, &c);
+/* R <- R * Rz: n0 = c*c0 + s*c1, n1 = c*c1 - s*c0 (fused as in rp_math.h) */
+static void f_rot(frame* f, float s, float c) {
+    float n0[3], n1[3];
     for (int k = 0; k < 3; ++k) {
-        n0[k] = c * f->R[0][k] + s * f->R[1][k];
-        n1[k] = c * f->R[1][k] - s * f->R[0][k];
+        n0[k] = fmaf(c, f->R[0][k], s * f->R[1][k]);
+        n1[k] = fmaf(c, f->R[1][k], -(s * f->R[0][k]));
     }
     for (int k = 0; k < 3; ++k) { f->R[0][k] = n0[k]; f->R[1][k] = n1[k]; }
+}
+static void f_rz(frame* f, float q) {
+    float s, c;
+    ro_sincos(q, &s, &c);
+    f_rot(f, s, c);
 }
 /* R * Rx(+90) = [c0, c2, -c1]; R * Rx(-90) = [c0, -c2, c1] */
 static void f_rx(frame* f, int plus) {
@@ -166,7 +162,7 @@ static void f_rx(frame* f, int plus) {
     }
 }
 static void f_shift(float P[3], float k, const float col[3]) {
-    for (int i = 0; i < 3; ++i) P[i] = P[i] + k * col[i];
+    for (int i = 0; i < 3; ++i) P[i] = fmaf(k, col[i], P[i]);
 }
 
 /* world frames of the 11 links (panda.xml, scenes.py:85) */
@@ -185,15 +181,7 @@ static void link_frames(const ro_scene* s, const float q[NQ], frame F[RP_NUM_LIN
     f_shift(f.P, 0.088f, f.R[0]); f_rx(&f, 1); f_rz(&f, q[6]); F[7] = f;
     /* hand: flange +0.107 z, Rz(-45deg) with the rounded constants */
     f_shift(f.P, 0.107f, f.R[2]);
-    {
-        const float c = 0.70710677f, sn = -0.70710677f;
-        float n0[3], n1[3];
-        for (int k = 0; k < 3; ++k) {
-            n0[k] = c * f.R[0][k] + sn * f.R[1][k];
-            n1[k] = c * f.R[1][k] - sn * f.R[0][k];
-        }
-        for (int k = 0; k < 3; ++k) { f.R[0][k] = n0[k]; f.R[1][k] = n1[k]; }
-    }
+    f_rot(&f, -0.70710677f, 0.70710677f);
     F[8] = f;
     f_shift(f.P, 0.0584f, f.R[2]);
     frame l = f;
@@ -207,9 +195,9 @@ static void link_frames(const ro_scene* s, const float q[NQ], frame F[RP_NUM_LIN
 
 static v3 to_world(const frame* f, const float a[3]) {
     v3 w;
-    w.x = ((f->P[0] + a[0] * f->R[0][0]) + a[1] * f->R[1][0]) + a[2] * f->R[2][0];
-    w.y = ((f->P[1] + a[0] * f->R[0][1]) + a[1] * f->R[1][1]) + a[2] * f->R[2][1];
-    w.z = ((f->P[2] + a[0] * f->R[0][2]) + a[1] * f->R[1][2]) + a[2] * f->R[2][2];
+    w.x = fmaf(a[2], f->R[2][0], fmaf(a[1], f->R[1][0], fmaf(a[0], f->R[0][0], f->P[0])));
+    w.y = fmaf(a[2], f->R[2][1], fmaf(a[1], f->R[1][1], fmaf(a[0], f->R[0][1], f->P[1])));
+    w.z = fmaf(a[2], f->R[2][2], fmaf(a[1], f->R[1][2], fmaf(a[0], f->R[0][2], f->P[2])));
     return w;
 }
 
@@ -250,12 +238,12 @@ static int disjoint(const aabb* u, const float lo[3], const float hi[3]) {
 static float g_of(const float a[3], const float d[3], const float h[3], float t, float* f2) {
     float qv[3];
     for (int k = 0; k < 3; ++k) {
-        float p = a[k] + t * d[k];
+        float p = fmaf(t, d[k], a[k]);
         float cl = p < -h[k] ? -h[k] : (p > h[k] ? h[k] : p);
         qv[k] = p - cl;
     }
-    *f2 = (qv[0] * qv[0] + qv[1] * qv[1]) + qv[2] * qv[2];
-    return (qv[0] * d[0] + qv[1] * d[1]) + qv[2] * d[2];
+    *f2 = fmaf(qv[2], qv[2], fmaf(qv[1], qv[1], qv[0] * qv[0]));
+    return fmaf(qv[2], d[2], fmaf(qv[1], d[1], qv[0] * d[0]));
 }
 
 /* squared distance segment a-b to box [-h,h] (box frame); DESIGN.md §3.3 */
@@ -291,7 +279,7 @@ static float seg_box_d2(const float a[3], const float b[3], const float h[3]) {
         tl = T[i];
         gl = gi;
     }
-    float ts = tl + (tk - tl) * ((-gl) / (gk - gl));
+    float ts = fmaf(tk - tl, (-gl) / (gk - gl), tl);
     g_of(a, d, h, ts, &f2);
     return f2;
 }
@@ -312,16 +300,16 @@ static float seg_seg_d2(v3 a1, v3 b1, v3 a2, v3 b2) {
             s = c01(-C / A);
         } else {
             float Bd = dot(d1, d2);
-            float den = A * E - Bd * Bd;
-            s = den > 0.0f ? c01((Bd * F - C * E) / den) : 0.0f;
-            float tn = Bd * s + F;
+            float den = fmaf(A, E, -(Bd * Bd));
+            s = den > 0.0f ? c01(fmaf(Bd, F, -(C * E)) / den) : 0.0f;
+            float tn = fmaf(Bd, s, F);
             if (tn < 0.0f) { t = 0.0f; s = c01(-C / A); }
             else if (tn > E) { t = 1.0f; s = c01((Bd - C) / A); }
             else t = tn / E;
         }
     }
-    v3 p1 = {a1.x + d1.x * s, a1.y + d1.y * s, a1.z + d1.z * s};
-    v3 p2 = {a2.x + d2.x * t, a2.y + d2.y * t, a2.z + d2.z * t};
+    v3 p1 = {fmaf(d1.x, s, a1.x), fmaf(d1.y, s, a1.y), fmaf(d1.z, s, a1.z)};
+    v3 p2 = {fmaf(d2.x, t, a2.x), fmaf(d2.y, t, a2.y), fmaf(d2.z, t, a2.z)};
     v3 dd = {p1.x - p2.x, p1.y - p2.y, p1.z - p2.z};
     return dot(dd, dd);
 }
@@ -332,9 +320,9 @@ static int cap_vs_box(const ro_scene* s, int c, v3 A, v3 B, const aabb* u, int j
     const float cs = s->box_cs[j], sn = s->box_sn[j];
     float pa[3], pb[3];
     float dx = A.x - s->box_c[j][0], dy = A.y - s->box_c[j][1], dz = A.z - s->box_c[j][2];
-    pa[0] = cs * dx + sn * dy; pa[1] = cs * dy - sn * dx; pa[2] = dz;
+    pa[0] = fmaf(cs, dx, sn * dy); pa[1] = fmaf(cs, dy, -(sn * dx)); pa[2] = dz;
     dx = B.x - s->box_c[j][0]; dy = B.y - s->box_c[j][1]; dz = B.z - s->box_c[j][2];
-    pb[0] = cs * dx + sn * dy; pb[1] = cs * dy - sn * dx; pb[2] = dz;
+    pb[0] = fmaf(cs, dx, sn * dy); pb[1] = fmaf(cs, dy, -(sn * dx)); pb[2] = dz;
     const float r = s->cap_r[c];
     return seg_box_d2(pa, pb, s->box_h[j]) <= r * r;
 }

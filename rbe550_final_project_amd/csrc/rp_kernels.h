@@ -393,14 +393,13 @@ __device__ void contacts_caps(const Capsules& k, const DevScene* sc, int32_t* ou
             if (n < cap) { out[2 * n] = CAP_LINK[C]; out[2 * n + 1] = -1; }
             ++n;
         }
-        // one box at a time through the same per-capsule test
-        DevScene one = *sc;
+        // every box, reported with its index in the caller's order
         for (int j = 0; j < sc->n_boxes; ++j) {
-            for (int w = 0; w < 16; ++w) one.box[0][w] = sc->box[j][w];
-            one.n_boxes = 1;
-            one.plane_z = -__builtin_inff();
-            if (capsule_hits_boxes<C>(k, &one)) {
-                if (n < cap) { out[2 * n] = CAP_LINK[C]; out[2 * n + 1] = j; }
+            const float* bx = sc->box[j];
+            if ((__float_as_uint(bx[14]) >> C) & 1u) continue;
+            if (aabb_disjoint(u, bx + 8, bx + 11)) continue;
+            if (capsule_box_narrow(k.a[C], k.b[C], r, bx)) {
+                if (n < cap) { out[2 * n] = CAP_LINK[C]; out[2 * n + 1] = __float_as_int(bx[15]); }
                 ++n;
             }
         }

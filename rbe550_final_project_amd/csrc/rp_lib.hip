@@ -7,6 +7,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <climits>
 #include <cmath>
@@ -86,6 +87,7 @@ struct rp_ctx {
     DevScene scene{};
     DevScene* d_scene = nullptr;
     bool have_scene = false;
+    std::vector<int> slot_of;            // caller box index -> stored (cluster-sorted) slot
     rp_robot_desc robot{};
     std::string err;
     rp_stats stats{};
@@ -717,6 +719,9 @@ int rp_set_scene(rp_ctx* c, const rp_box* boxes, int32_t n, float plane_z, const
     if (!c || n < 0 || n > MAX_BOXES || (n > 0 && !boxes)) return RP_ERR_ARG;
     RP_GUARD_BEGIN
     HIP_TRY(hipSetDevice(c->device));
+    // box records in the caller's order (cos/sin of yaw in double, rounded once;
+    // world AABB of the yawed box)
+    std::vector<std::array<float, 16>> rec(n);
     for (int j = 0; j < n; ++j) {
         const rp_box& b = boxes[j];
         const float cs = (float)std::cos((double)b.yaw);
@@ -726,7 +731,7 @@ int rp_set_scene(rp_ctx* c, const rp_box* boxes, int32_t n, float plane_z, const
         ext[0] = acs * b.half[0] + asn * b.half[1];
         ext[1] = asn * b.half[0] + acs * b.half[1];
         ext[2] = b.half[2];
-        float* r = c->scene.box[j];
+        float* r = rec[j].data();
         for (int k = 0; k < 3; ++k) {
             r[k] = b.center[k];
             r[3 + k] = b.half[k];
@@ -736,7 +741,57 @@ int rp_set_scene(rp_ctx* c, const rp_box* boxes, int32_t n, float plane_z, const
         r[6] = cs;
         r[7] = sn;
         r[14] = 0.0f;  // exempt bits = 0
-        r[15] = 0.0f;
+        int32_t orig = j;
+        std::memcpy(&r[15], &orig, 4);
+    }
+    // broad-phase clusters: recursive median split along the widest centre spread
+    // into groups of <= CLUSTER boxes (a two-level AABB tree: <= 8 clusters)
+    std::vector<int> order(n);
+    for (int j = 0; j < n; ++j) order[j] = j;
+    std::vector<std::pair<int, int>> groups;
+    std::vector<std::pair<int, int>> todo;
+    if (n > 0) todo.push_back({0, n});
+    while (!todo.empty()) {
+        auto [b0, e0] = todo.back();
+        todo.pop_back();
+        if (e0 - b0 <= CLUSTER) {
+            groups.push_back({b0, e0});
+            continue;
+        }
+        int axis = 0;
+        float best = -1.0f;
+        for (int k = 0; k < 3; ++k) {
+            float lo = 1e30f, hi = -1e30f;
+            for (int i = b0; i < e0; ++i) {
+                lo = std::min(lo, rec[order[i]][k]);
+                hi = std::max(hi, rec[order[i]][k]);
+            }
+            if (hi - lo > best) { best = hi - lo; axis = k; }
+        }
+        std::stable_sort(order.begin() + b0, order.begin() + e0,
+                         [&](int x, int y) { return rec[x][axis] < rec[y][axis]; });
+        const int mid = b0 + (e0 - b0 + 1) / 2;
+        todo.push_back({mid, e0});
+        todo.push_back({b0, mid});
+    }
+    std::sort(groups.begin(), groups.end());
+    c->slot_of.assign(n, 0);
+    for (int s = 0; s < n; ++s) {
+        std::memcpy(c->scene.box[s], rec[order[s]].data(), sizeof(float) * 16);
+        c->slot_of[order[s]] = s;
+    }
+    c->scene.n_clusters = (int)groups.size();
+    for (size_t g = 0; g < groups.size(); ++g) {
+        float* cr = c->scene.cluster[g];
+        for (int k = 0; k < 3; ++k) { cr[k] = 1e30f; cr[4 + k] = -1e30f; }
+        for (int s = groups[g].first; s < groups[g].second; ++s)
+            for (int k = 0; k < 3; ++k) {
+                cr[k] = std::min(cr[k], c->scene.box[s][8 + k]);
+                cr[4 + k] = std::max(cr[4 + k], c->scene.box[s][11 + k]);
+            }
+        const int32_t first = groups[g].first, cnt = groups[g].second - groups[g].first;
+        std::memcpy(&cr[3], &first, 4);
+        std::memcpy(&cr[7], &cnt, 4);
     }
     c->scene.n_boxes = n;
     c->scene.plane_z = plane_z;
@@ -757,7 +812,7 @@ int rp_set_attached(rp_ctx* c, int32_t box, uint32_t link_mask) {
         uint32_t bits = 0;
         for (int i = 0; i < NCAP; ++i)
             if ((link_mask >> CAP_LINK[i]) & 1u) bits |= 1u << i;
-        std::memcpy(&c->scene.box[box][14], &bits, 4);
+        std::memcpy(&c->scene.box[c->slot_of[box]][14], &bits, 4);
     }
     upload_scene(c);
     return RP_OK;

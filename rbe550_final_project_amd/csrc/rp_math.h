@@ -5,10 +5,16 @@
 //   robot.detect_collision()  -> Genesis broad+narrow phase   => state_collides()
 //   collision_with_attached_object()                          => per-box exempt bits
 //
-// Numerics contract: float32, every operation written out in a fixed
-// order, compiled with -ffp-contract=off, so the CPU oracle (oracle/rbe_oracle.c),
-// which restates the same sequence, produces bit-identical flags. sin/cos come from
-// rp_sincos() (polynomial, +,-,* only), never from the device libm.
+// Numerics contract: float32; every operation written out in a fixed
+// order with explicit fused multiply-adds (fmaf, one rounding) and otherwise plain
+// IEEE ops; compiled with -ffp-contract=off so the compiler adds no other fusion.
+// The CPU oracle (oracle/rbe_oracle.c) restates the same sequence with C99 fmaf, so
+// flags are bit-identical. sin/cos come from rp_sincos() (polynomial), never libm.
+//
+// Code shape: FK and the broad phases are straight-line code; the two narrow phases
+// (segment-box, segment-segment) are single out-of-line functions: they run only
+// for overlapping AABBs, and inlining them at 12 + 35 call sites made a 12k-
+// instruction kernel that thrashed the instruction cache.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -21,29 +27,22 @@ struct V3 { float x, y, z; };
 __device__ __forceinline__ float fminr(float a, float b) { return a < b ? a : b; }
 __device__ __forceinline__ float fmaxr(float a, float b) { return a > b ? a : b; }
 __device__ __forceinline__ float clamp01(float x) { return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x); }
-__device__ __forceinline__ float dot3(V3 u, V3 v) { return (u.x * v.x + u.y * v.y) + u.z * v.z; }
+__device__ __forceinline__ float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+// (u . v) = fma(uz, vz, fma(uy, vy, ux * vx))
+__device__ __forceinline__ float dot3(V3 u, V3 v) { return fma_(u.z, v.z, fma_(u.y, v.y, u.x * v.x)); }
 
-// sin and cos of x, |x| < ~100: quadrant reduction with a 3-part pi/2, then
-// minimax polynomials on [-pi/4, pi/4].
+// sin and cos of x, |x| < ~100: quadrant reduction with a 3-part pi/2 (FMA
+// Cody-Waite), then minimax polynomials on [-pi/4, pi/4].
 __device__ __forceinline__ void rp_sincos(float x, float* sn, float* cs) {
-    const float t = x * 0.636619772f;
-    const float k = floorf(t + 0.5f);
-    float r = x - k * 1.5703125f;
-    r = r - k * 4.837512969970703125e-4f;
-    r = r - k * 7.54978995489188216e-8f;
+    const float k = floorf(x * 0.636619772f + 0.5f);
+    float r = fma_(-k, 1.5703125f, x);
+    r = fma_(-k, 4.837512969970703125e-4f, r);
+    r = fma_(-k, 7.54978995489188216e-8f, r);
     const float z = r * r;
-    float ps = -1.9515295891e-4f;
-    ps = ps * z;
-    ps = ps + 8.3321608736e-3f;
-    ps = ps * z;
-    ps = ps + -1.6666654611e-1f;
-    const float sr = r + (r * z) * ps;
-    float pc = 2.443315711809948e-5f;
-    pc = pc * z;
-    pc = pc + -1.388731625493765e-3f;
-    pc = pc * z;
-    pc = pc + 4.166664568298827e-2f;
-    const float cr = (1.0f - 0.5f * z) + (z * z) * pc;
+    const float ps = fma_(fma_(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f);
+    const float sr = fma_(r * z, ps, r);
+    const float pc = fma_(fma_(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f);
+    const float cr = fma_(z * z, pc, fma_(-0.5f, z, 1.0f));
     const int qd = ((int)k) & 3;
     float s = sr, c = cr;
     if (qd == 1) { s = cr; c = -sr; }
@@ -56,19 +55,22 @@ __device__ __forceinline__ void rp_sincos(float x, float* sn, float* cs) {
 // A rigid frame: rotation columns c0, c1, c2 and origin p (world).
 struct Frame { V3 c0, c1, c2, p; };
 
-// R <- R * Rz(q)
+// R <- R * Rz(angle) given (s, c): n0 = c*c0 + s*c1, n1 = c*c1 - s*c0
+__device__ __forceinline__ void rot_sc(Frame& f, float s, float c) {
+    V3 n0, n1;
+    n0.x = fma_(c, f.c0.x, s * f.c1.x);
+    n0.y = fma_(c, f.c0.y, s * f.c1.y);
+    n0.z = fma_(c, f.c0.z, s * f.c1.z);
+    n1.x = fma_(c, f.c1.x, -(s * f.c0.x));
+    n1.y = fma_(c, f.c1.y, -(s * f.c0.y));
+    n1.z = fma_(c, f.c1.z, -(s * f.c0.z));
+    f.c0 = n0;
+    f.c1 = n1;
+}
 __device__ __forceinline__ void rot_z(Frame& f, float q) {
     float s, c;
     rp_sincos(q, &s, &c);
-    V3 n0, n1;
-    n0.x = c * f.c0.x + s * f.c1.x;
-    n0.y = c * f.c0.y + s * f.c1.y;
-    n0.z = c * f.c0.z + s * f.c1.z;
-    n1.x = c * f.c1.x - s * f.c0.x;
-    n1.y = c * f.c1.y - s * f.c0.y;
-    n1.z = c * f.c1.z - s * f.c0.z;
-    f.c0 = n0;
-    f.c1 = n1;
+    rot_sc(f, s, c);
 }
 // R <- R * Rx(+90deg): [c0, c2, -c1]
 __device__ __forceinline__ void rot_xp(Frame& f) {
@@ -84,16 +86,16 @@ __device__ __forceinline__ void rot_xm(Frame& f) {
 }
 // p <- p + k * col
 __device__ __forceinline__ void shift(V3& p, float k, V3 col) {
-    p.x = p.x + k * col.x;
-    p.y = p.y + k * col.y;
-    p.z = p.z + k * col.z;
+    p.x = fma_(k, col.x, p.x);
+    p.y = fma_(k, col.y, p.y);
+    p.z = fma_(k, col.z, p.z);
 }
 // world point of link-frame point (a0, a1, a2)
 __device__ __forceinline__ V3 xform(const Frame& f, float a0, float a1, float a2) {
     V3 w;
-    w.x = ((f.p.x + a0 * f.c0.x) + a1 * f.c1.x) + a2 * f.c2.x;
-    w.y = ((f.p.y + a0 * f.c0.y) + a1 * f.c1.y) + a2 * f.c2.y;
-    w.z = ((f.p.z + a0 * f.c0.z) + a1 * f.c1.z) + a2 * f.c2.z;
+    w.x = fma_(a2, f.c2.x, fma_(a1, f.c1.x, fma_(a0, f.c0.x, f.p.x)));
+    w.y = fma_(a2, f.c2.y, fma_(a1, f.c1.y, fma_(a0, f.c0.y, f.p.y)));
+    w.z = fma_(a2, f.c2.z, fma_(a1, f.c1.z, fma_(a0, f.c0.z, f.p.z)));
     return w;
 }
 
@@ -116,57 +118,37 @@ __device__ __forceinline__ void fk_capsules(const float q[NQ], const DevScene* _
     f.c2 = {0.0f, 0.0f, 1.0f};
     f.p = {sc->base[0], sc->base[1], sc->base[2]};
     place<C_LINK0>(k, f, sc);
-    // link1: pos (0,0,0.333), joint 1
-    shift(f.p, 0.333f, f.c2);
+    shift(f.p, 0.333f, f.c2);               // link1: pos (0,0,0.333), joint 1
     rot_z(f, q[0]);
     place<C_LINK1>(k, f, sc);
-    // link2: quat (1,-1,0,0) = Rx(-90), joint 2
-    rot_xm(f);
+    rot_xm(f);                              // link2: quat (1,-1,0,0) = Rx(-90), joint 2
     rot_z(f, q[1]);
     place<C_LINK2>(k, f, sc);
-    // link3: pos (0,-0.316,0), Rx(+90), joint 3
-    shift(f.p, -0.316f, f.c1);
+    shift(f.p, -0.316f, f.c1);              // link3: pos (0,-0.316,0), Rx(+90), joint 3
     rot_xp(f);
     rot_z(f, q[2]);
     place<C_LINK3>(k, f, sc);
-    // link4: pos (0.0825,0,0), Rx(+90), joint 4
-    shift(f.p, 0.0825f, f.c0);
+    shift(f.p, 0.0825f, f.c0);              // link4: pos (0.0825,0,0), Rx(+90), joint 4
     rot_xp(f);
     rot_z(f, q[3]);
     place<C_LINK4>(k, f, sc);
-    // link5: pos (-0.0825,0.384,0), Rx(-90), joint 5
-    shift(f.p, -0.0825f, f.c0);
+    shift(f.p, -0.0825f, f.c0);             // link5: pos (-0.0825,0.384,0), Rx(-90), joint 5
     shift(f.p, 0.384f, f.c1);
     rot_xm(f);
     rot_z(f, q[4]);
     place<C_LINK5A>(k, f, sc);
     place<C_LINK5B>(k, f, sc);
-    // link6: Rx(+90), joint 6
-    rot_xp(f);
+    rot_xp(f);                              // link6: Rx(+90), joint 6
     rot_z(f, q[5]);
     place<C_LINK6>(k, f, sc);
-    // link7: pos (0.088,0,0), Rx(+90), joint 7
-    shift(f.p, 0.088f, f.c0);
+    shift(f.p, 0.088f, f.c0);               // link7: pos (0.088,0,0), Rx(+90), joint 7
     rot_xp(f);
     rot_z(f, q[6]);
     place<C_LINK7>(k, f, sc);
-    // hand: pos (0,0,0.107), quat (0.9238795,0,0,-0.3826834) = Rz(-45deg)
-    shift(f.p, 0.107f, f.c2);
-    {
-        const float c = 0.70710677f, s = -0.70710677f;
-        V3 n0, n1;
-        n0.x = c * f.c0.x + s * f.c1.x;
-        n0.y = c * f.c0.y + s * f.c1.y;
-        n0.z = c * f.c0.z + s * f.c1.z;
-        n1.x = c * f.c1.x - s * f.c0.x;
-        n1.y = c * f.c1.y - s * f.c0.y;
-        n1.z = c * f.c1.z - s * f.c0.z;
-        f.c0 = n0;
-        f.c1 = n1;
-    }
+    shift(f.p, 0.107f, f.c2);               // hand: pos (0,0,0.107), Rz(-45deg)
+    rot_sc(f, -0.70710677f, 0.70710677f);
     place<C_HAND>(k, f, sc);
-    // fingers: pos (0,0,0.0584) from the hand, prismatic along +-hand y
-    shift(f.p, 0.0584f, f.c2);
+    shift(f.p, 0.0584f, f.c2);              // fingers: (0,0,0.0584), prismatic +-hand y
     {
         Frame l = f;
         shift(l.p, q[7], f.c1);
@@ -199,49 +181,44 @@ __device__ __forceinline__ bool aabb_disjoint2(const Aabb& u, const Aabb& v) {
 
 // g(t) = q(t) . d with q the excess of a + t d over the box [-h, h]; also |q|^2.
 __device__ __forceinline__ float excess_dot(V3 a, V3 d, V3 h, float t, float* f2) {
-    float px = a.x + t * d.x, py = a.y + t * d.y, pz = a.z + t * d.z;
-    float cx = px < -h.x ? -h.x : (px > h.x ? h.x : px);
-    float cy = py < -h.y ? -h.y : (py > h.y ? h.y : py);
-    float cz = pz < -h.z ? -h.z : (pz > h.z ? h.z : pz);
-    V3 qv = {px - cx, py - cy, pz - cz};
+    const float px = fma_(t, d.x, a.x), py = fma_(t, d.y, a.y), pz = fma_(t, d.z, a.z);
+    const float cx = px < -h.x ? -h.x : (px > h.x ? h.x : px);
+    const float cy = py < -h.y ? -h.y : (py > h.y ? h.y : py);
+    const float cz = pz < -h.z ? -h.z : (pz > h.z ? h.z : pz);
+    const V3 qv = {px - cx, py - cy, pz - cz};
     *f2 = dot3(qv, qv);
     return dot3(qv, d);
 }
 
-// Segment a-b (box frame) vs box [-h, h]: squared distance is a convex piecewise
+// Segment a-b (box frame) vs box [-h, h]: the squared distance is a convex piecewise
 // quadratic in t with C^1 joins; its derivative g is piecewise linear and
 // nondecreasing with breakpoints where a coordinate crosses +-h. Locate the root of
 // g between the sorted breakpoints and interpolate linearly inside that piece.
-__device__ __forceinline__ float segment_box_dist2(V3 a, V3 b, V3 h) {
-    V3 d = {b.x - a.x, b.y - a.y, b.z - a.z};
+__device__ __attribute__((noinline)) float segment_box_dist2(V3 a, V3 b, V3 h) {
+    const V3 d = {b.x - a.x, b.y - a.y, b.z - a.z};
     float T[6];
     {
         float u = 0.0f, v = 0.0f;
-        if (d.x != 0.0f) { float inv = 1.0f / d.x; u = (-h.x - a.x) * inv; v = (h.x - a.x) * inv; }
+        if (d.x != 0.0f) { const float inv = 1.0f / d.x; u = (-h.x - a.x) * inv; v = (h.x - a.x) * inv; }
         T[0] = clamp01(u); T[1] = clamp01(v);
         u = 0.0f; v = 0.0f;
-        if (d.y != 0.0f) { float inv = 1.0f / d.y; u = (-h.y - a.y) * inv; v = (h.y - a.y) * inv; }
+        if (d.y != 0.0f) { const float inv = 1.0f / d.y; u = (-h.y - a.y) * inv; v = (h.y - a.y) * inv; }
         T[2] = clamp01(u); T[3] = clamp01(v);
         u = 0.0f; v = 0.0f;
-        if (d.z != 0.0f) { float inv = 1.0f / d.z; u = (-h.z - a.z) * inv; v = (h.z - a.z) * inv; }
+        if (d.z != 0.0f) { const float inv = 1.0f / d.z; u = (-h.z - a.z) * inv; v = (h.z - a.z) * inv; }
         T[4] = clamp01(u); T[5] = clamp01(v);
     }
     // sorting network (12 exchanges) — the sorted multiset is order independent
-#define RP_CX(i, j) { float lo_ = fminr(T[i], T[j]); float hi_ = fmaxr(T[i], T[j]); T[i] = lo_; T[j] = hi_; }
+#define RP_CX(i, j) { const float lo_ = fminr(T[i], T[j]); const float hi_ = fmaxr(T[i], T[j]); T[i] = lo_; T[j] = hi_; }
     RP_CX(0, 1) RP_CX(2, 3) RP_CX(4, 5) RP_CX(0, 2) RP_CX(3, 5) RP_CX(1, 4)
     RP_CX(0, 1) RP_CX(2, 3) RP_CX(4, 5) RP_CX(1, 2) RP_CX(3, 4) RP_CX(2, 3)
 #undef RP_CX
     float f2;
     const float g0 = excess_dot(a, d, h, 0.0f, &f2);
-    float ts;
-    if (g0 >= 0.0f) {
-        return f2;
-    }
+    if (g0 >= 0.0f) return f2;
     float f2e;
     const float g7 = excess_dot(a, d, h, 1.0f, &f2e);
-    if (g7 <= 0.0f) {
-        return f2e;
-    }
+    if (g7 <= 0.0f) return f2e;
     float tl = 0.0f, gl = g0, tk = 1.0f, gk = g7;
     bool found = false;
 #pragma unroll
@@ -253,16 +230,16 @@ __device__ __forceinline__ float segment_box_dist2(V3 a, V3 b, V3 h) {
             else { tl = T[i]; gl = gi; }
         }
     }
-    ts = tl + (tk - tl) * ((-gl) / (gk - gl));
+    const float ts = fma_(tk - tl, (-gl) / (gk - gl), tl);
     excess_dot(a, d, h, ts, &f2);
     return f2;
 }
 
 // Closest distance^2 between segments a1-b1 and a2-b2.
-__device__ __forceinline__ float segment_segment_dist2(V3 a1, V3 b1, V3 a2, V3 b2) {
-    V3 d1 = {b1.x - a1.x, b1.y - a1.y, b1.z - a1.z};
-    V3 d2 = {b2.x - a2.x, b2.y - a2.y, b2.z - a2.z};
-    V3 w = {a1.x - a2.x, a1.y - a2.y, a1.z - a2.z};
+__device__ __attribute__((noinline)) float segment_segment_dist2(V3 a1, V3 b1, V3 a2, V3 b2) {
+    const V3 d1 = {b1.x - a1.x, b1.y - a1.y, b1.z - a1.z};
+    const V3 d2 = {b2.x - a2.x, b2.y - a2.y, b2.z - a2.z};
+    const V3 w = {a1.x - a2.x, a1.y - a2.y, a1.z - a2.z};
     const float A = dot3(d1, d1), E = dot3(d2, d2), F = dot3(d2, w);
     float s, t;
     if (A <= 1e-12f) {
@@ -275,48 +252,58 @@ __device__ __forceinline__ float segment_segment_dist2(V3 a1, V3 b1, V3 a2, V3 b
             s = clamp01(-C / A);
         } else {
             const float B = dot3(d1, d2);
-            const float den = A * E - B * B;
-            s = den > 0.0f ? clamp01((B * F - C * E) / den) : 0.0f;
-            const float tn = B * s + F;
+            const float den = fma_(A, E, -(B * B));
+            s = den > 0.0f ? clamp01(fma_(B, F, -(C * E)) / den) : 0.0f;
+            const float tn = fma_(B, s, F);
             if (tn < 0.0f) { t = 0.0f; s = clamp01(-C / A); }
             else if (tn > E) { t = 1.0f; s = clamp01((B - C) / A); }
             else { t = tn / E; }
         }
     }
-    V3 p1 = {a1.x + d1.x * s, a1.y + d1.y * s, a1.z + d1.z * s};
-    V3 p2 = {a2.x + d2.x * t, a2.y + d2.y * t, a2.z + d2.z * t};
-    V3 dd = {p1.x - p2.x, p1.y - p2.y, p1.z - p2.z};
+    const V3 p1 = {fma_(d1.x, s, a1.x), fma_(d1.y, s, a1.y), fma_(d1.z, s, a1.z)};
+    const V3 p2 = {fma_(d2.x, t, a2.x), fma_(d2.y, t, a2.y), fma_(d2.z, t, a2.z)};
+    const V3 dd = {p1.x - p2.x, p1.y - p2.y, p1.z - p2.z};
     return dot3(dd, dd);
 }
 
-// Capsule C vs every box of the scene (skipping exempt pairs).
+// narrow phase of capsule (a, b, r) against box record bx (world -> box frame:
+// rotation by -yaw about z)
+__device__ __forceinline__ bool capsule_box_narrow(V3 a, V3 b, float r, const float* __restrict__ bx) {
+    const float cs = bx[6], sn = bx[7];
+    V3 pa, pb;
+    {
+        const float dx = a.x - bx[0], dy = a.y - bx[1], dz = a.z - bx[2];
+        pa.x = fma_(cs, dx, sn * dy); pa.y = fma_(cs, dy, -(sn * dx)); pa.z = dz;
+    }
+    {
+        const float dx = b.x - bx[0], dy = b.y - bx[1], dz = b.z - bx[2];
+        pb.x = fma_(cs, dx, sn * dy); pb.y = fma_(cs, dy, -(sn * dx)); pb.z = dz;
+    }
+    const V3 h = {bx[3], bx[4], bx[5]};
+    return segment_box_dist2(pa, pb, h) <= r * r;
+}
+
+// Capsule C vs the plane and every box of the scene (skipping exempt pairs). The
+// cluster AABB tests are an exact reject (a box AABB lies inside its cluster's), so
+// they change no result, only how much broad-phase work a lane does.
 template <int C>
-__device__ __forceinline__ bool capsule_hits_boxes(const Capsules& k, const DevScene* __restrict__ sc) {
+__device__ __forceinline__ bool capsule_hits_env(const Capsules& k, const DevScene* __restrict__ sc) {
     const float r = sc->cap[C][6];
     const Aabb u = capsule_aabb(k.a[C], k.b[C], r);
     if (u.lo.z <= sc->plane_z) return true;  // capsule vs ground plane
-    const int nb = sc->n_boxes;
-    bool hit = false;
-    for (int j = 0; j < nb && !hit; ++j) {
-        const float* bx = sc->box[j];
-        const uint32_t ex = __float_as_uint(bx[14]);
-        if ((ex >> C) & 1u) continue;
-        if (aabb_disjoint(u, bx + 8, bx + 11)) continue;
-        // narrow phase in the box frame (rotate by -yaw about z)
-        const float cs = bx[6], sn = bx[7];
-        V3 pa, pb;
-        {
-            const float dx = k.a[C].x - bx[0], dy = k.a[C].y - bx[1], dz = k.a[C].z - bx[2];
-            pa.x = cs * dx + sn * dy; pa.y = cs * dy - sn * dx; pa.z = dz;
+    const int ncl = sc->n_clusters;
+    for (int cl = 0; cl < ncl; ++cl) {
+        const float* cr = sc->cluster[cl];
+        if (aabb_disjoint(u, cr, cr + 4)) continue;
+        const int j0 = __float_as_int(cr[3]), nj = __float_as_int(cr[7]);
+        for (int j = j0; j < j0 + nj; ++j) {
+            const float* bx = sc->box[j];
+            if ((__float_as_uint(bx[14]) >> C) & 1u) continue;
+            if (aabb_disjoint(u, bx + 8, bx + 11)) continue;
+            if (capsule_box_narrow(k.a[C], k.b[C], r, bx)) return true;
         }
-        {
-            const float dx = k.b[C].x - bx[0], dy = k.b[C].y - bx[1], dz = k.b[C].z - bx[2];
-            pb.x = cs * dx + sn * dy; pb.y = cs * dy - sn * dx; pb.z = dz;
-        }
-        V3 h = {bx[3], bx[4], bx[5]};
-        if (segment_box_dist2(pa, pb, h) <= r * r) hit = true;
     }
-    return hit;
+    return false;
 }
 
 template <int P>
@@ -331,12 +318,12 @@ __device__ __forceinline__ bool pair_hits(const Capsules& k, const DevScene* __r
 }
 
 template <int C>
-__device__ __forceinline__ bool boxes_from(const Capsules& k, const DevScene* __restrict__ sc) {
+__device__ __forceinline__ bool env_from(const Capsules& k, const DevScene* __restrict__ sc) {
     if constexpr (C == NCAP) {
         return false;
     } else {
-        if (capsule_hits_boxes<C>(k, sc)) return true;
-        return boxes_from<C + 1>(k, sc);
+        if (capsule_hits_env<C>(k, sc)) return true;
+        return env_from<C + 1>(k, sc);
     }
 }
 template <int P>
@@ -355,7 +342,7 @@ __device__ __forceinline__ bool pairs_from(const Capsules& k, const DevScene* __
 __device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene* __restrict__ sc) {
     Capsules k;
     fk_capsules(q, sc, k);
-    if (boxes_from<0>(k, sc)) return true;
+    if (env_from<0>(k, sc)) return true;
     return pairs_from<0>(k, sc);
 }
 

@@ -36,18 +36,25 @@ constexpr int PAIRS[NPAIR][2] = {
 };
 
 constexpr int MAX_BOXES = 64;
+constexpr int CLUSTER = 8;                       // boxes per broad-phase cluster
+constexpr int MAX_CLUSTERS = MAX_BOXES / CLUSTER;
 
 // Device scene record (one constant buffer, read by wave-uniform scalar loads).
 // Box record: 16 floats so one s_load_dwordx16 fetches it.
 //   [0..2] centre  [3..5] half extents  [6] cos(yaw) [7] sin(yaw)
-//   [8..10] world AABB lo  [11..13] world AABB hi  [14] exempt-capsule bits  [15] pad
+//   [8..10] world AABB lo  [11..13] world AABB hi  [14] exempt-capsule bits
+//   [15] index of the box in the caller's order (boxes are stored cluster-sorted)
+// Cluster record: [0..2] AABB lo, [4..6] AABB hi (union of its boxes' AABBs),
+//   [3] first box, [7] box count (as int bits).
 struct DevScene {
     float cap[NCAP][8];          // ax ay az bx by bz radius pad (link frame)
     float box[MAX_BOXES][16];
+    float cluster[MAX_CLUSTERS][8];
     float base[4];               // robot base translation (scenes.py:29-34), pad
     float plane_z;
     int n_boxes;
-    int pad[2];
+    int n_clusters;
+    int pad;
 };
 
 }  // namespace rp

@@ -83,7 +83,6 @@ struct rp_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
-    bool use_lds = false;
     DevScene scene{};
     DevScene* d_scene = nullptr;
     bool have_scene = false;
@@ -144,12 +143,7 @@ namespace {
 
 void launch_validity(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, hipStream_t s) {
     if (n <= 0) return;
-    if (c->use_lds)
-        hipLaunchKernelGGL(k_validity<true>, dim3(blocks_for(n, VBLOCK)), dim3(VBLOCK), 0, s, q, n, flags,
-                           c->d_scene);
-    else
-        hipLaunchKernelGGL(k_validity<false>, dim3(blocks_for(n, VBLOCK)), dim3(VBLOCK), 0, s, q, n, flags,
-                           c->d_scene);
+    hipLaunchKernelGGL(k_validity, dim3(blocks_for(n, VBLOCK)), dim3(VBLOCK), 0, s, q, n, flags, c->d_scene);
     HIP_TRY(hipGetLastError());
 }
 
@@ -157,12 +151,8 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
                   int mode, uint8_t* valid, int group, int* gfail, hipStream_t s) {
     if (n <= 0) return;
     const int64_t threads = n * (int64_t)kmax;
-    if (c->use_lds)
-        hipLaunchKernelGGL(k_edges<true>, dim3(blocks_for(threads, VBLOCK)), dim3(VBLOCK), 0, s, from, to, nd, n,
-                           kmax, mode, valid, group, gfail, c->counter.p, c->d_scene);
-    else
-        hipLaunchKernelGGL(k_edges<false>, dim3(blocks_for(threads, VBLOCK)), dim3(VBLOCK), 0, s, from, to, nd,
-                           n, kmax, mode, valid, group, gfail, c->counter.p, c->d_scene);
+    hipLaunchKernelGGL(k_edges, dim3(blocks_for(threads, VBLOCK)), dim3(VBLOCK), 0, s, from, to, nd, n, kmax, mode,
+                       valid, group, gfail, c->counter.p, c->d_scene);
     HIP_TRY(hipGetLastError());
 }
 
@@ -589,24 +579,13 @@ bool structure_matches(const rp_robot_desc& r) {
         if (r.capsules[i].link != CAP_LINK[i]) return false;
     for (int i = 0; i < NPAIR; ++i)
         if (r.self_pairs[i][0] != PAIRS[i][0] || r.self_pairs[i][1] != PAIRS[i][1]) return false;
+    for (int i = 0; i < NCAP; ++i) {  // the geometry is compiled into the kernels (rp_model.h)
+        for (int k = 0; k < 3; ++k)
+            if (r.capsules[i].a[k] != CAP_GEOM[i][k] || r.capsules[i].b[k] != CAP_GEOM[i][3 + k]) return false;
+        if (r.capsules[i].radius != CAP_GEOM[i][6]) return false;
+    }
     return true;
 }
-
-// built-in model = spec/franka_capsules.json
-const float kCaps[NCAP][7] = {
-    {-0.09f, 0.0f, 0.06f, -0.06f, 0.0f, 0.06f, 0.06f},       // link0
-    {0.0f, 0.0f, -0.193f, 0.0f, 0.0f, -0.05f, 0.06f},        // link1
-    {0.0f, 0.0f, -0.06f, 0.0f, 0.0f, 0.06f, 0.06f},          // link2
-    {0.0f, 0.0f, -0.22f, 0.0f, 0.0f, -0.07f, 0.06f},         // link3
-    {0.0f, 0.0f, -0.06f, 0.0f, 0.0f, 0.06f, 0.06f},          // link4
-    {0.0f, 0.0f, -0.31f, 0.0f, 0.0f, -0.21f, 0.06f},         // link5a
-    {0.0f, 0.08f, -0.20f, 0.0f, 0.08f, -0.06f, 0.025f},      // link5b
-    {0.0f, 0.0f, -0.07f, 0.0f, 0.0f, 0.01f, 0.05f},          // link6
-    {0.0f, 0.0f, -0.06f, 0.0f, 0.0f, 0.08f, 0.04f},          // link7
-    {0.0f, -0.05f, 0.04f, 0.0f, 0.05f, 0.04f, 0.04f},        // hand
-    {0.0f, 0.012f, 0.012f, 0.0f, 0.012f, 0.040f, 0.010f},    // left finger
-    {0.0f, 0.012f, 0.012f, 0.0f, 0.012f, 0.040f, 0.010f},    // right finger
-};
 
 }  // namespace
 
@@ -637,10 +616,10 @@ int rp_default_robot(rp_robot_desc* out) {
     for (int i = 0; i < NCAP; ++i) {
         out->capsules[i].link = CAP_LINK[i];
         for (int k = 0; k < 3; ++k) {
-            out->capsules[i].a[k] = kCaps[i][k];
-            out->capsules[i].b[k] = kCaps[i][3 + k];
+            out->capsules[i].a[k] = CAP_GEOM[i][k];
+            out->capsules[i].b[k] = CAP_GEOM[i][3 + k];
         }
-        out->capsules[i].radius = kCaps[i][6];
+        out->capsules[i].radius = CAP_GEOM[i][6];
     }
     out->n_self_pairs = NPAIR;
     for (int i = 0; i < NPAIR; ++i) {
@@ -660,7 +639,7 @@ int rp_create(rp_ctx** out, int device, const rp_robot_desc* robot) {
         robot = &def;
     }
     if (!structure_matches(*robot)) {
-        g_create_error = "robot description does not match the compiled Franka capsule structure";
+        g_create_error = "robot description does not match the compiled Franka capsule model (structure and geometry)";
         return RP_ERR_ARG;
     }
     int ndev = 0;
@@ -686,21 +665,11 @@ int rp_create(rp_ctx** out, int device, const rp_robot_desc* robot) {
         HIP_TRY(hipEventCreate(&c->ev1));
         HIP_TRY(hipMalloc(&c->d_scene, sizeof(DevScene)));
         c->robot = *robot;
-        for (int i = 0; i < NCAP; ++i) {
-            for (int k = 0; k < 3; ++k) {
-                c->scene.cap[i][k] = robot->capsules[i].a[k];
-                c->scene.cap[i][3 + k] = robot->capsules[i].b[k];
-            }
-            c->scene.cap[i][6] = robot->capsules[i].radius;
-            c->scene.cap[i][7] = 0.0f;
-        }
         c->scene.base[0] = 0.0f;
         c->scene.base[1] = 0.0f;
         c->scene.base[2] = 0.01f;
         c->scene.plane_z = 0.0f;
         c->scene.n_boxes = 0;
-        const char* lds = std::getenv("RP_SCENE_LDS");
-        c->use_lds = lds && lds[0] == '1';
         c->counter.ensure(1);
         c->scalar.ensure(16);
         upload_scene(c);

@@ -101,64 +101,103 @@ __device__ __forceinline__ V3 xform(const Frame& f, float a0, float a1, float a2
 
 struct Capsules { V3 a[NCAP]; V3 b[NCAP]; };
 
+// fma(a2, c2, fma(a1, c1, fma(a0, c0, p))) with compile-time a: a zero term is
+// skipped (fma(0, x, p) == p for finite x, up to the sign of a zero result, which
+// no later comparison can observe).
+template <int C, int O>
+__device__ __forceinline__ V3 xform_c(const Frame& f) {
+    constexpr float a0 = CAP_GEOM[C][O], a1 = CAP_GEOM[C][O + 1], a2 = CAP_GEOM[C][O + 2];
+    V3 w = f.p;
+    if constexpr (a0 != 0.0f) { w.x = fma_(a0, f.c0.x, w.x); w.y = fma_(a0, f.c0.y, w.y); w.z = fma_(a0, f.c0.z, w.z); }
+    if constexpr (a1 != 0.0f) { w.x = fma_(a1, f.c1.x, w.x); w.y = fma_(a1, f.c1.y, w.y); w.z = fma_(a1, f.c1.z, w.z); }
+    if constexpr (a2 != 0.0f) { w.x = fma_(a2, f.c2.x, w.x); w.y = fma_(a2, f.c2.y, w.y); w.z = fma_(a2, f.c2.z, w.z); }
+    return w;
+}
+
 template <int C>
-__device__ __forceinline__ void place(Capsules& k, const Frame& f, const DevScene* __restrict__ sc) {
-    const float* g = sc->cap[C];
-    k.a[C] = xform(f, g[0], g[1], g[2]);
-    k.b[C] = xform(f, g[3], g[4], g[5]);
+__device__ __forceinline__ void place(Capsules& k, const Frame& f) {
+    k.a[C] = xform_c<C, 0>(f);
+    k.b[C] = xform_c<C, 3>(f);
 }
 
 // Franka Panda forward kinematics (MJCF bodies of
 // panda.xml that Genesis loads at code/scenes.py:85) -> world capsule endpoints.
-__device__ __forceinline__ void fk_capsules(const float q[NQ], const DevScene* __restrict__ sc,
-                                            Capsules& k) {
+// After each capsule is placed, v.template at<C>(k) runs; a true return stops the
+// walk (a collision found: the rest of the chain is not needed). Capsules whose
+// last use has passed are dead, so their registers are reused.
+template <class Visit>
+__device__ __forceinline__ bool fk_walk(const float q[NQ], const DevScene* __restrict__ sc, Capsules& k,
+                                        Visit& v) {
     Frame f;
     f.c0 = {1.0f, 0.0f, 0.0f};
     f.c1 = {0.0f, 1.0f, 0.0f};
     f.c2 = {0.0f, 0.0f, 1.0f};
     f.p = {sc->base[0], sc->base[1], sc->base[2]};
-    place<C_LINK0>(k, f, sc);
+    place<C_LINK0>(k, f);
+    if (v.template at<C_LINK0>(k)) return true;
     shift(f.p, 0.333f, f.c2);               // link1: pos (0,0,0.333), joint 1
     rot_z(f, q[0]);
-    place<C_LINK1>(k, f, sc);
+    place<C_LINK1>(k, f);
+    if (v.template at<C_LINK1>(k)) return true;
     rot_xm(f);                              // link2: quat (1,-1,0,0) = Rx(-90), joint 2
     rot_z(f, q[1]);
-    place<C_LINK2>(k, f, sc);
+    place<C_LINK2>(k, f);
+    if (v.template at<C_LINK2>(k)) return true;
     shift(f.p, -0.316f, f.c1);              // link3: pos (0,-0.316,0), Rx(+90), joint 3
     rot_xp(f);
     rot_z(f, q[2]);
-    place<C_LINK3>(k, f, sc);
+    place<C_LINK3>(k, f);
+    if (v.template at<C_LINK3>(k)) return true;
     shift(f.p, 0.0825f, f.c0);              // link4: pos (0.0825,0,0), Rx(+90), joint 4
     rot_xp(f);
     rot_z(f, q[3]);
-    place<C_LINK4>(k, f, sc);
+    place<C_LINK4>(k, f);
+    if (v.template at<C_LINK4>(k)) return true;
     shift(f.p, -0.0825f, f.c0);             // link5: pos (-0.0825,0.384,0), Rx(-90), joint 5
     shift(f.p, 0.384f, f.c1);
     rot_xm(f);
     rot_z(f, q[4]);
-    place<C_LINK5A>(k, f, sc);
-    place<C_LINK5B>(k, f, sc);
+    place<C_LINK5A>(k, f);
+    if (v.template at<C_LINK5A>(k)) return true;
+    place<C_LINK5B>(k, f);
+    if (v.template at<C_LINK5B>(k)) return true;
     rot_xp(f);                              // link6: Rx(+90), joint 6
     rot_z(f, q[5]);
-    place<C_LINK6>(k, f, sc);
+    place<C_LINK6>(k, f);
+    if (v.template at<C_LINK6>(k)) return true;
     shift(f.p, 0.088f, f.c0);               // link7: pos (0.088,0,0), Rx(+90), joint 7
     rot_xp(f);
     rot_z(f, q[6]);
-    place<C_LINK7>(k, f, sc);
+    place<C_LINK7>(k, f);
+    if (v.template at<C_LINK7>(k)) return true;
     shift(f.p, 0.107f, f.c2);               // hand: pos (0,0,0.107), Rz(-45deg)
     rot_sc(f, -0.70710677f, 0.70710677f);
-    place<C_HAND>(k, f, sc);
+    place<C_HAND>(k, f);
+    if (v.template at<C_HAND>(k)) return true;
     shift(f.p, 0.0584f, f.c2);              // fingers: (0,0,0.0584), prismatic +-hand y
     {
         Frame l = f;
         shift(l.p, q[7], f.c1);
-        place<C_LFINGER>(k, l, sc);
+        place<C_LFINGER>(k, l);
+        if (v.template at<C_LFINGER>(k)) return true;
         Frame r = f;
         shift(r.p, -q[8], f.c1);
         r.c0.x = -f.c0.x; r.c0.y = -f.c0.y; r.c0.z = -f.c0.z;  // Rz(180)
         r.c1.x = -f.c1.x; r.c1.y = -f.c1.y; r.c1.z = -f.c1.z;
-        place<C_RFINGER>(k, r, sc);
+        place<C_RFINGER>(k, r);
+        if (v.template at<C_RFINGER>(k)) return true;
     }
+    return false;
+}
+
+struct NoVisit {
+    template <int C>
+    __device__ __forceinline__ bool at(const Capsules&) { return false; }
+};
+
+__device__ __forceinline__ void fk_capsules(const float q[NQ], const DevScene* __restrict__ sc, Capsules& k) {
+    NoVisit v;
+    fk_walk(q, sc, k, v);
 }
 
 // Capsule AABB expanded by its radius.
@@ -288,7 +327,7 @@ __device__ __forceinline__ bool capsule_box_narrow(V3 a, V3 b, float r, const fl
 // they change no result, only how much broad-phase work a lane does.
 template <int C>
 __device__ __forceinline__ bool capsule_hits_env(const Capsules& k, const DevScene* __restrict__ sc) {
-    const float r = sc->cap[C][6];
+    constexpr float r = CAP_GEOM[C][6];
     const Aabb u = capsule_aabb(k.a[C], k.b[C], r);
     if (u.lo.z <= sc->plane_z) return true;  // capsule vs ground plane
     const int ncl = sc->n_clusters;
@@ -300,50 +339,196 @@ __device__ __forceinline__ bool capsule_hits_env(const Capsules& k, const DevSce
             const float* bx = sc->box[j];
             if ((__float_as_uint(bx[14]) >> C) & 1u) continue;
             if (aabb_disjoint(u, bx + 8, bx + 11)) continue;
+#ifndef RP_ABLATE_BOX_NARROW
             if (capsule_box_narrow(k.a[C], k.b[C], r, bx)) return true;
+#else
+            return true;
+#endif
         }
     }
     return false;
 }
 
 template <int P>
-__device__ __forceinline__ bool pair_hits(const Capsules& k, const DevScene* __restrict__ sc) {
+__device__ __forceinline__ bool pair_hits(const Capsules& k) {
     constexpr int I = PAIRS[P][0], J = PAIRS[P][1];
-    const float ri = sc->cap[I][6], rj = sc->cap[J][6];
+    constexpr float ri = CAP_GEOM[I][6], rj = CAP_GEOM[J][6];
     const Aabb u = capsule_aabb(k.a[I], k.b[I], ri);
     const Aabb v = capsule_aabb(k.a[J], k.b[J], rj);
     if (aabb_disjoint2(u, v)) return false;
-    const float rr = ri + rj;
+#ifdef RP_ABLATE_SELF_NARROW
+    return true;
+#endif
+    constexpr float rr = ri + rj;
     return segment_segment_dist2(k.a[I], k.b[I], k.a[J], k.b[J]) <= rr * rr;
 }
 
-template <int C>
-__device__ __forceinline__ bool env_from(const Capsules& k, const DevScene* __restrict__ sc) {
-    if constexpr (C == NCAP) {
-        return false;
-    } else {
-        if (capsule_hits_env<C>(k, sc)) return true;
-        return env_from<C + 1>(k, sc);
-    }
-}
-template <int P>
-__device__ __forceinline__ bool pairs_from(const Capsules& k, const DevScene* __restrict__ sc) {
+// every self pair whose second capsule is J (all first capsules precede J in the
+// chain, so the pair is complete as soon as J is placed)
+template <int J, int P = 0>
+__device__ __forceinline__ bool pairs_ending_at(const Capsules& k) {
     if constexpr (P == NPAIR) {
         return false;
     } else {
-        if (pair_hits<P>(k, sc)) return true;
-        return pairs_from<P + 1>(k, sc);
+        if constexpr (PAIRS[P][1] == J) {
+            static_assert(PAIRS[P][0] < J, "self pair out of chain order");
+            if (pair_hits<P>(k)) return true;
+        }
+        return pairs_ending_at<J, P + 1>(k);
     }
 }
 
-// true if the state collides with the plane, a (non-exempt) box, or itself.
-// The result is the OR over all tests; the order only decides how early a lane
-// stops (environment first: most random samples hit the ground or a box).
-__device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene* __restrict__ sc) {
+// ---------------------------------------------------------------------------
+// Wave-compacted narrow phases
+// ---------------------------------------------------------------------------
+// A narrow phase in SIMT code costs the whole wave whenever ANY of its 64 lanes
+// needs it: with ~35 self pairs and per-lane candidate rates of 0.1-7 %, a wave
+// ran ~11 narrow phases although a lane needs ~0.4 on average. Instead, a lane
+// whose broad phase passes appends the candidate (endpoints already in the box /
+// world frame) to a per-wave LDS queue; when the queue holds >= 64 items, or at
+// the end of the chain, the active lanes drain it together, one item per lane.
+// The set of tests and their arithmetic are unchanged, so results are identical.
+// All queue operations sit in wave-uniform control flow (ballot + mbcnt).
+constexpr int QCAP = 128;
+
+struct WaveQ {
+    float ss[QCAP][16];   // self pair: a1 b1 a2 b2 (12), (r1+r2)^2, owner lane
+    float sb[QCAP][12];   // capsule-box: pa pb (box frame) h, r^2, owner lane
+    int hit[64];          // per-lane collision found by a drained item
+};
+
+__device__ __forceinline__ int rank_in(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+struct QueueState {
+    WaveQ* Q;
+    int nss, nsb;     // wave-uniform item counts
+    int lane;
+};
+
+__device__ __forceinline__ void drain_ss(QueueState& s) {
+    const unsigned long long act = __ballot(1);
+    const int nact = __popcll(act), r = rank_in(act);
+    __builtin_amdgcn_wave_barrier();
+    for (int i = r; i < s.nss; i += nact) {
+        const float* it = s.Q->ss[i];
+        const V3 a1 = {it[0], it[1], it[2]}, b1 = {it[3], it[4], it[5]};
+        const V3 a2 = {it[6], it[7], it[8]}, b2 = {it[9], it[10], it[11]};
+        if (segment_segment_dist2(a1, b1, a2, b2) <= it[12]) s.Q->hit[__float_as_int(it[13])] = 1;
+    }
+    __builtin_amdgcn_wave_barrier();
+    s.nss = 0;
+}
+
+__device__ __forceinline__ void drain_sb(QueueState& s) {
+    const unsigned long long act = __ballot(1);
+    const int nact = __popcll(act), r = rank_in(act);
+    __builtin_amdgcn_wave_barrier();
+    for (int i = r; i < s.nsb; i += nact) {
+        const float* it = s.Q->sb[i];
+        const V3 pa = {it[0], it[1], it[2]}, pb = {it[3], it[4], it[5]}, h = {it[6], it[7], it[8]};
+        if (segment_box_dist2(pa, pb, h) <= it[9]) s.Q->hit[__float_as_int(it[10])] = 1;
+    }
+    __builtin_amdgcn_wave_barrier();
+    s.nsb = 0;
+}
+
+// capsule C vs plane (immediate) and boxes (queued)
+template <int C>
+__device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __restrict__ sc, QueueState& s) {
+    constexpr float r = CAP_GEOM[C][6];
+    const Aabb u = capsule_aabb(k.a[C], k.b[C], r);
+    if (u.lo.z <= sc->plane_z) return true;  // capsule vs ground plane
+    const int ncl = sc->n_clusters;
+    for (int cl = 0; cl < ncl; ++cl) {
+        const float* cr = sc->cluster[cl];
+        const bool near_cl = !aabb_disjoint(u, cr, cr + 4);
+        if (!__any(near_cl)) continue;
+        const int j0 = __float_as_int(cr[3]), nj = __float_as_int(cr[7]);
+        for (int j = j0; j < j0 + nj; ++j) {
+            const float* bx = sc->box[j];
+            const bool cand = near_cl && !((__float_as_uint(bx[14]) >> C) & 1u) && !aabb_disjoint(u, bx + 8, bx + 11);
+            const unsigned long long m = __ballot(cand);
+            if (!m) continue;
+            if (cand) {
+                float* it = s.Q->sb[s.nsb + rank_in(m)];
+                const float cs = bx[6], sn = bx[7];
+                float dx = k.a[C].x - bx[0], dy = k.a[C].y - bx[1];
+                it[0] = fma_(cs, dx, sn * dy); it[1] = fma_(cs, dy, -(sn * dx)); it[2] = k.a[C].z - bx[2];
+                dx = k.b[C].x - bx[0]; dy = k.b[C].y - bx[1];
+                it[3] = fma_(cs, dx, sn * dy); it[4] = fma_(cs, dy, -(sn * dx)); it[5] = k.b[C].z - bx[2];
+                it[6] = bx[3]; it[7] = bx[4]; it[8] = bx[5];
+                it[9] = r * r;
+                it[10] = __int_as_float(s.lane);
+            }
+            s.nsb += __popcll(m);
+            if (s.nsb > QCAP - 64) drain_sb(s);
+        }
+    }
+    return false;
+}
+
+template <int P>
+__device__ __forceinline__ void pair_queued(const Capsules& k, QueueState& s) {
+    constexpr int I = PAIRS[P][0], J = PAIRS[P][1];
+    constexpr float ri = CAP_GEOM[I][6], rj = CAP_GEOM[J][6];
+    constexpr float rr = ri + rj;
+    const Aabb u = capsule_aabb(k.a[I], k.b[I], ri);
+    const Aabb v = capsule_aabb(k.a[J], k.b[J], rj);
+    const bool cand = !aabb_disjoint2(u, v);
+    const unsigned long long m = __ballot(cand);
+    if (!m) return;
+    if (cand) {
+        float* it = s.Q->ss[s.nss + rank_in(m)];
+        it[0] = k.a[I].x; it[1] = k.a[I].y; it[2] = k.a[I].z;
+        it[3] = k.b[I].x; it[4] = k.b[I].y; it[5] = k.b[I].z;
+        it[6] = k.a[J].x; it[7] = k.a[J].y; it[8] = k.a[J].z;
+        it[9] = k.b[J].x; it[10] = k.b[J].y; it[11] = k.b[J].z;
+        it[12] = rr * rr;
+        it[13] = __int_as_float(s.lane);
+    }
+    s.nss += __popcll(m);
+    if (s.nss > QCAP - 64) drain_ss(s);
+}
+
+template <int J, int P = 0>
+__device__ __forceinline__ void pairs_queued(const Capsules& k, QueueState& s) {
+    if constexpr (P < NPAIR) {
+        if constexpr (PAIRS[P][1] == J) {
+            static_assert(PAIRS[P][0] < J, "self pair out of chain order");
+            pair_queued<P>(k, s);
+        }
+        pairs_queued<J, P + 1>(k, s);
+    }
+}
+
+struct QueuedVisit {
+    const DevScene* __restrict__ sc;
+    QueueState s;
+    template <int C>
+    __device__ __forceinline__ bool at(const Capsules& k) {
+        if (env_queued<C>(k, sc, s)) return true;
+#ifndef RP_ABLATE_SELF
+        pairs_queued<C>(k, s);
+#endif
+        return false;
+    }
+};
+
+// true if the state collides with the plane, a (non-exempt) box, or itself: the OR
+// over every test. Plane tests decide at once (a colliding lane stops walking);
+// box and self narrow phases are queued and drained wave-compacted. Every lane of
+// the wave that is still running must call this at the same point.
+__device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene* __restrict__ sc, WaveQ& Q) {
     Capsules k;
-    fk_capsules(q, sc, k);
-    if (env_from<0>(k, sc)) return true;
-    return pairs_from<0>(k, sc);
+    QueuedVisit v{sc, QueueState{&Q, 0, 0, (int)__lane_id()}};
+    Q.hit[v.s.lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    if (fk_walk(q, sc, k, v)) return true;
+    if (__any(v.s.nsb > 0)) drain_sb(v.s);
+    if (__any(v.s.nss > 0)) drain_ss(v.s);
+    return Q.hit[v.s.lane] != 0;
 }
 
 }  // namespace rp

@@ -35,6 +35,24 @@ constexpr int PAIRS[NPAIR][2] = {
     {C_LINK5B, C_HAND}, {C_LINK5B, C_LFINGER}, {C_LINK5B, C_RFINGER},
 };
 
+// Capsule geometry (spec/franka_capsules.json): a(3), b(3), radius, in the link
+// frame. Compiled into the kernels (zero terms of the link->world transform fold
+// away, no scalar loads); rp_create rejects a descriptor with other numbers.
+constexpr float CAP_GEOM[NCAP][7] = {
+    {-0.09f, 0.0f, 0.06f, -0.06f, 0.0f, 0.06f, 0.06f},       // link0
+    {0.0f, 0.0f, -0.193f, 0.0f, 0.0f, -0.05f, 0.06f},        // link1
+    {0.0f, 0.0f, -0.06f, 0.0f, 0.0f, 0.06f, 0.06f},          // link2
+    {0.0f, 0.0f, -0.22f, 0.0f, 0.0f, -0.07f, 0.06f},         // link3
+    {0.0f, 0.0f, -0.06f, 0.0f, 0.0f, 0.06f, 0.06f},          // link4
+    {0.0f, 0.0f, -0.31f, 0.0f, 0.0f, -0.21f, 0.06f},         // link5a
+    {0.0f, 0.08f, -0.20f, 0.0f, 0.08f, -0.06f, 0.025f},      // link5b
+    {0.0f, 0.0f, -0.07f, 0.0f, 0.0f, 0.01f, 0.05f},          // link6
+    {0.0f, 0.0f, -0.06f, 0.0f, 0.0f, 0.08f, 0.04f},          // link7
+    {0.0f, -0.05f, 0.04f, 0.0f, 0.05f, 0.04f, 0.04f},        // hand
+    {0.0f, 0.012f, 0.012f, 0.0f, 0.012f, 0.040f, 0.010f},    // left finger
+    {0.0f, 0.012f, 0.012f, 0.0f, 0.012f, 0.040f, 0.010f},    // right finger
+};
+
 constexpr int MAX_BOXES = 64;
 constexpr int CLUSTER = 8;                       // boxes per broad-phase cluster
 constexpr int MAX_CLUSTERS = MAX_BOXES / CLUSTER;
@@ -47,7 +65,6 @@ constexpr int MAX_CLUSTERS = MAX_BOXES / CLUSTER;
 // Cluster record: [0..2] AABB lo, [4..6] AABB hi (union of its boxes' AABBs),
 //   [3] first box, [7] box count (as int bits).
 struct DevScene {
-    float cap[NCAP][8];          // ax ay az bx by bz radius pad (link frame)
     float box[MAX_BOXES][16];
     float cluster[MAX_CLUSTERS][8];
     float base[4];               // robot base translation (scenes.py:29-34), pad

@@ -1,0 +1,12 @@
+#!/bin/bash
+# build librbe variants into build/variants/ : name:flags pairs
+set -e
+cd "$(dirname "$0")/.."
+mkdir -p build/variants
+for spec in "$@"; do
+  name=${spec%%:*}; flags=${spec#*:}
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math $flags \
+    -o build/variants/lib_$name.so rbe550_final_project_amd/csrc/rp_lib.hip &
+done
+wait
+ls build/variants

@@ -28,6 +28,7 @@ constexpr int NNTILE = 256;     // tree nodes per LDS tile (256 x 72 B = 18 KiB)
 // One lane per state; one wave per workgroup, whose LDS holds the wave's
 // narrow-phase queue (rp_math.h WaveQ). The scene record is read with wave-uniform
 // scalar loads (measured faster than staging it in LDS: 10.74 vs 10.52 G states/s).
+template <int NCL>
 __global__ __launch_bounds__(VBLOCK, RP_VALIDITY_WAVES) void k_validity(const float* __restrict__ q, int64_t n,
                                                                        uint8_t* __restrict__ flags,
                                                                        const DevScene* __restrict__ sc) {
@@ -37,7 +38,7 @@ __global__ __launch_bounds__(VBLOCK, RP_VALIDITY_WAVES) void k_validity(const fl
     float qq[NQ];
 #pragma unroll
     for (int k = 0; k < NQ; ++k) qq[k] = q[i * NQ + k];
-    flags[i] = state_collides(qq, sc, wq) ? 0 : 1;
+    flags[i] = state_collides<NCL>(qq, sc, wq) ? 0 : 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -49,6 +50,7 @@ __global__ __launch_bounds__(VBLOCK, RP_VALIDITY_WAVES) void k_validity(const fl
 // slot clears it. Optional prefix groups (connect chains): edges are grouped
 // `group` at a time; gfail[g] = first failing edge index within the group, and
 // slots of later edges of that group are skipped.
+template <int NCL>
 __global__ __launch_bounds__(VBLOCK, RP_VALIDITY_WAVES) void k_edges(const double* __restrict__ from,
                                                   const double* __restrict__ to,
                                                   const int* __restrict__ nd, int64_t n_edges,
@@ -86,7 +88,7 @@ __global__ __launch_bounds__(VBLOCK, RP_VALIDITY_WAVES) void k_edges(const doubl
     float qq[NQ];
 #pragma unroll
     for (int k = 0; k < NQ; ++k) qq[k] = (float)st[k];
-    if (state_collides(qq, sc, wq)) {
+    if (state_collides<NCL>(qq, sc, wq)) {
         valid[e] = 0;
         if (gfail) {
             const int g = (int)(e / group), s = (int)(e - (int64_t)g * group);

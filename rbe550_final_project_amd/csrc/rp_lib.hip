@@ -141,9 +141,19 @@ namespace {
 // launch helpers
 // ---------------------------------------------------------------------------
 
+// kernel instantiation for a cluster count (the cluster AABBs live in registers)
+int ncl_bucket(int n) { return n <= 0 ? 0 : n == 1 ? 1 : n == 2 ? 2 : n <= 4 ? 4 : 8; }
+
 void launch_validity(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, hipStream_t s) {
     if (n <= 0) return;
-    hipLaunchKernelGGL(k_validity, dim3(blocks_for(n, VBLOCK)), dim3(VBLOCK), 0, s, q, n, flags, c->d_scene);
+    const dim3 g(blocks_for(n, VBLOCK)), b(VBLOCK);
+    switch (ncl_bucket(c->scene.n_clusters)) {
+        case 0: hipLaunchKernelGGL(k_validity<0>, g, b, 0, s, q, n, flags, c->d_scene); break;
+        case 1: hipLaunchKernelGGL(k_validity<1>, g, b, 0, s, q, n, flags, c->d_scene); break;
+        case 2: hipLaunchKernelGGL(k_validity<2>, g, b, 0, s, q, n, flags, c->d_scene); break;
+        case 4: hipLaunchKernelGGL(k_validity<4>, g, b, 0, s, q, n, flags, c->d_scene); break;
+        default: hipLaunchKernelGGL(k_validity<8>, g, b, 0, s, q, n, flags, c->d_scene); break;
+    }
     HIP_TRY(hipGetLastError());
 }
 
@@ -151,8 +161,17 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
                   int mode, uint8_t* valid, int group, int* gfail, hipStream_t s) {
     if (n <= 0) return;
     const int64_t threads = n * (int64_t)kmax;
-    hipLaunchKernelGGL(k_edges, dim3(blocks_for(threads, VBLOCK)), dim3(VBLOCK), 0, s, from, to, nd, n, kmax, mode,
-                       valid, group, gfail, c->counter.p, c->d_scene);
+    const dim3 g(blocks_for(threads, VBLOCK)), b(VBLOCK);
+#define RP_EDGES(N) hipLaunchKernelGGL(k_edges<N>, g, b, 0, s, from, to, nd, n, kmax, mode, valid, group, gfail, \
+                                       c->counter.p, c->d_scene)
+    switch (ncl_bucket(c->scene.n_clusters)) {
+        case 0: RP_EDGES(0); break;
+        case 1: RP_EDGES(1); break;
+        case 2: RP_EDGES(2); break;
+        case 4: RP_EDGES(4); break;
+        default: RP_EDGES(8); break;
+    }
+#undef RP_EDGES
     HIP_TRY(hipGetLastError());
 }
 
@@ -750,6 +769,13 @@ int rp_set_scene(rp_ctx* c, const rp_box* boxes, int32_t n, float plane_z, const
         c->slot_of[order[s]] = s;
     }
     c->scene.n_clusters = (int)groups.size();
+    for (int g = (int)groups.size(); g < MAX_CLUSTERS; ++g) {  // empty: no capsule overlaps it
+        float* cr = c->scene.cluster[g];
+        for (int k = 0; k < 3; ++k) { cr[k] = INFINITY; cr[4 + k] = -INFINITY; }
+        const int32_t zero = 0;
+        std::memcpy(&cr[3], &zero, 4);
+        std::memcpy(&cr[7], &zero, 4);
+    }
     for (size_t g = 0; g < groups.size(); ++g) {
         float* cr = c->scene.cluster[g];
         for (int k = 0; k < 3; ++k) { cr[k] = 1e30f; cr[4 + k] = -1e30f; }

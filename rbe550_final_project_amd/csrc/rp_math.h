@@ -389,25 +389,58 @@ __device__ __forceinline__ bool pairs_ending_at(const Capsules& k) {
 // the end of the chain, the active lanes drain it together, one item per lane.
 // The set of tests and their arithmetic are unchanged, so results are identical.
 // All queue operations sit in wave-uniform control flow (ballot + mbcnt).
-constexpr int QCAP = 128;
+#ifndef RP_QCAP
+#define RP_QCAP 96
+#endif
+constexpr int QCAP = RP_QCAP;   // items per queue; drained once more than QCAP-64 are pending
 
 struct WaveQ {
-    float ss[QCAP][16];   // self pair: a1 b1 a2 b2 (12), (r1+r2)^2, owner lane
-    float sb[QCAP][12];   // capsule-box: pa pb (box frame) h, r^2, owner lane
+    float ss[QCAP][13];   // self pair: a1 b1 a2 b2 (12), owner lane | pair << 8
+    float sb[QCAP][11];   // capsule-box: pa pb (box frame) h (9), r^2, owner lane
     int hit[64];          // per-lane collision found by a drained item
 };
+
+// radii of each self pair: r_i, r_j (read by pair id when a queue item is drained)
+struct PairRadii { float r[NPAIR][2]; };
+constexpr PairRadii make_pair_radii() {
+    PairRadii t{};
+    for (int p = 0; p < NPAIR; ++p) {
+        t.r[p][0] = CAP_GEOM[PAIRS[p][0]][6];
+        t.r[p][1] = CAP_GEOM[PAIRS[p][1]][6];
+    }
+    return t;
+}
+__device__ constexpr PairRadii PAIR_RADII = make_pair_radii();
 
 __device__ __forceinline__ int rank_in(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// Cluster AABBs of the scene, hoisted into (scalar) registers once per state: the
+// kernels are instantiated for NCL = 0, 1, 2, 4, 8 clusters; unused slots hold an
+// empty box (lo = +inf) that no capsule overlaps.
+template <int NCL>
+struct ClusterRegs {
+    float c[NCL > 0 ? NCL : 1][8];
+    __device__ __forceinline__ void load(const DevScene* __restrict__ sc) {
+#pragma unroll
+        for (int i = 0; i < NCL; ++i)
+#pragma unroll
+            for (int w = 0; w < 8; ++w) c[i][w] = sc->cluster[i][w];
+    }
+};
+
+template <int NCL>
 struct QueueState {
     WaveQ* Q;
     int nss, nsb;     // wave-uniform item counts
     int lane;
+    float plane_z;
+    ClusterRegs<NCL> cl;
 };
 
-__device__ __forceinline__ void drain_ss(QueueState& s) {
+template <class S>
+__device__ __forceinline__ void drain_ss(S& s) {
     const unsigned long long act = __ballot(1);
     const int nact = __popcll(act), r = rank_in(act);
     __builtin_amdgcn_wave_barrier();
@@ -415,13 +448,22 @@ __device__ __forceinline__ void drain_ss(QueueState& s) {
         const float* it = s.Q->ss[i];
         const V3 a1 = {it[0], it[1], it[2]}, b1 = {it[3], it[4], it[5]};
         const V3 a2 = {it[6], it[7], it[8]}, b2 = {it[9], it[10], it[11]};
-        if (segment_segment_dist2(a1, b1, a2, b2) <= it[12]) s.Q->hit[__float_as_int(it[13])] = 1;
+        const int tag = __float_as_int(it[12]);
+        const int p = tag >> 8;
+        const float ri = PAIR_RADII.r[p][0], rj = PAIR_RADII.r[p][1];
+        // the oracle's exact decision: AABB reject, then segment distance
+        const Aabb u = capsule_aabb(a1, b1, ri);
+        const Aabb v = capsule_aabb(a2, b2, rj);
+        if (aabb_disjoint2(u, v)) continue;
+        const float rr = ri + rj;
+        if (segment_segment_dist2(a1, b1, a2, b2) <= rr * rr) s.Q->hit[tag & 63] = 1;
     }
     __builtin_amdgcn_wave_barrier();
     s.nss = 0;
 }
 
-__device__ __forceinline__ void drain_sb(QueueState& s) {
+template <class S>
+__device__ __forceinline__ void drain_sb(S& s) {
     const unsigned long long act = __ballot(1);
     const int nact = __popcll(act), r = rank_in(act);
     __builtin_amdgcn_wave_barrier();
@@ -435,14 +477,15 @@ __device__ __forceinline__ void drain_sb(QueueState& s) {
 }
 
 // capsule C vs plane (immediate) and boxes (queued)
-template <int C>
-__device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __restrict__ sc, QueueState& s) {
+template <int C, int NCL>
+__device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __restrict__ sc,
+                                           QueueState<NCL>& s) {
     constexpr float r = CAP_GEOM[C][6];
     const Aabb u = capsule_aabb(k.a[C], k.b[C], r);
-    if (u.lo.z <= sc->plane_z) return true;  // capsule vs ground plane
-    const int ncl = sc->n_clusters;
-    for (int cl = 0; cl < ncl; ++cl) {
-        const float* cr = sc->cluster[cl];
+    if (u.lo.z <= s.plane_z) return true;  // capsule vs ground plane
+#pragma unroll
+    for (int cl = 0; cl < NCL; ++cl) {
+        const float* cr = s.cl.c[cl];
         const bool near_cl = !aabb_disjoint(u, cr, cr + 4);
         if (!__any(near_cl)) continue;
         const int j0 = __float_as_int(cr[3]), nj = __float_as_int(cr[7]);
@@ -469,14 +512,32 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
     return false;
 }
 
-template <int P>
-__device__ __forceinline__ void pair_queued(const Capsules& k, QueueState& s) {
+// Bounding-sphere radius of capsule C: radius + half its length + 1e-4 m. The
+// margin dwarfs float rounding (~1e-7 m here), so two disjoint spheres prove the
+// capsules are farther apart than any rounding could hide: the prefilter can never
+// drop a pair that the exact test (AABB + narrow phase, as in the oracle) would
+// report, i.e. it changes no result.
+constexpr double csqrt(double x) {
+    double r = x > 1.0 ? x : 1.0;
+    for (int i = 0; i < 64; ++i) r = 0.5 * (r + x / r);
+    return r;
+}
+template <int C>
+constexpr float sphere_radius() {
+    constexpr double dx = (double)CAP_GEOM[C][3] - CAP_GEOM[C][0];
+    constexpr double dy = (double)CAP_GEOM[C][4] - CAP_GEOM[C][1];
+    constexpr double dz = (double)CAP_GEOM[C][5] - CAP_GEOM[C][2];
+    return (float)((double)CAP_GEOM[C][6] + 0.5 * csqrt(dx * dx + dy * dy + dz * dz) + 1e-4);
+}
+
+template <int P, class S>
+__device__ __forceinline__ void pair_queued(const Capsules& k, S& s) {
     constexpr int I = PAIRS[P][0], J = PAIRS[P][1];
-    constexpr float ri = CAP_GEOM[I][6], rj = CAP_GEOM[J][6];
-    constexpr float rr = ri + rj;
-    const Aabb u = capsule_aabb(k.a[I], k.b[I], ri);
-    const Aabb v = capsule_aabb(k.a[J], k.b[J], rj);
-    const bool cand = !aabb_disjoint2(u, v);
+    constexpr float RS = sphere_radius<I>() + sphere_radius<J>();
+    const V3 d = {(k.a[I].x + k.b[I].x) - (k.a[J].x + k.b[J].x), (k.a[I].y + k.b[I].y) - (k.a[J].y + k.b[J].y),
+                  (k.a[I].z + k.b[I].z) - (k.a[J].z + k.b[J].z)};
+    // |centre_I - centre_J| <= RS  <=>  |2 centre_I - 2 centre_J|^2 <= (2 RS)^2
+    const bool cand = dot3(d, d) <= (2.0f * RS) * (2.0f * RS);
     const unsigned long long m = __ballot(cand);
     if (!m) return;
     if (cand) {
@@ -485,15 +546,14 @@ __device__ __forceinline__ void pair_queued(const Capsules& k, QueueState& s) {
         it[3] = k.b[I].x; it[4] = k.b[I].y; it[5] = k.b[I].z;
         it[6] = k.a[J].x; it[7] = k.a[J].y; it[8] = k.a[J].z;
         it[9] = k.b[J].x; it[10] = k.b[J].y; it[11] = k.b[J].z;
-        it[12] = rr * rr;
-        it[13] = __int_as_float(s.lane);
+        it[12] = __int_as_float(s.lane | (P << 8));
     }
     s.nss += __popcll(m);
     if (s.nss > QCAP - 64) drain_ss(s);
 }
 
-template <int J, int P = 0>
-__device__ __forceinline__ void pairs_queued(const Capsules& k, QueueState& s) {
+template <int J, int P = 0, class S>
+__device__ __forceinline__ void pairs_queued(const Capsules& k, S& s) {
     if constexpr (P < NPAIR) {
         if constexpr (PAIRS[P][1] == J) {
             static_assert(PAIRS[P][0] < J, "self pair out of chain order");
@@ -503,9 +563,10 @@ __device__ __forceinline__ void pairs_queued(const Capsules& k, QueueState& s) {
     }
 }
 
+template <int NCL>
 struct QueuedVisit {
     const DevScene* __restrict__ sc;
-    QueueState s;
+    QueueState<NCL> s;
     template <int C>
     __device__ __forceinline__ bool at(const Capsules& k) {
         if (env_queued<C>(k, sc, s)) return true;
@@ -519,10 +580,19 @@ struct QueuedVisit {
 // true if the state collides with the plane, a (non-exempt) box, or itself: the OR
 // over every test. Plane tests decide at once (a colliding lane stops walking);
 // box and self narrow phases are queued and drained wave-compacted. Every lane of
-// the wave that is still running must call this at the same point.
+// the wave that is still running must call this at the same point. NCL >= the
+// scene's cluster count (rp_lib.hip picks the instantiation).
+template <int NCL>
 __device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene* __restrict__ sc, WaveQ& Q) {
     Capsules k;
-    QueuedVisit v{sc, QueueState{&Q, 0, 0, (int)__lane_id()}};
+    QueuedVisit<NCL> v;
+    v.sc = sc;
+    v.s.Q = &Q;
+    v.s.nss = 0;
+    v.s.nsb = 0;
+    v.s.lane = (int)__lane_id();
+    v.s.plane_z = sc->plane_z;
+    v.s.cl.load(sc);
     Q.hit[v.s.lane] = 0;
     __builtin_amdgcn_wave_barrier();
     if (fk_walk(q, sc, k, v)) return true;

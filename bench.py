@@ -222,7 +222,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            sample = 1 << 23
+            sample = 1 << 25
             rate, dt = cpu_baseline(scene, sample, threads)
             ptimes = cpu_plan_baseline(wl, 0)
             cpu = {"value": round(rate, 1), "unit": "states/s", "cores": threads, "kind": "port",

@@ -1,0 +1,82 @@
+"""GPU test of the rank-group path of rp_plan (C++ sharding + exchange) on ONE GPU:
+two contexts (rank 0 and 1 of world 2) planned from two host threads, with an
+all-gather over device buffers done by torch copies. The plan must equal the
+world-1 plan and the CPU oracle (SURVEY.md §8(e) acceptance: result independent of
+world size). The RCCL transport itself is exercised by bench.py at N > 1."""
+import json
+import os
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from rbe550_final_project_amd import _abi, model, scenes
+from rbe550_final_project_amd.native import Context
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+class ThreadGroup:
+    """world ranks in one process; all-gather = barrier + torch.cat on the GPU."""
+
+    def __init__(self, world, cap):
+        self.world = world
+        self.cap = cap
+        self.send = [torch.zeros(cap, dtype=torch.uint8, device="cuda") for _ in range(world)]
+        self.recv = [torch.zeros(cap * world, dtype=torch.uint8, device="cuda") for _ in range(world)]
+        self.bar = threading.Barrier(world)
+        self.calls = 0
+
+    def fn(self, rank):
+        def allgather(nbytes):
+            self.bar.wait()
+            if rank == 0:
+                self.calls += 1
+                cat = torch.cat([s[:nbytes] for s in self.send])
+                for r in self.recv:
+                    r[: nbytes * self.world].copy_(cat)
+                torch.cuda.synchronize()
+            self.bar.wait()
+        return allgather
+
+
+@pytest.mark.parametrize("wl,qi,batch", [("goal4_pentagon_10box", 2, 64), ("goal3_tallest_10box", 5, 256),
+                                         ("clutter64", 0, 128)])
+def test_two_rank_plan_equals_single(oracle_lib, wl, qi, batch):
+    q = json.load(open(os.path.join(GOLD, "workloads", wl + ".json")))["queries"][qi]
+    sc = scenes.Scene.from_json(q["scene"])
+    p = _abi.make_params(seed=13, batch=batch, n_waypoints=150, timeout_s=60)
+    world = 2
+    g = ThreadGroup(world, 8 * (batch // world + 4))
+    ctxs = []
+    for r in range(world):
+        c = Context(device=0, robot=model.robot_desc())
+        c.set_scene(sc.boxes, sc.plane_z, sc.base)
+        c.set_attached(q["attached"])
+        c.group_init(r, world, g.send[r].data_ptr(), g.recv[r].data_ptr(), g.cap, g.fn(r))
+        ctxs.append(c)
+    out = [None] * world
+
+    def run(r):
+        out[r] = ctxs[r].plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    [t.start() for t in th]
+    [t.join(timeout=300) for t in th]
+    assert all(o is not None for o in out), "a rank did not finish"
+    single = Context(device=0, robot=model.robot_desc())
+    single.set_scene(sc.boxes, sc.plane_z, sc.base)
+    single.set_attached(q["attached"])
+    ref, st = single.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+    o = oracle_lib.OracleScene()
+    o.set_scene(sc.boxes, sc.plane_z, sc.base)
+    o.set_attached(q["attached"])
+    ref_cpu, st_cpu, _ = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+    assert g.calls >= 2
+    for path, status in out:
+        assert status == st == st_cpu == _abi.STATUS_EXACT
+        assert np.array_equal(path, ref) and np.array_equal(path, ref_cpu)
+    for c in ctxs + [single]:
+        c.close()

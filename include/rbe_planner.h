@@ -102,7 +102,10 @@ typedef struct rp_box {
 /* rp_plan parameters. Zero / negative fields take the default shown. */
 typedef struct rp_plan_params {
     uint64_t seed;          /* Philox key; the reference is unseeded (scenes.py:9)          */
-    int64_t batch;          /* samples per RRT-Connect iteration (global over ranks), 4096  */
+    int64_t batch;          /* max samples per RRT-Connect iteration (global), 4096         */
+    int64_t batch_min;      /* samples in iteration 0; iteration k draws
+                               min(batch, batch_min << k). Default min(batch, 256); easy
+                               queries solve in the first, cheap iterations              */
     double range;           /* steering distance, default 0.2 * maxExtent (OMPL RRTConnect) */
     double resolution;      /* edge resolution, default 0.01 * maxExtent (OMPL default)     */
     double timeout_s;       /* wall-clock budget of the solve, default 5.0 (planning.py:63) */

@@ -674,6 +674,12 @@ int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], co
     if (p.max_iters <= 0) p.max_iters = INT64_MAX;
     if (p.tree_capacity <= 0) p.tree_capacity = 1 << 22;
     if (p.batch % world) return RP_ERR_ARG;
+    /* batch schedule: iteration k draws min(batch, batch_min << k) samples; the
+     * global sample counter keeps running, so the schedule is part of the
+     * algorithm's definition (same on every rank and on the GPU) */
+    if (p.batch_min <= 0) p.batch_min = p.batch < 256 ? p.batch : 256;
+    if (p.batch_min > p.batch) p.batch_min = p.batch;
+    p.batch_min = ((p.batch_min + world - 1) / world) * world;
     const int cmax = (int)ceil(max_extent / p.range) + 1;
 
     /* PlannerInputStates: invalid start / goal are skipped -> status */
@@ -696,14 +702,15 @@ int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], co
     tree_add(&T[0], start, -1);
     tree_add(&T[1], goal, -1);
 
-    const int64_t B = p.batch;
-    const int64_t per = B / world;
-    int32_t* res = (int32_t*)malloc(sizeof(int32_t) * B);
-    int32_t* mine = (int32_t*)malloc(sizeof(int32_t) * (per + 1));
-    int32_t* rbuf = (int32_t*)malloc(sizeof(int32_t) * (per + 1) * world);
-    int64_t* tnode = (int64_t*)malloc(sizeof(int64_t) * B);
-    int32_t* trec = (int32_t*)malloc(sizeof(int32_t) * 2 * (B + world));
-    int32_t* tmine = (int32_t*)malloc(sizeof(int32_t) * 2 * (B + world));
+    const int64_t BMAX = p.batch;
+    int64_t B = p.batch_min;
+    uint64_t gbase = 0;
+    int32_t* res = (int32_t*)malloc(sizeof(int32_t) * BMAX);
+    int32_t* mine = (int32_t*)malloc(sizeof(int32_t) * (BMAX / world + 1));
+    int32_t* rbuf = (int32_t*)malloc(sizeof(int32_t) * (BMAX / world + 1) * world);
+    int64_t* tnode = (int64_t*)malloc(sizeof(int64_t) * BMAX);
+    int32_t* trec = (int32_t*)malloc(sizeof(int32_t) * 2 * (BMAX + world));
+    int32_t* tmine = (int32_t*)malloc(sizeof(int32_t) * 2 * (BMAX + world));
     double (*chain)[NQ] = (double(*)[NQ])malloc(sizeof(double) * NQ * cmax);
 
     int solved = 0;
@@ -720,7 +727,8 @@ int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], co
         tree_t* Bt = a_start ? &T[1] : &T[0];
         if (A->n + B > A->cap || Bt->n + B * cmax > Bt->cap) break;
         const int64_t TA = A->n, TB = Bt->n;
-        const uint64_t g0 = (uint64_t)iter * (uint64_t)B;
+        const uint64_t g0 = gbase;
+        const int64_t per = B / world;
         /* extension: my slice of the batch */
         for (int64_t k = 0; k < per; ++k) {
             const int64_t i = rank * per + k;
@@ -811,6 +819,8 @@ int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], co
             }
             if (!reached && a_start) A->cand[tnode[t]] = 1;
         }
+        gbase += (uint64_t)B;
+        B = 2 * B < BMAX ? 2 * B : BMAX;
         if (solved) { ++iter; break; }
     }
     st.iterations = iter;

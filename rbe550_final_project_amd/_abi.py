@@ -34,7 +34,7 @@ class Box(C.Structure):
 
 
 class PlanParams(C.Structure):
-    _fields_ = [("seed", C.c_uint64), ("batch", C.c_int64), ("range", C.c_double),
+    _fields_ = [("seed", C.c_uint64), ("batch", C.c_int64), ("batch_min", C.c_int64), ("range", C.c_double),
                 ("resolution", C.c_double), ("timeout_s", C.c_double), ("max_iters", C.c_int64),
                 ("n_waypoints", C.c_int32), ("simplify", C.c_int32), ("tree_capacity", C.c_int64)]
 
@@ -61,11 +61,12 @@ def make_boxes(boxes):
     return arr, len(boxes)
 
 
-def make_params(seed=0, batch=4096, range_=0.0, resolution=0.0, timeout_s=5.0, max_iters=0,
+def make_params(seed=0, batch=4096, range_=0.0, resolution=0.0, timeout_s=5.0, max_iters=0, batch_min=0,
                 n_waypoints=100, simplify=True, tree_capacity=0):
     p = PlanParams()
     p.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     p.batch = int(batch)
+    p.batch_min = int(batch_min)
     p.range = float(range_)
     p.resolution = float(resolution)
     p.timeout_s = float(timeout_s)

@@ -56,8 +56,12 @@ __global__ __launch_bounds__(VBLOCK, RP_VALIDITY_WAVES) void k_edges(const doubl
                                                   const int* __restrict__ nd, int64_t n_edges,
                                                   int kmax, int mode, uint8_t* valid, int group,
                                                   int* gfail, unsigned long long* counter,
-                                                  const DevScene* __restrict__ sc) {
+                                                  const DevScene* __restrict__ sc,
+                                                  const int* __restrict__ dcount, int per_item) {
     __shared__ WaveQ wq;
+    // device-side edge count (planner iterations: dcount = accepted targets)
+    if (dcount) n_edges = min(n_edges, (int64_t)dcount[0] * per_item);
+    if ((int64_t)blockIdx.x * VBLOCK >= n_edges * kmax) return;
     const int64_t idx = (int64_t)blockIdx.x * VBLOCK + threadIdx.x;
     const int64_t e = idx / kmax;
     const int slot = (int)(idx - e * kmax);
@@ -172,6 +176,16 @@ __global__ void k_ext_result(const uint8_t* __restrict__ valid, const int32_t* _
     if (k < n) res[k] = valid[k] ? near[k] : -1;
 }
 
+// world == 1: res[k] and its accept flag in one pass
+__global__ void k_ext_result_flag(const uint8_t* __restrict__ valid, const int32_t* __restrict__ near, int64_t n,
+                                  int32_t* __restrict__ res, int32_t* __restrict__ acc) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const int32_t v = valid[k] ? near[k] : -1;
+    res[k] = v;
+    acc[k] = v >= 0 ? 1 : 0;
+}
+
 // unpack the gathered extension records (rank-major, `per`+1 int32 per rank)
 __global__ void k_ext_unpack(const int32_t* __restrict__ rbuf, int64_t per, int world,
                              int32_t* __restrict__ res, int* any_flag) {
@@ -189,11 +203,20 @@ __global__ void k_flag(const int32_t* __restrict__ v, int64_t n, int32_t* __rest
 }
 
 // append accepted extension nodes at TA + exclusive_scan position
+// Iteration status record (device): [0] accepted extension nodes, [1] nodes added
+// to the other tree, [2] first REACHED target (INT_MAX: none), [3] start-side and
+// [4] goal-side join nodes of the solution.
+enum { ST_NACC = 0, ST_ADDED = 1, ST_FIRST = 2, ST_SNODE = 3, ST_GNODE = 4, ST_WORDS = 8 };
+
 __global__ void k_ext_append(const int32_t* __restrict__ res, const int32_t* __restrict__ incl, int64_t B,
                              uint64_t seed, uint64_t g0, Bounds bd, double range, double* A, int32_t* Apar,
-                             uint8_t* Acand, int64_t TA) {
+                             uint8_t* Acand, int64_t TA, int* status) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= B) return;
+    if (status && i == B - 1) {
+        status[ST_NACC] = incl[B - 1];
+        status[ST_FIRST] = 0x7fffffff;
+    }
     const int32_t nn = res[i];
     if (nn < 0) return;
     const int64_t pos = TA + incl[i] - 1;
@@ -216,8 +239,10 @@ __global__ __launch_bounds__(NNBLOCK) void k_conn_nn(const double* __restrict__ 
                                                      double* __restrict__ efrom, double* __restrict__ eto,
                                                      int* __restrict__ nd, uint8_t* __restrict__ valid,
                                                      int* __restrict__ gfail, int32_t* __restrict__ yout,
-                                                     int32_t* __restrict__ mout) {
+                                                     int32_t* __restrict__ mout, const int* __restrict__ status) {
     __shared__ double tile[NNTILE * NQ];
+    if (status) n = min(n, (int64_t)status[ST_NACC] - t0);
+    if ((int64_t)blockIdx.x * NNBLOCK >= n) return;   // whole block idle (uniform)
     const int64_t k = (int64_t)blockIdx.x * NNBLOCK + threadIdx.x;
     const bool active = k < n;
     double x[NQ];
@@ -270,6 +295,22 @@ __global__ void k_conn_record(const int32_t* __restrict__ y, const int32_t* __re
     }
 }
 
+// world == 1: record and L in one pass over the batch bound B (L = 0 past nacc)
+__global__ void k_conn_record_len(const int32_t* __restrict__ y, const int32_t* __restrict__ m,
+                                  const int* __restrict__ gfail, const int* __restrict__ status, int64_t B,
+                                  int32_t* __restrict__ rec, int32_t* __restrict__ L) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= B) return;
+    if (k < status[ST_NACC]) {
+        const int l = gfail[k] < m[k] ? gfail[k] : m[k];
+        rec[2 * k] = y[k];
+        rec[2 * k + 1] = l;
+        L[k] = l;
+    } else {
+        L[k] = 0;
+    }
+}
+
 __global__ void k_conn_len(const int32_t* __restrict__ rec, int64_t n, int32_t* __restrict__ L) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t < n) L[t] = rec[2 * t + 1];
@@ -280,8 +321,9 @@ __global__ void k_conn_len(const int32_t* __restrict__ rec, int64_t n, int32_t* 
 __global__ void k_conn_append(const int32_t* __restrict__ rec, const int32_t* __restrict__ incl, int64_t n,
                               const double* A, int64_t TA0, double* Bt, int32_t* Bpar, uint8_t* Bcand,
                               int64_t TB, double range, int cmax, int a_start, uint8_t* Acand,
-                              int* first_reached, int32_t* chain_end) {
+                              int* first_reached, int32_t* chain_end, const int* __restrict__ status) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (status) n = min(n, (int64_t)status[ST_NACC]);
     if (t >= n) return;
     const int32_t y = rec[2 * t];
     const int L = rec[2 * t + 1];
@@ -313,18 +355,82 @@ __global__ void k_conn_append(const int32_t* __restrict__ rec, const int32_t* __
     if (!reached && a_start) Acand[TA0 + t] = 1;
 }
 
-// walk parents from `node` to the root (single lane); returns count or -1 on overflow
-__global__ void k_walk(const double* __restrict__ T, const int32_t* __restrict__ par, int32_t node,
+// end of an iteration (single lane): nodes added to tree B; on success the join
+// nodes (OMPL steps back one node on the start side to avoid a duplicate state).
+__global__ void k_finalize(int* status, const int32_t* __restrict__ inclL, int64_t TA, int a_start,
+                           const int32_t* __restrict__ Apar, const int32_t* __restrict__ Bpar,
+                           const int32_t* __restrict__ chain_end) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    const int nacc = status[ST_NACC];
+    status[ST_ADDED] = nacc > 0 ? inclL[nacc - 1] : 0;
+    const int fr = status[ST_FIRST];
+    if (fr != 0x7fffffff) {
+        const int32_t end = chain_end[fr];
+        if (a_start) {   // x in the start tree (tree A), chain end in the goal tree
+            status[ST_SNODE] = Apar[TA + fr];
+            status[ST_GNODE] = end;
+        } else {         // chain end in the start tree (tree B), x in the goal tree
+            status[ST_SNODE] = Bpar[end];
+            status[ST_GNODE] = (int32_t)(TA + fr);
+        }
+    }
+}
+
+// solution path (single lane): start branch root..s_node, then goal branch
+// g_node..root (g_node < 0: start branch only). n_out = -1 if longer than cap.
+__global__ void k_path(const double* __restrict__ S, const int32_t* __restrict__ Spar, int32_t s_node,
+                       const double* __restrict__ G, const int32_t* __restrict__ Gpar, int32_t g_node,
                        double* __restrict__ out, int cap, int* n_out) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    int n = 0;
-    while (node >= 0) {
-        if (n >= cap) { *n_out = -1; return; }
-        for (int d = 0; d < NQ; ++d) out[n * NQ + d] = T[(int64_t)node * NQ + d];
-        ++n;
-        node = par[node];
+    int ns = 0;
+    for (int32_t v = s_node; v >= 0; v = Spar[v]) ++ns;
+    int ng = 0;
+    for (int32_t v = g_node; v >= 0; v = Gpar[v]) ++ng;
+    if (ns + ng > cap) { *n_out = -1; return; }
+    int i = ns - 1;
+    for (int32_t v = s_node; v >= 0; v = Spar[v], --i)
+        for (int d = 0; d < NQ; ++d) out[i * NQ + d] = S[(int64_t)v * NQ + d];
+    i = ns;
+    for (int32_t v = g_node; v >= 0; v = Gpar[v], ++i)
+        for (int d = 0; d < NQ; ++d) out[i * NQ + d] = G[(int64_t)v * NQ + d];
+    *n_out = ns + ng;
+}
+
+// shortcut candidates of a device path of *n_in <= SMAX states: edge (i, j) at
+// index i * SMAX + j for j >= i + 2 (others nd = -1).
+constexpr int SMAX = 64;
+__global__ void k_shortcut_edges(const double* __restrict__ path, const int* __restrict__ n_in, double res,
+                                 double* __restrict__ from, double* __restrict__ to, int* __restrict__ nd,
+                                 uint8_t* __restrict__ valid) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= SMAX * SMAX) return;
+    const int i = e / SMAX, j = e - i * SMAX, n = *n_in;
+    if (n > SMAX || j < i + 2 || j >= n) { nd[e] = -1; return; }
+    for (int d = 0; d < NQ; ++d) {
+        from[(int64_t)e * NQ + d] = path[i * NQ + d];
+        to[(int64_t)e * NQ + d] = path[j * NQ + d];
     }
-    *n_out = n;
+    nd[e] = segment_count(path + i * NQ, path + j * NQ, res);
+    valid[e] = 1;
+}
+
+// greedy farthest-valid walk (single lane): out = simplified path, *n_out states
+__global__ void k_shortcut_select(const double* __restrict__ path, const int* __restrict__ n_in,
+                                  const uint8_t* __restrict__ valid, double* __restrict__ out, int* n_out) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    const int n = *n_in;
+    int m = 0;
+    for (int d = 0; d < NQ; ++d) out[d] = path[d];
+    m = 1;
+    int i = 0;
+    while (i < n - 1) {
+        int j = n - 1;
+        while (j > i + 1 && !valid[i * SMAX + j]) --j;
+        for (int d = 0; d < NQ; ++d) out[m * NQ + d] = path[j * NQ + d];
+        ++m;
+        i = j;
+    }
+    *n_out = m;
 }
 
 // approximate solution: argmin over candidate start-tree nodes of dist2(node, goal),

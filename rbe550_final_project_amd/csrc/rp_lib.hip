@@ -69,6 +69,8 @@ struct DevBuf {
 
 inline unsigned blocks_for(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
+constexpr int PATH_CAP = 1 << 16;   // states of a raw solution path (device buffer)
+
 }  // namespace
 
 struct Tree {
@@ -109,7 +111,8 @@ struct rp_ctx {
     DevBuf<int32_t> near_, res, acc, incl, yv, mv, rec, Lv, chain_end, mine;
     DevBuf<int> gfail;
     DevBuf<char> cub_tmp;
-    DevBuf<double> path;
+    DevBuf<double> path, spath;
+    DevBuf<int> status;                  // per-iteration status record (rp_kernels.h ST_*)
     DevBuf<DI> partial;
 
     // rank group
@@ -127,7 +130,7 @@ struct rp_ctx {
         scalar.release(); counter.release(); efrom.release(); eto.release(); nd.release(); valid.release();
         near_.release(); res.release(); acc.release(); incl.release(); yv.release(); mv.release();
         rec.release(); Lv.release(); chain_end.release(); mine.release(); gfail.release();
-        cub_tmp.release(); path.release(); partial.release();
+        cub_tmp.release(); path.release(); spath.release(); status.release(); partial.release();
         if (d_scene) (void)hipFree(d_scene);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
@@ -158,12 +161,13 @@ void launch_validity(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, hipSt
 }
 
 void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd, int64_t n, int kmax,
-                  int mode, uint8_t* valid, int group, int* gfail, hipStream_t s) {
+                  int mode, uint8_t* valid, int group, int* gfail, hipStream_t s, const int* dcount = nullptr,
+                  int per_item = 1) {
     if (n <= 0) return;
     const int64_t threads = n * (int64_t)kmax;
     const dim3 g(blocks_for(threads, VBLOCK)), b(VBLOCK);
 #define RP_EDGES(N) hipLaunchKernelGGL(k_edges<N>, g, b, 0, s, from, to, nd, n, kmax, mode, valid, group, gfail, \
-                                       c->counter.p, c->d_scene)
+                                       c->counter.p, c->d_scene, dcount, per_item)
     switch (ncl_bucket(c->scene.n_clusters)) {
         case 0: RP_EDGES(0); break;
         case 1: RP_EDGES(1); break;
@@ -322,37 +326,6 @@ bool out_of_bounds(const double* q, const double* lo, const double* hi) {
     return false;
 }
 
-bool state_valid_host(rp_ctx* c, const double* qd) {
-    float q[NQ];
-    for (int i = 0; i < NQ; ++i) q[i] = (float)qd[i];
-    c->q32.ensure(NQ);
-    c->flags.ensure(1);
-    HIP_TRY(hipMemcpyAsync(c->q32.p, q, sizeof q, hipMemcpyHostToDevice, c->stream));
-    launch_validity(c, c->q32.p, 1, c->flags.p, c->stream);
-    return read_scalar(c, c->flags.p) != 0;
-}
-
-std::vector<double> walk_tree(rp_ctx* c, int t, int32_t node) {
-    const int cap = (int)std::min<int64_t>(c->tree[t].n, 1 << 20);
-    c->path.ensure((size_t)cap * NQ);
-    c->scalar.ensure(16);
-    hipLaunchKernelGGL(k_walk, dim3(1), dim3(64), 0, c->stream, c->tree[t].q.p, c->tree[t].par.p, node, c->path.p,
-                       cap, c->scalar.p);
-    HIP_TRY(hipGetLastError());
-    const int n = read_scalar(c, c->scalar.p);
-    if (n < 0) throw HipError{"path walk overflow"};
-    std::vector<double> out((size_t)n * NQ);
-    HIP_TRY(hipMemcpyAsync(out.data(), c->path.p, sizeof(double) * NQ * n, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    return out;
-}
-
-void reverse_states(std::vector<double>& v) {
-    const size_t n = v.size() / NQ;
-    for (size_t i = 0; i < n / 2; ++i)
-        for (int k = 0; k < NQ; ++k) std::swap(v[NQ * i + k], v[NQ * (n - 1 - i) + k]);
-}
-
 // ---------------------------------------------------------------------------
 // the batched RRT-Connect solve
 // ---------------------------------------------------------------------------
@@ -383,21 +356,15 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         c->err = "batch must be a multiple of the group size";
         return RP_ERR_ARG;
     }
+    // batch schedule (mirrored by oracle/rbe_oracle.c ro_plan): iteration k draws
+    // min(batch, batch_min << k) samples from a running global sample counter
+    if (p.batch_min <= 0) p.batch_min = std::min<int64_t>(p.batch, 256);
+    p.batch_min = std::min(p.batch_min, p.batch);
+    p.batch_min = ((p.batch_min + world - 1) / world) * world;
     const int cmax = (int)std::ceil(max_extent / p.range) + 1;
     const int kmax = (int)std::ceil(p.range / p.resolution) + 2;
-    const int64_t B = p.batch, per = B / world;
-
-    if (out_of_bounds(start, lo, hi) || !state_valid_host(c, start)) {
-        *status_out = RP_STATUS_INVALID_START;
-        c->stats.states_checked = 1;
-        return RP_OK;
-    }
-    if (out_of_bounds(goal, lo, hi) || !state_valid_host(c, goal)) {
-        *status_out = RP_STATUS_INVALID_GOAL;
-        c->stats.states_checked = 2;
-        return RP_OK;
-    }
-    c->stats.states_checked = 2;
+    const int kfull = (int)std::ceil(max_extent / p.resolution) + 2;   // any in-bounds edge
+    const int64_t BMAX = p.batch, PMAX = BMAX / world;
 
     // workspace
     const int64_t cap = p.tree_capacity;
@@ -407,30 +374,36 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         t.cand.ensure(cap);
         t.n = 0;
     }
-    const int64_t ne = std::max<int64_t>(per, ((B + world - 1) / world) * cmax);
+    const int64_t ne = std::max<int64_t>({PMAX, ((BMAX + world - 1) / world) * cmax, (int64_t)SMAX * SMAX});
     c->efrom.ensure(ne * NQ);
     c->eto.ensure(ne * NQ);
     c->nd.ensure(ne);
     c->valid.ensure(ne);
-    c->near_.ensure(B);
-    c->res.ensure(B);
-    c->acc.ensure(B);
-    c->incl.ensure(B);
-    c->yv.ensure(B);
-    c->mv.ensure(B);
-    c->rec.ensure(2 * (B + world));
-    c->Lv.ensure(B);
-    c->chain_end.ensure(B);
-    c->gfail.ensure(B);
-    c->mine.ensure(per + 1);
+    c->near_.ensure(BMAX);
+    c->res.ensure(BMAX);
+    c->acc.ensure(BMAX);
+    c->incl.ensure(BMAX);
+    c->yv.ensure(BMAX);
+    c->mv.ensure(BMAX);
+    c->rec.ensure(2 * (BMAX + world));
+    c->Lv.ensure(BMAX);
+    c->chain_end.ensure(BMAX);
+    c->gfail.ensure(BMAX);
+    c->mine.ensure(PMAX + 1);
     c->scalar.ensure(16);
     c->counter.ensure(1);
-    HIP_TRY(hipMemsetAsync(c->counter.p, 0, sizeof(unsigned long long), c->stream));
+    c->status.ensure(ST_WORDS);
+    c->q32.ensure(2 * NQ);
+    c->flags.ensure(2);
+    c->path.ensure((size_t)PATH_CAP * NQ);
+    c->spath.ensure((size_t)SMAX * NQ);
 
-    Bounds bd;
-    for (int i = 0; i < NQ; ++i) { bd.lo[i] = lo[i]; bd.hi[i] = hi[i]; }
-    // roots
+    // start / goal validity in one launch; tree roots; all behind one sync
     {
+        float sg[2 * NQ];
+        for (int i = 0; i < NQ; ++i) { sg[i] = (float)start[i]; sg[NQ + i] = (float)goal[i]; }
+        HIP_TRY(hipMemcpyAsync(c->q32.p, sg, sizeof sg, hipMemcpyHostToDevice, c->stream));
+        launch_validity(c, c->q32.p, 2, c->flags.p, c->stream);
         const int32_t m1 = -1;
         const uint8_t z = 0;
         HIP_TRY(hipMemcpyAsync(c->tree[0].q.p, start, sizeof(double) * NQ, hipMemcpyHostToDevice, c->stream));
@@ -440,14 +413,32 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             HIP_TRY(hipMemcpyAsync(t.cand.p, &z, 1, hipMemcpyHostToDevice, c->stream));
             t.n = 1;
         }
+        HIP_TRY(hipMemsetAsync(c->counter.p, 0, sizeof(unsigned long long), c->stream));
+        uint8_t fl[2];
+        HIP_TRY(hipMemcpyAsync(fl, c->flags.p, 2, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
+        if (out_of_bounds(start, lo, hi) || !fl[0]) {
+            *status_out = RP_STATUS_INVALID_START;
+            c->stats.states_checked = 1;
+            return RP_OK;
+        }
+        if (out_of_bounds(goal, lo, hi) || !fl[1]) {
+            *status_out = RP_STATUS_INVALID_GOAL;
+            c->stats.states_checked = 2;
+            return RP_OK;
+        }
+        c->stats.states_checked = 2;
     }
 
+    Bounds bd;
+    for (int i = 0; i < NQ; ++i) { bd.lo[i] = lo[i]; bd.hi[i] = hi[i]; }
     int solved = 0;
     int32_t s_node = -1, g_node = -1;
     const double t_solve = now_s();
-    int64_t iter = 0;
-    for (; iter < p.max_iters; ++iter) {
+    int64_t iter = 0, B = p.batch_min;
+    uint64_t gbase = 0;
+    for (; iter < p.max_iters; ++iter, gbase += (uint64_t)B, B = std::min(BMAX, 2 * B)) {
+        const int64_t per = B / world;
         const int tflag = (now_s() - t_solve) >= p.timeout_s;
         if (world == 1 && tflag) break;
         const int a_start = (iter % 2) == 0;
@@ -455,7 +446,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         Tree& Bt = c->tree[a_start ? 1 : 0];
         if (A.n + B > cap || Bt.n + B * cmax > cap) break;
         const int64_t TA = A.n, TB = Bt.n;
-        const uint64_t g0 = (uint64_t)iter * (uint64_t)B;
+        const uint64_t g0 = gbase;
 
         // ---- extension: my slice of the samples
         hipLaunchKernelGGL(k_ext_nn, dim3(blocks_for(per, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA, p.seed,
@@ -465,39 +456,73 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, per, kmax, a_start ? 0 : 1, c->valid.p, 1, nullptr,
                      c->stream);
         c->stats.edges_checked += per;
-        if (world > 1) {
-            hipLaunchKernelGGL(k_ext_result, dim3(blocks_for(per, 256)), dim3(256), 0, c->stream, c->valid.p,
-                               c->near_.p, per, c->mine.p);
-            HIP_TRY(hipMemcpyAsync(c->mine.p + per, &tflag, sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
-            exchange(c, c->mine.p, sizeof(int32_t) * (per + 1));
-            HIP_TRY(hipMemsetAsync(c->scalar.p, 0, sizeof(int), c->stream));
-            hipLaunchKernelGGL(k_ext_unpack, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream,
-                               (const int32_t*)c->g_recv, per, world, c->res.p, c->scalar.p);
+        c->stats.samples += B;
+
+        if (world == 1) {
+            // ---- single rank: device-side counts, one host sync per iteration
+            hipLaunchKernelGGL(k_ext_result_flag, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->valid.p,
+                               c->near_.p, B, c->res.p, c->acc.p);
+            scan_incl(c, c->acc.p, c->incl.p, B);
+            hipLaunchKernelGGL(k_ext_append, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->res.p,
+                               c->incl.p, B, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA, c->status.p);
+            hipLaunchKernelGGL(k_conn_nn, dim3(blocks_for(B, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
+                               (int64_t)0, B, Bt.q.p, TB, p.range, p.resolution, cmax, a_start, c->efrom.p,
+                               c->eto.p, c->nd.p, c->valid.p, c->gfail.p, c->yv.p, c->mv.p,
+                               (const int*)c->status.p);
             HIP_TRY(hipGetLastError());
-            if (read_scalar(c, c->scalar.p)) break;  // some rank timed out
-        } else {
-            hipLaunchKernelGGL(k_ext_result, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->valid.p,
-                               c->near_.p, B, c->res.p);
+            launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, B * cmax, kmax, a_start ? 1 : 0, c->valid.p, cmax,
+                         c->gfail.p, c->stream, c->status.p, cmax);
+            hipLaunchKernelGGL(k_conn_record_len, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->yv.p,
+                               c->mv.p, c->gfail.p, (const int*)c->status.p, B, c->rec.p, c->Lv.p);
+            scan_incl(c, c->Lv.p, c->incl.p, B);
+            hipLaunchKernelGGL(k_conn_append, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->rec.p,
+                               c->incl.p, B, A.q.p, TA, Bt.q.p, Bt.par.p, Bt.cand.p, TB, p.range, cmax, a_start,
+                               A.cand.p, c->status.p + ST_FIRST, c->chain_end.p, (const int*)c->status.p);
+            hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, c->stream, c->status.p, c->incl.p, TA, a_start,
+                               A.par.p, Bt.par.p, c->chain_end.p);
             HIP_TRY(hipGetLastError());
+            int st[ST_WORDS];
+            HIP_TRY(hipMemcpyAsync(st, c->status.p, sizeof st, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            A.n = TA + st[ST_NACC];
+            Bt.n = TB + st[ST_ADDED];
+            c->stats.edges_checked += (int64_t)st[ST_NACC] * cmax;
+            if (st[ST_FIRST] != INT_MAX) {
+                solved = 1;
+                s_node = st[ST_SNODE];
+                g_node = st[ST_GNODE];
+                ++iter;
+                break;
+            }
+            continue;
         }
+
+        // ---- rank group: host-visible counts (the exchange is a host callback)
+        hipLaunchKernelGGL(k_ext_result, dim3(blocks_for(per, 256)), dim3(256), 0, c->stream, c->valid.p,
+                           c->near_.p, per, c->mine.p);
+        HIP_TRY(hipMemcpyAsync(c->mine.p + per, &tflag, sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+        exchange(c, c->mine.p, sizeof(int32_t) * (per + 1));
+        HIP_TRY(hipMemsetAsync(c->scalar.p, 0, sizeof(int), c->stream));
+        hipLaunchKernelGGL(k_ext_unpack, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream,
+                           (const int32_t*)c->g_recv, per, world, c->res.p, c->scalar.p);
+        HIP_TRY(hipGetLastError());
+        if (read_scalar(c, c->scalar.p)) break;  // some rank timed out
         hipLaunchKernelGGL(k_flag, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->res.p, B, c->acc.p);
         scan_incl(c, c->acc.p, c->incl.p, B);
         hipLaunchKernelGGL(k_ext_append, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->res.p, c->incl.p, B,
-                           p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA);
+                           p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA, (int*)nullptr);
         HIP_TRY(hipGetLastError());
         const int32_t nacc = read_scalar(c, c->incl.p + (B - 1));
         A.n = TA + nacc;
-        c->stats.samples += B;
         if (nacc == 0) continue;
 
-        // ---- connect: my slice of the accepted targets
         const int64_t pt = (nacc + world - 1) / world;
         const int64_t t0 = (int64_t)rank * pt;
         const int64_t nmine = std::max<int64_t>(0, std::min<int64_t>(pt, nacc - t0));
         if (nmine > 0) {
             hipLaunchKernelGGL(k_conn_nn, dim3(blocks_for(nmine, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
                                t0, nmine, Bt.q.p, TB, p.range, p.resolution, cmax, a_start, c->efrom.p, c->eto.p,
-                               c->nd.p, c->valid.p, c->gfail.p, c->yv.p, c->mv.p);
+                               c->nd.p, c->valid.p, c->gfail.p, c->yv.p, c->mv.p, (const int*)nullptr);
             HIP_TRY(hipGetLastError());
             launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, nmine * cmax, kmax, a_start ? 1 : 0, c->valid.p, cmax,
                          c->gfail.p, c->stream);
@@ -505,11 +530,8 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         hipLaunchKernelGGL(k_conn_record, dim3(blocks_for(pt, 256)), dim3(256), 0, c->stream, c->yv.p, c->mv.p,
                            c->gfail.p, nmine, pt, c->rec.p);
         HIP_TRY(hipGetLastError());
-        const int32_t* rec = c->rec.p;
-        if (world > 1) {
-            exchange(c, c->rec.p, sizeof(int32_t) * 2 * pt);
-            rec = (const int32_t*)c->g_recv;
-        }
+        exchange(c, c->rec.p, sizeof(int32_t) * 2 * pt);
+        const int32_t* rec = (const int32_t*)c->g_recv;
         hipLaunchKernelGGL(k_conn_len, dim3(blocks_for(nacc, 256)), dim3(256), 0, c->stream, rec, (int64_t)nacc,
                            c->Lv.p);
         scan_incl(c, c->Lv.p, c->incl.p, nacc);
@@ -517,7 +539,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         HIP_TRY(hipMemcpyAsync(c->scalar.p, &big, sizeof(int), hipMemcpyHostToDevice, c->stream));
         hipLaunchKernelGGL(k_conn_append, dim3(blocks_for(nacc, 256)), dim3(256), 0, c->stream, rec, c->incl.p,
                            (int64_t)nacc, A.q.p, TA, Bt.q.p, Bt.par.p, Bt.cand.p, TB, p.range, cmax, a_start,
-                           A.cand.p, c->scalar.p, c->chain_end.p);
+                           A.cand.p, c->scalar.p, c->chain_end.p, (const int*)nullptr);
         HIP_TRY(hipGetLastError());
         int32_t hdr[2];
         HIP_TRY(hipMemcpyAsync(&hdr[0], c->incl.p + (nacc - 1), sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
@@ -529,10 +551,10 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         if (fr != INT_MAX) {
             solved = 1;
             const int32_t end = read_scalar(c, c->chain_end.p + fr);
-            if (a_start) {   // x in the start tree; its parent is the join on the start side
+            if (a_start) {
                 s_node = read_scalar(c, A.par.p + (TA + fr));
                 g_node = end;
-            } else {         // chain end in the start tree; step back one node
+            } else {
                 s_node = read_scalar(c, Bt.par.p + end);
                 g_node = (int32_t)(TA + fr);
             }
@@ -545,15 +567,8 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     c->stats.start_tree_size = c->tree[0].n;
     c->stats.goal_tree_size = c->tree[1].n;
 
-    std::vector<double> raw;
-    if (solved) {
-        raw = walk_tree(c, 0, s_node);
-        reverse_states(raw);
-        std::vector<double> g = walk_tree(c, 1, g_node);
-        raw.insert(raw.end(), g.begin(), g.end());
-        *status_out = RP_STATUS_EXACT;
-    } else {
-        // approximate: closest start-tree extension node to the goal
+    if (!solved) {
+        // approximate: closest start-tree extension node to the goal (OMPL >= 1.5)
         const int64_t n0 = c->tree[0].n;
         const int nb = (int)std::min<int64_t>(1024, blocks_for(n0, 256));
         c->partial.ensure(nb + 1);
@@ -564,30 +579,66 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         hipLaunchKernelGGL(k_argmin2, dim3(1), dim3(256), 0, c->stream, c->partial.p, nb, c->partial.p + nb);
         HIP_TRY(hipGetLastError());
         const DI best = read_scalar(c, c->partial.p + nb);
-        if (best.i >= 0) {
-            raw = walk_tree(c, 0, (int32_t)best.i);
-            reverse_states(raw);
-            *status_out = RP_STATUS_APPROXIMATE;
-        } else {
+        if (best.i < 0) {
             *status_out = RP_STATUS_TIMEOUT;
+            c->stats.states_checked += (int64_t)read_scalar(c, c->counter.p);
+            c->stats.total_ms = 1e3 * (now_s() - t_begin);
+            return RP_OK;
         }
+        s_node = (int32_t)best.i;
+        g_node = -1;
     }
-    c->stats.states_checked += (int64_t)read_scalar(c, c->counter.p);
-    c->stats.path_states_raw = (int64_t)(raw.size() / NQ);
-    if (!raw.empty()) {
-        const double t0 = now_s();
+    *status_out = solved ? RP_STATUS_EXACT : RP_STATUS_APPROXIMATE;
+
+    // path extraction (+ shortcut simplification for paths of <= SMAX states) on the
+    // device, then ONE read-back of counts, counter and the simplified path
+    const double t_simp = now_s();
+    hipLaunchKernelGGL(k_path, dim3(1), dim3(64), 0, c->stream, c->tree[0].q.p, c->tree[0].par.p, s_node,
+                       c->tree[1].q.p, c->tree[1].par.p, g_node, c->path.p, PATH_CAP, c->scalar.p);
+    const bool dev_simp = p.simplify != 0;
+    if (dev_simp) {
+        hipLaunchKernelGGL(k_shortcut_edges, dim3(blocks_for(SMAX * SMAX, 256)), dim3(256), 0, c->stream, c->path.p,
+                           (const int*)c->scalar.p, p.resolution, c->efrom.p, c->eto.p, c->nd.p, c->valid.p);
+        launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, SMAX * SMAX, kfull, 0, c->valid.p, 1, nullptr, c->stream);
+        hipLaunchKernelGGL(k_shortcut_select, dim3(1), dim3(64), 0, c->stream, c->path.p, (const int*)c->scalar.p,
+                           c->valid.p, c->spath.p, c->scalar.p + 1);
+    }
+    HIP_TRY(hipGetLastError());
+    int hdr[2] = {0, 0};
+    unsigned long long cnt = 0;
+    std::vector<double> raw((size_t)SMAX * NQ);
+    HIP_TRY(hipMemcpyAsync(hdr, c->scalar.p, sizeof hdr, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(&cnt, c->counter.p, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(raw.data(), dev_simp ? c->spath.p : c->path.p, sizeof(double) * SMAX * NQ,
+                           hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const int n_raw = hdr[0];
+    if (n_raw < 0) {
+        c->err = "solution path longer than PATH_CAP";
+        return RP_ERR_CAPACITY;
+    }
+    c->stats.states_checked += (int64_t)cnt;
+    c->stats.path_states_raw = n_raw;
+    if (n_raw <= SMAX) {
+        raw.resize((size_t)(dev_simp && n_raw >= 3 ? hdr[1] : n_raw) * NQ);
+        if (dev_simp && n_raw >= 3) c->stats.edges_checked += (int64_t)(n_raw - 1) * (n_raw - 2) / 2;
+    } else {
+        // long path: read it back, simplify with host-driven batched edge checks
+        raw.resize((size_t)n_raw * NQ);
+        HIP_TRY(hipMemcpyAsync(raw.data(), c->path.p, sizeof(double) * NQ * n_raw, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
         if (p.simplify) raw = simplify_path(c, raw, p.resolution);
-        c->stats.simplify_ms = 1e3 * (now_s() - t0);
-        c->stats.path_states_simplified = (int64_t)(raw.size() / NQ);
-        if (p.n_waypoints > 0) raw = interpolate_path(raw, p.n_waypoints);
-        const int m = (int)(raw.size() / NQ);
-        if (m > path_cap) {
-            c->err = "path_cap too small";
-            return RP_ERR_CAPACITY;
-        }
-        std::memcpy(path_out, raw.data(), sizeof(double) * NQ * m);
-        *n_out = m;
     }
+    c->stats.simplify_ms = 1e3 * (now_s() - t_simp);
+    c->stats.path_states_simplified = (int64_t)(raw.size() / NQ);
+    if (p.n_waypoints > 0) raw = interpolate_path(raw, p.n_waypoints);
+    const int m = (int)(raw.size() / NQ);
+    if (m > path_cap) {
+        c->err = "path_cap too small";
+        return RP_ERR_CAPACITY;
+    }
+    std::memcpy(path_out, raw.data(), sizeof(double) * NQ * m);
+    *n_out = m;
     c->stats.total_ms = 1e3 * (now_s() - t_begin);
     return RP_OK;
 }

@@ -158,18 +158,22 @@ def test_plan_parity(gpu_ctx, oracle_lib, wl, qi, batch, seed):
         (stats_ref["start_tree_size"], stats_ref["goal_tree_size"], stats_ref["iterations"])
 
 
-def test_plan_parity_hard_iterations(gpu_ctx, oracle_lib):
-    """Many iterations, no simplification/interpolation: raw tree path equality on a
-    tight pentagon query with a small range (more nodes, more NN work)."""
+@pytest.mark.parametrize("simplify,rng", [(False, 0.3), (True, 0.3), (True, 0.15)])
+def test_plan_parity_hard_iterations(gpu_ctx, oracle_lib, simplify, rng):
+    """Many iterations with a small range (more nodes, more NN work, long raw paths:
+    > 64 states exercises the host-side simplification fallback): path equality."""
     q = _wl("goal4_pentagon_10box")["queries"][8]
     sc = scenes.Scene.from_json(q["scene"])
     o = _both(gpu_ctx, oracle_lib, sc, q["attached"])
-    p = _abi.make_params(seed=21, batch=256, range_=0.3, n_waypoints=0, simplify=False, timeout_s=120)
+    p = _abi.make_params(seed=21, batch=256, range_=rng, n_waypoints=0, simplify=simplify, timeout_s=120)
     ref, st_ref, s_ref = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
     path, st = gpu_ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
     assert st == st_ref
     assert np.array_equal(path, ref)
-    assert gpu_ctx.stats()["start_tree_size"] == s_ref["start_tree_size"]
+    gs = gpu_ctx.stats()
+    assert gs["start_tree_size"] == s_ref["start_tree_size"]
+    assert gs["path_states_raw"] == s_ref["path_states_raw"]
+    assert gs["path_states_simplified"] == s_ref["path_states_simplified"]
 
 
 def test_plan_invalid_start_goal(gpu_ctx, oracle_lib):

@@ -1,0 +1,39 @@
+"""Run a plan workload (for rocprofv3 tracing of the plan path): warm-up pass +
+timed pass; prints per-query wall ms and the context's stats split."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from rbe550_final_project_amd import _abi, model, scenes  # noqa: E402
+from rbe550_final_project_amd.native import Context  # noqa: E402
+
+
+def main():
+    name = sys.argv[1] if len(sys.argv) > 1 else "goal3_tallest_10box"
+    batch = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+    wl = json.load(open(os.path.join(ROOT, "tests", "golden", "workloads", name + ".json")))
+    ctx = Context(0, model.robot_desc())
+    for rep in range(2):
+        rows = []
+        for i, q in enumerate(wl["queries"]):
+            sc = scenes.Scene.from_json(q["scene"])
+            ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+            ctx.set_attached(q["attached"])
+            p = _abi.make_params(seed=i, batch=batch, n_waypoints=150, timeout_s=10.0)
+            t0 = time.perf_counter()
+            path, st = ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+            wall = 1e3 * (time.perf_counter() - t0)
+            s = ctx.stats()
+            rows.append((wall, s["total_ms"], s["solve_ms"], s["simplify_ms"], s["iterations"], st))
+        r = np.array([x[:5] for x in rows])
+        print(f"pass {rep}: wall median {np.median(r[:, 0]):.3f} ms  total {np.median(r[:, 1]):.3f}  "
+              f"solve {np.median(r[:, 2]):.3f}  simplify {np.median(r[:, 3]):.3f}  iters {np.median(r[:, 4])}")
+
+
+if __name__ == "__main__":
+    main()

@@ -202,11 +202,61 @@ __global__ void k_flag(const int32_t* __restrict__ v, int64_t n, int32_t* __rest
     if (i < n) out[i] = v[i] >= 0 ? 1 : 0;
 }
 
-// append accepted extension nodes at TA + exclusive_scan position
 // Iteration status record (device): [0] accepted extension nodes, [1] nodes added
 // to the other tree, [2] first REACHED target (INT_MAX: none), [3] start-side and
-// [4] goal-side join nodes of the solution.
-enum { ST_NACC = 0, ST_ADDED = 1, ST_FIRST = 2, ST_SNODE = 3, ST_GNODE = 4, ST_WORDS = 8 };
+// [4] goal-side join nodes of the solution, [5] start / goal validity flags (bytes
+// 0 and 1, written by the first validity launch of rp_plan).
+enum { ST_NACC = 0, ST_ADDED = 1, ST_FIRST = 2, ST_SNODE = 3, ST_GNODE = 4, ST_SG = 5, ST_WORDS = 8 };
+
+// Device I/O record of one rp_plan call, mirrored in pinned host memory: the
+// iteration status is read back alone (32 B), the whole record once at the end.
+constexpr int SMAX = 64;   // device-simplified paths: <= SMAX raw states
+struct PlanIO {
+    int status[ST_WORDS];
+    int n_raw;                      // raw solution states (-1: longer than the path cap)
+    int n_out;                      // states in path[] (simplified when requested)
+    unsigned long long counter;     // snapshot of the states-checked counter
+    double path[SMAX * NQ];
+};
+
+// rp_plan prologue (one block): tree roots, float32 copies of start / goal for
+// their validity check, counters. Replaces per-field host->device copies.
+struct PlanRoots { double start[NQ]; double goal[NQ]; };
+__global__ void k_plan_init(PlanRoots r, double* S, int32_t* Spar, uint8_t* Scand, double* G, int32_t* Gpar,
+                            uint8_t* Gcand, float* q32, unsigned long long* counter, PlanIO* io) {
+    const int t = threadIdx.x;
+    if (t < NQ) {
+        S[t] = r.start[t];
+        G[t] = r.goal[t];
+        q32[t] = (float)r.start[t];
+        q32[NQ + t] = (float)r.goal[t];
+    }
+    if (t < ST_WORDS) io->status[t] = 0;
+    if (t == 0) {
+        Spar[0] = -1;
+        Gpar[0] = -1;
+        Scand[0] = 0;
+        Gcand[0] = 0;
+        *counter = 0;
+        io->n_raw = 0;
+        io->n_out = 0;
+    }
+}
+
+// append accepted extension nodes at TA + exclusive_scan position
+
+__device__ __forceinline__ void ext_append_one(int64_t i, int32_t nn, int64_t pos, uint64_t seed, uint64_t g0,
+                                               const Bounds& bd, double range, double* A, int32_t* Apar,
+                                               uint8_t* Acand) {
+    double qr[NQ], qn[NQ];
+    sample_state(seed, g0 + (uint64_t)i, bd.lo, bd.hi, qr);
+    steer(A + (int64_t)nn * NQ, qr, range, qn);
+    double* dst = A + pos * NQ;
+#pragma unroll
+    for (int d = 0; d < NQ; ++d) dst[d] = qn[d];
+    Apar[pos] = nn;
+    Acand[pos] = 0;
+}
 
 __global__ void k_ext_append(const int32_t* __restrict__ res, const int32_t* __restrict__ incl, int64_t B,
                              uint64_t seed, uint64_t g0, Bounds bd, double range, double* A, int32_t* Apar,
@@ -219,15 +269,66 @@ __global__ void k_ext_append(const int32_t* __restrict__ res, const int32_t* __r
     }
     const int32_t nn = res[i];
     if (nn < 0) return;
-    const int64_t pos = TA + incl[i] - 1;
-    double qr[NQ], qn[NQ];
-    sample_state(seed, g0 + (uint64_t)i, bd.lo, bd.hi, qr);
-    steer(A + (int64_t)nn * NQ, qr, range, qn);
-    double* dst = A + pos * NQ;
+    ext_append_one(i, nn, TA + incl[i] - 1, seed, g0, bd, range, A, Apar, Acand);
+}
+
+// ---- single-block variants for batches <= FUSE_MAX (one launch instead of
+// flag + scan + append): each thread owns FUSE_ITEMS consecutive items, so a scan
+// over threads keeps the global item order.
+constexpr int FUSE_THREADS = 1024, FUSE_ITEMS = 4, FUSE_MAX = FUSE_THREADS * FUSE_ITEMS;
+
+// exclusive scan of one int per thread over a FUSE_THREADS block; *total = sum
+__device__ __forceinline__ int block_scan_excl(int v, int* lds, int* total) {
+    constexpr int NW = FUSE_THREADS / 64;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int x = v;
 #pragma unroll
-    for (int d = 0; d < NQ; ++d) dst[d] = qn[d];
-    Apar[pos] = nn;
-    Acand[pos] = 0;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) lds[w] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int run = 0;
+        for (int k = 0; k < NW; ++k) {
+            const int t = lds[k];
+            lds[k] = run;
+            run += t;
+        }
+        lds[NW] = run;
+    }
+    __syncthreads();
+    const int ex = lds[w] + x - v;
+    *total = lds[NW];
+    __syncthreads();
+    return ex;
+}
+
+__global__ __launch_bounds__(FUSE_THREADS) void k_ext_accept_small(const uint8_t* __restrict__ valid,
+                                                                   const int32_t* __restrict__ near, int64_t B,
+                                                                   uint64_t seed, uint64_t g0, Bounds bd,
+                                                                   double range, double* A, int32_t* Apar,
+                                                                   uint8_t* Acand, int64_t TA, int* status) {
+    __shared__ int lds[FUSE_THREADS / 64 + 1];
+    const int64_t i0 = (int64_t)threadIdx.x * FUSE_ITEMS;
+    int32_t nn[FUSE_ITEMS];
+    int cnt = 0;
+#pragma unroll
+    for (int r = 0; r < FUSE_ITEMS; ++r) {
+        const int64_t i = i0 + r;
+        nn[r] = (i < B && valid[i]) ? near[i] : -1;
+        cnt += nn[r] >= 0;
+    }
+    int total;
+    int64_t pos = TA + block_scan_excl(cnt, lds, &total);
+#pragma unroll
+    for (int r = 0; r < FUSE_ITEMS; ++r)
+        if (nn[r] >= 0) ext_append_one(i0 + r, nn[r], pos++, seed, g0, bd, range, A, Apar, Acand);
+    if (threadIdx.x == 0) {
+        status[ST_NACC] = total;
+        status[ST_FIRST] = 0x7fffffff;
+    }
 }
 
 // Connect targets [t0, t0 + n): x = A[TA0 + t]; nearest node y of tree B; chain
@@ -316,18 +417,12 @@ __global__ void k_conn_len(const int32_t* __restrict__ rec, int64_t n, int32_t* 
     if (t < n) L[t] = rec[2 * t + 1];
 }
 
-// rebuild every target's chain from (y, L), append its first L nodes to tree B,
-// record the first REACHED target and approximate-solution candidates.
-__global__ void k_conn_append(const int32_t* __restrict__ rec, const int32_t* __restrict__ incl, int64_t n,
-                              const double* A, int64_t TA0, double* Bt, int32_t* Bpar, uint8_t* Bcand,
-                              int64_t TB, double range, int cmax, int a_start, uint8_t* Acand,
-                              int* first_reached, int32_t* chain_end, const int* __restrict__ status) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (status) n = min(n, (int64_t)status[ST_NACC]);
-    if (t >= n) return;
-    const int32_t y = rec[2 * t];
-    const int L = rec[2 * t + 1];
-    const int64_t off = TB + incl[t] - L;
+// rebuild target t's chain from (y, L), append its first L nodes to tree B at
+// `off`; returns whether the chain REACHED the target.
+__device__ __forceinline__ bool conn_append_one(int64_t t, int32_t y, int L, int64_t off, const double* A,
+                                                int64_t TA0, double* Bt, int32_t* Bpar, uint8_t* Bcand,
+                                                double range, int cmax, int a_start, uint8_t* Acand,
+                                                int32_t* chain_end) {
     double x[NQ], cur[NQ], nxt[NQ];
     const double* xs = A + (TA0 + t) * NQ;
     const double* ys = Bt + (int64_t)y * NQ;
@@ -351,18 +446,30 @@ __global__ void k_conn_append(const int32_t* __restrict__ rec, const int32_t* __
     }
     const bool reached = (L == m) && reach;
     chain_end[t] = L > 0 ? par : -1;
-    if (reached) atomicMin(first_reached, (int)t);
     if (!reached && a_start) Acand[TA0 + t] = 1;
+    return reached;
+}
+
+// rebuild every target's chain from (y, L), append its first L nodes to tree B,
+// record the first REACHED target and approximate-solution candidates.
+__global__ void k_conn_append(const int32_t* __restrict__ rec, const int32_t* __restrict__ incl, int64_t n,
+                              const double* A, int64_t TA0, double* Bt, int32_t* Bpar, uint8_t* Bcand,
+                              int64_t TB, double range, int cmax, int a_start, uint8_t* Acand,
+                              int* first_reached, int32_t* chain_end, const int* __restrict__ status) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (status) n = min(n, (int64_t)status[ST_NACC]);
+    if (t >= n) return;
+    const int L = rec[2 * t + 1];
+    if (conn_append_one(t, rec[2 * t], L, TB + incl[t] - L, A, TA0, Bt, Bpar, Bcand, range, cmax, a_start, Acand,
+                        chain_end))
+        atomicMin(first_reached, (int)t);
 }
 
 // end of an iteration (single lane): nodes added to tree B; on success the join
 // nodes (OMPL steps back one node on the start side to avoid a duplicate state).
-__global__ void k_finalize(int* status, const int32_t* __restrict__ inclL, int64_t TA, int a_start,
-                           const int32_t* __restrict__ Apar, const int32_t* __restrict__ Bpar,
-                           const int32_t* __restrict__ chain_end) {
-    if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    const int nacc = status[ST_NACC];
-    status[ST_ADDED] = nacc > 0 ? inclL[nacc - 1] : 0;
+__device__ __forceinline__ void finalize_one(int* status, int added, int64_t TA, int a_start,
+                                             const int32_t* Apar, const int32_t* Bpar, const int32_t* chain_end) {
+    status[ST_ADDED] = added;
     const int fr = status[ST_FIRST];
     if (fr != 0x7fffffff) {
         const int32_t end = chain_end[fr];
@@ -376,61 +483,117 @@ __global__ void k_finalize(int* status, const int32_t* __restrict__ inclL, int64
     }
 }
 
+__global__ void k_finalize(int* status, const int32_t* __restrict__ inclL, int64_t TA, int a_start,
+                           const int32_t* __restrict__ Apar, const int32_t* __restrict__ Bpar,
+                           const int32_t* __restrict__ chain_end) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    const int nacc = status[ST_NACC];
+    finalize_one(status, nacc > 0 ? inclL[nacc - 1] : 0, TA, a_start, Apar, Bpar, chain_end);
+}
+
+// single-block connect record + scan + append + finalize (targets <= FUSE_MAX)
+__global__ __launch_bounds__(FUSE_THREADS) void k_conn_accept_small(
+    const int32_t* __restrict__ y, const int32_t* __restrict__ m, const int* __restrict__ gfail, int* status,
+    const double* A, int64_t TA0, double* Bt, int32_t* Bpar, uint8_t* Bcand, int64_t TB, double range, int cmax,
+    int a_start, uint8_t* Acand, const int32_t* Apar, int32_t* chain_end) {
+    __shared__ int lds[FUSE_THREADS / 64 + 1];
+    __shared__ int first;
+    const int nacc = status[ST_NACC];
+    if (threadIdx.x == 0) first = 0x7fffffff;
+    const int64_t t0 = (int64_t)threadIdx.x * FUSE_ITEMS;
+    int L[FUSE_ITEMS];
+    int cnt = 0;
+#pragma unroll
+    for (int r = 0; r < FUSE_ITEMS; ++r) {
+        const int64_t t = t0 + r;
+        L[r] = t < nacc ? (gfail[t] < m[t] ? gfail[t] : m[t]) : -1;
+        cnt += L[r] > 0 ? L[r] : 0;
+    }
+    int total;
+    int64_t off = TB + block_scan_excl(cnt, lds, &total);   // (its barriers also order `first`)
+#pragma unroll
+    for (int r = 0; r < FUSE_ITEMS; ++r) {
+        if (L[r] < 0) continue;
+        const int64_t t = t0 + r;
+        if (conn_append_one(t, y[t], L[r], off, A, TA0, Bt, Bpar, Bcand, range, cmax, a_start, Acand, chain_end))
+            atomicMin(&first, (int)t);
+        off += L[r];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        status[ST_FIRST] = first;
+        finalize_one(status, total, TA0, a_start, Apar, Bpar, chain_end);
+    }
+}
+
 // solution path (single lane): start branch root..s_node, then goal branch
-// g_node..root (g_node < 0: start branch only). n_out = -1 if longer than cap.
+// g_node..root (g_node < 0: start branch only). io->n_raw = -1 if longer than cap.
 __global__ void k_path(const double* __restrict__ S, const int32_t* __restrict__ Spar, int32_t s_node,
                        const double* __restrict__ G, const int32_t* __restrict__ Gpar, int32_t g_node,
-                       double* __restrict__ out, int cap, int* n_out) {
+                       double* __restrict__ out, int cap, PlanIO* io) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
     int ns = 0;
     for (int32_t v = s_node; v >= 0; v = Spar[v]) ++ns;
     int ng = 0;
     for (int32_t v = g_node; v >= 0; v = Gpar[v]) ++ng;
-    if (ns + ng > cap) { *n_out = -1; return; }
+    if (ns + ng > cap) { io->n_raw = -1; return; }
     int i = ns - 1;
     for (int32_t v = s_node; v >= 0; v = Spar[v], --i)
         for (int d = 0; d < NQ; ++d) out[i * NQ + d] = S[(int64_t)v * NQ + d];
     i = ns;
     for (int32_t v = g_node; v >= 0; v = Gpar[v], ++i)
         for (int d = 0; d < NQ; ++d) out[i * NQ + d] = G[(int64_t)v * NQ + d];
-    *n_out = ns + ng;
+    io->n_raw = ns + ng;
 }
 
-// shortcut candidates of a device path of *n_in <= SMAX states: edge (i, j) at
-// index i * SMAX + j for j >= i + 2 (others nd = -1).
-constexpr int SMAX = 64;
-__global__ void k_shortcut_edges(const double* __restrict__ path, const int* __restrict__ n_in, double res,
+// compact index of shortcut (i, j), j >= i + 2, of an n-state path (row-major)
+__device__ __forceinline__ int pair_index(int i, int j, int n) { return i * (n - 2) - i * (i - 1) / 2 + (j - i - 2); }
+
+// shortcut candidates of the device path when 3 <= n_raw <= SMAX: edge
+// pair_index(i, j) for every j >= i + 2; *npairs = their count (0 otherwise).
+__global__ void k_shortcut_edges(const double* __restrict__ path, const PlanIO* __restrict__ io, double res,
                                  double* __restrict__ from, double* __restrict__ to, int* __restrict__ nd,
-                                 uint8_t* __restrict__ valid) {
+                                 uint8_t* __restrict__ valid, int* npairs) {
     const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= SMAX * SMAX) return;
-    const int i = e / SMAX, j = e - i * SMAX, n = *n_in;
-    if (n > SMAX || j < i + 2 || j >= n) { nd[e] = -1; return; }
+    const int n = io->n_raw;
+    const bool on = n >= 3 && n <= SMAX;
+    if (e == 0) *npairs = on ? (n - 1) * (n - 2) / 2 : 0;
+    if (!on || e >= SMAX * SMAX) return;
+    const int i = e / SMAX, j = e - i * SMAX;
+    if (j < i + 2 || j >= n) return;
+    const int k = pair_index(i, j, n);
     for (int d = 0; d < NQ; ++d) {
-        from[(int64_t)e * NQ + d] = path[i * NQ + d];
-        to[(int64_t)e * NQ + d] = path[j * NQ + d];
+        from[(int64_t)k * NQ + d] = path[i * NQ + d];
+        to[(int64_t)k * NQ + d] = path[j * NQ + d];
     }
-    nd[e] = segment_count(path + i * NQ, path + j * NQ, res);
-    valid[e] = 1;
+    nd[k] = segment_count(path + i * NQ, path + j * NQ, res);
+    valid[k] = 1;
 }
 
-// greedy farthest-valid walk (single lane): out = simplified path, *n_out states
-__global__ void k_shortcut_select(const double* __restrict__ path, const int* __restrict__ n_in,
-                                  const uint8_t* __restrict__ valid, double* __restrict__ out, int* n_out) {
+// output record (single lane): the greedy farthest-valid walk over the checked
+// shortcuts (simplify) or the raw path, when n_raw <= SMAX; counter snapshot.
+__global__ void k_path_out(const double* __restrict__ path, const uint8_t* __restrict__ valid, int simplify,
+                           const unsigned long long* __restrict__ counter, PlanIO* io) {
     if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    const int n = *n_in;
-    int m = 0;
+    io->counter = *counter;
+    const int n = io->n_raw;
+    if (n < 0 || n > SMAX) { io->n_out = 0; return; }
+    double* out = io->path;
+    if (!simplify || n < 3) {
+        for (int k = 0; k < n * NQ; ++k) out[k] = path[k];
+        io->n_out = n;
+        return;
+    }
     for (int d = 0; d < NQ; ++d) out[d] = path[d];
-    m = 1;
-    int i = 0;
+    int m = 1, i = 0;
     while (i < n - 1) {
         int j = n - 1;
-        while (j > i + 1 && !valid[i * SMAX + j]) --j;
+        while (j > i + 1 && !valid[pair_index(i, j, n)]) --j;
         for (int d = 0; d < NQ; ++d) out[m * NQ + d] = path[j * NQ + d];
         ++m;
         i = j;
     }
-    *n_out = m;
+    io->n_out = m;
 }
 
 // approximate solution: argmin over candidate start-tree nodes of dist2(node, goal),

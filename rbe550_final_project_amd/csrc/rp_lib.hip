@@ -111,8 +111,9 @@ struct rp_ctx {
     DevBuf<int32_t> near_, res, acc, incl, yv, mv, rec, Lv, chain_end, mine;
     DevBuf<int> gfail;
     DevBuf<char> cub_tmp;
-    DevBuf<double> path, spath;
-    DevBuf<int> status;                  // per-iteration status record (rp_kernels.h ST_*)
+    DevBuf<double> path;                 // raw solution path (PATH_CAP states)
+    DevBuf<PlanIO> io;                   // iteration status + output record (rp_kernels.h)
+    PlanIO* h_io = nullptr;              // its pinned host mirror
     DevBuf<DI> partial;
 
     // rank group
@@ -130,7 +131,8 @@ struct rp_ctx {
         scalar.release(); counter.release(); efrom.release(); eto.release(); nd.release(); valid.release();
         near_.release(); res.release(); acc.release(); incl.release(); yv.release(); mv.release();
         rec.release(); Lv.release(); chain_end.release(); mine.release(); gfail.release();
-        cub_tmp.release(); path.release(); spath.release(); status.release(); partial.release();
+        cub_tmp.release(); path.release(); io.release(); partial.release();
+        if (h_io) (void)hipHostFree(h_io);
         if (d_scene) (void)hipFree(d_scene);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
@@ -392,43 +394,55 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     c->mine.ensure(PMAX + 1);
     c->scalar.ensure(16);
     c->counter.ensure(1);
-    c->status.ensure(ST_WORDS);
+    c->io.ensure(1);
+    if (!c->h_io) HIP_TRY(hipHostMalloc((void**)&c->h_io, sizeof(PlanIO), hipHostMallocDefault));
     c->q32.ensure(2 * NQ);
     c->flags.ensure(2);
     c->path.ensure((size_t)PATH_CAP * NQ);
-    c->spath.ensure((size_t)SMAX * NQ);
 
-    // start / goal validity in one launch; tree roots; all behind one sync
-    {
-        float sg[2 * NQ];
-        for (int i = 0; i < NQ; ++i) { sg[i] = (float)start[i]; sg[NQ + i] = (float)goal[i]; }
-        HIP_TRY(hipMemcpyAsync(c->q32.p, sg, sizeof sg, hipMemcpyHostToDevice, c->stream));
-        launch_validity(c, c->q32.p, 2, c->flags.p, c->stream);
-        const int32_t m1 = -1;
-        const uint8_t z = 0;
-        HIP_TRY(hipMemcpyAsync(c->tree[0].q.p, start, sizeof(double) * NQ, hipMemcpyHostToDevice, c->stream));
-        HIP_TRY(hipMemcpyAsync(c->tree[1].q.p, goal, sizeof(double) * NQ, hipMemcpyHostToDevice, c->stream));
-        for (auto& t : c->tree) {
-            HIP_TRY(hipMemcpyAsync(t.par.p, &m1, sizeof m1, hipMemcpyHostToDevice, c->stream));
-            HIP_TRY(hipMemcpyAsync(t.cand.p, &z, 1, hipMemcpyHostToDevice, c->stream));
-            t.n = 1;
-        }
-        HIP_TRY(hipMemsetAsync(c->counter.p, 0, sizeof(unsigned long long), c->stream));
-        uint8_t fl[2];
-        HIP_TRY(hipMemcpyAsync(fl, c->flags.p, 2, hipMemcpyDeviceToHost, c->stream));
+    PlanIO* io = c->io.p;
+    int* status = io->status;
+    PlanIO* h = c->h_io;
+    auto read_status = [&]() {
+        HIP_TRY(hipMemcpyAsync(h->status, status, sizeof h->status, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
-        if (out_of_bounds(start, lo, hi) || !fl[0]) {
-            *status_out = RP_STATUS_INVALID_START;
-            c->stats.states_checked = 1;
-            return RP_OK;
-        }
-        if (out_of_bounds(goal, lo, hi) || !fl[1]) {
-            *status_out = RP_STATUS_INVALID_GOAL;
-            c->stats.states_checked = 2;
-            return RP_OK;
-        }
-        c->stats.states_checked = 2;
+    };
+
+    // Prologue: tree roots and counters from kernel arguments, then start / goal
+    // validity into the status record. No host sync here: single-rank plans read
+    // the flags back with the first iteration's status (a plan with an invalid
+    // start or goal discards that iteration).
+    {
+        PlanRoots roots;
+        for (int i = 0; i < NQ; ++i) { roots.start[i] = start[i]; roots.goal[i] = goal[i]; }
+        hipLaunchKernelGGL(k_plan_init, dim3(1), dim3(64), 0, c->stream, roots, c->tree[0].q.p, c->tree[0].par.p,
+                           c->tree[0].cand.p, c->tree[1].q.p, c->tree[1].par.p, c->tree[1].cand.p, c->q32.p,
+                           c->counter.p, io);
+        HIP_TRY(hipGetLastError());
+        launch_validity(c, c->q32.p, 2, (uint8_t*)(status + ST_SG), c->stream);
+        for (auto& t : c->tree) t.n = 1;
     }
+    // OMPL's PlannerInputStates: bounds and validity of start, then goal
+    auto endpoint_status = [&](int sg) {
+        if (out_of_bounds(start, lo, hi) || !(sg & 0xff)) return (int)RP_STATUS_INVALID_START;
+        if (out_of_bounds(goal, lo, hi) || !((sg >> 8) & 0xff)) return (int)RP_STATUS_INVALID_GOAL;
+        return 0;
+    };
+    auto endpoint_fail = [&](int code) {
+        c->stats = rp_stats{};
+        c->stats.states_checked = code == RP_STATUS_INVALID_START ? 1 : 2;
+        c->stats.total_ms = 1e3 * (now_s() - t_begin);
+        *status_out = code;
+        return RP_OK;
+    };
+    bool sg_known = false;
+    if (world > 1 || out_of_bounds(start, lo, hi) || out_of_bounds(goal, lo, hi)) {
+        // rank groups agree on the endpoints before the first exchange
+        read_status();
+        if (const int code = endpoint_status(h->status[ST_SG])) return endpoint_fail(code);
+        sg_known = true;
+    }
+    c->stats.states_checked = 2;
 
     Bounds bd;
     for (int i = 0; i < NQ; ++i) { bd.lo[i] = lo[i]; bd.hi[i] = hi[i]; }
@@ -459,31 +473,46 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         c->stats.samples += B;
 
         if (world == 1) {
-            // ---- single rank: device-side counts, one host sync per iteration
-            hipLaunchKernelGGL(k_ext_result_flag, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->valid.p,
-                               c->near_.p, B, c->res.p, c->acc.p);
-            scan_incl(c, c->acc.p, c->incl.p, B);
-            hipLaunchKernelGGL(k_ext_append, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->res.p,
-                               c->incl.p, B, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA, c->status.p);
+            // ---- single rank: device-side counts, one host sync per iteration;
+            // batches <= FUSE_MAX use the single-block accept kernels
+            const bool fused = B <= FUSE_MAX;
+            if (fused) {
+                hipLaunchKernelGGL(k_ext_accept_small, dim3(1), dim3(FUSE_THREADS), 0, c->stream, c->valid.p,
+                                   c->near_.p, B, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA, status);
+            } else {
+                hipLaunchKernelGGL(k_ext_result_flag, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream,
+                                   c->valid.p, c->near_.p, B, c->res.p, c->acc.p);
+                scan_incl(c, c->acc.p, c->incl.p, B);
+                hipLaunchKernelGGL(k_ext_append, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->res.p,
+                                   c->incl.p, B, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA, status);
+            }
             hipLaunchKernelGGL(k_conn_nn, dim3(blocks_for(B, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
                                (int64_t)0, B, Bt.q.p, TB, p.range, p.resolution, cmax, a_start, c->efrom.p,
-                               c->eto.p, c->nd.p, c->valid.p, c->gfail.p, c->yv.p, c->mv.p,
-                               (const int*)c->status.p);
+                               c->eto.p, c->nd.p, c->valid.p, c->gfail.p, c->yv.p, c->mv.p, (const int*)status);
             HIP_TRY(hipGetLastError());
             launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, B * cmax, kmax, a_start ? 1 : 0, c->valid.p, cmax,
-                         c->gfail.p, c->stream, c->status.p, cmax);
-            hipLaunchKernelGGL(k_conn_record_len, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->yv.p,
-                               c->mv.p, c->gfail.p, (const int*)c->status.p, B, c->rec.p, c->Lv.p);
-            scan_incl(c, c->Lv.p, c->incl.p, B);
-            hipLaunchKernelGGL(k_conn_append, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->rec.p,
-                               c->incl.p, B, A.q.p, TA, Bt.q.p, Bt.par.p, Bt.cand.p, TB, p.range, cmax, a_start,
-                               A.cand.p, c->status.p + ST_FIRST, c->chain_end.p, (const int*)c->status.p);
-            hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, c->stream, c->status.p, c->incl.p, TA, a_start,
-                               A.par.p, Bt.par.p, c->chain_end.p);
+                         c->gfail.p, c->stream, status, cmax);
+            if (fused) {
+                hipLaunchKernelGGL(k_conn_accept_small, dim3(1), dim3(FUSE_THREADS), 0, c->stream, c->yv.p, c->mv.p,
+                                   c->gfail.p, status, A.q.p, TA, Bt.q.p, Bt.par.p, Bt.cand.p, TB, p.range, cmax,
+                                   a_start, A.cand.p, A.par.p, c->chain_end.p);
+            } else {
+                hipLaunchKernelGGL(k_conn_record_len, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->yv.p,
+                                   c->mv.p, c->gfail.p, (const int*)status, B, c->rec.p, c->Lv.p);
+                scan_incl(c, c->Lv.p, c->incl.p, B);
+                hipLaunchKernelGGL(k_conn_append, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->rec.p,
+                                   c->incl.p, B, A.q.p, TA, Bt.q.p, Bt.par.p, Bt.cand.p, TB, p.range, cmax,
+                                   a_start, A.cand.p, status + ST_FIRST, c->chain_end.p, (const int*)status);
+                hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, c->stream, status, c->incl.p, TA, a_start,
+                                   A.par.p, Bt.par.p, c->chain_end.p);
+            }
             HIP_TRY(hipGetLastError());
-            int st[ST_WORDS];
-            HIP_TRY(hipMemcpyAsync(st, c->status.p, sizeof st, hipMemcpyDeviceToHost, c->stream));
-            HIP_TRY(hipStreamSynchronize(c->stream));
+            read_status();
+            if (!sg_known) {
+                if (const int code = endpoint_status(h->status[ST_SG])) return endpoint_fail(code);
+                sg_known = true;
+            }
+            const int* st = h->status;
             A.n = TA + st[ST_NACC];
             Bt.n = TB + st[ST_ADDED];
             c->stats.edges_checked += (int64_t)st[ST_NACC] * cmax;
@@ -562,6 +591,10 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             break;
         }
     }
+    if (!sg_known) {   // the loop ran no iteration
+        read_status();
+        if (const int code = endpoint_status(h->status[ST_SG])) return endpoint_fail(code);
+    }
     c->stats.iterations = iter;
     c->stats.solve_ms = 1e3 * (now_s() - t_solve);
     c->stats.start_tree_size = c->tree[0].n;
@@ -591,37 +624,32 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     *status_out = solved ? RP_STATUS_EXACT : RP_STATUS_APPROXIMATE;
 
     // path extraction (+ shortcut simplification for paths of <= SMAX states) on the
-    // device, then ONE read-back of counts, counter and the simplified path
+    // device, then ONE read-back of the output record
     const double t_simp = now_s();
     hipLaunchKernelGGL(k_path, dim3(1), dim3(64), 0, c->stream, c->tree[0].q.p, c->tree[0].par.p, s_node,
-                       c->tree[1].q.p, c->tree[1].par.p, g_node, c->path.p, PATH_CAP, c->scalar.p);
-    const bool dev_simp = p.simplify != 0;
-    if (dev_simp) {
+                       c->tree[1].q.p, c->tree[1].par.p, g_node, c->path.p, PATH_CAP, io);
+    if (p.simplify) {
         hipLaunchKernelGGL(k_shortcut_edges, dim3(blocks_for(SMAX * SMAX, 256)), dim3(256), 0, c->stream, c->path.p,
-                           (const int*)c->scalar.p, p.resolution, c->efrom.p, c->eto.p, c->nd.p, c->valid.p);
-        launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, SMAX * SMAX, kfull, 0, c->valid.p, 1, nullptr, c->stream);
-        hipLaunchKernelGGL(k_shortcut_select, dim3(1), dim3(64), 0, c->stream, c->path.p, (const int*)c->scalar.p,
-                           c->valid.p, c->spath.p, c->scalar.p + 1);
+                           (const PlanIO*)io, p.resolution, c->efrom.p, c->eto.p, c->nd.p, c->valid.p, c->scalar.p);
+        launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, (SMAX - 1) * (SMAX - 2) / 2, kfull, 0, c->valid.p, 1, nullptr,
+                     c->stream, c->scalar.p, 1);
     }
+    hipLaunchKernelGGL(k_path_out, dim3(1), dim3(64), 0, c->stream, c->path.p, c->valid.p, p.simplify ? 1 : 0,
+                       (const unsigned long long*)c->counter.p, io);
     HIP_TRY(hipGetLastError());
-    int hdr[2] = {0, 0};
-    unsigned long long cnt = 0;
-    std::vector<double> raw((size_t)SMAX * NQ);
-    HIP_TRY(hipMemcpyAsync(hdr, c->scalar.p, sizeof hdr, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(&cnt, c->counter.p, sizeof cnt, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipMemcpyAsync(raw.data(), dev_simp ? c->spath.p : c->path.p, sizeof(double) * SMAX * NQ,
-                           hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(h, io, sizeof(PlanIO), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    const int n_raw = hdr[0];
+    const int n_raw = h->n_raw;
     if (n_raw < 0) {
         c->err = "solution path longer than PATH_CAP";
         return RP_ERR_CAPACITY;
     }
-    c->stats.states_checked += (int64_t)cnt;
+    c->stats.states_checked += (int64_t)h->counter;
     c->stats.path_states_raw = n_raw;
+    std::vector<double> raw;
     if (n_raw <= SMAX) {
-        raw.resize((size_t)(dev_simp && n_raw >= 3 ? hdr[1] : n_raw) * NQ);
-        if (dev_simp && n_raw >= 3) c->stats.edges_checked += (int64_t)(n_raw - 1) * (n_raw - 2) / 2;
+        raw.assign(h->path, h->path + (size_t)h->n_out * NQ);
+        if (p.simplify && n_raw >= 3) c->stats.edges_checked += (int64_t)(n_raw - 1) * (n_raw - 2) / 2;
     } else {
         // long path: read it back, simplify with host-driven batched edge checks
         raw.resize((size_t)n_raw * NQ);

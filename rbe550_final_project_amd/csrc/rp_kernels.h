@@ -208,28 +208,44 @@ __global__ void k_flag(const int32_t* __restrict__ v, int64_t n, int32_t* __rest
 // 0 and 1, written by the first validity launch of rp_plan).
 enum { ST_NACC = 0, ST_ADDED = 1, ST_FIRST = 2, ST_SNODE = 3, ST_GNODE = 4, ST_SG = 5, ST_WORDS = 8 };
 
-// Device I/O record of one rp_plan call, mirrored in pinned host memory: the
-// iteration status is read back alone (32 B), the whole record once at the end.
+// I/O record of one rp_plan call. The device copy holds the live status; a
+// pinned, host-coherent mirror receives what the host needs (status after every
+// iteration, the output path at the end), written by the kernels themselves and
+// published by a release store of `seq` that the host spins on (no copy, no
+// stream synchronisation on the per-iteration round trip).
 constexpr int SMAX = 64;   // device-simplified paths: <= SMAX raw states
 struct PlanIO {
     int status[ST_WORDS];
     int n_raw;                      // raw solution states (-1: longer than the path cap)
     int n_out;                      // states in path[] (simplified when requested)
     unsigned long long counter;     // snapshot of the states-checked counter
+    int seq;                        // publication sequence number (host mirror)
+    int pad;
     double path[SMAX * NQ];
 };
 
-// rp_plan prologue (one block): tree roots, float32 copies of start / goal for
-// their validity check, counters. Replaces per-field host->device copies.
+__device__ __forceinline__ void publish_seq(PlanIO* hio, int seq) {
+    __hip_atomic_store(&hio->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// rp_plan prologue (one block): tree roots, float32 copies of start / goal, counters
+// (replaces per-field host->device copies). sg_edge >= 0: start and goal also
+// become two zero-length edges at [sg_edge, sg_edge + 1] of the first extension
+// launch, so their validity is checked by it rather than by a separate launch.
 struct PlanRoots { double start[NQ]; double goal[NQ]; };
 __global__ void k_plan_init(PlanRoots r, double* S, int32_t* Spar, uint8_t* Scand, double* G, int32_t* Gpar,
-                            uint8_t* Gcand, float* q32, unsigned long long* counter, PlanIO* io) {
+                            uint8_t* Gcand, float* q32, unsigned long long* counter, PlanIO* io, int64_t sg_edge,
+                            double* efrom, double* eto, int* nd, uint8_t* valid) {
     const int t = threadIdx.x;
     if (t < NQ) {
         S[t] = r.start[t];
         G[t] = r.goal[t];
         q32[t] = (float)r.start[t];
         q32[NQ + t] = (float)r.goal[t];
+        if (sg_edge >= 0) {
+            efrom[sg_edge * NQ + t] = eto[sg_edge * NQ + t] = r.start[t];
+            efrom[(sg_edge + 1) * NQ + t] = eto[(sg_edge + 1) * NQ + t] = r.goal[t];
+        }
     }
     if (t < ST_WORDS) io->status[t] = 0;
     if (t == 0) {
@@ -240,7 +256,15 @@ __global__ void k_plan_init(PlanRoots r, double* S, int32_t* Spar, uint8_t* Scan
         *counter = 0;
         io->n_raw = 0;
         io->n_out = 0;
+        if (sg_edge >= 0) {
+            nd[sg_edge] = nd[sg_edge + 1] = 0;
+            valid[sg_edge] = valid[sg_edge + 1] = 1;
+        }
     }
+}
+
+__device__ __forceinline__ int sg_flags(const uint8_t* valid, int64_t sg_edge) {
+    return (valid[sg_edge] ? 1 : 0) | (valid[sg_edge + 1] ? 0x100 : 0);
 }
 
 // append accepted extension nodes at TA + exclusive_scan position
@@ -260,12 +284,13 @@ __device__ __forceinline__ void ext_append_one(int64_t i, int32_t nn, int64_t po
 
 __global__ void k_ext_append(const int32_t* __restrict__ res, const int32_t* __restrict__ incl, int64_t B,
                              uint64_t seed, uint64_t g0, Bounds bd, double range, double* A, int32_t* Apar,
-                             uint8_t* Acand, int64_t TA, int* status) {
+                             uint8_t* Acand, int64_t TA, int* status, const uint8_t* valid, int64_t sg_edge) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= B) return;
     if (status && i == B - 1) {
         status[ST_NACC] = incl[B - 1];
         status[ST_FIRST] = 0x7fffffff;
+        if (sg_edge >= 0) status[ST_SG] = sg_flags(valid, sg_edge);
     }
     const int32_t nn = res[i];
     if (nn < 0) return;
@@ -273,9 +298,9 @@ __global__ void k_ext_append(const int32_t* __restrict__ res, const int32_t* __r
 }
 
 // ---- single-block variants for batches <= FUSE_MAX (one launch instead of
-// flag + scan + append): each thread owns FUSE_ITEMS consecutive items, so a scan
-// over threads keeps the global item order.
-constexpr int FUSE_THREADS = 1024, FUSE_ITEMS = 4, FUSE_MAX = FUSE_THREADS * FUSE_ITEMS;
+// flag + scan + append): each thread owns ITEMS consecutive items, so a scan over
+// threads keeps the global item order.
+constexpr int FUSE_THREADS = 1024, FUSE_MAX = FUSE_THREADS * 4;
 
 // exclusive scan of one int per thread over a FUSE_THREADS block; *total = sum
 __device__ __forceinline__ int block_scan_excl(int v, int* lds, int* total) {
@@ -305,17 +330,19 @@ __device__ __forceinline__ int block_scan_excl(int v, int* lds, int* total) {
     return ex;
 }
 
+template <int ITEMS>
 __global__ __launch_bounds__(FUSE_THREADS) void k_ext_accept_small(const uint8_t* __restrict__ valid,
                                                                    const int32_t* __restrict__ near, int64_t B,
                                                                    uint64_t seed, uint64_t g0, Bounds bd,
                                                                    double range, double* A, int32_t* Apar,
-                                                                   uint8_t* Acand, int64_t TA, int* status) {
+                                                                   uint8_t* Acand, int64_t TA, int* status,
+                                                                   int64_t sg_edge) {
     __shared__ int lds[FUSE_THREADS / 64 + 1];
-    const int64_t i0 = (int64_t)threadIdx.x * FUSE_ITEMS;
-    int32_t nn[FUSE_ITEMS];
+    const int64_t i0 = (int64_t)threadIdx.x * ITEMS;
+    int32_t nn[ITEMS];
     int cnt = 0;
 #pragma unroll
-    for (int r = 0; r < FUSE_ITEMS; ++r) {
+    for (int r = 0; r < ITEMS; ++r) {
         const int64_t i = i0 + r;
         nn[r] = (i < B && valid[i]) ? near[i] : -1;
         cnt += nn[r] >= 0;
@@ -323,11 +350,12 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_ext_accept_small(const uint8_t
     int total;
     int64_t pos = TA + block_scan_excl(cnt, lds, &total);
 #pragma unroll
-    for (int r = 0; r < FUSE_ITEMS; ++r)
+    for (int r = 0; r < ITEMS; ++r)
         if (nn[r] >= 0) ext_append_one(i0 + r, nn[r], pos++, seed, g0, bd, range, A, Apar, Acand);
     if (threadIdx.x == 0) {
         status[ST_NACC] = total;
         status[ST_FIRST] = 0x7fffffff;
+        if (sg_edge >= 0) status[ST_SG] = sg_flags(valid, sg_edge);
     }
 }
 
@@ -483,28 +511,109 @@ __device__ __forceinline__ void finalize_one(int* status, int added, int64_t TA,
     }
 }
 
-__global__ void k_finalize(int* status, const int32_t* __restrict__ inclL, int64_t TA, int a_start,
-                           const int32_t* __restrict__ Apar, const int32_t* __restrict__ Bpar,
-                           const int32_t* __restrict__ chain_end) {
-    if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    const int nacc = status[ST_NACC];
-    finalize_one(status, nacc > 0 ? inclL[nacc - 1] : 0, TA, a_start, Apar, Bpar, chain_end);
+// where a solution path goes and how its shortcut candidates are emitted
+struct PathArgs {
+    const double* S;      // start tree
+    const int32_t* Spar;
+    const double* G;      // goal tree
+    const int32_t* Gpar;
+    double* out;          // raw path, `cap` states
+    int cap;
+    int simplify;
+    double res;
+    double* efrom;        // shortcut candidate edges
+    double* eto;
+    int* nd;
+    uint8_t* valid;
+    int* npairs;          // candidate count (0: none)
+};
+
+// compact index of shortcut (i, j), j >= i + 2, of an n-state path (row-major)
+__device__ __forceinline__ int pair_index(int i, int j, int n) { return i * (n - 2) - i * (i - 1) / 2 + (j - i - 2); }
+
+// Block-cooperative (every thread calls it): lane 0 writes the solution path
+// (start branch root..s_node, goal branch g_node..root; g_node < 0: start branch
+// only; io->n_raw = -1 if longer than cap), then the block emits the shortcut
+// candidates (i, j >= i + 2) when simplifying a path of 3..SMAX states.
+__device__ void build_path(const PathArgs& pa, int32_t s_node, int32_t g_node, PlanIO* io) {
+    __shared__ int n_sh;
+    if (threadIdx.x == 0) {
+        int ns = 0, ng = 0;
+        for (int32_t v = s_node; v >= 0; v = pa.Spar[v]) ++ns;
+        for (int32_t v = g_node; v >= 0; v = pa.Gpar[v]) ++ng;
+        int n = ns + ng;
+        if (n > pa.cap) {
+            n = -1;
+        } else {
+            int i = ns - 1;
+            for (int32_t v = s_node; v >= 0; v = pa.Spar[v], --i)
+                for (int d = 0; d < NQ; ++d) pa.out[i * NQ + d] = pa.S[(int64_t)v * NQ + d];
+            i = ns;
+            for (int32_t v = g_node; v >= 0; v = pa.Gpar[v], ++i)
+                for (int d = 0; d < NQ; ++d) pa.out[i * NQ + d] = pa.G[(int64_t)v * NQ + d];
+        }
+        io->n_raw = n;
+        n_sh = n;
+    }
+    __syncthreads();
+    const int n = n_sh;
+    const bool on = pa.simplify && n >= 3 && n <= SMAX;
+    if (threadIdx.x == 0) *pa.npairs = on ? (n - 1) * (n - 2) / 2 : 0;
+    if (!on) return;
+    for (int e = threadIdx.x; e < SMAX * SMAX; e += blockDim.x) {
+        const int i = e / SMAX, j = e - i * SMAX;
+        if (j < i + 2 || j >= n) continue;
+        const int k = pair_index(i, j, n);
+        const double* a = pa.out + i * NQ;
+        const double* b = pa.out + j * NQ;
+        for (int d = 0; d < NQ; ++d) {
+            pa.efrom[(int64_t)k * NQ + d] = a[d];
+            pa.eto[(int64_t)k * NQ + d] = b[d];
+        }
+        pa.nd[k] = segment_count(a, b, pa.res);
+        pa.valid[k] = 1;
+    }
 }
 
-// single-block connect record + scan + append + finalize (targets <= FUSE_MAX)
+// block tail of the last kernel of an iteration: join nodes and, on success, the
+// solution path with its shortcut candidates (none otherwise). The status reaches
+// the host through k_path_out, which always follows.
+__device__ void iteration_tail(int* status, int added, int64_t TA, int a_start, const int32_t* Apar,
+                               const int32_t* Bpar, const int32_t* chain_end, const PathArgs& pa, PlanIO* io) {
+    __shared__ int sn, gn;
+    if (threadIdx.x == 0) {
+        finalize_one(status, added, TA, a_start, Apar, Bpar, chain_end);
+        const bool ok = status[ST_FIRST] != 0x7fffffff;
+        sn = ok ? status[ST_SNODE] : -2;
+        gn = status[ST_GNODE];
+        if (!ok) *pa.npairs = 0;
+    }
+    __syncthreads();
+    if (sn != -2) build_path(pa, sn, gn, io);
+}
+
+__global__ void k_finalize(int* status, const int32_t* __restrict__ inclL, int64_t TA, int a_start,
+                           const int32_t* __restrict__ Apar, const int32_t* __restrict__ Bpar,
+                           const int32_t* __restrict__ chain_end, PathArgs pa, PlanIO* io) {
+    const int nacc = status[ST_NACC];
+    iteration_tail(status, nacc > 0 ? inclL[nacc - 1] : 0, TA, a_start, Apar, Bpar, chain_end, pa, io);
+}
+
+// single-block connect record + scan + append + iteration tail (targets <= FUSE_MAX)
+template <int ITEMS>
 __global__ __launch_bounds__(FUSE_THREADS) void k_conn_accept_small(
     const int32_t* __restrict__ y, const int32_t* __restrict__ m, const int* __restrict__ gfail, int* status,
     const double* A, int64_t TA0, double* Bt, int32_t* Bpar, uint8_t* Bcand, int64_t TB, double range, int cmax,
-    int a_start, uint8_t* Acand, const int32_t* Apar, int32_t* chain_end) {
+    int a_start, uint8_t* Acand, const int32_t* Apar, int32_t* chain_end, PathArgs pa, PlanIO* io) {
     __shared__ int lds[FUSE_THREADS / 64 + 1];
     __shared__ int first;
     const int nacc = status[ST_NACC];
     if (threadIdx.x == 0) first = 0x7fffffff;
-    const int64_t t0 = (int64_t)threadIdx.x * FUSE_ITEMS;
-    int L[FUSE_ITEMS];
+    const int64_t t0 = (int64_t)threadIdx.x * ITEMS;
+    int L[ITEMS];
     int cnt = 0;
 #pragma unroll
-    for (int r = 0; r < FUSE_ITEMS; ++r) {
+    for (int r = 0; r < ITEMS; ++r) {
         const int64_t t = t0 + r;
         L[r] = t < nacc ? (gfail[t] < m[t] ? gfail[t] : m[t]) : -1;
         cnt += L[r] > 0 ? L[r] : 0;
@@ -512,7 +621,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_conn_accept_small(
     int total;
     int64_t off = TB + block_scan_excl(cnt, lds, &total);   // (its barriers also order `first`)
 #pragma unroll
-    for (int r = 0; r < FUSE_ITEMS; ++r) {
+    for (int r = 0; r < ITEMS; ++r) {
         if (L[r] < 0) continue;
         const int64_t t = t0 + r;
         if (conn_append_one(t, y[t], L[r], off, A, TA0, Bt, Bpar, Bcand, range, cmax, a_start, Acand, chain_end))
@@ -520,80 +629,57 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_conn_accept_small(
         off += L[r];
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        status[ST_FIRST] = first;
-        finalize_one(status, total, TA0, a_start, Apar, Bpar, chain_end);
-    }
+    if (threadIdx.x == 0) status[ST_FIRST] = first;
+    iteration_tail(status, total, TA0, a_start, Apar, Bpar, chain_end, pa, io);
 }
 
-// solution path (single lane): start branch root..s_node, then goal branch
-// g_node..root (g_node < 0: start branch only). io->n_raw = -1 if longer than cap.
-__global__ void k_path(const double* __restrict__ S, const int32_t* __restrict__ Spar, int32_t s_node,
-                       const double* __restrict__ G, const int32_t* __restrict__ Gpar, int32_t g_node,
-                       double* __restrict__ out, int cap, PlanIO* io) {
-    if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    int ns = 0;
-    for (int32_t v = s_node; v >= 0; v = Spar[v]) ++ns;
-    int ng = 0;
-    for (int32_t v = g_node; v >= 0; v = Gpar[v]) ++ng;
-    if (ns + ng > cap) { io->n_raw = -1; return; }
-    int i = ns - 1;
-    for (int32_t v = s_node; v >= 0; v = Spar[v], --i)
-        for (int d = 0; d < NQ; ++d) out[i * NQ + d] = S[(int64_t)v * NQ + d];
-    i = ns;
-    for (int32_t v = g_node; v >= 0; v = Gpar[v], ++i)
-        for (int d = 0; d < NQ; ++d) out[i * NQ + d] = G[(int64_t)v * NQ + d];
-    io->n_raw = ns + ng;
+// solution path for host-chosen join nodes (approximate solutions, rank groups)
+__global__ void k_path(PathArgs pa, int32_t s_node, int32_t g_node, PlanIO* io) {
+    build_path(pa, s_node, g_node, io);
 }
 
-// compact index of shortcut (i, j), j >= i + 2, of an n-state path (row-major)
-__device__ __forceinline__ int pair_index(int i, int j, int n) { return i * (n - 2) - i * (i - 1) / 2 + (j - i - 2); }
-
-// shortcut candidates of the device path when 3 <= n_raw <= SMAX: edge
-// pair_index(i, j) for every j >= i + 2; *npairs = their count (0 otherwise).
-__global__ void k_shortcut_edges(const double* __restrict__ path, const PlanIO* __restrict__ io, double res,
-                                 double* __restrict__ from, double* __restrict__ to, int* __restrict__ nd,
-                                 uint8_t* __restrict__ valid, int* npairs) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    const int n = io->n_raw;
-    const bool on = n >= 3 && n <= SMAX;
-    if (e == 0) *npairs = on ? (n - 1) * (n - 2) / 2 : 0;
-    if (!on || e >= SMAX * SMAX) return;
-    const int i = e / SMAX, j = e - i * SMAX;
-    if (j < i + 2 || j >= n) return;
-    const int k = pair_index(i, j, n);
-    for (int d = 0; d < NQ; ++d) {
-        from[(int64_t)k * NQ + d] = path[i * NQ + d];
-        to[(int64_t)k * NQ + d] = path[j * NQ + d];
-    }
-    nd[k] = segment_count(path + i * NQ, path + j * NQ, res);
-    valid[k] = 1;
-}
-
-// output record (single lane): the greedy farthest-valid walk over the checked
-// shortcuts (simplify) or the raw path, when n_raw <= SMAX; counter snapshot.
+// output record (64 lanes) straight into the host mirror: status words, the
+// greedy farthest-valid walk over the checked shortcuts (simplify) or the raw
+// path when 0 < n_raw <= SMAX, the states-checked counter; then seq. Ends every
+// single-rank iteration (no path yet: n_raw = 0) and every post-processing.
 __global__ void k_path_out(const double* __restrict__ path, const uint8_t* __restrict__ valid, int simplify,
-                           const unsigned long long* __restrict__ counter, PlanIO* io) {
-    if (blockIdx.x != 0 || threadIdx.x != 0) return;
-    io->counter = *counter;
+                           const unsigned long long* __restrict__ counter, const PlanIO* __restrict__ io,
+                           PlanIO* hio, int seq) {
+    __shared__ int sel[SMAX];
+    __shared__ int m_sh;
     const int n = io->n_raw;
-    if (n < 0 || n > SMAX) { io->n_out = 0; return; }
-    double* out = io->path;
-    if (!simplify || n < 3) {
-        for (int k = 0; k < n * NQ; ++k) out[k] = path[k];
-        io->n_out = n;
-        return;
+    if (threadIdx.x == 0) {
+        int m = 0;
+        if (n >= 0 && n <= SMAX) {
+            if (!simplify || n < 3) {
+                for (int k = 0; k < n; ++k) sel[m++] = k;
+            } else {
+                sel[m++] = 0;
+                int i = 0;
+                while (i < n - 1) {
+                    int j = n - 1;
+                    while (j > i + 1 && !valid[pair_index(i, j, n)]) --j;
+                    sel[m++] = j;
+                    i = j;
+                }
+            }
+        }
+        m_sh = m;
+#pragma unroll
+        for (int w = 0; w < ST_WORDS; ++w) hio->status[w] = io->status[w];
+        hio->n_raw = n;
+        hio->n_out = m;
+        hio->counter = *counter;
     }
-    for (int d = 0; d < NQ; ++d) out[d] = path[d];
-    int m = 1, i = 0;
-    while (i < n - 1) {
-        int j = n - 1;
-        while (j > i + 1 && !valid[pair_index(i, j, n)]) --j;
-        for (int d = 0; d < NQ; ++d) out[m * NQ + d] = path[j * NQ + d];
-        ++m;
-        i = j;
+    __syncthreads();
+    const int m = m_sh;
+    for (int k = threadIdx.x; k < m * NQ; k += blockDim.x) {
+        const int r = k / NQ, d = k - r * NQ;
+        hio->path[k] = path[sel[r] * NQ + d];
     }
-    io->n_out = m;
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) publish_seq(hio, seq);
 }
 
 // approximate solution: argmin over candidate start-tree nodes of dist2(node, goal),

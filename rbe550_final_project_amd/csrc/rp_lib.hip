@@ -114,6 +114,7 @@ struct rp_ctx {
     DevBuf<double> path;                 // raw solution path (PATH_CAP states)
     DevBuf<PlanIO> io;                   // iteration status + output record (rp_kernels.h)
     PlanIO* h_io = nullptr;              // its pinned host mirror
+    int seq = 0;                         // last publication number awaited on h_io
     DevBuf<DI> partial;
 
     // rank group
@@ -328,6 +329,28 @@ bool out_of_bounds(const double* q, const double* lo, const double* hi) {
     return false;
 }
 
+// Wait for a kernel to publish `seq` into the host mirror (rp_kernels.h PlanIO).
+// Spins on the host-coherent word; polls the stream now and then so that a failed
+// or finished-without-publishing stream turns into an error instead of a hang.
+void wait_seq(rp_ctx* c, int seq) {
+    const volatile int* f = &c->h_io->seq;
+    for (uint64_t spin = 1;; ++spin) {
+        if (*f == seq) break;
+        if ((spin & 4095) == 0) {
+            const hipError_t e = hipStreamQuery(c->stream);
+            if (e == hipSuccess) {
+                if (*f == seq) break;
+                throw HipError{"plan status was not published"};
+            }
+            if (e != hipErrorNotReady) HIP_TRY(e);
+        }
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+        __builtin_ia32_pause();
+#endif
+    }
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+}
+
 // ---------------------------------------------------------------------------
 // the batched RRT-Connect solve
 // ---------------------------------------------------------------------------
@@ -376,7 +399,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         t.cand.ensure(cap);
         t.n = 0;
     }
-    const int64_t ne = std::max<int64_t>({PMAX, ((BMAX + world - 1) / world) * cmax, (int64_t)SMAX * SMAX});
+    const int64_t ne = std::max<int64_t>({PMAX + 2, ((BMAX + world - 1) / world) * cmax, (int64_t)SMAX * SMAX});
     c->efrom.ensure(ne * NQ);
     c->eto.ensure(ne * NQ);
     c->nd.ensure(ne);
@@ -395,7 +418,10 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     c->scalar.ensure(16);
     c->counter.ensure(1);
     c->io.ensure(1);
-    if (!c->h_io) HIP_TRY(hipHostMalloc((void**)&c->h_io, sizeof(PlanIO), hipHostMallocDefault));
+    if (!c->h_io) {
+        HIP_TRY(hipHostMalloc((void**)&c->h_io, sizeof(PlanIO), hipHostMallocCoherent));
+        c->h_io->seq = c->seq;
+    }
     c->q32.ensure(2 * NQ);
     c->flags.ensure(2);
     c->path.ensure((size_t)PATH_CAP * NQ);
@@ -408,18 +434,20 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         HIP_TRY(hipStreamSynchronize(c->stream));
     };
 
-    // Prologue: tree roots and counters from kernel arguments, then start / goal
-    // validity into the status record. No host sync here: single-rank plans read
-    // the flags back with the first iteration's status (a plan with an invalid
-    // start or goal discards that iteration).
+    // Prologue: tree roots and counters from kernel arguments. Single rank with
+    // in-bounds endpoints: start and goal ride along as two zero-length edges of
+    // the first extension launch and their flags come back with the first
+    // iteration's status (a plan with an invalid start or goal discards that
+    // iteration). Otherwise: a validity launch and a read-back before the loop.
+    const bool oob = out_of_bounds(start, lo, hi) || out_of_bounds(goal, lo, hi);
+    const int64_t sg_edge = (world == 1 && !oob) ? p.batch_min : -1;
     {
         PlanRoots roots;
         for (int i = 0; i < NQ; ++i) { roots.start[i] = start[i]; roots.goal[i] = goal[i]; }
         hipLaunchKernelGGL(k_plan_init, dim3(1), dim3(64), 0, c->stream, roots, c->tree[0].q.p, c->tree[0].par.p,
                            c->tree[0].cand.p, c->tree[1].q.p, c->tree[1].par.p, c->tree[1].cand.p, c->q32.p,
-                           c->counter.p, io);
+                           c->counter.p, io, sg_edge, c->efrom.p, c->eto.p, c->nd.p, c->valid.p);
         HIP_TRY(hipGetLastError());
-        launch_validity(c, c->q32.p, 2, (uint8_t*)(status + ST_SG), c->stream);
         for (auto& t : c->tree) t.n = 1;
     }
     // OMPL's PlannerInputStates: bounds and validity of start, then goal
@@ -435,14 +463,42 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         *status_out = code;
         return RP_OK;
     };
-    bool sg_known = false;
-    if (world > 1 || out_of_bounds(start, lo, hi) || out_of_bounds(goal, lo, hi)) {
-        // rank groups agree on the endpoints before the first exchange
+    auto check_endpoints_now = [&]() {
+        launch_validity(c, c->q32.p, 2, (uint8_t*)(status + ST_SG), c->stream);
         read_status();
-        if (const int code = endpoint_status(h->status[ST_SG])) return endpoint_fail(code);
+        return endpoint_status(h->status[ST_SG]);
+    };
+    bool sg_known = false;
+    if (sg_edge < 0) {
+        if (const int code = check_endpoints_now()) return endpoint_fail(code);
         sg_known = true;
     }
-    c->stats.states_checked = 2;
+    // start / goal count as 2 checked states (in the edge counter when they ride along)
+    c->stats.states_checked = sg_edge < 0 ? 2 : 0;
+    // shortcut checks (gated by the device candidate count) + output record
+    auto post_tail = [&](int seq) {
+        if (p.simplify)
+            launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, (SMAX - 1) * (SMAX - 2) / 2, kfull, 0, c->valid.p, 1,
+                         nullptr, c->stream, c->scalar.p, 1);
+        hipLaunchKernelGGL(k_path_out, dim3(1), dim3(64), 0, c->stream, (const double*)c->path.p,
+                           (const uint8_t*)c->valid.p, p.simplify ? 1 : 0, (const unsigned long long*)c->counter.p,
+                           (const PlanIO*)io, h, seq);
+        HIP_TRY(hipGetLastError());
+    };
+    PathArgs pa;
+    pa.S = c->tree[0].q.p;
+    pa.Spar = c->tree[0].par.p;
+    pa.G = c->tree[1].q.p;
+    pa.Gpar = c->tree[1].par.p;
+    pa.out = c->path.p;
+    pa.cap = PATH_CAP;
+    pa.simplify = p.simplify ? 1 : 0;
+    pa.res = p.resolution;
+    pa.efrom = c->efrom.p;
+    pa.eto = c->eto.p;
+    pa.nd = c->nd.p;
+    pa.valid = c->valid.p;
+    pa.npairs = c->scalar.p;
 
     Bounds bd;
     for (int i = 0; i < NQ; ++i) { bd.lo[i] = lo[i]; bd.hi[i] = hi[i]; }
@@ -467,8 +523,9 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                            g0, (int64_t)rank * per, per, bd, p.range, p.resolution, a_start, c->efrom.p, c->eto.p,
                            c->nd.p, c->valid.p, c->near_.p);
         HIP_TRY(hipGetLastError());
-        launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, per, kmax, a_start ? 0 : 1, c->valid.p, 1, nullptr,
-                     c->stream);
+        const int64_t sg = (iter == 0) ? sg_edge : -1;   // == per when riding along
+        launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, per + (sg >= 0 ? 2 : 0), kmax, a_start ? 0 : 1, c->valid.p,
+                     1, nullptr, c->stream);
         c->stats.edges_checked += per;
         c->stats.samples += B;
 
@@ -476,15 +533,23 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             // ---- single rank: device-side counts, one host sync per iteration;
             // batches <= FUSE_MAX use the single-block accept kernels
             const bool fused = B <= FUSE_MAX;
+            const int seq = ++c->seq;
             if (fused) {
-                hipLaunchKernelGGL(k_ext_accept_small, dim3(1), dim3(FUSE_THREADS), 0, c->stream, c->valid.p,
-                                   c->near_.p, B, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA, status);
+                if (B <= FUSE_THREADS)
+                    hipLaunchKernelGGL(k_ext_accept_small<1>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, c->valid.p,
+                                       c->near_.p, B, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA, status,
+                                       sg);
+                else
+                    hipLaunchKernelGGL(k_ext_accept_small<4>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, c->valid.p,
+                                       c->near_.p, B, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA, status,
+                                       sg);
             } else {
                 hipLaunchKernelGGL(k_ext_result_flag, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream,
                                    c->valid.p, c->near_.p, B, c->res.p, c->acc.p);
                 scan_incl(c, c->acc.p, c->incl.p, B);
                 hipLaunchKernelGGL(k_ext_append, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->res.p,
-                                   c->incl.p, B, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA, status);
+                                   c->incl.p, B, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA, status,
+                                   (const uint8_t*)c->valid.p, sg);
             }
             hipLaunchKernelGGL(k_conn_nn, dim3(blocks_for(B, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
                                (int64_t)0, B, Bt.q.p, TB, p.range, p.resolution, cmax, a_start, c->efrom.p,
@@ -493,9 +558,13 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, B * cmax, kmax, a_start ? 1 : 0, c->valid.p, cmax,
                          c->gfail.p, c->stream, status, cmax);
             if (fused) {
-                hipLaunchKernelGGL(k_conn_accept_small, dim3(1), dim3(FUSE_THREADS), 0, c->stream, c->yv.p, c->mv.p,
-                                   c->gfail.p, status, A.q.p, TA, Bt.q.p, Bt.par.p, Bt.cand.p, TB, p.range, cmax,
-                                   a_start, A.cand.p, A.par.p, c->chain_end.p);
+#define RP_CONN_SMALL(IT)                                                                                        \
+    hipLaunchKernelGGL(k_conn_accept_small<IT>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, c->yv.p, c->mv.p,      \
+                       c->gfail.p, status, A.q.p, TA, Bt.q.p, Bt.par.p, Bt.cand.p, TB, p.range, cmax, a_start,   \
+                       A.cand.p, A.par.p, c->chain_end.p, pa, io)
+                if (B <= FUSE_THREADS) RP_CONN_SMALL(1);
+                else RP_CONN_SMALL(4);
+#undef RP_CONN_SMALL
             } else {
                 hipLaunchKernelGGL(k_conn_record_len, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->yv.p,
                                    c->mv.p, c->gfail.p, (const int*)status, B, c->rec.p, c->Lv.p);
@@ -503,11 +572,13 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                 hipLaunchKernelGGL(k_conn_append, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->rec.p,
                                    c->incl.p, B, A.q.p, TA, Bt.q.p, Bt.par.p, Bt.cand.p, TB, p.range, cmax,
                                    a_start, A.cand.p, status + ST_FIRST, c->chain_end.p, (const int*)status);
-                hipLaunchKernelGGL(k_finalize, dim3(1), dim3(64), 0, c->stream, status, c->incl.p, TA, a_start,
-                                   A.par.p, Bt.par.p, c->chain_end.p);
+                hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, c->stream, status, c->incl.p, TA, a_start,
+                                   A.par.p, Bt.par.p, c->chain_end.p, pa, io);
             }
-            HIP_TRY(hipGetLastError());
-            read_status();
+            // the output stage runs every iteration (empty unless this one solved),
+            // so a solving iteration needs no second host round trip
+            post_tail(seq);
+            wait_seq(c, seq);
             if (!sg_known) {
                 if (const int code = endpoint_status(h->status[ST_SG])) return endpoint_fail(code);
                 sg_known = true;
@@ -539,7 +610,8 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         hipLaunchKernelGGL(k_flag, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->res.p, B, c->acc.p);
         scan_incl(c, c->acc.p, c->incl.p, B);
         hipLaunchKernelGGL(k_ext_append, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->res.p, c->incl.p, B,
-                           p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA, (int*)nullptr);
+                           p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA, (int*)nullptr,
+                           (const uint8_t*)nullptr, (int64_t)-1);
         HIP_TRY(hipGetLastError());
         const int32_t nacc = read_scalar(c, c->incl.p + (B - 1));
         A.n = TA + nacc;
@@ -592,8 +664,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         }
     }
     if (!sg_known) {   // the loop ran no iteration
-        read_status();
-        if (const int code = endpoint_status(h->status[ST_SG])) return endpoint_fail(code);
+        if (const int code = check_endpoints_now()) return endpoint_fail(code);
     }
     c->stats.iterations = iter;
     c->stats.solve_ms = 1e3 * (now_s() - t_solve);
@@ -624,21 +695,18 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     *status_out = solved ? RP_STATUS_EXACT : RP_STATUS_APPROXIMATE;
 
     // path extraction (+ shortcut simplification for paths of <= SMAX states) on the
-    // device, then ONE read-back of the output record
+    // device; a solved single-rank iteration has already written the path and the
+    // shortcut candidates. The output record lands in the host mirror.
     const double t_simp = now_s();
-    hipLaunchKernelGGL(k_path, dim3(1), dim3(64), 0, c->stream, c->tree[0].q.p, c->tree[0].par.p, s_node,
-                       c->tree[1].q.p, c->tree[1].par.p, g_node, c->path.p, PATH_CAP, io);
-    if (p.simplify) {
-        hipLaunchKernelGGL(k_shortcut_edges, dim3(blocks_for(SMAX * SMAX, 256)), dim3(256), 0, c->stream, c->path.p,
-                           (const PlanIO*)io, p.resolution, c->efrom.p, c->eto.p, c->nd.p, c->valid.p, c->scalar.p);
-        launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, (SMAX - 1) * (SMAX - 2) / 2, kfull, 0, c->valid.p, 1, nullptr,
-                     c->stream, c->scalar.p, 1);
+    if (!(world == 1 && solved)) {
+        hipLaunchKernelGGL(k_path, dim3(1), dim3(256), 0, c->stream, pa, s_node, g_node, io);
+        HIP_TRY(hipGetLastError());
     }
-    hipLaunchKernelGGL(k_path_out, dim3(1), dim3(64), 0, c->stream, c->path.p, c->valid.p, p.simplify ? 1 : 0,
-                       (const unsigned long long*)c->counter.p, io);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(h, io, sizeof(PlanIO), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (!(world == 1 && solved)) {
+        const int seq = ++c->seq;
+        post_tail(seq);
+        wait_seq(c, seq);
+    }
     const int n_raw = h->n_raw;
     if (n_raw < 0) {
         c->err = "solution path longer than PATH_CAP";

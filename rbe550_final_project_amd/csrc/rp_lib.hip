@@ -12,6 +12,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -70,6 +71,7 @@ struct DevBuf {
 inline unsigned blocks_for(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
 constexpr int PATH_CAP = 1 << 16;   // states of a raw solution path (device buffer)
+constexpr int GRID_MIN_BOXES = 16;  // scenes with more boxes use the axis-grid broad phase
 
 }  // namespace
 
@@ -147,13 +149,17 @@ namespace {
 // launch helpers
 // ---------------------------------------------------------------------------
 
-// kernel instantiation for a cluster count (the cluster AABBs live in registers)
-int ncl_bucket(int n) { return n <= 0 ? 0 : n == 1 ? 1 : n == 2 ? 2 : n <= 4 ? 4 : 8; }
+// kernel instantiation: axis grid, or the cluster count (cluster AABBs in registers)
+int ncl_bucket(const DevScene& sc) {
+    const int n = sc.n_clusters;
+    return sc.grid ? NCL_GRID : n <= 0 ? 0 : n == 1 ? 1 : n == 2 ? 2 : n <= 4 ? 4 : 8;
+}
 
 void launch_validity(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, hipStream_t s) {
     if (n <= 0) return;
     const dim3 g(blocks_for(n, VBLOCK)), b(VBLOCK);
-    switch (ncl_bucket(c->scene.n_clusters)) {
+    switch (ncl_bucket(c->scene)) {
+        case NCL_GRID: hipLaunchKernelGGL(k_validity<NCL_GRID>, g, b, 0, s, q, n, flags, c->d_scene); break;
         case 0: hipLaunchKernelGGL(k_validity<0>, g, b, 0, s, q, n, flags, c->d_scene); break;
         case 1: hipLaunchKernelGGL(k_validity<1>, g, b, 0, s, q, n, flags, c->d_scene); break;
         case 2: hipLaunchKernelGGL(k_validity<2>, g, b, 0, s, q, n, flags, c->d_scene); break;
@@ -171,7 +177,8 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
     const dim3 g(blocks_for(threads, VBLOCK)), b(VBLOCK);
 #define RP_EDGES(N) hipLaunchKernelGGL(k_edges<N>, g, b, 0, s, from, to, nd, n, kmax, mode, valid, group, gfail, \
                                        c->counter.p, c->d_scene, dcount, per_item)
-    switch (ncl_bucket(c->scene.n_clusters)) {
+    switch (ncl_bucket(c->scene)) {
+        case NCL_GRID: RP_EDGES(NCL_GRID); break;
         case 0: RP_EDGES(0); break;
         case 1: RP_EDGES(1); break;
         case 2: RP_EDGES(2); break;
@@ -936,6 +943,30 @@ int rp_set_scene(rp_ctx* c, const rp_box* boxes, int32_t n, float plane_z, const
         std::memcpy(&cr[7], &cnt, 4);
     }
     c->scene.n_boxes = n;
+    // axis grid for many-box scenes (rp_model.h); RBE_SCENE_GRID=0/1 forces it
+    {
+        DevScene& S = c->scene;
+        const char* env = std::getenv("RBE_SCENE_GRID");
+        S.grid = env && *env ? (std::atoi(env) != 0 && n > 0) : (n > GRID_MIN_BOXES);
+        std::memset(S.grid_lo, 0, sizeof S.grid_lo);
+        std::memset(S.grid_hi, 0, sizeof S.grid_hi);
+        for (int a = 0; a < 3; ++a) {
+            float lo = 1e30f, hi = -1e30f;
+            for (int j = 0; j < n; ++j) {
+                lo = std::min(lo, S.box[j][8 + a]);
+                hi = std::max(hi, S.box[j][11 + a]);
+            }
+            S.grid_o[a] = n > 0 ? lo : 0.0f;
+            S.grid_s[a] = n > 0 ? (float)GRID_CELLS / std::max(hi - lo, 1e-6f) : 1.0f;
+            for (int j = 0; j < n; ++j) {
+                const unsigned long long bit = 1ull << j;
+                const int cl = std::max(grid_cell(S.box[j][8 + a], S.grid_o[a], S.grid_s[a]) - 1, 0);
+                const int ch = std::min(grid_cell(S.box[j][11 + a], S.grid_o[a], S.grid_s[a]) + 1, GRID_CELLS - 1);
+                for (int cc = cl; cc < GRID_CELLS; ++cc) S.grid_lo[a][cc] |= bit;
+                for (int cc = 0; cc <= ch; ++cc) S.grid_hi[a][cc] |= bit;
+            }
+        }
+    }
     c->scene.plane_z = plane_z;
     if (base)
         for (int k = 0; k < 3; ++k) c->scene.base[k] = base[k];

@@ -419,6 +419,8 @@ __device__ __forceinline__ int rank_in(unsigned long long m) {
 // Cluster AABBs of the scene, hoisted into (scalar) registers once per state: the
 // kernels are instantiated for NCL = 0, 1, 2, 4, 8 clusters; unused slots hold an
 // empty box (lo = +inf) that no capsule overlaps.
+constexpr int NCL_GRID = -1;   // broad-phase instantiation for axis-grid scenes
+
 template <int NCL>
 struct ClusterRegs {
     float c[NCL > 0 ? NCL : 1][8];
@@ -476,6 +478,21 @@ __device__ __forceinline__ void drain_sb(S& s) {
     s.nsb = 0;
 }
 
+// queue item of capsule C vs box record bx (box frame segment, half extents, r^2)
+template <int C, class S>
+__device__ __forceinline__ void enqueue_sb(const Capsules& k, const float* bx, float r, S& s,
+                                           unsigned long long m) {
+    float* it = s.Q->sb[s.nsb + rank_in(m)];
+    const float cs = bx[6], sn = bx[7];
+    float dx = k.a[C].x - bx[0], dy = k.a[C].y - bx[1];
+    it[0] = fma_(cs, dx, sn * dy); it[1] = fma_(cs, dy, -(sn * dx)); it[2] = k.a[C].z - bx[2];
+    dx = k.b[C].x - bx[0]; dy = k.b[C].y - bx[1];
+    it[3] = fma_(cs, dx, sn * dy); it[4] = fma_(cs, dy, -(sn * dx)); it[5] = k.b[C].z - bx[2];
+    it[6] = bx[3]; it[7] = bx[4]; it[8] = bx[5];
+    it[9] = r * r;
+    it[10] = __int_as_float(s.lane);
+}
+
 // capsule C vs plane (immediate) and boxes (queued)
 template <int C, int NCL>
 __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __restrict__ sc,
@@ -483,6 +500,32 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
     constexpr float r = CAP_GEOM[C][6];
     const Aabb u = capsule_aabb(k.a[C], k.b[C], r);
     if (u.lo.z <= s.plane_z) return true;  // capsule vs ground plane
+    if constexpr (NCL == NCL_GRID) {
+        // superset of the AABB-overlapping boxes from the axis grid (per-lane
+        // gathers), then the exact AABB test on each candidate, one per lane per
+        // round: rounds = the largest candidate count in the wave
+        unsigned long long m = ~0ull;
+        const float ulo[3] = {u.lo.x, u.lo.y, u.lo.z}, uhi[3] = {u.hi.x, u.hi.y, u.hi.z};
+#pragma unroll
+        for (int a = 0; a < 3; ++a)
+            m &= sc->grid_lo[a][grid_cell(uhi[a], sc->grid_o[a], sc->grid_s[a])] &
+                 sc->grid_hi[a][grid_cell(ulo[a], sc->grid_o[a], sc->grid_s[a])];
+        while (__any(m != 0)) {
+            bool cand = false;
+            const float* bx = sc->box[0];
+            if (m) {
+                bx = sc->box[__builtin_ctzll(m)];
+                m &= m - 1;
+                cand = !((__float_as_uint(bx[14]) >> C) & 1u) && !aabb_disjoint(u, bx + 8, bx + 11);
+            }
+            const unsigned long long bm = __ballot(cand);
+            if (!bm) continue;
+            if (cand) enqueue_sb<C>(k, bx, r, s, bm);
+            s.nsb += __popcll(bm);
+            if (s.nsb > QCAP - 64) drain_sb(s);
+        }
+        return false;
+    }
 #pragma unroll
     for (int cl = 0; cl < NCL; ++cl) {
         const float* cr = s.cl.c[cl];
@@ -494,17 +537,7 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
             const bool cand = near_cl && !((__float_as_uint(bx[14]) >> C) & 1u) && !aabb_disjoint(u, bx + 8, bx + 11);
             const unsigned long long m = __ballot(cand);
             if (!m) continue;
-            if (cand) {
-                float* it = s.Q->sb[s.nsb + rank_in(m)];
-                const float cs = bx[6], sn = bx[7];
-                float dx = k.a[C].x - bx[0], dy = k.a[C].y - bx[1];
-                it[0] = fma_(cs, dx, sn * dy); it[1] = fma_(cs, dy, -(sn * dx)); it[2] = k.a[C].z - bx[2];
-                dx = k.b[C].x - bx[0]; dy = k.b[C].y - bx[1];
-                it[3] = fma_(cs, dx, sn * dy); it[4] = fma_(cs, dy, -(sn * dx)); it[5] = k.b[C].z - bx[2];
-                it[6] = bx[3]; it[7] = bx[4]; it[8] = bx[5];
-                it[9] = r * r;
-                it[10] = __int_as_float(s.lane);
-            }
+            if (cand) enqueue_sb<C>(k, bx, r, s, m);
             s.nsb += __popcll(m);
             if (s.nsb > QCAP - 64) drain_sb(s);
         }

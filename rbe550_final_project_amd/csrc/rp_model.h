@@ -64,6 +64,14 @@ constexpr int MAX_CLUSTERS = MAX_BOXES / CLUSTER;
 //   [15] index of the box in the caller's order (boxes are stored cluster-sorted)
 // Cluster record: [0..2] AABB lo, [4..6] AABB hi (union of its boxes' AABBs),
 //   [3] first box, [7] box count (as int bits).
+// Axis grid (many-box scenes, `grid` = 1): per axis, GRID_CELLS cells over the
+//   boxes' extent; grid_lo[a][c] = boxes whose AABB-lo cell is <= c (widened by
+//   one cell), grid_hi[a][c] = boxes whose AABB-hi cell is >= c (widened). For a
+//   capsule AABB [u, v], grid_lo[a][cell(v)] & grid_hi[a][cell(u)] over the three
+//   axes is a superset of the boxes whose AABB overlaps it (cell() is monotone;
+//   the widening absorbs any host/device rounding difference), so the exact AABB
+//   test on that superset finds exactly the boxes the full scan would.
+constexpr int GRID_CELLS = 64;
 struct DevScene {
     float box[MAX_BOXES][16];
     float cluster[MAX_CLUSTERS][8];
@@ -71,7 +79,20 @@ struct DevScene {
     float plane_z;
     int n_boxes;
     int n_clusters;
-    int pad;
+    int grid;                    // 1: broad phase through the axis grid
+    float grid_o[4];             // per-axis origin, pad
+    float grid_s[4];             // per-axis cells per metre, pad
+    unsigned long long grid_lo[3][GRID_CELLS];
+    unsigned long long grid_hi[3][GRID_CELLS];
 };
+
+// cell of coordinate v on an axis with origin o and scale s (cells per metre),
+// clamped to [0, GRID_CELLS - 1]; monotone in v. Shared by host and device.
+__host__ __device__ inline int grid_cell(float v, float o, float s) {
+    float t = (v - o) * s;
+    t = t < 0.0f ? 0.0f : t;
+    t = t > (float)(GRID_CELLS - 1) ? (float)(GRID_CELLS - 1) : t;
+    return (int)t;
+}
 
 }  // namespace rp

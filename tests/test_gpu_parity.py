@@ -50,9 +50,14 @@ def _both(gpu_ctx, oracle_lib, sc, attached=-1):
     return o
 
 
+@pytest.mark.parametrize("grid", ["auto", "0", "1"])
 @pytest.mark.parametrize("name", list(SCENES))
-def test_validity_flags_bit_exact(gpu_ctx, oracle_lib, name):
+def test_validity_flags_bit_exact(gpu_ctx, oracle_lib, name, grid, monkeypatch):
+    """Both box broad phases (cluster AABBs, axis grid; RBE_SCENE_GRID forces one)
+    must give the oracle's flags."""
     sc = SCENES[name]
+    if grid != "auto":
+        monkeypatch.setenv("RBE_SCENE_GRID", grid)
     o = _both(gpu_ctx, oracle_lib, sc)
     q = np.concatenate([_uniform(65536, 1), _near(model.SAFE_HOME, 65536, 2)])
     g = gpu_ctx.check_states(q)

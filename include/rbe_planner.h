@@ -111,7 +111,9 @@ typedef struct rp_plan_params {
     double timeout_s;       /* wall-clock budget of the solve, default 5.0 (planning.py:63) */
     int64_t max_iters;      /* iteration cap (deterministic tests), default unlimited        */
     int32_t n_waypoints;    /* path.interpolate(n) (planning.py:198), default 100; 0 = none */
-    int32_t simplify;       /* 1 = simplify the solution (smooth_path, planning.py:195)     */
+    int32_t simplify;       /* smooth_path (planning.py:195-196): 0 = off; 1 = simplifyMax
+                               structure (shortcuts + B-spline rounds);
+                               2 = vertex shortcuts only                                */
     int64_t tree_capacity;  /* nodes per tree, default 1<<22                                */
 } rp_plan_params;
 

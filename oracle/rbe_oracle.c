@@ -629,11 +629,27 @@ static int walk(const tree_t* t, int32_t node, double* out, int cap) {
     return n;
 }
 
+/* Path simplification: a deterministic restatement of the
+ * structure of OMPL PathSimplifier::simplifyMax [EXT-OMPL] (planning.py:195-196):
+ * reduceVertices + collapseCloseVertices -> a greedy farthest-valid shortcut over
+ * all vertex pairs; smoothBSpline(path, 3, length / 100) restated exactly (it is
+ * deterministic in OMPL); its subdivision midpoints then give the next reduction
+ * the segment-interior shortcut points of shortcutPath. Rounds repeat while the
+ * path gets shorter. Level 1 = all of it, level 2 = the shortcut only. */
 #define SIMPLIFY_MAXN 1024
+#define SIMPLIFY_ROUNDS 2
+#define SMOOTH_STEPS 3
+#define SMOOTH_MAX 256   /* a smoothing round runs only if 8n - 7 <= SMOOTH_MAX */
 
-/* greedy vertex reduction: from each kept vertex jump to the
- * farthest later vertex with a valid straight edge. */
-static int simplify_path(const ro_scene* s, double* path, int n, double res, int64_t* states) {
+static double path_length(const double* P, int n) {
+    double L = 0.0;
+    for (int i = 0; i + 1 < n; ++i) L = L + sqrt(dist2(P + NQ * i, P + NQ * (i + 1)));
+    return L;
+}
+
+/* greedy vertex reduction: from each kept vertex jump to the farthest later
+ * vertex with a valid straight edge */
+static int reduce_vertices(const ro_scene* s, double* path, int n, double res, int64_t* states) {
     if (n < 3 || n > SIMPLIFY_MAXN) return n;
     double* out = (double*)malloc(sizeof(double) * NQ * n);
     int m = 0, i = 0;
@@ -648,6 +664,66 @@ static int simplify_path(const ro_scene* s, double* path, int n, double res, int
     memcpy(path, out, sizeof(double) * NQ * m);
     free(out);
     return m;
+}
+
+/* OMPL PathSimplifier::smoothBSpline(path, steps, min_change) [EXT-OMPL]; P has
+ * room for 2^steps (n - 1) + 1 states */
+static int smooth_bspline(const ro_scene* s, double* P, int n, int steps, double min_change, double res,
+                          int64_t* states) {
+    if (n < 3) return n;
+    double* Q = (double*)malloc(sizeof(double) * NQ * (2 * n));
+    for (int step = 0; step < steps; ++step) {
+        /* PathGeometric::subdivide: a midpoint between every pair of states */
+        memcpy(Q, P, sizeof(double) * NQ);
+        for (int k = 1; k < n; ++k) {
+            interp(P + NQ * (k - 1), P + NQ * k, 0.5, Q + NQ * (2 * k - 1));
+            memcpy(Q + NQ * (2 * k), P + NQ * k, sizeof(double) * NQ);
+        }
+        n = 2 * n - 1;
+        memcpy(P, Q, sizeof(double) * NQ * n);
+        Q = (double*)realloc(Q, sizeof(double) * NQ * (2 * n));
+        int u = 0;
+        for (int i = 2; i < n - 1; i += 2) {
+            double t1[NQ], t2[NQ];
+            const double* a = P + NQ * (i - 1);
+            const double* b = P + NQ * (i + 1);
+            ++*states;
+            if (!valid_d(s, a)) continue;
+            interp(a, P + NQ * i, 0.5, t1);
+            interp(P + NQ * i, b, 0.5, t2);
+            interp(t1, t2, 0.5, t1);
+            if (edge_valid(s, a, t1, 0, res, states) && edge_valid(s, t1, b, 0, res, states)) {
+                if (sqrt(dist2(P + NQ * i, t1)) > min_change) {
+                    memcpy(P + NQ * i, t1, sizeof(double) * NQ);
+                    ++u;
+                }
+            }
+        }
+        if (u == 0) break;
+    }
+    free(Q);
+    return n;
+}
+
+/* level 1: reduce, then rounds of smooth + reduce while the length decreases;
+ * level 2: reduce only. path has room for max(n, SMOOTH_MAX) states. */
+static int simplify_path(const ro_scene* s, double* path, int n, int level, double res, int64_t* states) {
+    if (n < 3 || n > SIMPLIFY_MAXN || level <= 0) return n;
+    n = reduce_vertices(s, path, n, res, states);
+    if (level == 2) return n;
+    double* Q = (double*)malloc(sizeof(double) * NQ * SMOOTH_MAX);
+    for (int r = 0; r < SIMPLIFY_ROUNDS; ++r) {
+        if (n < 3 || 8 * n - 7 > SMOOTH_MAX) break;
+        const double L0 = path_length(path, n);
+        memcpy(Q, path, sizeof(double) * NQ * n);
+        int m = smooth_bspline(s, Q, n, SMOOTH_STEPS, L0 / 100.0, res, states);
+        m = reduce_vertices(s, Q, m, res, states);
+        if (!(path_length(Q, m) < L0)) break;
+        memcpy(path, Q, sizeof(double) * NQ * m);
+        n = m;
+    }
+    free(Q);
+    return n;
 }
 
 int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], const double lo[NQ],
@@ -830,6 +906,7 @@ int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], co
 
     int rc = RP_OK;
     int64_t cap = T[0].n + T[1].n + 2;
+    if (cap < SMOOTH_MAX) cap = SMOOTH_MAX;   /* simplification may return more states than it got */
     double* raw = (double*)malloc(sizeof(double) * NQ * cap);
     int n_raw = 0;
     if (solved == 1) {
@@ -871,7 +948,7 @@ int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], co
     st.path_states_raw = n_raw;
     if (n_raw > 0) {
         double t0 = now_s();
-        if (p.simplify) n_raw = simplify_path(s, raw, n_raw, p.resolution, &st.states_checked);
+        if (p.simplify) n_raw = simplify_path(s, raw, n_raw, p.simplify, p.resolution, &st.states_checked);
         st.simplify_ms = 1e3 * (now_s() - t0);
         st.path_states_simplified = n_raw;
         int m = (p.n_waypoints > 0) ? ro_interpolate(raw, n_raw, p.n_waypoints, path_out, path_cap)

@@ -59,44 +59,49 @@ __global__ __launch_bounds__(VBLOCK, RP_VALIDITY_WAVES) void k_edges(const doubl
                                                   const DevScene* __restrict__ sc,
                                                   const int* __restrict__ dcount, int per_item) {
     __shared__ WaveQ wq;
-    // device-side edge count (planner iterations: dcount = accepted targets)
+    // device-side edge count (planner iterations: dcount = accepted targets); the
+    // grid may be smaller than the work (gated launches): grid-stride over it
     if (dcount) n_edges = min(n_edges, (int64_t)dcount[0] * per_item);
-    if ((int64_t)blockIdx.x * VBLOCK >= n_edges * kmax) return;
-    const int64_t idx = (int64_t)blockIdx.x * VBLOCK + threadIdx.x;
-    const int64_t e = idx / kmax;
-    const int slot = (int)(idx - e * kmax);
-    bool run = false;
-    int nde = -1;
-    if (e < n_edges) {
-        nde = nd[e];
-        const int slots = nde > 1 ? nde : 1;
-        run = nde >= 0 && slot < slots && valid[e] != 0;
-        if (run && gfail) {
-            const int g = (int)(e / group), s = (int)(e - (int64_t)g * group);
-            run = gfail[g] > s;
+    const int64_t total = n_edges * kmax;
+    for (int64_t base = (int64_t)blockIdx.x * VBLOCK; base < total; base += (int64_t)gridDim.x * VBLOCK) {
+        const int64_t idx = base + threadIdx.x;
+        const int64_t e = idx / kmax;
+        const int slot = (int)(idx - e * kmax);
+        bool run = false;
+        int nde = -1;
+        if (e < n_edges) {
+            nde = nd[e];
+            const int slots = nde > 1 ? nde : 1;
+            run = nde >= 0 && slot < slots && valid[e] != 0;
+            if (run && gfail) {
+                const int g = (int)(e / group), s = (int)(e - (int64_t)g * group);
+                run = gfail[g] > s;
+            }
         }
-    }
-    const unsigned long long ballot = __ballot(run);
-    if (counter && (threadIdx.x & 63) == 0 && ballot) atomicAdd(counter, (unsigned long long)__popcll(ballot));
-    if (!run) return;
-    double st[NQ];
-    const double* a = from + e * NQ;
-    const double* b = to + e * NQ;
-    if (slot == 0) {
-        const double* ep = mode ? a : b;
+        const unsigned long long ballot = __ballot(run);
+        if (counter && (threadIdx.x & 63) == 0 && ballot) atomicAdd(counter, (unsigned long long)__popcll(ballot));
+        if (!ballot) continue;
+        if (run) {
+            double st[NQ];
+            const double* a = from + e * NQ;
+            const double* b = to + e * NQ;
+            if (slot == 0) {
+                const double* ep = mode ? a : b;
 #pragma unroll
-        for (int k = 0; k < NQ; ++k) st[k] = ep[k];
-    } else {
-        interp(a, b, (double)slot / (double)nde, st);
-    }
-    float qq[NQ];
+                for (int k = 0; k < NQ; ++k) st[k] = ep[k];
+            } else {
+                interp(a, b, (double)slot / (double)nde, st);
+            }
+            float qq[NQ];
 #pragma unroll
-    for (int k = 0; k < NQ; ++k) qq[k] = (float)st[k];
-    if (state_collides<NCL>(qq, sc, wq)) {
-        valid[e] = 0;
-        if (gfail) {
-            const int g = (int)(e / group), s = (int)(e - (int64_t)g * group);
-            atomicMin(&gfail[g], s);
+            for (int k = 0; k < NQ; ++k) qq[k] = (float)st[k];
+            if (state_collides<NCL>(qq, sc, wq)) {
+                valid[e] = 0;
+                if (gfail) {
+                    const int g = (int)(e / group), s = (int)(e - (int64_t)g * group);
+                    atomicMin(&gfail[g], s);
+                }
+            }
         }
     }
 }
@@ -213,15 +218,16 @@ enum { ST_NACC = 0, ST_ADDED = 1, ST_FIRST = 2, ST_SNODE = 3, ST_GNODE = 4, ST_S
 // iteration, the output path at the end), written by the kernels themselves and
 // published by a release store of `seq` that the host spins on (no copy, no
 // stream synchronisation on the per-iteration round trip).
-constexpr int SMAX = 64;   // device-simplified paths: <= SMAX raw states
+constexpr int SPMAX = 256;   // device-simplified paths: <= SPMAX states (raw and smoothed)
 struct PlanIO {
     int status[ST_WORDS];
     int n_raw;                      // raw solution states (-1: longer than the path cap)
-    int n_out;                      // states in path[] (simplified when requested)
+    int n_out;                      // states in path[] (0: the host takes over)
     unsigned long long counter;     // snapshot of the states-checked counter
+    long long simp_edges;           // edges checked by the simplification
     int seq;                        // publication sequence number (host mirror)
-    int pad;
-    double path[SMAX * NQ];
+    int out;                        // 1: this publication carries the final output
+    double path[SPMAX * NQ];
 };
 
 __device__ __forceinline__ void publish_seq(PlanIO* hio, int seq) {
@@ -519,65 +525,31 @@ struct PathArgs {
     const int32_t* Gpar;
     double* out;          // raw path, `cap` states
     int cap;
-    int simplify;
-    double res;
-    double* efrom;        // shortcut candidate edges
-    double* eto;
-    int* nd;
-    uint8_t* valid;
-    int* npairs;          // candidate count (0: none)
 };
 
-// compact index of shortcut (i, j), j >= i + 2, of an n-state path (row-major)
-__device__ __forceinline__ int pair_index(int i, int j, int n) { return i * (n - 2) - i * (i - 1) / 2 + (j - i - 2); }
 
-// Block-cooperative (every thread calls it): lane 0 writes the solution path
-// (start branch root..s_node, goal branch g_node..root; g_node < 0: start branch
-// only; io->n_raw = -1 if longer than cap), then the block emits the shortcut
-// candidates (i, j >= i + 2) when simplifying a path of 3..SMAX states.
+// solution path (lane 0): start branch root..s_node, then goal branch g_node..root
+// (g_node < 0: start branch only); io->n_raw = -1 if longer than cap.
 __device__ void build_path(const PathArgs& pa, int32_t s_node, int32_t g_node, PlanIO* io) {
-    __shared__ int n_sh;
-    if (threadIdx.x == 0) {
-        int ns = 0, ng = 0;
-        for (int32_t v = s_node; v >= 0; v = pa.Spar[v]) ++ns;
-        for (int32_t v = g_node; v >= 0; v = pa.Gpar[v]) ++ng;
-        int n = ns + ng;
-        if (n > pa.cap) {
-            n = -1;
-        } else {
-            int i = ns - 1;
-            for (int32_t v = s_node; v >= 0; v = pa.Spar[v], --i)
-                for (int d = 0; d < NQ; ++d) pa.out[i * NQ + d] = pa.S[(int64_t)v * NQ + d];
-            i = ns;
-            for (int32_t v = g_node; v >= 0; v = pa.Gpar[v], ++i)
-                for (int d = 0; d < NQ; ++d) pa.out[i * NQ + d] = pa.G[(int64_t)v * NQ + d];
-        }
-        io->n_raw = n;
-        n_sh = n;
+    if (threadIdx.x != 0) return;
+    int ns = 0, ng = 0;
+    for (int32_t v = s_node; v >= 0; v = pa.Spar[v]) ++ns;
+    for (int32_t v = g_node; v >= 0; v = pa.Gpar[v]) ++ng;
+    if (ns + ng > pa.cap) {
+        io->n_raw = -1;
+        return;
     }
-    __syncthreads();
-    const int n = n_sh;
-    const bool on = pa.simplify && n >= 3 && n <= SMAX;
-    if (threadIdx.x == 0) *pa.npairs = on ? (n - 1) * (n - 2) / 2 : 0;
-    if (!on) return;
-    for (int e = threadIdx.x; e < SMAX * SMAX; e += blockDim.x) {
-        const int i = e / SMAX, j = e - i * SMAX;
-        if (j < i + 2 || j >= n) continue;
-        const int k = pair_index(i, j, n);
-        const double* a = pa.out + i * NQ;
-        const double* b = pa.out + j * NQ;
-        for (int d = 0; d < NQ; ++d) {
-            pa.efrom[(int64_t)k * NQ + d] = a[d];
-            pa.eto[(int64_t)k * NQ + d] = b[d];
-        }
-        pa.nd[k] = segment_count(a, b, pa.res);
-        pa.valid[k] = 1;
-    }
+    int i = ns - 1;
+    for (int32_t v = s_node; v >= 0; v = pa.Spar[v], --i)
+        for (int d = 0; d < NQ; ++d) pa.out[i * NQ + d] = pa.S[(int64_t)v * NQ + d];
+    i = ns;
+    for (int32_t v = g_node; v >= 0; v = pa.Gpar[v], ++i)
+        for (int d = 0; d < NQ; ++d) pa.out[i * NQ + d] = pa.G[(int64_t)v * NQ + d];
+    io->n_raw = ns + ng;
 }
 
 // block tail of the last kernel of an iteration: join nodes and, on success, the
-// solution path with its shortcut candidates (none otherwise). The status reaches
-// the host through k_path_out, which always follows.
+// solution path. The status reaches the host through k_simp, which follows.
 __device__ void iteration_tail(int* status, int added, int64_t TA, int a_start, const int32_t* Apar,
                                const int32_t* Bpar, const int32_t* chain_end, const PathArgs& pa, PlanIO* io) {
     __shared__ int sn, gn;
@@ -586,7 +558,6 @@ __device__ void iteration_tail(int* status, int added, int64_t TA, int a_start, 
         const bool ok = status[ST_FIRST] != 0x7fffffff;
         sn = ok ? status[ST_SNODE] : -2;
         gn = status[ST_GNODE];
-        if (!ok) *pa.npairs = 0;
     }
     __syncthreads();
     if (sn != -2) build_path(pa, sn, gn, io);
@@ -638,48 +609,214 @@ __global__ void k_path(PathArgs pa, int32_t s_node, int32_t g_node, PlanIO* io) 
     build_path(pa, s_node, g_node, io);
 }
 
-// output record (64 lanes) straight into the host mirror: status words, the
-// greedy farthest-valid walk over the checked shortcuts (simplify) or the raw
-// path when 0 < n_raw <= SMAX, the states-checked counter; then seq. Ends every
-// single-rank iteration (no path yet: n_raw = 0) and every post-processing.
-__global__ void k_path_out(const double* __restrict__ path, const uint8_t* __restrict__ valid, int simplify,
-                           const unsigned long long* __restrict__ counter, const PlanIO* __restrict__ io,
-                           PlanIO* hio, int seq) {
-    __shared__ int sel[SMAX];
-    __shared__ int m_sh;
-    const int n = io->n_raw;
-    if (threadIdx.x == 0) {
-        int m = 0;
-        if (n >= 0 && n <= SMAX) {
-            if (!simplify || n < 3) {
-                for (int k = 0; k < n; ++k) sel[m++] = k;
-            } else {
-                sel[m++] = 0;
-                int i = 0;
-                while (i < n - 1) {
-                    int j = n - 1;
-                    while (j > i + 1 && !valid[pair_index(i, j, n)]) --j;
-                    sel[m++] = j;
-                    i = j;
+// ---------------------------------------------------------------------------
+// path simplification (oracle/rbe_oracle.c simplify_path)
+// ---------------------------------------------------------------------------
+// A fixed program of k_simp steps (one block) alternating with gated edge launches
+// (device count ss->nedges): each step applies the previous stage's edge results
+// and prepares the next stage's candidate edges. Stages: REDUCE (greedy
+// farthest-valid shortcut over all vertex pairs) and SMOOTH (one pass of OMPL
+// smoothBSpline: subdivide, then for every original interior vertex i the checks
+// valid(P[i-1]), motion(P[i-1] -> t), motion(t -> P[i+1]) of its corner cut t).
+// Rounds (ROUND_BEGIN .. ROUND_END) keep their result only if the path got shorter.
+enum : int {
+    OP_BEGIN = 1, OP_APPLY_REDUCE = 2, OP_APPLY_SMOOTH = 4, OP_ROUND_END = 8, OP_ROUND_BEGIN = 16,
+    OP_PREP_REDUCE = 32, OP_PREP_SMOOTH = 64, OP_OUT = 128, OP_STATUS = 256
+};
+constexpr int SIMPLIFY_ROUNDS = 2, SMOOTH_STEPS = 3;
+
+struct SimpState {
+    int n;          // states in P
+    int on;         // device simplification of this path (0 < level, n_raw <= dev_max <= SPMAX)
+    int done;       // nothing changes any more in this call
+    int stop;       // this round's smoothing stopped (a pass changed nothing)
+    int nprev;      // states at the round start
+    int nedges;     // candidate edges of the pending stage
+    int ncand;      // smoothing candidates of the pending stage
+    int changed;
+    long long edges_total;
+    double len0, min_change;
+    double P[SPMAX * NQ];
+    double Pprev[SPMAX * NQ];
+    double Q[SPMAX * NQ];          // subdivision scratch
+    double T[(SPMAX / 2) * NQ];    // corner cuts of the smoothing candidates
+};
+
+// compact index of shortcut (i, j), j >= i + 2, of an n-state path (row-major)
+__device__ __forceinline__ int pair_index(int i, int j, int n) { return i * (n - 2) - i * (i - 1) / 2 + (j - i - 2); }
+
+__device__ __forceinline__ double path_length(const double* P, int n) {
+    double L = 0.0;
+    for (int i = 0; i + 1 < n; ++i) L = L + sqrt(dist2(P + i * NQ, P + (i + 1) * NQ));
+    return L;
+}
+
+__device__ __forceinline__ void emit_edge(int e, const double* a, const double* b, double res, double* efrom,
+                                          double* eto, int* nd, uint8_t* valid) {
+    for (int d = 0; d < NQ; ++d) {
+        efrom[(int64_t)e * NQ + d] = a[d];
+        eto[(int64_t)e * NQ + d] = b[d];
+    }
+    nd[e] = segment_count(a, b, res);
+    valid[e] = 1;
+}
+
+__global__ __launch_bounds__(256) void k_simp(int ops, int level, int dev_max, double res,
+                                              const double* __restrict__ raw,
+                                              PlanIO* io, SimpState* ss, double* efrom, double* eto, int* nd,
+                                              uint8_t* valid, const unsigned long long* __restrict__ counter,
+                                              PlanIO* hio, int seq) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    if (ops & OP_BEGIN) {
+        if (tid == 0) {
+            const int n = io->n_raw;
+            ss->on = level > 0 && n >= 0 && n <= dev_max;
+            ss->n = ss->on ? n : 0;
+            ss->done = !(ss->on && n >= 3);
+            ss->stop = 0;
+            ss->nedges = 0;
+            ss->edges_total = 0;
+        }
+        __syncthreads();
+        for (int k = tid; k < ss->n * NQ; k += nt) ss->P[k] = raw[k];
+        __syncthreads();
+    }
+    if (ops & OP_APPLY_REDUCE) {
+        if (tid == 0 && !ss->done && ss->nedges > 0) {   // greedy walk, in place (writes trail reads)
+            const int n = ss->n;
+            int m = 1, i = 0;
+            while (i < n - 1) {
+                int j = n - 1;
+                while (j > i + 1 && !valid[pair_index(i, j, n)]) --j;
+                for (int d = 0; d < NQ; ++d) ss->P[m * NQ + d] = ss->P[j * NQ + d];
+                ++m;
+                i = j;
+            }
+            ss->n = m;
+        }
+        __syncthreads();
+    }
+    if (ops & OP_APPLY_SMOOTH) {
+        if (tid == 0) ss->changed = 0;
+        __syncthreads();
+        if (!ss->done && !ss->stop && ss->nedges > 0) {
+            for (int c = tid; c < ss->ncand; c += nt) {
+                if (!(valid[3 * c] && valid[3 * c + 1] && valid[3 * c + 2])) continue;
+                double* pi = ss->P + (2 * c + 2) * NQ;
+                const double* t = ss->T + c * NQ;
+                if (sqrt(dist2(pi, t)) > ss->min_change) {
+                    for (int d = 0; d < NQ; ++d) pi[d] = t[d];
+                    atomicOr(&ss->changed, 1);
                 }
             }
+            __syncthreads();
+            if (tid == 0 && !ss->changed) ss->stop = 1;
         }
-        m_sh = m;
+        __syncthreads();
+    }
+    if (ops & OP_ROUND_END) {
+        __shared__ int rollback;
+        if (tid == 0) {
+            rollback = !ss->done && !(path_length(ss->P, ss->n) < ss->len0);
+            if (rollback) {
+                ss->n = ss->nprev;
+                ss->done = 1;
+            }
+        }
+        __syncthreads();
+        if (rollback)
+            for (int k = tid; k < ss->n * NQ; k += nt) ss->P[k] = ss->Pprev[k];
+        __syncthreads();
+    }
+    if (ops & OP_ROUND_BEGIN) {
+        if (tid == 0 && !ss->done) {
+            const int n = ss->n;
+            if (n < 3 || 8 * n - 7 > SPMAX) {
+                ss->done = 1;
+            } else {
+                ss->nprev = n;
+                ss->len0 = path_length(ss->P, n);
+                ss->min_change = ss->len0 / 100.0;
+                ss->stop = 0;
+            }
+        }
+        __syncthreads();
+        if (!ss->done)
+            for (int k = tid; k < ss->n * NQ; k += nt) ss->Pprev[k] = ss->P[k];
+        __syncthreads();
+    }
+    if (ops & OP_PREP_REDUCE) {
+        const int n = ss->n;
+        const bool on = !ss->done && n >= 3;
+        if (on)
+            for (int e = tid; e < n * n; e += nt) {
+                const int i = e / n, j = e - i * n;
+                if (j >= i + 2) emit_edge(pair_index(i, j, n), ss->P + i * NQ, ss->P + j * NQ, res, efrom, eto, nd, valid);
+            }
+        if (tid == 0) ss->nedges = on ? (n - 1) * (n - 2) / 2 : 0;
+        __syncthreads();
+    }
+    if (ops & OP_PREP_SMOOTH) {
+        const bool on = !ss->done && !ss->stop;
+        if (on) {   // PathGeometric::subdivide
+            const int n = ss->n;
+            for (int k = tid; k < 2 * n - 1; k += nt) {
+                double* q = ss->Q + k * NQ;
+                if (k & 1) {
+                    interp(ss->P + (k / 2) * NQ, ss->P + (k / 2 + 1) * NQ, 0.5, q);
+                } else {
+                    for (int d = 0; d < NQ; ++d) q[d] = ss->P[(k / 2) * NQ + d];
+                }
+            }
+            __syncthreads();
+            for (int k = tid; k < (2 * n - 1) * NQ; k += nt) ss->P[k] = ss->Q[k];
+            __syncthreads();
+            const int n2 = 2 * n - 1, ncand = (n2 - 3) / 2;
+            for (int c = tid; c < ncand; c += nt) {
+                const int i = 2 * c + 2;
+                const double* a = ss->P + (i - 1) * NQ;
+                const double* b = ss->P + (i + 1) * NQ;
+                double t1[NQ], t2[NQ];
+                interp(a, ss->P + i * NQ, 0.5, t1);
+                interp(ss->P + i * NQ, b, 0.5, t2);
+                interp(t1, t2, 0.5, t1);
+                for (int d = 0; d < NQ; ++d) ss->T[c * NQ + d] = t1[d];
+                emit_edge(3 * c, a, a, res, efrom, eto, nd, valid);
+                emit_edge(3 * c + 1, a, t1, res, efrom, eto, nd, valid);
+                emit_edge(3 * c + 2, t1, b, res, efrom, eto, nd, valid);
+            }
+            __syncthreads();
+            if (tid == 0) {
+                ss->n = n2;
+                ss->ncand = ncand;
+                ss->nedges = 3 * ncand;
+            }
+        } else if (tid == 0) {
+            ss->nedges = 0;
+        }
+        __syncthreads();
+    }
+    if ((ops & (OP_PREP_REDUCE | OP_PREP_SMOOTH)) && tid == 0) ss->edges_total += ss->nedges;
+    if (ops & (OP_OUT | OP_STATUS)) {
+        // a status publication carries the output too once nothing is left to do
+        const int n_raw = io->n_raw;
+        const bool out = (ops & OP_OUT) != 0 || ss->done;
+        const int m = !out ? 0 : ss->on ? ss->n : (n_raw >= 0 && n_raw <= dev_max ? n_raw : 0);
+        const double* src = ss->on ? ss->P : raw;
+        for (int k = tid; k < m * NQ; k += nt) hio->path[k] = src[k];
+        if (tid == 0) {
 #pragma unroll
-        for (int w = 0; w < ST_WORDS; ++w) hio->status[w] = io->status[w];
-        hio->n_raw = n;
-        hio->n_out = m;
-        hio->counter = *counter;
+            for (int w = 0; w < ST_WORDS; ++w) hio->status[w] = io->status[w];
+            hio->n_raw = n_raw;
+            hio->n_out = m;
+            hio->counter = *counter;
+            hio->simp_edges = ss->edges_total;
+            hio->out = out ? 1 : 0;
+        }
+        __threadfence_system();
+        __syncthreads();
+        if (tid == 0) publish_seq(hio, seq);
     }
-    __syncthreads();
-    const int m = m_sh;
-    for (int k = threadIdx.x; k < m * NQ; k += blockDim.x) {
-        const int r = k / NQ, d = k - r * NQ;
-        hio->path[k] = path[sel[r] * NQ + d];
-    }
-    __threadfence_system();
-    __syncthreads();
-    if (threadIdx.x == 0) publish_seq(hio, seq);
 }
 
 // approximate solution: argmin over candidate start-tree nodes of dist2(node, goal),

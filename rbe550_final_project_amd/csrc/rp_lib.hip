@@ -115,6 +115,7 @@ struct rp_ctx {
     DevBuf<char> cub_tmp;
     DevBuf<double> path;                 // raw solution path (PATH_CAP states)
     DevBuf<PlanIO> io;                   // iteration status + output record (rp_kernels.h)
+    DevBuf<SimpState> simp;              // device path simplification state
     PlanIO* h_io = nullptr;              // its pinned host mirror
     int seq = 0;                         // last publication number awaited on h_io
     DevBuf<DI> partial;
@@ -134,7 +135,7 @@ struct rp_ctx {
         scalar.release(); counter.release(); efrom.release(); eto.release(); nd.release(); valid.release();
         near_.release(); res.release(); acc.release(); incl.release(); yv.release(); mv.release();
         rec.release(); Lv.release(); chain_end.release(); mine.release(); gfail.release();
-        cub_tmp.release(); path.release(); io.release(); partial.release();
+        cub_tmp.release(); path.release(); io.release(); simp.release(); partial.release();
         if (h_io) (void)hipHostFree(h_io);
         if (d_scene) (void)hipFree(d_scene);
         if (ev0) (void)hipEventDestroy(ev0);
@@ -171,10 +172,12 @@ void launch_validity(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, hipSt
 
 void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd, int64_t n, int kmax,
                   int mode, uint8_t* valid, int group, int* gfail, hipStream_t s, const int* dcount = nullptr,
-                  int per_item = 1) {
+                  int per_item = 1, unsigned max_blocks = 0) {
     if (n <= 0) return;
     const int64_t threads = n * (int64_t)kmax;
-    const dim3 g(blocks_for(threads, VBLOCK)), b(VBLOCK);
+    unsigned nb = blocks_for(threads, VBLOCK);
+    if (max_blocks && nb > max_blocks) nb = max_blocks;   // grid-stride (gated launches)
+    const dim3 g(nb), b(VBLOCK);
 #define RP_EDGES(N) hipLaunchKernelGGL(k_edges<N>, g, b, 0, s, from, to, nd, n, kmax, mode, valid, group, gfail, \
                                        c->counter.p, c->d_scene, dcount, per_item)
     switch (ncl_bucket(c->scene)) {
@@ -299,11 +302,30 @@ std::vector<double> interpolate_path(const std::vector<double>& P, int count) {
     return out;
 }
 
+// Host-driven simplification for raw paths longer than SPMAX states: the same
+// algorithm as the device program (k_simp) and the oracle (simplify_path), with
+// every stage's candidate edges checked in one batched launch.
 constexpr int SIMPLIFY_MAXN = 1024;
+constexpr int SMOOTH_MAX = SPMAX;    // a smoothing round runs only if 8n - 7 <= SMOOTH_MAX
 
-// Greedy vertex reduction: every candidate shortcut (i, j>i+1) is
-// checked in ONE batched edge launch; then the greedy farthest-valid walk.
-std::vector<double> simplify_path(rp_ctx* c, const std::vector<double>& P, double res) {
+double h_length(const std::vector<double>& P) {
+    double L = 0.0;
+    const int n = (int)(P.size() / NQ);
+    for (int i = 0; i + 1 < n; ++i) L = L + std::sqrt(h_dist2(&P[NQ * i], &P[NQ * (i + 1)]));
+    return L;
+}
+
+int64_t check_edge_list(rp_ctx* c, const std::vector<double>& qa, const std::vector<double>& qb, double res,
+                        std::vector<uint8_t>& ok) {
+    const int64_t ne = (int64_t)(qa.size() / NQ);
+    ok.assign(ne, 0);
+    c->stats.edges_checked += ne;
+    return check_edges_host(c, qa.data(), qb.data(), ne, res, ok.data());
+}
+
+// greedy vertex reduction: every candidate shortcut (i, j > i + 1) in one launch,
+// then the farthest-valid walk
+std::vector<double> reduce_host(rp_ctx* c, const std::vector<double>& P, double res) {
     const int n = (int)(P.size() / NQ);
     if (n < 3 || n > SIMPLIFY_MAXN) return P;
     std::vector<double> qa, qb;
@@ -314,10 +336,8 @@ std::vector<double> simplify_path(rp_ctx* c, const std::vector<double>& P, doubl
             qa.insert(qa.end(), &P[NQ * i], &P[NQ * i] + NQ);
             qb.insert(qb.end(), &P[NQ * j], &P[NQ * j] + NQ);
         }
-    const int64_t ne = (int64_t)(qa.size() / NQ);
-    std::vector<uint8_t> ok(ne);
-    c->stats.states_checked += check_edges_host(c, qa.data(), qb.data(), ne, res, ok.data());
-    c->stats.edges_checked += ne;
+    std::vector<uint8_t> ok;
+    c->stats.states_checked += check_edge_list(c, qa, qb, res, ok);
     std::vector<double> out(P.begin(), P.begin() + NQ);
     int i = 0;
     while (i < n - 1) {
@@ -327,6 +347,82 @@ std::vector<double> simplify_path(rp_ctx* c, const std::vector<double>& P, doubl
         i = j;
     }
     return out;
+}
+
+// OMPL smoothBSpline(path, steps, min_change): each pass's candidates in one launch
+std::vector<double> smooth_host(rp_ctx* c, std::vector<double> P, int steps, double min_change, double res) {
+    if (P.size() / NQ < 3) return P;
+    for (int step = 0; step < steps; ++step) {
+        const int n = (int)(P.size() / NQ);
+        std::vector<double> Q((size_t)(2 * n - 1) * NQ);
+        std::copy(P.begin(), P.begin() + NQ, Q.begin());
+        for (int k = 1; k < n; ++k) {
+            h_interp(&P[NQ * (k - 1)], &P[NQ * k], 0.5, &Q[NQ * (2 * k - 1)]);
+            std::copy(&P[NQ * k], &P[NQ * k] + NQ, &Q[NQ * (2 * k)]);
+        }
+        P.swap(Q);
+        const int n2 = 2 * n - 1, ncand = (n2 - 3) / 2;
+        std::vector<double> qa, qb, T((size_t)ncand * NQ);
+        for (int cnd = 0; cnd < ncand; ++cnd) {
+            const int i = 2 * cnd + 2;
+            const double* a = &P[NQ * (i - 1)];
+            const double* b = &P[NQ * (i + 1)];
+            double t1[NQ], t2[NQ];
+            h_interp(a, &P[NQ * i], 0.5, t1);
+            h_interp(&P[NQ * i], b, 0.5, t2);
+            h_interp(t1, t2, 0.5, t1);
+            std::copy(t1, t1 + NQ, &T[NQ * cnd]);
+            qa.insert(qa.end(), a, a + NQ); qb.insert(qb.end(), a, a + NQ);
+            qa.insert(qa.end(), a, a + NQ); qb.insert(qb.end(), t1, t1 + NQ);
+            qa.insert(qa.end(), t1, t1 + NQ); qb.insert(qb.end(), b, b + NQ);
+        }
+        std::vector<uint8_t> ok;
+        c->stats.states_checked += check_edge_list(c, qa, qb, res, ok);
+        int u = 0;
+        for (int cnd = 0; cnd < ncand; ++cnd) {
+            if (!(ok[3 * cnd] && ok[3 * cnd + 1] && ok[3 * cnd + 2])) continue;
+            double* pi = &P[NQ * (2 * cnd + 2)];
+            if (std::sqrt(h_dist2(pi, &T[NQ * cnd])) > min_change) {
+                std::copy(&T[NQ * cnd], &T[NQ * cnd] + NQ, pi);
+                ++u;
+            }
+        }
+        if (u == 0) break;
+    }
+    return P;
+}
+
+// level 1: reduce, then rounds of smooth + reduce kept while the path gets
+// shorter; level 2: reduce only
+std::vector<double> simplify_host(rp_ctx* c, std::vector<double> P, int level, double res) {
+    const int n0 = (int)(P.size() / NQ);
+    if (n0 < 3 || n0 > SIMPLIFY_MAXN || level <= 0) return P;
+    P = reduce_host(c, P, res);
+    if (level == 2) return P;
+    for (int r = 0; r < SIMPLIFY_ROUNDS; ++r) {
+        const int n = (int)(P.size() / NQ);
+        if (n < 3 || 8 * n - 7 > SMOOTH_MAX) break;
+        const double L0 = h_length(P);
+        std::vector<double> Q = reduce_host(c, smooth_host(c, P, SMOOTH_STEPS, L0 / 100.0, res), res);
+        if (!(h_length(Q) < L0)) break;
+        P.swap(Q);
+    }
+    return P;
+}
+
+// the device simplification program for a level (k_simp steps; an edge launch
+// follows every step that prepares candidates)
+std::vector<int> simplify_program(int level) {
+    if (level <= 0) return {OP_BEGIN | OP_OUT};
+    if (level == 2) return {OP_BEGIN | OP_PREP_REDUCE, OP_APPLY_REDUCE | OP_OUT};
+    std::vector<int> prog = {OP_BEGIN | OP_PREP_REDUCE};
+    for (int r = 0; r < SIMPLIFY_ROUNDS; ++r) {
+        prog.push_back(OP_APPLY_REDUCE | (r ? OP_ROUND_END : 0) | OP_ROUND_BEGIN | OP_PREP_SMOOTH);
+        for (int st = 1; st < SMOOTH_STEPS; ++st) prog.push_back(OP_APPLY_SMOOTH | OP_PREP_SMOOTH);
+        prog.push_back(OP_APPLY_SMOOTH | OP_PREP_REDUCE);
+    }
+    prog.push_back(OP_APPLY_REDUCE | OP_ROUND_END | OP_OUT);
+    return prog;
 }
 
 bool out_of_bounds(const double* q, const double* lo, const double* hi) {
@@ -406,7 +502,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         t.cand.ensure(cap);
         t.n = 0;
     }
-    const int64_t ne = std::max<int64_t>({PMAX + 2, ((BMAX + world - 1) / world) * cmax, (int64_t)SMAX * SMAX});
+    const int64_t ne = std::max<int64_t>({PMAX + 2, ((BMAX + world - 1) / world) * cmax, (int64_t)SPMAX * SPMAX / 2});
     c->efrom.ensure(ne * NQ);
     c->eto.ensure(ne * NQ);
     c->nd.ensure(ne);
@@ -425,6 +521,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     c->scalar.ensure(16);
     c->counter.ensure(1);
     c->io.ensure(1);
+    c->simp.ensure(1);
     if (!c->h_io) {
         HIP_TRY(hipHostMalloc((void**)&c->h_io, sizeof(PlanIO), hipHostMallocCoherent));
         c->h_io->seq = c->seq;
@@ -482,15 +579,28 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     }
     // start / goal count as 2 checked states (in the edge counter when they ride along)
     c->stats.states_checked = sg_edge < 0 ? 2 : 0;
-    // shortcut checks (gated by the device candidate count) + output record
-    auto post_tail = [&](int seq) {
-        if (p.simplify)
-            launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, (SMAX - 1) * (SMAX - 2) / 2, kfull, 0, c->valid.p, 1,
-                         nullptr, c->stream, c->scalar.p, 1);
-        hipLaunchKernelGGL(k_path_out, dim3(1), dim3(64), 0, c->stream, (const double*)c->path.p,
-                           (const uint8_t*)c->valid.p, p.simplify ? 1 : 0, (const unsigned long long*)c->counter.p,
-                           (const PlanIO*)io, h, seq);
-        HIP_TRY(hipGetLastError());
+    // simplification program steps [from, to) (rp_kernels.h k_simp); the last one
+    // publishes `seq` (with the output record when it is the program's end)
+    const int level = p.simplify < 0 ? 0 : p.simplify > 2 ? 1 : p.simplify;
+    const std::vector<int> prog = simplify_program(level);
+    const size_t tail_steps = level == 1 ? 2 : prog.size();   // run inside every single-rank iteration
+    // raw paths longer than dev_max states are simplified host-driven (same
+    // algorithm); RBE_SIMPLIFY_DEVICE_MAX lowers the limit (tests of that path)
+    int dev_max = SPMAX;
+    if (const char* e = std::getenv("RBE_SIMPLIFY_DEVICE_MAX"))
+        if (*e) dev_max = std::max(0, std::min(SPMAX, std::atoi(e)));
+    auto run_program = [&](size_t from, size_t to, int seq) {
+        for (size_t k = from; k < to; ++k) {
+            int ops = prog[k];
+            if (k + 1 == to) ops |= (ops & OP_OUT) ? 0 : OP_STATUS;
+            hipLaunchKernelGGL(k_simp, dim3(1), dim3(256), 0, c->stream, ops, level, dev_max, p.resolution,
+                               (const double*)c->path.p, io, c->simp.p, c->efrom.p, c->eto.p, c->nd.p, c->valid.p,
+                               (const unsigned long long*)c->counter.p, h, k + 1 == to ? seq : 0);
+            HIP_TRY(hipGetLastError());
+            if (ops & (OP_PREP_REDUCE | OP_PREP_SMOOTH))
+                launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, (int64_t)(SPMAX - 1) * (SPMAX - 2) / 2, kfull, 0,
+                             c->valid.p, 1, nullptr, c->stream, &c->simp.p->nedges, 1, 2048);
+        }
     };
     PathArgs pa;
     pa.S = c->tree[0].q.p;
@@ -499,13 +609,6 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     pa.Gpar = c->tree[1].par.p;
     pa.out = c->path.p;
     pa.cap = PATH_CAP;
-    pa.simplify = p.simplify ? 1 : 0;
-    pa.res = p.resolution;
-    pa.efrom = c->efrom.p;
-    pa.eto = c->eto.p;
-    pa.nd = c->nd.p;
-    pa.valid = c->valid.p;
-    pa.npairs = c->scalar.p;
 
     Bounds bd;
     for (int i = 0; i < NQ; ++i) { bd.lo[i] = lo[i]; bd.hi[i] = hi[i]; }
@@ -582,9 +685,9 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                 hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, c->stream, status, c->incl.p, TA, a_start,
                                    A.par.p, Bt.par.p, c->chain_end.p, pa, io);
             }
-            // the output stage runs every iteration (empty unless this one solved),
-            // so a solving iteration needs no second host round trip
-            post_tail(seq);
+            // the first simplification steps run every iteration (empty unless this
+            // one solved), so a solving iteration needs no extra host round trip
+            run_program(0, tail_steps, seq);
             wait_seq(c, seq);
             if (!sg_known) {
                 if (const int code = endpoint_status(h->status[ST_SG])) return endpoint_fail(code);
@@ -701,17 +804,18 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     }
     *status_out = solved ? RP_STATUS_EXACT : RP_STATUS_APPROXIMATE;
 
-    // path extraction (+ shortcut simplification for paths of <= SMAX states) on the
-    // device; a solved single-rank iteration has already written the path and the
-    // shortcut candidates. The output record lands in the host mirror.
+    // the rest of the simplification program on the device (a solving single-rank
+    // iteration has run its first steps); the output record lands in the host mirror
     const double t_simp = now_s();
-    if (!(world == 1 && solved)) {
-        hipLaunchKernelGGL(k_path, dim3(1), dim3(256), 0, c->stream, pa, s_node, g_node, io);
+    const bool tail_ran = world == 1 && solved;
+    if (!tail_ran) {
+        hipLaunchKernelGGL(k_path, dim3(1), dim3(64), 0, c->stream, pa, s_node, g_node, io);
         HIP_TRY(hipGetLastError());
     }
-    if (!(world == 1 && solved)) {
+    const size_t from = tail_ran ? tail_steps : 0;
+    if (from < prog.size() && !(tail_ran && h->out)) {
         const int seq = ++c->seq;
-        post_tail(seq);
+        run_program(from, prog.size(), seq);
         wait_seq(c, seq);
     }
     const int n_raw = h->n_raw;
@@ -720,17 +824,17 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         return RP_ERR_CAPACITY;
     }
     c->stats.states_checked += (int64_t)h->counter;
+    c->stats.edges_checked += h->simp_edges;
     c->stats.path_states_raw = n_raw;
     std::vector<double> raw;
-    if (n_raw <= SMAX) {
+    if (n_raw <= dev_max) {
         raw.assign(h->path, h->path + (size_t)h->n_out * NQ);
-        if (p.simplify && n_raw >= 3) c->stats.edges_checked += (int64_t)(n_raw - 1) * (n_raw - 2) / 2;
     } else {
-        // long path: read it back, simplify with host-driven batched edge checks
+        // long raw path: read it back, simplify with host-driven batched edge checks
         raw.resize((size_t)n_raw * NQ);
         HIP_TRY(hipMemcpyAsync(raw.data(), c->path.p, sizeof(double) * NQ * n_raw, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
-        if (p.simplify) raw = simplify_path(c, raw, p.resolution);
+        raw = simplify_host(c, raw, level, p.resolution);
     }
     c->stats.simplify_ms = 1e3 * (now_s() - t_simp);
     c->stats.path_states_simplified = (int64_t)(raw.size() / NQ);

@@ -163,14 +163,19 @@ def test_plan_parity(gpu_ctx, oracle_lib, wl, qi, batch, seed):
         (stats_ref["start_tree_size"], stats_ref["goal_tree_size"], stats_ref["iterations"])
 
 
-@pytest.mark.parametrize("simplify,rng", [(False, 0.3), (True, 0.3), (True, 0.15)])
-def test_plan_parity_hard_iterations(gpu_ctx, oracle_lib, simplify, rng):
-    """Many iterations with a small range (more nodes, more NN work, long raw paths:
-    > 64 states exercises the host-side simplification fallback): path equality."""
+@pytest.mark.parametrize("simplify,rng,dev_max", [(0, 0.3, ""), (1, 0.3, ""), (2, 0.3, ""), (1, 0.15, ""),
+                                                   (1, 0.15, "2"), (2, 0.3, "2")])
+def test_plan_parity_hard_iterations(gpu_ctx, oracle_lib, simplify, rng, dev_max, monkeypatch):
+    """Many iterations with a small range (more nodes, more NN work, long raw paths)
+    and every simplification level: path equality. dev_max "2" moves the
+    simplification to the host-driven fallback (raw paths > RBE_SIMPLIFY_DEVICE_MAX)."""
+    if dev_max:
+        monkeypatch.setenv("RBE_SIMPLIFY_DEVICE_MAX", dev_max)
     q = _wl("goal4_pentagon_10box")["queries"][8]
     sc = scenes.Scene.from_json(q["scene"])
     o = _both(gpu_ctx, oracle_lib, sc, q["attached"])
-    p = _abi.make_params(seed=21, batch=256, range_=rng, n_waypoints=0, simplify=simplify, timeout_s=120)
+    p = _abi.make_params(seed=21, batch=256, range_=rng, n_waypoints=0, timeout_s=120)
+    p.simplify = simplify
     ref, st_ref, s_ref = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
     path, st = gpu_ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
     assert st == st_ref
@@ -179,6 +184,28 @@ def test_plan_parity_hard_iterations(gpu_ctx, oracle_lib, simplify, rng):
     assert gs["start_tree_size"] == s_ref["start_tree_size"]
     assert gs["path_states_raw"] == s_ref["path_states_raw"]
     assert gs["path_states_simplified"] == s_ref["path_states_simplified"]
+
+
+@pytest.mark.parametrize("wl,qi", [("clutter64", 0), ("goal3_tallest_10box", 20)])
+@pytest.mark.parametrize("dev_max", ["", "2"])
+def test_plan_parity_smoothing(gpu_ctx, oracle_lib, wl, qi, dev_max, monkeypatch):
+    """Queries whose simplified path keeps corners, so the B-spline rounds change
+    it (oracle: level 1 shorter than level 2); device and host-driven paths."""
+    if dev_max:
+        monkeypatch.setenv("RBE_SIMPLIFY_DEVICE_MAX", dev_max)
+    q = _wl(wl)["queries"][qi]
+    sc = scenes.Scene.from_json(q["scene"])
+    o = _both(gpu_ctx, oracle_lib, sc, q["attached"])
+    lens = {}
+    for level in (2, 1):
+        p = _abi.make_params(seed=qi, batch=64, range_=0.15, n_waypoints=0, timeout_s=120)
+        p.simplify = level
+        ref, st_ref, _ = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+        path, st = gpu_ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+        assert st == st_ref == _abi.STATUS_EXACT
+        assert np.array_equal(path, ref)
+        lens[level] = float(np.sum(np.linalg.norm(np.diff(path, axis=0), axis=1)))
+    assert lens[1] < lens[2]
 
 
 def test_plan_invalid_start_goal(gpu_ctx, oracle_lib):

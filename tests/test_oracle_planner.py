@@ -134,3 +134,26 @@ def test_world_size_independence_gloo(oracle_lib, tmp_path, qi):
     ref, st, _ = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
     r0, r1 = _run_two_ranks(str(tmp_path), batch, seed, qi)
     assert np.array_equal(r0, ref) and np.array_equal(r1, ref)
+
+
+def test_oracle_simplification_levels(oracle_lib):
+    """Level 1 (shortcuts + B-spline rounds) never returns a longer path than level
+    2 (shortcuts only), which never returns a longer one than the raw path; all
+    three keep the endpoints."""
+    import json
+    import os
+    wl = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "workloads", "clutter64.json")))
+    q = wl["queries"][0]
+    sc = scenes.Scene.from_json(q["scene"])
+    o = oracle_lib.OracleScene()
+    o.set_scene(sc.boxes, sc.plane_z, sc.base)
+    o.set_attached(q["attached"])
+    lens = {}
+    for level in (0, 2, 1):
+        p = _abi.make_params(seed=0, batch=64, range_=0.15, n_waypoints=0, timeout_s=60)
+        p.simplify = level
+        path, st, _ = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+        assert st == _abi.STATUS_EXACT
+        assert np.allclose(path[0], q["start"]) and np.allclose(path[-1], q["goal"])
+        lens[level] = float(np.sum(np.linalg.norm(np.diff(path, axis=0), axis=1)))
+    assert lens[1] < lens[2] < lens[0]

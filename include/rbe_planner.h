@@ -18,6 +18,8 @@
  *                               interpolated path: RealVectorStateSpace bounds,
  *                               RRTConnect solve, simplifySolution,
  *                               path.interpolate(num_waypoints)                   code/planning.py:139-200
+ *   rp_ik                       robot.inverse_kinematics(link=hand, pos, quat) that
+ *                               makes plan_path's goals (Genesis, batched restarts)  code/motion_primitives.py:131-134
  *   rp_group_*                  (new) data-parallel sharding of each RRT-Connect
  *                               iteration across ranks with an all-gather;
  *                               the reference is single-process                   code/planning.py:121-122
@@ -117,6 +119,20 @@ typedef struct rp_plan_params {
     int64_t tree_capacity;  /* nodes per tree, default 1<<22                                */
 } rp_plan_params;
 
+/* rp_ik parameters (defaults follow Genesis inverse_kinematics). Zero / negative
+ * fields take the default shown. */
+typedef struct rp_ik_params {
+    uint64_t seed;          /* Philox key of the random restarts                          */
+    int32_t n_seeds;        /* restarts per target, restart 0 = init (max_samples), 256   */
+    int32_t iters;          /* damped-least-squares steps per restart, 64                  */
+    double damping;         /* 0.01                                                        */
+    double pos_tol;         /* position tolerance, 5e-4 m                                  */
+    double rot_tol;         /* orientation tolerance, 5e-3                                 */
+} rp_ik_params;
+
+/* rp_ik per-target status */
+enum { RP_IK_OK = 0, RP_IK_COLLIDING = 1, RP_IK_NOT_CONVERGED = 2 };
+
 /* Counters of the last call (per rank). */
 typedef struct rp_stats {
     int64_t states_checked;     /* validity evaluations actually executed             */
@@ -191,6 +207,18 @@ int rp_state_contacts(rp_ctx* ctx, const double q[RP_NQ], int32_t* pairs_out, in
 int rp_plan(rp_ctx* ctx, const double start[RP_NQ], const double goal[RP_NQ],
             const double lo[RP_NQ], const double hi[RP_NQ], const rp_plan_params* params,
             double* path_out, int32_t path_cap, int32_t* n_out, int32_t* status_out);
+
+/* Batched IK of the hand link: for each of n_targets poses (pos[3], quat[4] as
+ * w, x, y, z; world frame, robot base from rp_set_scene) run n_seeds damped-least-
+ * squares restarts on the 7 arm joints at once (restart 0 from init[t], the others
+ * from seeded samples; fingers stay at init[t]), check the converged ones against
+ * the current scene, and return per target the collision-free converged solution
+ * closest to init[t] (status RP_IK_OK), else the closest converged one
+ * (RP_IK_COLLIDING), else the restart with the smallest pose error
+ * (RP_IK_NOT_CONVERGED). q_out: n_targets x 9. */
+int rp_ik(rp_ctx* ctx, int32_t n_targets, const double* pos, const double* quat, const double* init,
+          const double lo[RP_NQ], const double hi[RP_NQ], const rp_ik_params* params, double* q_out,
+          int32_t* status_out);
 
 /* Data-parallel rank group. Each rank (one process per GPU) owns one context; the
  * caller allocates `send`/`recv` device buffers of `cap_bytes` and cap_bytes*world

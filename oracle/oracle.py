@@ -52,6 +52,12 @@ def lib():
         L.ro_seg_seg_d2.restype = C.c_float
         L.ro_seg_seg_d2.argtypes = [C.POINTER(C.c_float)] * 4
         L.ro_interpolate.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_int32]
+        L.ro_ik.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                            C.POINTER(_abi.IkParams), C.c_void_p, C.c_void_p]
+        L.ro_hand_pose.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+        L.ro_hand_pose.restype = None
+        L.ro_sincos64.argtypes = [C.c_double, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        L.ro_sincos64.restype = None
         _lib = L
     return _lib
 
@@ -115,6 +121,30 @@ class OracleScene:
         n = lib().ro_state_contacts(self.h, _ptr(q), _ptr(out), cap)
         return [tuple(x) for x in out[:min(n, cap)]]
 
+    def ik(self, pos, quat, init, lo, hi, params=None):
+        """ro_ik: the batched hand-link IK of rp_ik."""
+        pos = np.ascontiguousarray(pos, dtype=np.float64).reshape(-1, 3)
+        quat = np.ascontiguousarray(quat, dtype=np.float64).reshape(-1, 4)
+        init = np.ascontiguousarray(init, dtype=np.float64).reshape(-1, _abi.NQ)
+        lo = np.ascontiguousarray(lo, dtype=np.float64)
+        hi = np.ascontiguousarray(hi, dtype=np.float64)
+        n = len(pos)
+        p = params if params is not None else _abi.make_ik_params()
+        q = np.zeros((n, _abi.NQ), dtype=np.float64)
+        st = np.zeros(n, dtype=np.int32)
+        rc = lib().ro_ik(self.h, n, _ptr(pos), _ptr(quat), _ptr(init), _ptr(lo), _ptr(hi), C.byref(p), _ptr(q), _ptr(st))
+        assert rc == 0, rc
+        return q, st
+
+
+    def hand_pose(self, q):
+        """(R 3x3, p 3) of the hand link (the IK's float64 kinematics)."""
+        q = np.ascontiguousarray(q, dtype=np.float64)
+        R = np.zeros(9, dtype=np.float64)
+        p = np.zeros(3, dtype=np.float64)
+        lib().ro_hand_pose(self.h, _ptr(q), _ptr(R), _ptr(p))
+        return R.reshape(3, 3), p
+
     def plan(self, start, goal, lo, hi, params, rank=0, world=1, allgather=None, path_cap=4096):
         start = np.ascontiguousarray(start, dtype=np.float64)
         goal = np.ascontiguousarray(goal, dtype=np.float64)
@@ -131,6 +161,12 @@ class OracleScene:
         if rc:
             raise RuntimeError(f"ro_plan rc={rc}")
         return out[:n.value].copy(), status.value, st.as_dict()
+
+
+def sincos64(x):
+    s, c = C.c_double(), C.c_double()
+    lib().ro_sincos64(float(x), C.byref(s), C.byref(c))
+    return s.value, c.value
 
 
 def sincos(x):

@@ -402,17 +402,21 @@ void ro_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
 #define SAMPLE_TAG 0x52425035u
 
 /* uniform sample g in [lo, hi] */
-static void sample_state(uint64_t seed, uint64_t g, const double* lo, const double* hi, double* q) {
+static void sample_state_tag(uint64_t seed, uint64_t g, const double* lo, const double* hi, double* q,
+                             uint32_t tag) {
     uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
     uint32_t u[12];
     for (uint32_t j = 0; j < 3; ++j) {
-        uint32_t ctr[4] = {(uint32_t)g, (uint32_t)(g >> 32), j, SAMPLE_TAG};
+        uint32_t ctr[4] = {(uint32_t)g, (uint32_t)(g >> 32), j, tag};
         ro_philox(ctr, key, u + 4 * j);
     }
     for (int i = 0; i < NQ; ++i) {
         double x = (double)u[i] * 2.3283064365386962890625e-10;
         q[i] = lo[i] + (hi[i] - lo[i]) * x;
     }
+}
+static void sample_state(uint64_t seed, uint64_t g, const double* lo, const double* hi, double* q) {
+    sample_state_tag(seed, g, lo, hi, q, SAMPLE_TAG);
 }
 
 /* ------------------------------------------------------------------------- */
@@ -970,4 +974,216 @@ float ro_seg_box_d2(const float a[3], const float b[3], const float h[3]) { retu
 float ro_seg_seg_d2(const float a1[3], const float b1[3], const float a2[3], const float b2[3]) {
     v3 p = {a1[0], a1[1], a1[2]}, q = {b1[0], b1[1], b1[2]}, r = {a2[0], a2[1], a2[2]}, s = {b2[0], b2[1], b2[2]};
     return seg_seg_d2(p, q, r, s);
+}
+
+/* ------------------------------------------------------------------------- */
+/* hand-link inverse kinematics (rp_ik; Genesis robot.inverse_kinematics as    */
+/* called by code/motion_primitives.py:131-134 [EXT-GS])                       */
+/* ------------------------------------------------------------------------- */
+/* Damped least squares on the hand pose from n_seeds restarts per target
+ * (restart 0 = init, the others Philox samples with tag IK_TAG), float64 in a
+ * fixed operation order so the GPU lanes are reproduced bit for bit. */
+#define IK_TAG 0x524B494Bu
+
+/* sin / cos: Cody-Waite reduction by pi/2 and the fdlibm kernel polynomials */
+void ro_sincos64(double x, double* s, double* c) {
+    const double kd = rint(x * 6.36619772367581382433e-01);
+    const double r = (x - kd * 1.57079632673412561417e+00) - kd * 6.07710050650619224932e-11;
+    const double w = r * r;
+    double ps = 1.58969099521155010221e-10;
+    ps = -2.50507602534068634195e-08 + w * ps;
+    ps = 2.75573137070700676789e-06 + w * ps;
+    ps = -1.98412698298579493134e-04 + w * ps;
+    ps = 8.33333333332248946124e-03 + w * ps;
+    ps = -1.66666666666666324348e-01 + w * ps;
+    const double sn = r + r * w * ps;
+    double pc = -1.13596475577881948265e-11;
+    pc = 2.08757232129817482790e-09 + w * pc;
+    pc = -2.75573143513906633035e-07 + w * pc;
+    pc = 2.48015872894767294178e-05 + w * pc;
+    pc = -1.38888888888741095749e-03 + w * pc;
+    pc = 4.16666666666666019037e-02 + w * pc;
+    const double cs = 1.0 - 0.5 * w + w * w * pc;
+    switch ((int)kd & 3) {
+        case 0: *s = sn; *c = cs; break;
+        case 1: *s = cs; *c = -sn; break;
+        case 2: *s = -sn; *c = -cs; break;
+        default: *s = -cs; *c = sn; break;
+    }
+}
+
+/* translation of each joint frame in its parent, then the
+ * x-rotation (+-90 deg) of the frame before the joint's z rotation */
+static const double IKT[7][3] = {{0.0, 0.0, 0.333}, {0.0, 0.0, 0.0}, {0.0, -0.316, 0.0}, {0.0825, 0.0, 0.0},
+                                 {-0.0825, 0.384, 0.0}, {0.0, 0.0, 0.0}, {0.088, 0.0, 0.0}};
+static const int IKRX[7] = {0, -1, 1, 1, -1, 1, 1};
+#define IK_FLANGE 0.107
+#define IK_C45 0.70710678118654757
+
+typedef struct { double R[3][3]; double p[3]; double z[7][3]; double o[7][3]; } hand_fk_t;
+
+static void hand_fk(const double* q, const double base[3], hand_fk_t* f) {
+    double c0[3] = {1.0, 0.0, 0.0}, c1[3] = {0.0, 1.0, 0.0}, c2[3] = {0.0, 0.0, 1.0};
+    double p[3] = {base[0], base[1], base[2]};
+    for (int j = 0; j < 7; ++j) {
+        const double* t = IKT[j];
+        for (int i = 0; i < 3; ++i) p[i] = p[i] + (c0[i] * t[0] + c1[i] * t[1] + c2[i] * t[2]);
+        for (int i = 0; i < 3; ++i) {
+            const double a = c1[i];
+            if (IKRX[j] > 0) { c1[i] = c2[i]; c2[i] = -a; }
+            else if (IKRX[j] < 0) { c1[i] = -c2[i]; c2[i] = a; }
+        }
+        for (int i = 0; i < 3; ++i) { f->z[j][i] = c2[i]; f->o[j][i] = p[i]; }
+        double sn, cs;
+        ro_sincos64(q[j], &sn, &cs);
+        for (int i = 0; i < 3; ++i) {
+            const double a = c0[i], b = c1[i];
+            c0[i] = cs * a + sn * b;
+            c1[i] = cs * b - sn * a;
+        }
+    }
+    for (int i = 0; i < 3; ++i) p[i] = p[i] + IK_FLANGE * c2[i];
+    for (int i = 0; i < 3; ++i) {
+        const double a = c0[i], b = c1[i];
+        c0[i] = IK_C45 * a + -IK_C45 * b;
+        c1[i] = IK_C45 * b - -IK_C45 * a;
+    }
+    for (int i = 0; i < 3; ++i) { f->R[0][i] = c0[i]; f->R[1][i] = c1[i]; f->R[2][i] = c2[i]; f->p[i] = p[i]; }
+}
+
+static void cross3(const double* a, const double* b, double* o) {
+    o[0] = a[1] * b[2] - a[2] * b[1];
+    o[1] = a[2] * b[0] - a[0] * b[2];
+    o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+static void quat_columns(const double* qt, double T[3][3]) {
+    const double n = sqrt(qt[0] * qt[0] + qt[1] * qt[1] + qt[2] * qt[2] + qt[3] * qt[3]);
+    const double w = qt[0] / n, x = qt[1] / n, y = qt[2] / n, z = qt[3] / n;
+    T[0][0] = 1.0 - 2.0 * (y * y + z * z); T[0][1] = 2.0 * (x * y + w * z); T[0][2] = 2.0 * (x * z - w * y);
+    T[1][0] = 2.0 * (x * y - w * z); T[1][1] = 1.0 - 2.0 * (x * x + z * z); T[1][2] = 2.0 * (y * z + w * x);
+    T[2][0] = 2.0 * (x * z + w * y); T[2][1] = 2.0 * (y * z - w * x); T[2][2] = 1.0 - 2.0 * (x * x + y * y);
+}
+
+static void pose_error(const hand_fk_t* f, const double* pt, double T[3][3], double e[6], double e2[2]) {
+    double x0[3], x1[3], x2[3];
+    cross3(f->R[0], T[0], x0);
+    cross3(f->R[1], T[1], x1);
+    cross3(f->R[2], T[2], x2);
+    for (int i = 0; i < 3; ++i) {
+        e[i] = pt[i] - f->p[i];
+        e[3 + i] = 0.5 * (x0[i] + x1[i] + x2[i]);
+    }
+    e2[0] = e[0] * e[0] + e[1] * e[1] + e[2] * e[2];
+    e2[1] = e[3] * e[3] + e[4] * e[4] + e[5] * e[5];
+}
+
+void ro_hand_pose(const ro_scene* s, const double q[NQ], double R[9], double p[3]) {
+    const double base[3] = {s->base[0], s->base[1], s->base[2]};
+    hand_fk_t f;
+    hand_fk(q, base, &f);
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) R[3 * r + c] = f.R[c][r];
+    for (int i = 0; i < 3; ++i) p[i] = f.p[i];
+}
+
+/* one restart: q (in/out, 9), squared pose errors e2; returns converged */
+static int ik_solve(const double* pt, double T[3][3], const double base[3], const double* lo, const double* hi,
+                    int iters, double damping, double pos_tol, double rot_tol, double* q, double e2[2]) {
+    const double lam2 = damping * damping;
+    const double stop_p = (0.01 * pos_tol) * (0.01 * pos_tol), stop_r = (0.01 * rot_tol) * (0.01 * rot_tol);
+    hand_fk_t f;
+    double e[6];
+    for (int it = 0; it < iters; ++it) {
+        hand_fk(q, base, &f);
+        pose_error(&f, pt, T, e, e2);
+        if (e2[0] <= stop_p && e2[1] <= stop_r) break;
+        double J[6][7];
+        for (int j = 0; j < 7; ++j) {
+            const double d[3] = {f.p[0] - f.o[j][0], f.p[1] - f.o[j][1], f.p[2] - f.o[j][2]};
+            double v[3];
+            cross3(f.z[j], d, v);
+            for (int i = 0; i < 3; ++i) { J[i][j] = v[i]; J[3 + i][j] = f.z[j][i]; }
+        }
+        double L[6][6];
+        for (int r = 0; r < 6; ++r)
+            for (int c = 0; c <= r; ++c) {
+                double sum = 0.0;
+                for (int j = 0; j < 7; ++j) sum = sum + J[r][j] * J[c][j];
+                if (r == c) sum = sum + lam2;
+                for (int m = 0; m < c; ++m) sum = sum - L[r][m] * L[c][m];
+                L[r][c] = (r == c) ? sqrt(sum) : sum / L[c][c];
+            }
+        double y[6], x[6];
+        for (int r = 0; r < 6; ++r) {
+            double sum = e[r];
+            for (int m = 0; m < r; ++m) sum = sum - L[r][m] * y[m];
+            y[r] = sum / L[r][r];
+        }
+        for (int r = 5; r >= 0; --r) {
+            double sum = y[r];
+            for (int m = r + 1; m < 6; ++m) sum = sum - L[m][r] * x[m];
+            x[r] = sum / L[r][r];
+        }
+        for (int j = 0; j < 7; ++j) {
+            double dq = 0.0;
+            for (int r = 0; r < 6; ++r) dq = dq + J[r][j] * x[r];
+            double v = q[j] + dq;
+            if (v < lo[j]) v = lo[j];
+            if (v > hi[j]) v = hi[j];
+            q[j] = v;
+        }
+    }
+    hand_fk(q, base, &f);
+    pose_error(&f, pt, T, e, e2);
+    return e2[0] <= pos_tol * pos_tol && e2[1] <= rot_tol * rot_tol;
+}
+
+int ro_ik(const ro_scene* s, int32_t n_targets, const double* pos, const double* quat, const double* init,
+          const double lo[NQ], const double hi[NQ], const rp_ik_params* pp, double* q_out, int32_t* status_out) {
+    if (!s || n_targets < 0 || !pp || (n_targets > 0 && (!pos || !quat || !init || !q_out || !status_out)))
+        return RP_ERR_ARG;
+    rp_ik_params p = *pp;
+    if (p.n_seeds <= 0) p.n_seeds = 256;
+    if (p.iters <= 0) p.iters = 64;
+    if (p.damping <= 0) p.damping = 0.01;
+    if (p.pos_tol <= 0) p.pos_tol = 5e-4;
+    if (p.rot_tol <= 0) p.rot_tol = 5e-3;
+    const double base[3] = {s->base[0], s->base[1], s->base[2]};
+    for (int t = 0; t < n_targets; ++t) {
+        double T[3][3];
+        quat_columns(quat + 4 * t, T);
+        const double* qi = init + NQ * t;
+        int best_c = 3, best_k = 0;
+        double best_v = 0.0, best_q[NQ];
+        for (int k = 0; k < p.n_seeds; ++k) {
+            const uint64_t g = (uint64_t)t * (uint64_t)p.n_seeds + (uint64_t)k;
+            double q[NQ], e2[2];
+            if (k == 0) {
+                memcpy(q, qi, sizeof q);
+            } else {
+                sample_state_tag(p.seed, g, lo, hi, q, IK_TAG);
+                q[7] = qi[7];
+                q[8] = qi[8];
+            }
+            const int conv = ik_solve(pos + 3 * t, T, base, lo, hi, p.iters, p.damping, p.pos_tol, p.rot_tol, q, e2);
+            int cls = 2;
+            if (conv) {
+                float f[NQ];
+                for (int i = 0; i < NQ; ++i) f[i] = (float)q[i];
+                cls = ro_state_valid(s, f) ? 0 : 1;
+            }
+            const double v = cls < 2 ? dist2(q, qi) : e2[0] + e2[1];
+            if (cls < best_c || (cls == best_c && v < best_v)) {
+                best_c = cls;
+                best_v = v;
+                best_k = k;
+                memcpy(best_q, q, sizeof q);
+            }
+        }
+        (void)best_k;
+        memcpy(q_out + NQ * t, best_q, sizeof best_q);
+        status_out[t] = best_c;
+    }
+    return RP_OK;
 }

@@ -71,6 +71,15 @@ int ro_plan(const ro_scene* s, const double start[RP_NQ], const double goal[RP_N
             rp_stats* stats);
 
 /* geometry primitives (unit tests) */
+/* batched hand-link IK, the algorithm of rp_ik (rbe550_final_project_amd/csrc/rp_ik.h) */
+int ro_ik(const ro_scene* s, int32_t n_targets, const double* pos, const double* quat, const double* init,
+          const double lo[RP_NQ], const double hi[RP_NQ], const rp_ik_params* params, double* q_out,
+          int32_t* status_out);
+/* hand pose of an arm configuration: R (row-major 3x3), p (3) */
+void ro_hand_pose(const ro_scene* s, const double q[RP_NQ], double R[9], double p[3]);
+/* float64 polynomial sin / cos of the IK */
+void ro_sincos64(double x, double* s, double* c);
+
 float ro_seg_box_d2(const float a[3], const float b[3], const float h[3]);
 float ro_seg_seg_d2(const float a1[3], const float b1[3], const float a2[3], const float b2[3]);
 

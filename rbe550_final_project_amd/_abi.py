@@ -39,6 +39,25 @@ class PlanParams(C.Structure):
                 ("n_waypoints", C.c_int32), ("simplify", C.c_int32), ("tree_capacity", C.c_int64)]
 
 
+class IkParams(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("n_seeds", C.c_int32), ("iters", C.c_int32), ("damping", C.c_double),
+                ("pos_tol", C.c_double), ("rot_tol", C.c_double)]
+
+
+IK_OK, IK_COLLIDING, IK_NOT_CONVERGED = 0, 1, 2
+
+
+def make_ik_params(seed=0, n_seeds=0, iters=0, damping=0.0, pos_tol=0.0, rot_tol=0.0):
+    p = IkParams()
+    p.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    p.n_seeds = int(n_seeds)
+    p.iters = int(iters)
+    p.damping = float(damping)
+    p.pos_tol = float(pos_tol)
+    p.rot_tol = float(rot_tol)
+    return p
+
+
 class Stats(C.Structure):
     _fields_ = [("states_checked", C.c_int64), ("edges_checked", C.c_int64), ("samples", C.c_int64),
                 ("iterations", C.c_int64), ("start_tree_size", C.c_int64), ("goal_tree_size", C.c_int64),

@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/rbe_planner.h"
+#include "rp_ik.h"
 #include "rp_kernels.h"
 
 using namespace rp;
@@ -1223,6 +1224,78 @@ int rp_get_stats(rp_ctx* c, rp_stats* out) {
 }
 
 const char* rp_last_error(rp_ctx* c) { return c ? c->err.c_str() : g_create_error.c_str(); }
+
+int rp_ik(rp_ctx* c, int32_t n_targets, const double* pos, const double* quat, const double* init,
+          const double lo[RP_NQ], const double hi[RP_NQ], const rp_ik_params* params, double* q_out,
+          int32_t* status_out) {
+    if (!c || n_targets < 0 || !params || !lo || !hi ||
+        (n_targets > 0 && (!pos || !quat || !init || !q_out || !status_out)))
+        return RP_ERR_ARG;
+    if (n_targets == 0) return RP_OK;
+    RP_GUARD_BEGIN
+    HIP_TRY(hipSetDevice(c->device));
+    if (!c->have_scene) {
+        c->err = "rp_ik before rp_set_scene";
+        return RP_ERR_STATE;
+    }
+    rp_ik_params p = *params;
+    if (p.n_seeds <= 0) p.n_seeds = 256;
+    if (p.iters <= 0) p.iters = 64;
+    if (p.damping <= 0) p.damping = 0.01;
+    if (p.pos_tol <= 0) p.pos_tol = 5e-4;
+    if (p.rot_tol <= 0) p.rot_tol = 5e-3;
+    const int64_t lanes = (int64_t)n_targets * p.n_seeds;
+    if (lanes > (int64_t)1 << 26) {
+        c->err = "rp_ik: n_targets * n_seeds too large";
+        return RP_ERR_ARG;
+    }
+    DevBuf<double> d_in, d_q, d_err, d_best;
+    DevBuf<float> d_q32;
+    DevBuf<uint8_t> d_conv, d_valid;
+    DevBuf<int32_t> d_status;
+    d_in.ensure((size_t)n_targets * (3 + 4 + NQ));
+    d_q.ensure((size_t)lanes * NQ);
+    d_q32.ensure((size_t)lanes * NQ);
+    d_err.ensure((size_t)lanes * 2);
+    d_conv.ensure(lanes);
+    d_valid.ensure(lanes);
+    d_best.ensure((size_t)n_targets * NQ);
+    d_status.ensure(n_targets);
+    double* d_pos = d_in.p;
+    double* d_quat = d_pos + 3 * n_targets;
+    double* d_init = d_quat + 4 * n_targets;
+    HIP_TRY(hipMemcpyAsync(d_pos, pos, sizeof(double) * 3 * n_targets, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_quat, quat, sizeof(double) * 4 * n_targets, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(d_init, init, sizeof(double) * NQ * n_targets, hipMemcpyHostToDevice, c->stream));
+    IkArgs a;
+    a.pos = d_pos;
+    a.quat = d_quat;
+    a.init = d_init;
+    for (int i = 0; i < NQ; ++i) { a.lo[i] = lo[i]; a.hi[i] = hi[i]; }
+    for (int i = 0; i < 3; ++i) a.base[i] = (double)c->scene.base[i];
+    a.seed = p.seed;
+    a.n_targets = n_targets;
+    a.n_seeds = p.n_seeds;
+    a.iters = p.iters;
+    a.damping = p.damping;
+    a.pos_tol = p.pos_tol;
+    a.rot_tol = p.rot_tol;
+    hipLaunchKernelGGL(k_ik, dim3(blocks_for(lanes, 64)), dim3(64), 0, c->stream, a, d_q.p, d_err.p, d_conv.p,
+                       d_q32.p);
+    HIP_TRY(hipGetLastError());
+    launch_validity(c, d_q32.p, lanes, d_valid.p, c->stream);
+    hipLaunchKernelGGL(k_ik_select, dim3(blocks_for(n_targets, 64)), dim3(64), 0, c->stream, a,
+                       (const double*)d_q.p, (const double*)d_err.p, (const uint8_t*)d_conv.p,
+                       (const uint8_t*)d_valid.p, d_best.p, d_status.p);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(q_out, d_best.p, sizeof(double) * NQ * n_targets, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(status_out, d_status.p, sizeof(int32_t) * n_targets, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    d_in.release(); d_q.release(); d_q32.release(); d_err.release(); d_conv.release(); d_valid.release();
+    d_best.release(); d_status.release();
+    return RP_OK;
+    RP_GUARD_END(c)
+}
 
 // Numerics self-test (test-only entry, not in the public header's contract list):
 // device sqrt / div / ceil / f64->f32 of x[i] -> out[4*i..4*i+3].

@@ -30,11 +30,11 @@ __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32
 
 // Global sample g of the query (counter-based: independent of batch split / rank).
 __device__ __forceinline__ void sample_state(uint64_t seed, uint64_t g, const double* lo,
-                                             const double* hi, double q[NQ]) {
+                                             const double* hi, double q[NQ], uint32_t tag = SAMPLE_TAG) {
     uint32_t u[12];
 #pragma unroll
     for (uint32_t j = 0; j < 3; ++j) {
-        uint32_t c[4] = {(uint32_t)g, (uint32_t)(g >> 32), j, SAMPLE_TAG};
+        uint32_t c[4] = {(uint32_t)g, (uint32_t)(g >> 32), j, tag};
         philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
         u[4 * j + 0] = c[0]; u[4 * j + 1] = c[1]; u[4 * j + 2] = c[2]; u[4 * j + 3] = c[3];
     }

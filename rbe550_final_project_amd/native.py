@@ -19,7 +19,7 @@ LIB_PATH = os.path.join(_HERE, LIB_NAME)
 EXPORTS = ("rp_version", "rp_default_robot", "rp_create", "rp_destroy", "rp_set_scene", "rp_set_attached",
            "rp_check_states", "rp_check_states_device", "rp_check_edges", "rp_check_edges_device",
            "rp_state_contacts", "rp_plan", "rp_group_init", "rp_get_stats", "rp_last_error",
-           "rp_last_kernel_ms", "rp_selftest_f64")
+           "rp_last_kernel_ms", "rp_selftest_f64", "rp_ik")
 
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64)
 
@@ -59,6 +59,7 @@ def load():
     L.rp_last_error.restype = C.c_char_p
     L.rp_last_kernel_ms.argtypes = [vp, C.POINTER(f64)]
     L.rp_selftest_f64.argtypes = [vp, vp, i64, vp]
+    L.rp_ik.argtypes = [vp, i32, vp, vp, vp, vp, vp, C.POINTER(_abi.IkParams), vp, vp]
     _lib = L
     return L
 
@@ -161,6 +162,23 @@ class Context:
         self._check(load().rp_plan(self._h, _ptr(start), _ptr(goal), _ptr(lo), _ptr(hi), C.byref(params),
                                    _ptr(out), path_cap, C.byref(n), C.byref(status)), "rp_plan")
         return out[:n.value].copy(), status.value
+
+    def ik(self, pos, quat, init, lo, hi, params=None):
+        """Batched hand-link IK (rp_ik): pos (T, 3), quat (T, 4) as w, x, y, z, init
+        (T, 9) -> (q (T, 9) float64, status (T,) int32)."""
+        pos = np.ascontiguousarray(pos, dtype=np.float64).reshape(-1, 3)
+        quat = np.ascontiguousarray(quat, dtype=np.float64).reshape(-1, 4)
+        init = np.ascontiguousarray(init, dtype=np.float64).reshape(-1, _abi.NQ)
+        lo = np.ascontiguousarray(lo, dtype=np.float64)
+        hi = np.ascontiguousarray(hi, dtype=np.float64)
+        n = len(pos)
+        assert len(quat) == n and len(init) == n
+        p = params if params is not None else _abi.make_ik_params()
+        q = np.zeros((n, _abi.NQ), dtype=np.float64)
+        st = np.zeros(n, dtype=np.int32)
+        self._check(load().rp_ik(self._h, n, _ptr(pos), _ptr(quat), _ptr(init), _ptr(lo), _ptr(hi), C.byref(p),
+                                 _ptr(q), _ptr(st)), "rp_ik")
+        return q, st
 
     def stats(self):
         st = _abi.Stats()

@@ -287,6 +287,31 @@ class PlannerInterface:
         self.robot.set_qpos(qpos_cur)
         return waypoints
 
+    # -- goal configurations (motion_primitives.py:131-134) ----------------------
+    def inverse_kinematics(self, pos, quat, init_qpos=None, n_seeds=256, iters=64, attached_object=None):
+        """Hand-link IK on the GPU (rp_ik): the drop-in for the Genesis
+        robot.inverse_kinematics(link=hand, pos, quat) that _ik_for_pose calls.
+        Restarts from init_qpos (default: current qpos) and seeded samples, keeps the
+        fingers of init_qpos, prefers a collision-free solution in the current scene.
+        Returns a float32 CPU tensor (9,), or None if no restart reached the pose."""
+        init = np.asarray(tensor_to_array(init_qpos if init_qpos is not None else self.robot.get_qpos()),
+                          dtype=np.float64)
+        lo = np.asarray(tensor_to_array(self.robot.q_limit[0]), dtype=float)
+        hi = np.asarray(tensor_to_array(self.robot.q_limit[1]), dtype=float)
+        self.attached_object = attached_object
+        ctx = self._context()
+        self._sync_scene()
+        p = _abi.make_ik_params(seed=_next_seed(), n_seeds=n_seeds, iters=iters)
+        q, st = ctx.ik(np.asarray(tensor_to_array(pos), dtype=np.float64)[None, :],
+                       np.asarray(tensor_to_array(quat), dtype=np.float64)[None, :], init[None, :], lo, hi, p)
+        self.last_ik_status = int(st[0])
+        if st[0] == _abi.IK_NOT_CONVERGED:
+            _logger().warning("IK did not reach the target pose.")
+            return None
+        if st[0] == _abi.IK_COLLIDING:
+            _logger().warning("IK solution is in collision.")
+        return torch.tensor(q[0], dtype=torch.float32)
+
     # -- single-state validity (planning.py:209-219) ------------------------------
     def _is_ompl_state_valid(self, state):
         q = np.asarray([float(state[i]) for i in range(_abi.NQ)], dtype=np.float32)

@@ -1,6 +1,7 @@
 """The drop-in planning.PlannerInterface (code/planning.py:24-242 contract) driven
 through a Genesis-free mock robot/scene."""
 import json
+import sys
 import os
 
 import numpy as np
@@ -102,3 +103,25 @@ def test_plan_path_attached_object_and_failure():
     bad = np.array(q["start"])
     bad[7:] = 0.04
     assert pi.plan_path(qpos_goal=np.array(q["goal"]), qpos_start=bad, num_waypoints=150) == []
+
+
+@pytest.mark.gpu
+def test_inverse_kinematics_then_plan():
+    """_ik_for_pose replacement (motion_primitives.py:131-134): IK of a grasp pose
+    from the current qpos, then plan_path to it."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import franka_np
+    wl = json.load(open(os.path.join(GOLD, "workloads", "goal3_tallest_10box.json")))
+    q = wl["queries"][1]
+    s = scenes.Scene.from_json(q["scene"])
+    sc = M.Scene(s.boxes)
+    sc.robot.q = torch.tensor(q["start"], dtype=torch.float32)
+    pi = planning.PlannerInterface(sc.robot, sc)
+    R, p = franka_np.hand_pose(q["goal"])
+    qg = pi.inverse_kinematics(p, franka_np.mat_to_quat(R))
+    assert isinstance(qg, torch.Tensor) and qg.dtype == torch.float32 and tuple(qg.shape) == (9,)
+    R2, p2 = franka_np.hand_pose(qg.double().numpy())
+    assert np.linalg.norm(p2 - p) < 1e-3 and pi.last_ik_status == 0
+    wps = pi.plan_path(qpos_goal=qg, num_waypoints=150, timeout=10.0)
+    assert len(wps) == 150
+    assert pi.inverse_kinematics([3.0, 0.0, 0.5], [0.0, 1.0, 0.0, 0.0]) is None

@@ -15,8 +15,14 @@
 namespace rp {
 
 constexpr int VBLOCK = 64;      // validity / edge block size: one wave (its LDS = its queue)
+// waves per SIMD requested from the register allocator: 4 holds k_validity at 128
+// VGPRs (4 waves/SIMD, no spills; measured +2 % goal3, +22 % clutter64 over letting
+// it take 130 and drop to 3); the edge kernel would spill at 4 and stays free
 #ifndef RP_VALIDITY_WAVES
-#define RP_VALIDITY_WAVES 1   // min waves per SIMD requested from the register allocator
+#define RP_VALIDITY_WAVES 4
+#endif
+#ifndef RP_EDGE_WAVES
+#define RP_EDGE_WAVES 1
 #endif
 constexpr int NNBLOCK = 256;    // NN block size
 constexpr int NNTILE = 256;     // tree nodes per LDS tile (256 x 72 B = 18 KiB)
@@ -51,7 +57,7 @@ __global__ __launch_bounds__(VBLOCK, RP_VALIDITY_WAVES) void k_validity(const fl
 // `group` at a time; gfail[g] = first failing edge index within the group, and
 // slots of later edges of that group are skipped.
 template <int NCL>
-__global__ __launch_bounds__(VBLOCK, RP_VALIDITY_WAVES) void k_edges(const double* __restrict__ from,
+__global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_edges(const double* __restrict__ from,
                                                   const double* __restrict__ to,
                                                   const int* __restrict__ nd, int64_t n_edges,
                                                   int kmax, int mode, uint8_t* valid, int group,

@@ -24,9 +24,19 @@ namespace rp {
 
 struct V3 { float x, y, z; };
 
+// min / max / clamp as single instructions (v_min_f32, v_max_f32, v_med3_f32). The
+// oracle writes them as compares; for the finite operands here the two agree except
+// possibly in the sign of a zero result, which no later comparison or square sees.
+#ifndef RP_OPT_SELECT
+__device__ __forceinline__ float fminr(float a, float b) { return __builtin_fminf(a, b); }
+__device__ __forceinline__ float fmaxr(float a, float b) { return __builtin_fmaxf(a, b); }
+__device__ __forceinline__ float clampr(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
+#else
 __device__ __forceinline__ float fminr(float a, float b) { return a < b ? a : b; }
 __device__ __forceinline__ float fmaxr(float a, float b) { return a > b ? a : b; }
-__device__ __forceinline__ float clamp01(float x) { return x < 0.0f ? 0.0f : (x > 1.0f ? 1.0f : x); }
+__device__ __forceinline__ float clampr(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
+#endif
+__device__ __forceinline__ float clamp01(float x) { return clampr(x, 0.0f, 1.0f); }
 __device__ __forceinline__ float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 // (u . v) = fma(uz, vz, fma(uy, vy, ux * vx))
 __device__ __forceinline__ float dot3(V3 u, V3 v) { return fma_(u.z, v.z, fma_(u.y, v.y, u.x * v.x)); }
@@ -221,9 +231,9 @@ __device__ __forceinline__ bool aabb_disjoint2(const Aabb& u, const Aabb& v) {
 // g(t) = q(t) . d with q the excess of a + t d over the box [-h, h]; also |q|^2.
 __device__ __forceinline__ float excess_dot(V3 a, V3 d, V3 h, float t, float* f2) {
     const float px = fma_(t, d.x, a.x), py = fma_(t, d.y, a.y), pz = fma_(t, d.z, a.z);
-    const float cx = px < -h.x ? -h.x : (px > h.x ? h.x : px);
-    const float cy = py < -h.y ? -h.y : (py > h.y ? h.y : py);
-    const float cz = pz < -h.z ? -h.z : (pz > h.z ? h.z : pz);
+    const float cx = clampr(px, -h.x, h.x);
+    const float cy = clampr(py, -h.y, h.y);
+    const float cz = clampr(pz, -h.z, h.z);
     const V3 qv = {px - cx, py - cy, pz - cz};
     *f2 = dot3(qv, qv);
     return dot3(qv, d);
@@ -441,11 +451,19 @@ struct QueueState {
     ClusterRegs<NCL> cl;
 };
 
+#ifdef RP_OPT_DRAIN_NOINLINE
+#define RP_DRAIN_ATTR __attribute__((noinline))
+#else
+#define RP_DRAIN_ATTR __forceinline__
+#endif
 template <class S>
-__device__ __forceinline__ void drain_ss(S& s) {
+__device__ RP_DRAIN_ATTR void drain_ss(S& s) {
     const unsigned long long act = __ballot(1);
     const int nact = __popcll(act), r = rank_in(act);
     __builtin_amdgcn_wave_barrier();
+#ifdef RP_ABLATE_DRAIN
+    s.nss = 0;
+#endif
     for (int i = r; i < s.nss; i += nact) {
         const float* it = s.Q->ss[i];
         const V3 a1 = {it[0], it[1], it[2]}, b1 = {it[3], it[4], it[5]};
@@ -465,10 +483,13 @@ __device__ __forceinline__ void drain_ss(S& s) {
 }
 
 template <class S>
-__device__ __forceinline__ void drain_sb(S& s) {
+__device__ RP_DRAIN_ATTR void drain_sb(S& s) {
     const unsigned long long act = __ballot(1);
     const int nact = __popcll(act), r = rank_in(act);
     __builtin_amdgcn_wave_barrier();
+#ifdef RP_ABLATE_DRAIN
+    s.nsb = 0;
+#endif
     for (int i = r; i < s.nsb; i += nact) {
         const float* it = s.Q->sb[i];
         const V3 pa = {it[0], it[1], it[2]}, pb = {it[3], it[4], it[5]}, h = {it[6], it[7], it[8]};
@@ -500,6 +521,9 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
     constexpr float r = CAP_GEOM[C][6];
     const Aabb u = capsule_aabb(k.a[C], k.b[C], r);
     if (u.lo.z <= s.plane_z) return true;  // capsule vs ground plane
+#ifdef RP_ABLATE_ENV
+    return false;
+#endif
     if constexpr (NCL == NCL_GRID) {
         // superset of the AABB-overlapping boxes from the axis grid (per-lane
         // gathers), then the exact AABB test on each candidate, one per lane per
@@ -533,8 +557,16 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
         if (!__any(near_cl)) continue;
         const int j0 = __float_as_int(cr[3]), nj = __float_as_int(cr[7]);
         for (int j = j0; j < j0 + nj; ++j) {
+#ifndef RP_OPT_BOXLOAD
+            // the whole 64-B record in one scalar load; branch-free candidate test
+            struct Rec { float v[16]; };
+            const Rec rec = *reinterpret_cast<const Rec*>(sc->box[j]);
+            const float* bx = rec.v;
+            const bool cand = near_cl & !((__float_as_uint(bx[14]) >> C) & 1u) & !aabb_disjoint(u, bx + 8, bx + 11);
+#else
             const float* bx = sc->box[j];
             const bool cand = near_cl && !((__float_as_uint(bx[14]) >> C) & 1u) && !aabb_disjoint(u, bx + 8, bx + 11);
+#endif
             const unsigned long long m = __ballot(cand);
             if (!m) continue;
             if (cand) enqueue_sb<C>(k, bx, r, s, m);

@@ -21,7 +21,7 @@ for s in "$@"; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     benchq) step bench 300 python bench.py --steps 20 --no-cpu ;;
-    ab) step ab 600 python tools/variant_bench.py build/variants/lib_sph.so build/variants/lib_ncl96.so build/variants/lib_ncl128.so && step ab_clutter 600 python tools/variant_bench.py --scene clutter64 build/variants/lib_sph.so build/variants/lib_ncl96.so build/variants/lib_ncl128.so && step ab_empty 600 python tools/variant_bench.py --scene empty build/variants/lib_sph.so build/variants/lib_ncl96.so build/variants/lib_ncl128.so ;;
+    ab) step ab 600 python tools/variant_bench.py build/variants/*.so && step ab_clutter 600 python tools/variant_bench.py --scene clutter64 build/variants/*.so ;;
     ptrace) step ptrace 600 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/ptrace -o pt -- python tools/plan_trace.py && step plantime 300 python tools/plan_trace.py ;;
     gridab) step gridab 600 python tools/grid_ab.py ;;
     lat) step lat 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/lat -o lt -- python tools/latency_probe.py && python tools/latency_probe.py --summarize gpurun_out/lat/lt_kernel_trace.csv > gpurun_out/lat_summary.txt ;;

@@ -83,6 +83,31 @@ def run_plans(ctx, wl, batch, seed, group):
     return times, states, statuses
 
 
+def config_scenes():
+    """BASELINE.md configs other than the headline C3: (name, scene, states per launch)."""
+    c4 = load_workload("goal4_pentagon_10box")["queries"][14]["scene"]
+    c5 = load_workload("clutter64")["queries"][0]["scene"]
+    return [("C2_goal1_5box_64k", scenes.Scene(boxes=scenes.goal1_scattered(0).boxes[:5]), 1 << 16),
+            ("C4_goal4_pentagon_256k", scenes.Scene.from_json(c4), 1 << 18),
+            ("C5_clutter64_1M", scenes.Scene.from_json(c5), 1 << 20)]
+
+
+def rate_on_scene(ctx, scene, q, n, flags, stream, steps):
+    """states/s of the validity kernel on one scene (this rank; events on the
+    kernel's stream)."""
+    ctx.set_scene(scene.boxes, scene.plane_z, scene.base)
+    for _ in range(3):
+        ctx.check_states_device(q.data_ptr(), n, flags.data_ptr(), stream.cuda_stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(steps):
+        ctx.check_states_device(q.data_ptr(), n, flags.data_ptr(), stream.cuda_stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    return n / (ms * 1e-3), ms, float(flags[:n].float().mean().item())
+
+
 def cpu_baseline(scene, n_states, threads):
     """CPU oracle (test infrastructure, the cpu_baseline leg only): OpenMP validity
     over `threads` host cores on a bounded sample of the same workload."""
@@ -185,6 +210,16 @@ def main():
     value = total_states / wall_max
     ms_per_step = 1e3 * wall_max / args.steps
 
+    # ---- the other BASELINE configs' scenes (validity throughput per GPU, no collective)
+    per_config = {}
+    for name, sc_c, n_c in config_scenes():
+        n_c = min(n_c, n)
+        rate, ms, vf = rate_on_scene(ctx, sc_c, q, n_c, flags, stream, 10)
+        per_config[name] = {"boxes": len(sc_c.boxes), "states_per_launch": n_c,
+                            "states_per_sec_per_gpu": round(rate, 1), "kernel_ms": round(ms, 5),
+                            "valid_fraction": round(vf, 4)}
+    ctx.set_scene(scene.boxes, scene.plane_z, scene.base)
+
     # ---- plan wall-time on the C3 workload (group-sharded when N > 1)
     plan = None
     if not args.no_plan:
@@ -206,6 +241,14 @@ def main():
                     "states_per_sec_in_plan": round(pstates / (sum(times) / 1e3), 1)}
         except Exception as ex:  # report, keep the primary metric
             plan = {"error": repr(ex)[:300]}
+        if not distributed:
+            try:   # C5: the clutter query with 131,072-sample iterations (N = 1 here)
+                c5 = load_workload("clutter64")
+                t5, s5, st5 = run_plans(ctx, c5, 131072, 0, None)
+                plan["C5_clutter64"] = {"batch": 131072, "wall_ms": round(t5[0], 3), "states_checked": int(s5),
+                                        "solved": int(st5[0] in (_abi.STATUS_EXACT, _abi.STATUS_APPROXIMATE))}
+            except Exception as ex:
+                plan["C5_clutter64"] = {"error": repr(ex)[:300]}
 
     flop = flops_per_state(len(scene.boxes))
     achieved_tflops = n * flop / (kernel_ms * 1e-3) / 1e12
@@ -241,7 +284,7 @@ def main():
                "config": {"workload": "C3 goal3_tallest 10-block scene: validity batch per GPU + 21-query plan",
                           "states_per_gpu": n, "global_batch": n * world, "parallelism": f"dp{world}",
                           "valid_fraction": round(valid_frac, 4)},
-               "plan_wall": plan, "roofline": roofline, "cpu_baseline": cpu}
+               "plan_wall": plan, "per_config": per_config, "roofline": roofline, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
     ctx.close()
     if distributed:

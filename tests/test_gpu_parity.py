@@ -208,6 +208,23 @@ def test_plan_parity_smoothing(gpu_ctx, oracle_lib, wl, qi, dev_max, monkeypatch
     assert lens[1] < lens[2]
 
 
+@pytest.mark.parametrize("max_iters,simplify", [(1, 0), (4, 1), (8, 2)])
+def test_plan_parity_approximate(gpu_ctx, oracle_lib, max_iters, simplify):
+    """Unsolved within the iteration cap: APPROXIMATE status and the same path to the
+    start-tree node closest to the goal (and its simplification)."""
+    from test_oracle_planner import WALLS, walled_query
+    sc = scenes.Scene(boxes=WALLS)
+    o = _both(gpu_ctx, oracle_lib, sc)
+    start, goal = walled_query()
+    p = _abi.make_params(seed=1, batch=64, max_iters=max_iters, range_=0.3, timeout_s=60, n_waypoints=100)
+    p.simplify = simplify
+    ref, st_ref, s_ref = o.plan(start, goal, model.Q_LO, model.Q_HI, p)
+    path, st = gpu_ctx.plan(start, goal, model.Q_LO, model.Q_HI, p)
+    assert st == st_ref == _abi.STATUS_APPROXIMATE
+    assert np.array_equal(path, ref)
+    assert gpu_ctx.stats()["start_tree_size"] == s_ref["start_tree_size"]
+
+
 def test_plan_invalid_start_goal(gpu_ctx, oracle_lib):
     gpu_ctx.set_scene([])
     gpu_ctx.set_attached(-1)

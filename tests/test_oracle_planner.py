@@ -79,29 +79,32 @@ def test_invalid_start_goal_status(oracle_lib):
     assert st == _abi.STATUS_INVALID_GOAL
 
 
-def test_approximate_on_iteration_cap(oracle_lib):
-    """Blocked goal region: the solve stops at max_iters and returns the start-tree
-    path to the node closest to the goal (OMPL RRTConnect approximate solution)."""
-    o = oracle_lib.OracleScene()
+WALLS = [((0.6, 0.0, 0.6), (0.45, 0.02, 0.6), 0.0), ((-0.6, 0.0, 0.6), (0.45, 0.02, 0.6), 0.0)]
+
+
+def walled_query():
+    """arm swung left -> right across two walls in the y = 0 plane: valid endpoints
+    that a few iterations cannot connect (approximate-solution cases)"""
     start = model.SAFE_HOME.copy()
-    start[7:] = 0.039
+    start[7:] = np.float32(0.04)
+    start[0] = -1.6
     goal = start.copy()
-    goal[0] = 2.0
-    # cage the goal's hand with boxes that leave it valid but unreachable
-    import franka_np as F
-    R, p = F.hand_pose(goal, model.BASE_POS)
-    walls = []
-    for dx, dy in [(0.15, 0), (-0.15, 0), (0, 0.15), (0, -0.15)]:
-        walls.append(((p[0] + dx, p[1] + dy, p[2]), (0.06 if dx else 0.2, 0.06 if dy else 0.2, 0.3), 0.0))
-    walls.append(((p[0], p[1], p[2] + 0.25), (0.2, 0.2, 0.04), 0.0))
-    o.set_scene(walls)
-    flags = o.check_states(np.stack([start, goal]))
-    if not flags.all():
-        pytest.skip("cage intersects start/goal")
-    p_ = _abi.make_params(seed=1, batch=32, max_iters=6, timeout_s=60, n_waypoints=0, simplify=False)
-    path, st, stats = o.plan(start, goal, model.Q_LO, model.Q_HI, p_)
-    assert st in (_abi.STATUS_APPROXIMATE, _abi.STATUS_EXACT)
-    if st == _abi.STATUS_APPROXIMATE:
+    goal[0] = 1.6
+    return start, goal
+
+
+def test_approximate_on_iteration_cap(oracle_lib):
+    """Blocked goal: the solve stops at max_iters and returns the start-tree path to
+    the extension node closest to the goal (OMPL RRTConnect approximate solution)."""
+    o = oracle_lib.OracleScene()
+    o.set_scene(WALLS)
+    start, goal = walled_query()
+    assert o.check_states(np.stack([start, goal]).astype(np.float32)).all()
+    for it in (1, 4):
+        p_ = _abi.make_params(seed=1, batch=64, max_iters=it, range_=0.3, timeout_s=60, n_waypoints=0,
+                              simplify=False)
+        path, st, stats = o.plan(start, goal, model.Q_LO, model.Q_HI, p_)
+        assert st == _abi.STATUS_APPROXIMATE and stats["iterations"] == it
         assert np.array_equal(path[0], start)
         assert np.linalg.norm(path[-1] - goal) < np.linalg.norm(start - goal)
 

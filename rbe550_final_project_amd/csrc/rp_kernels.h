@@ -51,11 +51,14 @@ __global__ __launch_bounds__(VBLOCK, RP_VALIDITY_WAVES) void k_validity(const fl
 // edge validity (DiscreteMotionValidator::checkMotion semantics)
 // ---------------------------------------------------------------------------
 // Edge e: states `from` -> `to`, nd[e] segments (nd < 0: no edge). Slot 0 is the
-// checked endpoint (mode 0: `to`, mode 1: `from`), slots 1..nd-1 the interior
+// checked endpoint (mode 0: `to`, mode 1: `from`; mode 2: per edge, bit ND_FROM
+// of nd[e] selects `from`), slots 1..nd-1 the interior
 // states from + (to - from) * slot / nd. valid[e] must be 1 on entry; a colliding
 // slot clears it. Optional prefix groups (connect chains): edges are grouped
 // `group` at a time; gfail[g] = first failing edge index within the group, and
 // slots of later edges of that group are skipped.
+constexpr int ND_FROM = 1 << 30;   // nd flag (mode 2): the edge's checked endpoint is `from`
+
 template <int NCL>
 __global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_edges(const double* __restrict__ from,
                                                   const double* __restrict__ to,
@@ -75,8 +78,13 @@ __global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_edges(const double* _
         const int slot = (int)(idx - e * kmax);
         bool run = false;
         int nde = -1;
+        int emode = mode;
         if (e < n_edges) {
             nde = nd[e];
+            if (mode == 2 && nde >= 0) {
+                emode = (nde & ND_FROM) ? 1 : 0;
+                nde &= ~ND_FROM;
+            }
             const int slots = nde > 1 ? nde : 1;
             run = nde >= 0 && slot < slots && valid[e] != 0;
             if (run && gfail) {
@@ -92,7 +100,7 @@ __global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_edges(const double* _
             const double* a = from + e * NQ;
             const double* b = to + e * NQ;
             if (slot == 0) {
-                const double* ep = mode ? a : b;
+                const double* ep = emode ? a : b;
 #pragma unroll
                 for (int k = 0; k < NQ; ++k) st[k] = ep[k];
             } else {
@@ -242,12 +250,13 @@ __device__ __forceinline__ void publish_seq(PlanIO* hio, int seq) {
 
 // rp_plan prologue (one block): tree roots, float32 copies of start / goal, counters
 // (replaces per-field host->device copies). sg_edge >= 0: start and goal also
-// become two zero-length edges at [sg_edge, sg_edge + 1] of the first extension
-// launch, so their validity is checked by it rather than by a separate launch.
+// become zero-length edges at sg_edge and sg_edge + stride of the first extension
+// launch (each the only edge of its prefix group when stride > 1: the other slots
+// are empty and gfail = stride), so their validity comes with it.
 struct PlanRoots { double start[NQ]; double goal[NQ]; };
 __global__ void k_plan_init(PlanRoots r, double* S, int32_t* Spar, uint8_t* Scand, double* G, int32_t* Gpar,
                             uint8_t* Gcand, float* q32, unsigned long long* counter, PlanIO* io, int64_t sg_edge,
-                            double* efrom, double* eto, int* nd, uint8_t* valid) {
+                            int sg_stride, double* efrom, double* eto, int* nd, uint8_t* valid, int* gfail) {
     const int t = threadIdx.x;
     if (t < NQ) {
         S[t] = r.start[t];
@@ -255,10 +264,13 @@ __global__ void k_plan_init(PlanRoots r, double* S, int32_t* Spar, uint8_t* Scan
         q32[t] = (float)r.start[t];
         q32[NQ + t] = (float)r.goal[t];
         if (sg_edge >= 0) {
+            const int64_t e1 = sg_edge + sg_stride;
             efrom[sg_edge * NQ + t] = eto[sg_edge * NQ + t] = r.start[t];
-            efrom[(sg_edge + 1) * NQ + t] = eto[(sg_edge + 1) * NQ + t] = r.goal[t];
+            efrom[e1 * NQ + t] = eto[e1 * NQ + t] = r.goal[t];
         }
     }
+    if (sg_edge >= 0)
+        for (int k = 1 + t; k < sg_stride; k += blockDim.x) nd[sg_edge + k] = nd[sg_edge + sg_stride + k] = -1;
     if (t < ST_WORDS) io->status[t] = 0;
     if (t == 0) {
         Spar[0] = -1;
@@ -269,14 +281,16 @@ __global__ void k_plan_init(PlanRoots r, double* S, int32_t* Spar, uint8_t* Scan
         io->n_raw = 0;
         io->n_out = 0;
         if (sg_edge >= 0) {
-            nd[sg_edge] = nd[sg_edge + 1] = 0;
-            valid[sg_edge] = valid[sg_edge + 1] = 1;
+            const int64_t e1 = sg_edge + sg_stride;
+            nd[sg_edge] = nd[e1] = 0;
+            valid[sg_edge] = valid[e1] = 1;
+            if (gfail) gfail[sg_edge / sg_stride] = gfail[e1 / sg_stride] = sg_stride;
         }
     }
 }
 
-__device__ __forceinline__ int sg_flags(const uint8_t* valid, int64_t sg_edge) {
-    return (valid[sg_edge] ? 1 : 0) | (valid[sg_edge + 1] ? 0x100 : 0);
+__device__ __forceinline__ int sg_flags(const uint8_t* valid, int64_t sg_edge, int sg_stride) {
+    return (valid[sg_edge] ? 1 : 0) | (valid[sg_edge + sg_stride] ? 0x100 : 0);
 }
 
 // append accepted extension nodes at TA + exclusive_scan position
@@ -296,13 +310,14 @@ __device__ __forceinline__ void ext_append_one(int64_t i, int32_t nn, int64_t po
 
 __global__ void k_ext_append(const int32_t* __restrict__ res, const int32_t* __restrict__ incl, int64_t B,
                              uint64_t seed, uint64_t g0, Bounds bd, double range, double* A, int32_t* Apar,
-                             uint8_t* Acand, int64_t TA, int* status, const uint8_t* valid, int64_t sg_edge) {
+                             uint8_t* Acand, int64_t TA, int* status, const uint8_t* valid, int64_t sg_edge,
+                             int sg_stride) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= B) return;
     if (status && i == B - 1) {
         status[ST_NACC] = incl[B - 1];
         status[ST_FIRST] = 0x7fffffff;
-        if (sg_edge >= 0) status[ST_SG] = sg_flags(valid, sg_edge);
+        if (sg_edge >= 0) status[ST_SG] = sg_flags(valid, sg_edge, sg_stride);
     }
     const int32_t nn = res[i];
     if (nn < 0) return;
@@ -348,7 +363,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_ext_accept_small(const uint8_t
                                                                    uint64_t seed, uint64_t g0, Bounds bd,
                                                                    double range, double* A, int32_t* Apar,
                                                                    uint8_t* Acand, int64_t TA, int* status,
-                                                                   int64_t sg_edge) {
+                                                                   int64_t sg_edge, int sg_stride) {
     __shared__ int lds[FUSE_THREADS / 64 + 1];
     const int64_t i0 = (int64_t)threadIdx.x * ITEMS;
     int32_t nn[ITEMS];
@@ -367,7 +382,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_ext_accept_small(const uint8_t
     if (threadIdx.x == 0) {
         status[ST_NACC] = total;
         status[ST_FIRST] = 0x7fffffff;
-        if (sg_edge >= 0) status[ST_SG] = sg_flags(valid, sg_edge);
+        if (sg_edge >= 0) status[ST_SG] = sg_flags(valid, sg_edge, sg_stride);
     }
 }
 
@@ -420,6 +435,82 @@ __global__ __launch_bounds__(NNBLOCK) void k_conn_nn(const double* __restrict__ 
     gfail[k] = cmax;
     yout[k] = y;
     mout[k] = m;
+}
+
+// mout flag of k_ext_conn_nn: the chain's last step lands on its target (REACHED)
+constexpr int CHAIN_REACHES = 1 << 16;
+
+// Speculative iteration front (single rank, batches <= FUSE_MAX): for every sample
+// the extension edge AND the connect chain toward its new node, as if the
+// extension were valid, so ONE edge launch checks both. Sample k owns the prefix
+// group of G = cmax + 1 edges at k * G: edge 0 the extension (mode of its tree),
+// edges 1..m the chain steps (the other tree's mode), the rest empty. A failing
+// extension ends the group (gfail = 0): its chain edges that have not started are
+// skipped, and the accept kernel drops the sample. Same trees as the two-phase
+// iteration: only wasted checks differ.
+__global__ __launch_bounds__(NNBLOCK) void k_ext_conn_nn(const double* __restrict__ A, int64_t TA,
+                                                         const double* __restrict__ Bt, int64_t TB, uint64_t seed,
+                                                         uint64_t g0, int64_t n, Bounds bd, double range, double res,
+                                                         int cmax, int a_start, double* __restrict__ efrom,
+                                                         double* __restrict__ eto, int* __restrict__ nd,
+                                                         uint8_t* __restrict__ valid, int* __restrict__ gfail,
+                                                         int32_t* __restrict__ near_out, int32_t* __restrict__ yout,
+                                                         int32_t* __restrict__ mout) {
+    __shared__ double tile[NNTILE * NQ];
+    const int64_t k = (int64_t)blockIdx.x * NNBLOCK + threadIdx.x;
+    const bool active = k < n;
+    double qr[NQ], x[NQ];
+    sample_state(seed, g0 + (uint64_t)(active ? k : 0), bd.lo, bd.hi, qr);
+    const int32_t nn = nn_tiled(A, TA, qr, active, tile);
+    const double* near = A + (int64_t)(nn >= 0 ? nn : 0) * NQ;
+    steer(near, qr, range, x);
+    const int32_t y = nn_tiled(Bt, TB, x, active, tile);
+    if (!active) return;
+    const int G = cmax + 1;
+    int64_t e = k * G;
+    {
+        double* f = efrom + e * NQ;
+        double* t = eto + e * NQ;
+#pragma unroll
+        for (int d = 0; d < NQ; ++d) {
+            f[d] = a_start ? near[d] : x[d];
+            t[d] = a_start ? x[d] : near[d];
+        }
+        nd[e] = segment_count(f, t, res) | (a_start ? 0 : ND_FROM);
+        valid[e] = 1;
+    }
+    double cur[NQ], nxt[NQ];
+    const double* ys = Bt + (int64_t)y * NQ;
+#pragma unroll
+    for (int d = 0; d < NQ; ++d) cur[d] = ys[d];
+    int m = cmax, reached = 0;
+    for (int s = 0; s < cmax; ++s) {
+        ++e;
+        if (m < cmax) {  // chain already reached x
+            nd[e] = -1;
+            continue;
+        }
+        const int reach = steer(cur, x, range, nxt);
+        double* f = efrom + e * NQ;
+        double* t = eto + e * NQ;
+#pragma unroll
+        for (int d = 0; d < NQ; ++d) {
+            f[d] = a_start ? nxt[d] : cur[d];
+            t[d] = a_start ? cur[d] : nxt[d];
+        }
+        nd[e] = segment_count(f, t, res) | (a_start ? ND_FROM : 0);
+        valid[e] = 1;
+#pragma unroll
+        for (int d = 0; d < NQ; ++d) cur[d] = nxt[d];
+        if (reach) {
+            m = s + 1;
+            reached = 1;
+        }
+    }
+    gfail[k] = G;
+    near_out[k] = nn;
+    yout[k] = y;
+    mout[k] = m | (reached ? CHAIN_REACHES : 0);
 }
 
 // per-target record (y, L) with L = leading valid steps
@@ -608,6 +699,77 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_conn_accept_small(
     __syncthreads();
     if (threadIdx.x == 0) status[ST_FIRST] = first;
     iteration_tail(status, total, TA0, a_start, Apar, Bpar, chain_end, pa, io);
+}
+
+// single-block accept of a speculative iteration (k_ext_conn_nn): extension
+// nodes appended in sample order, then every accepted sample's valid chain prefix
+// (L = min(gfail - 1, m)) in the same order, first REACHED target, iteration tail.
+// The nodes are copied from the edge records k_ext_conn_nn wrote (sample k's new
+// node is the checked endpoint of edge k * G, chain node s that of edge k * G + 1 +
+// s), not recomputed.
+template <int ITEMS>
+__global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
+    const int* __restrict__ gfail, const int32_t* __restrict__ near, const int32_t* __restrict__ y,
+    const int32_t* __restrict__ m, int64_t B, int G, const double* __restrict__ efrom,
+    const double* __restrict__ eto, double* A, int32_t* Apar, uint8_t* Acand, int64_t TA, double* Bt,
+    int32_t* Bpar, uint8_t* Bcand, int64_t TB, int a_start, int32_t* chain_end, int* status,
+    const uint8_t* valid, int64_t sg_edge, int sg_stride, PathArgs pa, PlanIO* io) {
+    __shared__ int lds[FUSE_THREADS / 64 + 1];
+    __shared__ int first;
+    const int64_t k0 = (int64_t)threadIdx.x * ITEMS;
+    int L[ITEMS];
+    int na = 0, nl = 0;
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+        const int64_t k = k0 + r;
+        const int g = k < B ? gfail[k] : 0;
+        const int mk = k < B ? (m[k] & (CHAIN_REACHES - 1)) : 0;
+        L[r] = g > 0 ? (g - 1 < mk ? g - 1 : mk) : -1;   // -1: extension rejected
+        na += L[r] >= 0;
+        nl += L[r] > 0 ? L[r] : 0;
+    }
+    int totalA, totalB;
+    const int exA = block_scan_excl(na, lds, &totalA);
+    const int exB = block_scan_excl(nl, lds, &totalB);
+    if (threadIdx.x == 0) first = 0x7fffffff;
+    __syncthreads();
+    // the checked endpoint of an edge is the new node: `to` on the start tree's
+    // side (a_start: extension near -> new; chain next -> prev), else `from`
+    const double* ext_node = a_start ? eto : efrom;
+    const double* chain_node = a_start ? efrom : eto;
+    int t = exA;
+    int64_t off = TB + exB;
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+        if (L[r] < 0) continue;
+        const int64_t k = k0 + r, e0 = k * G;
+        const int64_t pos = TA + t;
+        const double* xs = ext_node + e0 * NQ;
+        for (int d = 0; d < NQ; ++d) A[pos * NQ + d] = xs[d];
+        Apar[pos] = near[k];
+        int32_t par = y[k];
+        for (int s = 0; s < L[r]; ++s) {
+            const double* cs = chain_node + (e0 + 1 + s) * NQ;
+            for (int d = 0; d < NQ; ++d) Bt[(off + s) * NQ + d] = cs[d];
+            Bpar[off + s] = par;
+            Bcand[off + s] = 0;
+            par = (int32_t)(off + s);
+        }
+        const int mk = m[k];
+        const bool reached = L[r] == (mk & (CHAIN_REACHES - 1)) && (mk & CHAIN_REACHES);
+        chain_end[t] = L[r] > 0 ? par : -1;
+        Acand[pos] = (!reached && a_start) ? 1 : 0;
+        if (reached) atomicMin(&first, t);
+        off += L[r];
+        ++t;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        status[ST_NACC] = totalA;
+        status[ST_FIRST] = first;
+        if (sg_edge >= 0) status[ST_SG] = sg_flags(valid, sg_edge, sg_stride);
+    }
+    iteration_tail(status, totalB, TA, a_start, Apar, Bpar, chain_end, pa, io);
 }
 
 // solution path for host-chosen join nodes (approximate solutions, rank groups)

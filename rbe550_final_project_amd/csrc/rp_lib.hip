@@ -503,7 +503,8 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         t.cand.ensure(cap);
         t.n = 0;
     }
-    const int64_t ne = std::max<int64_t>({PMAX + 2, ((BMAX + world - 1) / world) * cmax, (int64_t)SPMAX * SPMAX / 2});
+    const int64_t ne = std::max<int64_t>({PMAX + 2, ((BMAX + world - 1) / world) * cmax, (int64_t)SPMAX * SPMAX / 2,
+                                          (std::min<int64_t>(BMAX, FUSE_MAX) + 2) * (cmax + 1)});
     c->efrom.ensure(ne * NQ);
     c->eto.ensure(ne * NQ);
     c->nd.ensure(ne);
@@ -517,7 +518,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     c->rec.ensure(2 * (BMAX + world));
     c->Lv.ensure(BMAX);
     c->chain_end.ensure(BMAX);
-    c->gfail.ensure(BMAX);
+    c->gfail.ensure(std::max<int64_t>(BMAX, FUSE_MAX + 2));
     c->mine.ensure(PMAX + 1);
     c->scalar.ensure(16);
     c->counter.ensure(1);
@@ -545,13 +546,23 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     // iteration's status (a plan with an invalid start or goal discards that
     // iteration). Otherwise: a validity launch and a read-back before the loop.
     const bool oob = out_of_bounds(start, lo, hi) || out_of_bounds(goal, lo, hi);
-    const int64_t sg_edge = (world == 1 && !oob) ? p.batch_min : -1;
+    // single-rank iterations of <= FUSE_MAX samples run speculatively (extension
+    // and connect edges in one launch, k_ext_conn_nn); RBE_PLAN_SPECULATE=0 keeps
+    // the two-phase iteration (same trees; the parity tests run both)
+    bool speculate = world == 1;
+    if (const char* e = std::getenv("RBE_PLAN_SPECULATE"))
+        if (*e) speculate = speculate && std::atoi(e) != 0;
+    const int G = cmax + 1;   // edges per sample in a speculative launch
+    const bool spec0 = speculate && p.batch_min <= FUSE_MAX;
+    const int64_t sg_edge = (world == 1 && !oob) ? (spec0 ? p.batch_min * G : p.batch_min) : -1;
+    const int sg_stride = spec0 ? G : 1;
     {
         PlanRoots roots;
         for (int i = 0; i < NQ; ++i) { roots.start[i] = start[i]; roots.goal[i] = goal[i]; }
         hipLaunchKernelGGL(k_plan_init, dim3(1), dim3(64), 0, c->stream, roots, c->tree[0].q.p, c->tree[0].par.p,
                            c->tree[0].cand.p, c->tree[1].q.p, c->tree[1].par.p, c->tree[1].cand.p, c->q32.p,
-                           c->counter.p, io, sg_edge, c->efrom.p, c->eto.p, c->nd.p, c->valid.p);
+                           c->counter.p, io, sg_edge, sg_stride, c->efrom.p, c->eto.p, c->nd.p, c->valid.p,
+                           c->gfail.p);
         HIP_TRY(hipGetLastError());
         for (auto& t : c->tree) t.n = 1;
     }
@@ -629,38 +640,79 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         const int64_t TA = A.n, TB = Bt.n;
         const uint64_t g0 = gbase;
 
+        const int64_t sg = (iter == 0) ? sg_edge : -1;   // start / goal ride along
+        c->stats.samples += B;
+        if (speculate && B <= FUSE_MAX) {
+            // ---- single rank, speculative: one NN kernel (both trees), one edge
+            // launch, one accept kernel, the first simplification steps (no-ops
+            // until a path exists), one host round trip
+            const int seq = ++c->seq;
+            hipLaunchKernelGGL(k_ext_conn_nn, dim3(blocks_for(B, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
+                               Bt.q.p, TB, p.seed, g0, B, bd, p.range, p.resolution, cmax, a_start, c->efrom.p,
+                               c->eto.p, c->nd.p, c->valid.p, c->gfail.p, c->near_.p, c->yv.p, c->mv.p);
+            HIP_TRY(hipGetLastError());
+            launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, (B + (sg >= 0 ? 2 : 0)) * G, kmax, 2, c->valid.p, G,
+                         c->gfail.p, c->stream);
+#define RP_ITER_SMALL(IT)                                                                                           \
+    hipLaunchKernelGGL(k_iter_accept_small<IT>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, (const int*)c->gfail.p,   \
+                       (const int32_t*)c->near_.p, (const int32_t*)c->yv.p, (const int32_t*)c->mv.p, B, G,          \
+                       (const double*)c->efrom.p, (const double*)c->eto.p, A.q.p, A.par.p, A.cand.p, TA, Bt.q.p,    \
+                       Bt.par.p, Bt.cand.p, TB, a_start, c->chain_end.p, status, (const uint8_t*)c->valid.p, sg,    \
+                       sg_stride, pa, io)
+            if (B <= FUSE_THREADS) RP_ITER_SMALL(1);
+            else RP_ITER_SMALL(4);
+#undef RP_ITER_SMALL
+            HIP_TRY(hipGetLastError());
+            run_program(0, tail_steps, seq);
+            wait_seq(c, seq);
+            if (!sg_known) {
+                if (const int code = endpoint_status(h->status[ST_SG])) return endpoint_fail(code);
+                sg_known = true;
+            }
+            const int* st = h->status;
+            A.n = TA + st[ST_NACC];
+            Bt.n = TB + st[ST_ADDED];
+            c->stats.edges_checked += B * G;
+            if (st[ST_FIRST] != INT_MAX) {
+                solved = 1;
+                s_node = st[ST_SNODE];
+                g_node = st[ST_GNODE];
+                ++iter;
+                break;
+            }
+            continue;
+        }
+
         // ---- extension: my slice of the samples
         hipLaunchKernelGGL(k_ext_nn, dim3(blocks_for(per, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA, p.seed,
                            g0, (int64_t)rank * per, per, bd, p.range, p.resolution, a_start, c->efrom.p, c->eto.p,
                            c->nd.p, c->valid.p, c->near_.p);
         HIP_TRY(hipGetLastError());
-        const int64_t sg = (iter == 0) ? sg_edge : -1;   // == per when riding along
         launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, per + (sg >= 0 ? 2 : 0), kmax, a_start ? 0 : 1, c->valid.p,
                      1, nullptr, c->stream);
         c->stats.edges_checked += per;
-        c->stats.samples += B;
 
         if (world == 1) {
-            // ---- single rank: device-side counts, one host sync per iteration;
-            // batches <= FUSE_MAX use the single-block accept kernels
+            // ---- single rank, two-phase: device-side counts, one host round trip
+            // per iteration; batches <= FUSE_MAX use the single-block accept kernels
             const bool fused = B <= FUSE_MAX;
             const int seq = ++c->seq;
             if (fused) {
                 if (B <= FUSE_THREADS)
                     hipLaunchKernelGGL(k_ext_accept_small<1>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, c->valid.p,
                                        c->near_.p, B, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA, status,
-                                       sg);
+                                       sg, sg_stride);
                 else
                     hipLaunchKernelGGL(k_ext_accept_small<4>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, c->valid.p,
                                        c->near_.p, B, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA, status,
-                                       sg);
+                                       sg, sg_stride);
             } else {
                 hipLaunchKernelGGL(k_ext_result_flag, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream,
                                    c->valid.p, c->near_.p, B, c->res.p, c->acc.p);
                 scan_incl(c, c->acc.p, c->incl.p, B);
                 hipLaunchKernelGGL(k_ext_append, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->res.p,
                                    c->incl.p, B, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA, status,
-                                   (const uint8_t*)c->valid.p, sg);
+                                   (const uint8_t*)c->valid.p, sg, sg_stride);
             }
             hipLaunchKernelGGL(k_conn_nn, dim3(blocks_for(B, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
                                (int64_t)0, B, Bt.q.p, TB, p.range, p.resolution, cmax, a_start, c->efrom.p,
@@ -722,7 +774,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         scan_incl(c, c->acc.p, c->incl.p, B);
         hipLaunchKernelGGL(k_ext_append, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->res.p, c->incl.p, B,
                            p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA, (int*)nullptr,
-                           (const uint8_t*)nullptr, (int64_t)-1);
+                           (const uint8_t*)nullptr, (int64_t)-1, 1);
         HIP_TRY(hipGetLastError());
         const int32_t nacc = read_scalar(c, c->incl.p + (B - 1));
         A.n = TA + nacc;

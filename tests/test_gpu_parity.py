@@ -146,12 +146,17 @@ PLAN_CASES = [("single_pick_place_5box", 0), ("single_pick_place_5box", 1), ("go
 
 
 @pytest.mark.parametrize("wl,qi", PLAN_CASES)
-@pytest.mark.parametrize("batch,seed", [(1, 3), (64, 11), (4096, 5)])
-def test_plan_parity(gpu_ctx, oracle_lib, wl, qi, batch, seed):
+@pytest.mark.parametrize("batch,seed,batch_min", [(1, 3, 0), (64, 11, 0), (4096, 5, 0), (16384, 8, 8192)])
+@pytest.mark.parametrize("speculate", ["1", "0"])
+def test_plan_parity(gpu_ctx, oracle_lib, wl, qi, batch, seed, batch_min, speculate, monkeypatch):
+    """Speculative (one edge launch per iteration) and two-phase single-rank
+    iterations build the oracle's trees; batch_min 8192 > FUSE_MAX starts on the
+    multi-kernel accept path."""
+    monkeypatch.setenv("RBE_PLAN_SPECULATE", speculate)
     q = _wl(wl)["queries"][qi]
     sc = scenes.Scene.from_json(q["scene"])
     o = _both(gpu_ctx, oracle_lib, sc, q["attached"])
-    p = _abi.make_params(seed=seed, batch=batch, n_waypoints=150, timeout_s=60)
+    p = _abi.make_params(seed=seed, batch=batch, batch_min=batch_min, n_waypoints=150, timeout_s=60)
     ref, st_ref, stats_ref = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
     path, st = gpu_ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
     gst = gpu_ctx.stats()

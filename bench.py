@@ -147,6 +147,7 @@ def main():
     ap.add_argument("--plan-batch", type=int, default=4096, help="RRT-Connect samples per iteration (global)")
     ap.add_argument("--no-plan", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-configs", action="store_true", help="skip the C2/C4/C5 scene rates (profiling runs)")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     args = ap.parse_args()
 
@@ -212,7 +213,7 @@ def main():
 
     # ---- the other BASELINE configs' scenes (validity throughput per GPU, no collective)
     per_config = {}
-    for name, sc_c, n_c in config_scenes():
+    for name, sc_c, n_c in ([] if args.no_configs else config_scenes()):
         n_c = min(n_c, n)
         rate, ms, vf = rate_on_scene(ctx, sc_c, q, n_c, flags, stream, 10)
         per_config[name] = {"boxes": len(sc_c.boxes), "states_per_launch": n_c,

@@ -15,8 +15,8 @@ from pmc_summary import load  # noqa: E402
 
 def main():
     fdir, wdir, n, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
-    f, meta = load([fdir], "k_validity")
-    w, _ = load([wdir], "k_validity")
+    f, meta = load([fdir], "k_validity", n)
+    w, _ = load([wdir], "k_validity", n)
     read_b = 2.0 * f["FETCH_SIZE"] * 1024.0
     write_b = w["WRITE_SIZE"] * 1024.0
     d = {"kernel": "k_validity", "states_per_launch": n, "fetch_size_kb": f["FETCH_SIZE"],

@@ -8,13 +8,15 @@ import json
 import os
 
 
-def load(dirs, kernel):
+def load(dirs, kernel, grid=None):
     vals = collections.defaultdict(list)
     meta = {}
     for d in dirs:
         for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(f)):
                 if kernel not in r["Kernel_Name"]:
+                    continue
+                if grid is not None and int(r["Grid_Size"]) != int(grid):
                     continue
                 vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
                 meta = {k: r[k] for k in ("Grid_Size", "Workgroup_Size", "LDS_Block_Size", "VGPR_Count",

@@ -33,6 +33,8 @@ METRIC = "states-checked/sec + plan wall-time, 7-DOF arm/10 blocks, 1/2/4/8 GPU"
 VALU_PEAK_TFLOPS = 157.3     # MI355X FP32 vector peak (MI355X_MICROARCH.md chip table)
 HBM_PEAK_GBPS = 8000.0       # spec
 BYTES_PER_STATE = 9 * 4 + 1  # 9 x fp32 in, 1 B flag out
+C4_BATCH = 262144            # BASELINE C4: 256k-sample iterations
+C5_BATCH = 131072            # BASELINE C5: 131,072-sample iterations (2^20 budget)
 
 
 def flops_per_state(n_boxes):
@@ -65,22 +67,40 @@ def pmc_traffic(n_states):
         return None
 
 
-def run_plans(ctx, wl, batch, seed, group):
+def run_plans(ctx, wl, batch, seed, group, batch_min=0, tree_capacity=0, stats_out=None):
     """Wall time of every query of a workload (ms), plus aggregate states checked."""
     times, states, statuses = [], 0, []
     for i, q in enumerate(wl["queries"]):
         sc = scenes.Scene.from_json(q["scene"])
         ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
         ctx.set_attached(q["attached"])
-        p = _abi.make_params(seed=seed + i, batch=batch, n_waypoints=150, timeout_s=10.0)
+        p = _abi.make_params(seed=seed + i, batch=batch, batch_min=batch_min, n_waypoints=150, timeout_s=10.0,
+                             tree_capacity=tree_capacity)
         if group is not None:
             dist.barrier()
         t0 = time.perf_counter()
         path, st = ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
         times.append(1e3 * (time.perf_counter() - t0))
-        states += ctx.stats()["states_checked"]
+        s = ctx.stats()
+        states += s["states_checked"]
         statuses.append(st)
+        if stats_out is not None:
+            for k in ("exchange_ms", "iterations", "samples"):
+                stats_out[k] = stats_out.get(k, 0) + s[k]
     return times, states, statuses
+
+
+def plan_record(times, states, statuses, batch, dev, distributed, extra=None):
+    """Summary of a plan workload; total = max over ranks of the summed wall time."""
+    tt = torch.tensor([sum(times)], dtype=torch.float64, device=dev)
+    if distributed:
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    rec = {"queries": len(times), "batch": batch, "total_ms": round(float(tt.item()), 3),
+           "median_ms": round(float(np.median(times)), 3), "max_ms": round(float(np.max(times)), 3),
+           "solved": int(sum(s in (_abi.STATUS_EXACT, _abi.STATUS_APPROXIMATE) for s in statuses)),
+           "states_checked": int(states), "states_per_sec_in_plan": round(states / (sum(times) / 1e3), 1)}
+    rec.update(extra or {})
+    return rec
 
 
 def config_scenes():
@@ -221,35 +241,32 @@ def main():
                             "valid_fraction": round(vf, 4)}
     ctx.set_scene(scene.boxes, scene.plane_z, scene.base)
 
-    # ---- plan wall-time on the C3 workload (group-sharded when N > 1)
+    # ---- plan wall-time: C3 (headline), C4 (262,144-sample iterations) and C5
+    # (131,072-sample iterations); every iteration is sharded over the ranks when
+    # N > 1 (RCCL all-gather per phase)
     plan = None
     if not args.no_plan:
         group = None
         try:
             if distributed:
                 from rbe550_final_project_amd.distributed import Group
-                group = Group(ctx, args.plan_batch, local)
+                group = Group(ctx, max(args.plan_batch, C4_BATCH), local)
             run_plans(ctx, {"queries": wl["queries"][:2]}, args.plan_batch, 100, group)   # warm-up
             times, pstates, st = run_plans(ctx, wl, args.plan_batch, 0, group)
-            tt = torch.tensor([sum(times)], dtype=torch.float64, device=dev)
-            if distributed:
-                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            plan = {"queries": len(times), "batch": args.plan_batch,
-                    "total_ms": round(float(tt.item()), 3), "median_ms": round(float(np.median(times)), 3),
-                    "max_ms": round(float(np.max(times)), 3),
-                    "solved": int(sum(s in (_abi.STATUS_EXACT, _abi.STATUS_APPROXIMATE) for s in st)),
-                    "states_checked": int(pstates),
-                    "states_per_sec_in_plan": round(pstates / (sum(times) / 1e3), 1)}
+            plan = plan_record(times, pstates, st, args.plan_batch, dev, distributed)
         except Exception as ex:  # report, keep the primary metric
             plan = {"error": repr(ex)[:300]}
-        if not distributed:
-            try:   # C5: the clutter query with 131,072-sample iterations (N = 1 here)
-                c5 = load_workload("clutter64")
-                t5, s5, st5 = run_plans(ctx, c5, 131072, 0, None)
-                plan["C5_clutter64"] = {"batch": 131072, "wall_ms": round(t5[0], 3), "states_checked": int(s5),
-                                        "solved": int(st5[0] in (_abi.STATUS_EXACT, _abi.STATUS_APPROXIMATE))}
+        for key, wname, batch, cap in (("C4_pentagon", "goal4_pentagon_10box", C4_BATCH, 1 << 24),
+                                       ("C5_clutter64", "clutter64", C5_BATCH, 1 << 23)):
+            try:
+                extra = {}
+                t4, s4, st4 = run_plans(ctx, load_workload(wname), batch, 0, group, batch_min=batch,
+                                        tree_capacity=cap, stats_out=extra)
+                extra = {"batch_min": batch, "exchange_ms": round(extra.get("exchange_ms", 0.0), 3),
+                         "iterations": int(extra.get("iterations", 0)), "samples": int(extra.get("samples", 0))}
+                plan[key] = plan_record(t4, s4, st4, batch, dev, distributed, extra)
             except Exception as ex:
-                plan["C5_clutter64"] = {"error": repr(ex)[:300]}
+                plan[key] = {"error": repr(ex)[:300]}
 
     flop = flops_per_state(len(scene.boxes))
     achieved_tflops = n * flop / (kernel_ms * 1e-3) / 1e12

@@ -120,6 +120,97 @@ __global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_edges(const double* _
     }
 }
 
+// ---- work-compacted edge launch (large batches): the (edge, slot) items of
+// real slots only. Connect chains mostly end (reach their target) after a step or
+// two of their cmax, so a dense n_edges x kmax grid is largely idle lanes.
+// slots[e] = checks of edge e (0 for an empty edge or one past the device count)
+__global__ void k_edge_slots(const int* __restrict__ nd, int64_t n_edges, const int* __restrict__ dcount,
+                             int per_item, int32_t* __restrict__ slots) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n_edges) return;
+    const int64_t n = dcount ? min(n_edges, (int64_t)dcount[0] * per_item) : n_edges;
+    int v = 0;
+    if (e < n) {
+        const int d = nd[e];
+        if (d >= 0) {
+            const int c = d & ~ND_FROM;
+            v = c > 1 ? c : 1;
+        }
+    }
+    slots[e] = v;
+}
+
+// incl = inclusive scan of slots: item t belongs to the edge e with
+// incl[e-1] <= t < incl[e]. Grid-stride over the items (the grid is fixed, the
+// item count lives on the device); per 64-item step lane 0 binary-searches the
+// first edge, the lanes then step forward over the (few) edges the step spans.
+template <int NCL>
+__global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_edges_packed(
+    const double* __restrict__ from, const double* __restrict__ to, const int* __restrict__ nd, int64_t n_edges,
+    int mode, uint8_t* valid, int group, int* gfail, unsigned long long* counter, const DevScene* __restrict__ sc,
+    const int32_t* __restrict__ incl) {
+    __shared__ WaveQ wq;
+    __shared__ int64_t e_first;
+    if (n_edges <= 0) return;
+    const int64_t total = incl[n_edges - 1];
+    for (int64_t base = (int64_t)blockIdx.x * VBLOCK; base < total; base += (int64_t)gridDim.x * VBLOCK) {
+        if (threadIdx.x == 0) {   // first e with incl[e] > base
+            int64_t lo = 0, hi = n_edges - 1;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if (incl[mid] > base) hi = mid;
+                else lo = mid + 1;
+            }
+            e_first = lo;
+        }
+        __syncthreads();
+        const int64_t t = base + threadIdx.x;
+        bool run = false;
+        int64_t e = e_first;
+        int slot = 0, nde = 0, emode = mode;
+        if (t < total) {
+            while (incl[e] <= t) ++e;
+            slot = (int)(t - (e > 0 ? (int64_t)incl[e - 1] : 0));
+            nde = nd[e];
+            if (mode == 2) {
+                emode = (nde & ND_FROM) ? 1 : 0;
+                nde &= ~ND_FROM;
+            }
+            run = valid[e] != 0;
+            if (run && gfail) {
+                const int g = (int)(e / group), s = (int)(e - (int64_t)g * group);
+                run = gfail[g] > s;
+            }
+        }
+        __syncthreads();
+        const unsigned long long ballot = __ballot(run);
+        if (counter && (threadIdx.x & 63) == 0 && ballot) atomicAdd(counter, (unsigned long long)__popcll(ballot));
+        if (!ballot) continue;
+        if (run) {
+            double st[NQ];
+            const double* a = from + e * NQ;
+            const double* b = to + e * NQ;
+            if (slot == 0) {
+                const double* ep = emode ? a : b;
+#pragma unroll
+                for (int k = 0; k < NQ; ++k) st[k] = ep[k];
+            } else {
+                interp(a, b, (double)slot / (double)nde, st);
+            }
+            float qq[NQ];
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) qq[k] = (float)st[k];
+            if (state_collides<NCL>(qq, sc, wq)) {
+                valid[e] = 0;
+                if (gfail) {
+                    const int g = (int)(e / group), s = (int)(e - (int64_t)g * group);
+                    atomicMin(&gfail[g], s);
+                }
+            }
+        }
+    }
+}
+
 // nd for arbitrary edges (API / simplification) and the max over edges
 __global__ void k_edge_prep(const double* __restrict__ from, const double* __restrict__ to, int64_t n,
                             double res, int* nd, uint8_t* valid, int* kmax) {

@@ -113,6 +113,7 @@ struct rp_ctx {
     DevBuf<uint8_t> valid;
     DevBuf<int32_t> near_, res, acc, incl, yv, mv, rec, Lv, chain_end, mine;
     DevBuf<int> gfail;
+    DevBuf<int32_t> eslot, eincl;        // work-compacted edge launches
     DevBuf<char> cub_tmp;
     DevBuf<double> path;                 // raw solution path (PATH_CAP states)
     DevBuf<PlanIO> io;                   // iteration status + output record (rp_kernels.h)
@@ -136,6 +137,7 @@ struct rp_ctx {
         scalar.release(); counter.release(); efrom.release(); eto.release(); nd.release(); valid.release();
         near_.release(); res.release(); acc.release(); incl.release(); yv.release(); mv.release();
         rec.release(); Lv.release(); chain_end.release(); mine.release(); gfail.release();
+        eslot.release(); eincl.release();
         cub_tmp.release(); path.release(); io.release(); simp.release(); partial.release();
         if (h_io) (void)hipHostFree(h_io);
         if (d_scene) (void)hipFree(d_scene);
@@ -193,6 +195,12 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
     HIP_TRY(hipGetLastError());
 }
 
+// Work-compacted edge check (rp_kernels.h k_edges_packed) for large launches:
+// slot counts, their scan, then a fixed grid striding over the real items.
+void launch_edges_packed(rp_ctx* c, const double* from, const double* to, const int* nd, int64_t n, int kmax,
+                         int mode, uint8_t* valid, int group, int* gfail, hipStream_t s, const int* dcount,
+                         int per_item);
+
 // inclusive scan of int32 (hipCUB) on the context stream
 void scan_incl(rp_ctx* c, const int32_t* in, int32_t* out, int64_t n) {
     if (n <= 0) return;
@@ -200,6 +208,30 @@ void scan_incl(rp_ctx* c, const int32_t* in, int32_t* out, int64_t n) {
     HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, bytes, in, out, (int)n, c->stream));
     c->cub_tmp.ensure(bytes + 16);
     HIP_TRY(hipcub::DeviceScan::InclusiveSum(c->cub_tmp.p, bytes, in, out, (int)n, c->stream));
+}
+
+void launch_edges_packed(rp_ctx* c, const double* from, const double* to, const int* nd, int64_t n, int kmax,
+                         int mode, uint8_t* valid, int group, int* gfail, hipStream_t s, const int* dcount,
+                         int per_item) {
+    if (n <= 0) return;
+    c->eslot.ensure(n);
+    c->eincl.ensure(n);
+    hipLaunchKernelGGL(k_edge_slots, dim3(blocks_for(n, 256)), dim3(256), 0, s, nd, n, dcount, per_item, c->eslot.p);
+    HIP_TRY(hipGetLastError());
+    scan_incl(c, c->eslot.p, c->eincl.p, n);
+    const dim3 g(std::min<unsigned>(blocks_for(n * (int64_t)kmax, VBLOCK), 8192u)), b(VBLOCK);
+#define RP_EDGESP(N) hipLaunchKernelGGL(k_edges_packed<N>, g, b, 0, s, from, to, nd, n, mode, valid, group, gfail, \
+                                        c->counter.p, c->d_scene, (const int32_t*)c->eincl.p)
+    switch (ncl_bucket(c->scene)) {
+        case NCL_GRID: RP_EDGESP(NCL_GRID); break;
+        case 0: RP_EDGESP(0); break;
+        case 1: RP_EDGESP(1); break;
+        case 2: RP_EDGESP(2); break;
+        case 4: RP_EDGESP(4); break;
+        default: RP_EDGESP(8); break;
+    }
+#undef RP_EDGESP
+    HIP_TRY(hipGetLastError());
 }
 
 template <typename T>
@@ -553,6 +585,14 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     if (const char* e = std::getenv("RBE_PLAN_SPECULATE"))
         if (*e) speculate = speculate && std::atoi(e) != 0;
     const int G = cmax + 1;   // edges per sample in a speculative launch
+    // connect chains end early, so large connect launches are work-compacted
+    // (k_edges_packed); RBE_EDGE_PACKED=0/1 forces the choice (tests)
+    int packed_mode = -1;
+    if (const char* e = std::getenv("RBE_EDGE_PACKED"))
+        if (*e) packed_mode = std::atoi(e) != 0;
+    auto packed = [&](int64_t n_edges) {
+        return packed_mode >= 0 ? packed_mode == 1 : n_edges * (int64_t)kmax >= ((int64_t)1 << 20);
+    };
     const bool spec0 = speculate && p.batch_min <= FUSE_MAX;
     const int64_t sg_edge = (world == 1 && !oob) ? (spec0 ? p.batch_min * G : p.batch_min) : -1;
     const int sg_stride = spec0 ? G : 1;
@@ -718,8 +758,12 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                                (int64_t)0, B, Bt.q.p, TB, p.range, p.resolution, cmax, a_start, c->efrom.p,
                                c->eto.p, c->nd.p, c->valid.p, c->gfail.p, c->yv.p, c->mv.p, (const int*)status);
             HIP_TRY(hipGetLastError());
-            launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, B * cmax, kmax, a_start ? 1 : 0, c->valid.p, cmax,
-                         c->gfail.p, c->stream, status, cmax);
+            if (packed(B * cmax))
+                launch_edges_packed(c, c->efrom.p, c->eto.p, c->nd.p, B * cmax, kmax, a_start ? 1 : 0, c->valid.p,
+                                    cmax, c->gfail.p, c->stream, status, cmax);
+            else
+                launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, B * cmax, kmax, a_start ? 1 : 0, c->valid.p, cmax,
+                             c->gfail.p, c->stream, status, cmax);
             if (fused) {
 #define RP_CONN_SMALL(IT)                                                                                        \
     hipLaunchKernelGGL(k_conn_accept_small<IT>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, c->yv.p, c->mv.p,      \
@@ -788,8 +832,12 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                                t0, nmine, Bt.q.p, TB, p.range, p.resolution, cmax, a_start, c->efrom.p, c->eto.p,
                                c->nd.p, c->valid.p, c->gfail.p, c->yv.p, c->mv.p, (const int*)nullptr);
             HIP_TRY(hipGetLastError());
-            launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, nmine * cmax, kmax, a_start ? 1 : 0, c->valid.p, cmax,
-                         c->gfail.p, c->stream);
+            if (packed(nmine * cmax))
+                launch_edges_packed(c, c->efrom.p, c->eto.p, c->nd.p, nmine * cmax, kmax, a_start ? 1 : 0,
+                                    c->valid.p, cmax, c->gfail.p, c->stream, nullptr, 1);
+            else
+                launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, nmine * cmax, kmax, a_start ? 1 : 0, c->valid.p,
+                             cmax, c->gfail.p, c->stream);
         }
         hipLaunchKernelGGL(k_conn_record, dim3(blocks_for(pt, 256)), dim3(256), 0, c->stream, c->yv.p, c->mv.p,
                            c->gfail.p, nmine, pt, c->rec.p);

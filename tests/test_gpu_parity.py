@@ -168,6 +168,26 @@ def test_plan_parity(gpu_ctx, oracle_lib, wl, qi, batch, seed, batch_min, specul
         (stats_ref["start_tree_size"], stats_ref["goal_tree_size"], stats_ref["iterations"])
 
 
+@pytest.mark.parametrize("wl,qi", PLAN_CASES)
+@pytest.mark.parametrize("batch,seed,batch_min", [(64, 11, 0), (16384, 8, 8192)])
+def test_plan_parity_packed_edges(gpu_ctx, oracle_lib, wl, qi, batch, seed, batch_min, monkeypatch):
+    """Two-phase iterations whose connect launches are work-compacted
+    (k_edges_packed forced on): same trees and paths as the oracle."""
+    monkeypatch.setenv("RBE_PLAN_SPECULATE", "0")
+    monkeypatch.setenv("RBE_EDGE_PACKED", "1")
+    q = _wl(wl)["queries"][qi]
+    sc = scenes.Scene.from_json(q["scene"])
+    o = _both(gpu_ctx, oracle_lib, sc, q["attached"])
+    p = _abi.make_params(seed=seed, batch=batch, batch_min=batch_min, n_waypoints=150, timeout_s=60)
+    ref, st_ref, stats_ref = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+    path, st = gpu_ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+    assert st == st_ref == _abi.STATUS_EXACT
+    assert np.array_equal(path, ref)
+    gst = gpu_ctx.stats()
+    assert (gst["start_tree_size"], gst["goal_tree_size"]) == (stats_ref["start_tree_size"],
+                                                                stats_ref["goal_tree_size"])
+
+
 @pytest.mark.parametrize("simplify,rng,dev_max", [(0, 0.3, ""), (1, 0.3, ""), (2, 0.3, ""), (1, 0.15, ""),
                                                    (1, 0.15, "2"), (2, 0.3, "2")])
 def test_plan_parity_hard_iterations(gpu_ctx, oracle_lib, simplify, rng, dev_max, monkeypatch):

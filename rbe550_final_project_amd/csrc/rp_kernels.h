@@ -59,6 +59,20 @@ __global__ __launch_bounds__(VBLOCK, RP_VALIDITY_WAVES) void k_validity(const fl
 // slots of later edges of that group are skipped.
 constexpr int ND_FROM = 1 << 30;   // nd flag (mode 2): the edge's checked endpoint is `from`
 
+// states-checked counter: COUNTER_SLOTS words, a wave adds to the word of its
+// block (one shared word made every wave's atomic queue at one L2 channel: ~1 ms
+// for a 90k-wave edge launch); readers sum the words
+constexpr int COUNTER_SLOTS = 256;
+__device__ __forceinline__ void count_states(unsigned long long* counter, unsigned long long ballot) {
+    if (counter && (threadIdx.x & 63) == 0 && ballot)
+        atomicAdd(counter + (blockIdx.x & (COUNTER_SLOTS - 1)), (unsigned long long)__popcll(ballot));
+}
+__device__ __forceinline__ unsigned long long counter_sum(const unsigned long long* counter) {
+    unsigned long long s = 0;
+    for (int i = 0; i < COUNTER_SLOTS; ++i) s += counter[i];
+    return s;
+}
+
 template <int NCL>
 __global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_edges(const double* __restrict__ from,
                                                   const double* __restrict__ to,
@@ -93,7 +107,7 @@ __global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_edges(const double* _
             }
         }
         const unsigned long long ballot = __ballot(run);
-        if (counter && (threadIdx.x & 63) == 0 && ballot) atomicAdd(counter, (unsigned long long)__popcll(ballot));
+        count_states(counter, ballot);
         if (!ballot) continue;
         if (run) {
             double st[NQ];
@@ -184,7 +198,7 @@ __global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_edges_packed(
         }
         __syncthreads();
         const unsigned long long ballot = __ballot(run);
-        if (counter && (threadIdx.x & 63) == 0 && ballot) atomicAdd(counter, (unsigned long long)__popcll(ballot));
+        count_states(counter, ballot);
         if (!ballot) continue;
         if (run) {
             double st[NQ];
@@ -363,12 +377,12 @@ __global__ void k_plan_init(PlanRoots r, double* S, int32_t* Spar, uint8_t* Scan
     if (sg_edge >= 0)
         for (int k = 1 + t; k < sg_stride; k += blockDim.x) nd[sg_edge + k] = nd[sg_edge + sg_stride + k] = -1;
     if (t < ST_WORDS) io->status[t] = 0;
+    for (int k = t; k < COUNTER_SLOTS; k += blockDim.x) counter[k] = 0;
     if (t == 0) {
         Spar[0] = -1;
         Gpar[0] = -1;
         Scand[0] = 0;
         Gcand[0] = 0;
-        *counter = 0;
         io->n_raw = 0;
         io->n_out = 0;
         if (sg_edge >= 0) {
@@ -1068,7 +1082,7 @@ __global__ __launch_bounds__(256) void k_simp(int ops, int level, int dev_max, d
             for (int w = 0; w < ST_WORDS; ++w) hio->status[w] = io->status[w];
             hio->n_raw = n_raw;
             hio->n_out = m;
-            hio->counter = *counter;
+            hio->counter = counter_sum(counter);
             hio->simp_edges = ss->edges_total;
             hio->out = out ? 1 : 0;
         }

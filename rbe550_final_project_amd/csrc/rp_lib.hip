@@ -242,6 +242,16 @@ T read_scalar(rp_ctx* c, const T* dev) {
     return v;
 }
 
+// states-checked counter (rp_kernels.h COUNTER_SLOTS words): synchronous sum
+int64_t read_counter(rp_ctx* c) {
+    unsigned long long w[COUNTER_SLOTS];
+    HIP_TRY(hipMemcpyAsync(w, c->counter.p, sizeof w, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    unsigned long long s = 0;
+    for (int i = 0; i < COUNTER_SLOTS; ++i) s += w[i];
+    return (int64_t)s;
+}
+
 // all-gather `bytes` from dev buffer src into the group's recv buffer
 void exchange(rp_ctx* c, const void* src, int64_t bytes) {
     if (bytes > c->g_cap) throw HipError{"group exchange buffer too small"};
@@ -269,15 +279,14 @@ int64_t check_edges_host(rp_ctx* c, const double* qa, const double* qb, int64_t 
     HIP_TRY(hipMemcpyAsync(c->ea.p, qa, sizeof(double) * NQ * n, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->eb.p, qb, sizeof(double) * NQ * n, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemsetAsync(c->scalar.p, 0, sizeof(int) * 16, c->stream));
-    HIP_TRY(hipMemsetAsync(c->counter.p, 0, sizeof(unsigned long long), c->stream));
+    HIP_TRY(hipMemsetAsync(c->counter.p, 0, sizeof(unsigned long long) * COUNTER_SLOTS, c->stream));
     hipLaunchKernelGGL(k_edge_prep, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, c->ea.p, c->eb.p, n, res,
                        c->end_nd.p, c->eval.p, c->scalar.p);
     HIP_TRY(hipGetLastError());
     const int kmax = read_scalar(c, c->scalar.p);
     launch_edges(c, c->ea.p, c->eb.p, c->end_nd.p, n, kmax, 0, c->eval.p, 1, nullptr, c->stream);
     HIP_TRY(hipMemcpyAsync(out, c->eval.p, n, hipMemcpyDeviceToHost, c->stream));
-    const unsigned long long st = read_scalar(c, c->counter.p);
-    return (int64_t)st;
+    return read_counter(c);
 }
 
 // ---------------------------------------------------------------------------
@@ -553,7 +562,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     c->gfail.ensure(std::max<int64_t>(BMAX, FUSE_MAX + 2));
     c->mine.ensure(PMAX + 1);
     c->scalar.ensure(16);
-    c->counter.ensure(1);
+    c->counter.ensure(COUNTER_SLOTS);
     c->io.ensure(1);
     c->simp.ensure(1);
     if (!c->h_io) {
@@ -896,7 +905,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         const DI best = read_scalar(c, c->partial.p + nb);
         if (best.i < 0) {
             *status_out = RP_STATUS_TIMEOUT;
-            c->stats.states_checked += (int64_t)read_scalar(c, c->counter.p);
+            c->stats.states_checked += read_counter(c);
             c->stats.total_ms = 1e3 * (now_s() - t_begin);
             return RP_OK;
         }
@@ -1048,7 +1057,7 @@ int rp_create(rp_ctx** out, int device, const rp_robot_desc* robot) {
         c->scene.base[2] = 0.01f;
         c->scene.plane_z = 0.0f;
         c->scene.n_boxes = 0;
-        c->counter.ensure(1);
+        c->counter.ensure(COUNTER_SLOTS);
         c->scalar.ensure(16);
         upload_scene(c);
     } catch (const HipError& e) {

@@ -16,6 +16,7 @@ from rbe550_final_project_amd.native import Context  # noqa: E402
 def main():
     name = sys.argv[1] if len(sys.argv) > 1 else "goal3_tallest_10box"
     batch = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+    batch_min = batch if (len(sys.argv) > 3 and sys.argv[3] == "full") else 0
     wl = json.load(open(os.path.join(ROOT, "tests", "golden", "workloads", name + ".json")))
     ctx = Context(0, model.robot_desc())
     for rep in range(2):
@@ -24,7 +25,8 @@ def main():
             sc = scenes.Scene.from_json(q["scene"])
             ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
             ctx.set_attached(q["attached"])
-            p = _abi.make_params(seed=i, batch=batch, n_waypoints=150, timeout_s=10.0)
+            p = _abi.make_params(seed=i, batch=batch, batch_min=batch_min, n_waypoints=150, timeout_s=10.0,
+                                 tree_capacity=1 << 24)
             t0 = time.perf_counter()
             path, st = ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
             wall = 1e3 * (time.perf_counter() - t0)

@@ -491,6 +491,11 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_ext_accept_small(const uint8_t
     }
 }
 
+// chain length flag (k_conn_nn, k_ext_conn_nn mout): the chain's last step lands
+// on its target (OMPL REACHED); the low bits are the chain length m
+constexpr int CHAIN_REACHES = 1 << 16;
+constexpr int CHAIN_LEN = CHAIN_REACHES - 1;
+
 // Connect targets [t0, t0 + n): x = A[TA0 + t]; nearest node y of tree B; chain
 // of steers from y toward x (<= cmax). Edge (t, s) direction by tree: B is the
 // start tree (a_start == 0): prev -> next, mode 0; else next -> prev, mode 1.
@@ -516,7 +521,7 @@ __global__ __launch_bounds__(NNBLOCK) void k_conn_nn(const double* __restrict__ 
     const double* ys = Bt + (int64_t)y * NQ;
 #pragma unroll
     for (int d = 0; d < NQ; ++d) cur[d] = ys[d];
-    int m = cmax;
+    int m = cmax, reached = 0;
     for (int s = 0; s < cmax; ++s) {
         const int64_t e = k * cmax + s;
         if (m < cmax) {  // chain already reached x
@@ -535,15 +540,16 @@ __global__ __launch_bounds__(NNBLOCK) void k_conn_nn(const double* __restrict__ 
         valid[e] = 1;
 #pragma unroll
         for (int d = 0; d < NQ; ++d) cur[d] = nxt[d];
-        if (reach) m = s + 1;
+        if (reach) {
+            m = s + 1;
+            reached = 1;
+        }
     }
     gfail[k] = cmax;
     yout[k] = y;
-    mout[k] = m;
+    mout[k] = m | (reached ? CHAIN_REACHES : 0);
 }
 
-// mout flag of k_ext_conn_nn: the chain's last step lands on its target (REACHED)
-constexpr int CHAIN_REACHES = 1 << 16;
 
 // Speculative iteration front (single rank, batches <= FUSE_MAX): for every sample
 // the extension edge AND the connect chain toward its new node, as if the
@@ -625,7 +631,8 @@ __global__ void k_conn_record(const int32_t* __restrict__ y, const int32_t* __re
     if (k >= pt) return;
     if (k < n) {
         rec[2 * k] = y[k];
-        rec[2 * k + 1] = gfail[k] < m[k] ? gfail[k] : m[k];
+        const int mk = m[k] & CHAIN_LEN;
+        rec[2 * k + 1] = gfail[k] < mk ? gfail[k] : mk;
     } else {
         rec[2 * k] = -1;
         rec[2 * k + 1] = 0;
@@ -639,7 +646,8 @@ __global__ void k_conn_record_len(const int32_t* __restrict__ y, const int32_t* 
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= B) return;
     if (k < status[ST_NACC]) {
-        const int l = gfail[k] < m[k] ? gfail[k] : m[k];
+        const int mk = m[k] & CHAIN_LEN;
+        const int l = gfail[k] < mk ? gfail[k] : mk;
         rec[2 * k] = y[k];
         rec[2 * k + 1] = l;
         L[k] = l;
@@ -687,18 +695,39 @@ __device__ __forceinline__ bool conn_append_one(int64_t t, int32_t y, int L, int
 }
 
 // rebuild every target's chain from (y, L), append its first L nodes to tree B,
-// record the first REACHED target and approximate-solution candidates.
+// record the first REACHED target and approximate-solution candidates. With
+// chain_nodes (single rank: this context computed every chain in k_conn_nn) the
+// nodes are copied from the edge records (target t's step s is the checked
+// endpoint of edge t * cmax + s) and REACHED comes from m's flag.
 __global__ void k_conn_append(const int32_t* __restrict__ rec, const int32_t* __restrict__ incl, int64_t n,
                               const double* A, int64_t TA0, double* Bt, int32_t* Bpar, uint8_t* Bcand,
                               int64_t TB, double range, int cmax, int a_start, uint8_t* Acand,
-                              int* first_reached, int32_t* chain_end, const int* __restrict__ status) {
+                              int* first_reached, int32_t* chain_end, const int* __restrict__ status,
+                              const double* __restrict__ chain_nodes, const int32_t* __restrict__ m) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (status) n = min(n, (int64_t)status[ST_NACC]);
     if (t >= n) return;
     const int L = rec[2 * t + 1];
-    if (conn_append_one(t, rec[2 * t], L, TB + incl[t] - L, A, TA0, Bt, Bpar, Bcand, range, cmax, a_start, Acand,
-                        chain_end))
-        atomicMin(first_reached, (int)t);
+    const int64_t off = TB + incl[t] - L;
+    if (!chain_nodes) {
+        if (conn_append_one(t, rec[2 * t], L, off, A, TA0, Bt, Bpar, Bcand, range, cmax, a_start, Acand,
+                            chain_end))
+            atomicMin(first_reached, (int)t);
+        return;
+    }
+    int32_t par = rec[2 * t];
+    for (int s = 0; s < L; ++s) {
+        const double* cs = chain_nodes + (t * cmax + s) * NQ;
+        for (int d = 0; d < NQ; ++d) Bt[(off + s) * NQ + d] = cs[d];
+        Bpar[off + s] = par;
+        Bcand[off + s] = 0;
+        par = (int32_t)(off + s);
+    }
+    const int mk = m[t];
+    const bool reached = L == (mk & CHAIN_LEN) && (mk & CHAIN_REACHES);
+    chain_end[t] = L > 0 ? par : -1;
+    if (!reached && a_start) Acand[TA0 + t] = 1;
+    if (reached) atomicMin(first_reached, (int)t);
 }
 
 // end of an iteration (single lane): nodes added to tree B; on success the join
@@ -788,7 +817,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_conn_accept_small(
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
         const int64_t t = t0 + r;
-        L[r] = t < nacc ? (gfail[t] < m[t] ? gfail[t] : m[t]) : -1;
+        L[r] = t < nacc ? (gfail[t] < (m[t] & CHAIN_LEN) ? gfail[t] : (m[t] & CHAIN_LEN)) : -1;
         cnt += L[r] > 0 ? L[r] : 0;
     }
     int total;
@@ -828,7 +857,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
     for (int r = 0; r < ITEMS; ++r) {
         const int64_t k = k0 + r;
         const int g = k < B ? gfail[k] : 0;
-        const int mk = k < B ? (m[k] & (CHAIN_REACHES - 1)) : 0;
+        const int mk = k < B ? (m[k] & CHAIN_LEN) : 0;
         L[r] = g > 0 ? (g - 1 < mk ? g - 1 : mk) : -1;   // -1: extension rejected
         na += L[r] >= 0;
         nl += L[r] > 0 ? L[r] : 0;
@@ -861,7 +890,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
             par = (int32_t)(off + s);
         }
         const int mk = m[k];
-        const bool reached = L[r] == (mk & (CHAIN_REACHES - 1)) && (mk & CHAIN_REACHES);
+        const bool reached = L[r] == (mk & CHAIN_LEN) && (mk & CHAIN_REACHES);
         chain_end[t] = L[r] > 0 ? par : -1;
         Acand[pos] = (!reached && a_start) ? 1 : 0;
         if (reached) atomicMin(&first, t);

@@ -787,7 +787,8 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                 scan_incl(c, c->Lv.p, c->incl.p, B);
                 hipLaunchKernelGGL(k_conn_append, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->rec.p,
                                    c->incl.p, B, A.q.p, TA, Bt.q.p, Bt.par.p, Bt.cand.p, TB, p.range, cmax,
-                                   a_start, A.cand.p, status + ST_FIRST, c->chain_end.p, (const int*)status);
+                                   a_start, A.cand.p, status + ST_FIRST, c->chain_end.p, (const int*)status,
+                                   (const double*)(a_start ? c->efrom.p : c->eto.p), (const int32_t*)c->mv.p);
                 hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, c->stream, status, c->incl.p, TA, a_start,
                                    A.par.p, Bt.par.p, c->chain_end.p, pa, io);
             }
@@ -860,7 +861,8 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         HIP_TRY(hipMemcpyAsync(c->scalar.p, &big, sizeof(int), hipMemcpyHostToDevice, c->stream));
         hipLaunchKernelGGL(k_conn_append, dim3(blocks_for(nacc, 256)), dim3(256), 0, c->stream, rec, c->incl.p,
                            (int64_t)nacc, A.q.p, TA, Bt.q.p, Bt.par.p, Bt.cand.p, TB, p.range, cmax, a_start,
-                           A.cand.p, c->scalar.p, c->chain_end.p, (const int*)nullptr);
+                           A.cand.p, c->scalar.p, c->chain_end.p, (const int*)nullptr, (const double*)nullptr,
+                           (const int32_t*)nullptr);
         HIP_TRY(hipGetLastError());
         int32_t hdr[2];
         HIP_TRY(hipMemcpyAsync(&hdr[0], c->incl.p + (nacc - 1), sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));

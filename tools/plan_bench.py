@@ -1,0 +1,39 @@
+"""Plan wall time of a workload with a given library build (A/B of variants):
+python tools/plan_bench.py [LIB.so] [workload] [batch] [full]"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from rbe550_final_project_amd import _abi, model, native, scenes  # noqa: E402
+
+
+def main():
+    if len(sys.argv) > 1 and sys.argv[1].endswith(".so"):
+        native.LIB_PATH = os.path.abspath(sys.argv.pop(1))
+    name = sys.argv[1] if len(sys.argv) > 1 else "goal4_pentagon_10box"
+    batch = int(sys.argv[2]) if len(sys.argv) > 2 else 262144
+    batch_min = batch if (len(sys.argv) > 3 and sys.argv[3] == "full") else 0
+    wl = json.load(open(os.path.join(ROOT, "tests", "golden", "workloads", name + ".json")))
+    ctx = native.Context(0, model.robot_desc())
+    for rep in range(3):
+        t = []
+        for i, q in enumerate(wl["queries"]):
+            sc = scenes.Scene.from_json(q["scene"])
+            ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+            ctx.set_attached(q["attached"])
+            p = _abi.make_params(seed=i, batch=batch, batch_min=batch_min, n_waypoints=150, timeout_s=10.0,
+                                 tree_capacity=1 << 24)
+            t0 = time.perf_counter()
+            ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+            t.append(1e3 * (time.perf_counter() - t0))
+        print(f"{os.path.basename(native.LIB_PATH)} {name} batch {batch}: total {sum(t):.2f} ms median "
+              f"{np.median(t):.3f} ms", flush=True)
+
+
+if __name__ == "__main__":
+    main()

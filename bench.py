@@ -128,18 +128,24 @@ def rate_on_scene(ctx, scene, q, n, flags, stream, steps):
     return n / (ms * 1e-3), ms, float(flags[:n].float().mean().item())
 
 
-def cpu_baseline(scene, n_states, threads):
+def cpu_baseline(scene, n_states, threads, chunk=1 << 24):
     """CPU oracle (test infrastructure, the cpu_baseline leg only): OpenMP validity
-    over `threads` host cores on a bounded sample of the same workload."""
+    over `threads` host cores on a bounded sample of the same workload (uniform
+    states, generated in chunks outside the timed calls)."""
     from oracle.oracle import OracleScene
     o = OracleScene()
     o.set_scene(scene.boxes, scene.plane_z, scene.base)
     rng = np.random.default_rng(123)
-    q = (model.Q_LO + (model.Q_HI - model.Q_LO) * rng.random((n_states, 9))).astype(np.float32)
-    o.check_states(q[:4096], threads=threads)
-    t0 = time.perf_counter()
-    o.check_states(q, threads=threads)
-    dt = time.perf_counter() - t0
+    lo32, span32 = model.Q_LO.astype(np.float32), (model.Q_HI - model.Q_LO).astype(np.float32)
+    o.check_states((lo32 + span32 * rng.random((4096, 9), dtype=np.float32)), threads=threads)
+    dt, done = 0.0, 0
+    while done < n_states:
+        m = min(chunk, n_states - done)
+        q = lo32 + span32 * rng.random((m, 9), dtype=np.float32)
+        t0 = time.perf_counter()
+        o.check_states(q, threads=threads)
+        dt += time.perf_counter() - t0
+        done += m
     return n_states / dt, dt
 
 
@@ -283,7 +289,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
             threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-            sample = 1 << 25
+            sample = 1 << 27   # ~8-10 s of oracle work on 16 cores
             rate, dt = cpu_baseline(scene, sample, threads)
             ptimes = cpu_plan_baseline(wl, 0)
             cpu = {"value": round(rate, 1), "unit": "states/s", "cores": threads, "kind": "port",

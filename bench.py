@@ -90,12 +90,19 @@ def run_plans(ctx, wl, batch, seed, group, batch_min=0, tree_capacity=0, stats_o
     return times, states, statuses
 
 
+def max_over_ranks(x, dev, distributed):
+    """max of a float over the ranks (device tensor on RCCL, host tensor on gloo)"""
+    if not distributed:
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def plan_record(times, states, statuses, batch, dev, distributed, extra=None):
     """Summary of a plan workload; total = max over ranks of the summed wall time."""
-    tt = torch.tensor([sum(times)], dtype=torch.float64, device=dev)
-    if distributed:
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-    rec = {"queries": len(times), "batch": batch, "total_ms": round(float(tt.item()), 3),
+    total = max_over_ranks(sum(times), dev, distributed)
+    rec = {"queries": len(times), "batch": batch, "total_ms": round(total, 3),
            "median_ms": round(float(np.median(times)), 3), "max_ms": round(float(np.max(times)), 3),
            "solved": int(sum(s in (_abi.STATUS_EXACT, _abi.STATUS_APPROXIMATE) for s in statuses)),
            "states_checked": int(states), "states_per_sec_in_plan": round(states / (sum(times) / 1e3), 1)}
@@ -174,6 +181,9 @@ def main():
     ap.add_argument("--no-plan", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-configs", action="store_true", help="skip the C2/C4/C5 scene rates (profiling runs)")
+    ap.add_argument("--backend", default="nccl",
+                    help="torch.distributed backend: nccl (= RCCL, the product path) or gloo (rehearsal of N > 1 "
+                         "with several ranks on one GPU; exchanges staged through host memory)")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     args = ap.parse_args()
 
@@ -181,9 +191,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
+    if args.backend == "gloo":   # rehearsal: ranks may share a GPU
+        local = local % max(1, torch.cuda.device_count())
     if distributed:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
     dev = torch.device("cuda", local)
 
     wl = load_workload("goal3_tallest_10box")
@@ -227,10 +242,7 @@ def main():
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
     kernel_ms = e0.elapsed_time(e1) / args.steps      # only the validity kernel is on this stream
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if distributed:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall_max = float(t.item())
+    wall_max = max_over_ranks(wall, dev, distributed)
     valid_frac = float(flags.float().mean().item())
 
     total_states = n * world * args.steps

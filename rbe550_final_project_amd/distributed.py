@@ -23,9 +23,16 @@ class Group:
         self.recv = torch.zeros(self.cap * self.world, dtype=torch.uint8, device=dev)
         self.calls = 0
 
+        staged = dist.get_backend() != "nccl"   # gloo: exchange through host memory
+
         def allgather(nbytes):
             self.calls += 1
-            dist.all_gather_into_tensor(self.recv[: nbytes * self.world], self.send[:nbytes])
+            if staged:
+                out = torch.empty(nbytes * self.world, dtype=torch.uint8)
+                dist.all_gather_into_tensor(out, self.send[:nbytes].cpu())
+                self.recv[: nbytes * self.world].copy_(out)
+            else:
+                dist.all_gather_into_tensor(self.recv[: nbytes * self.world], self.send[:nbytes])
             torch.cuda.synchronize(dev)
 
         ctx.group_init(self.rank, self.world, self.send.data_ptr(), self.recv.data_ptr(), self.cap, allgather)

@@ -44,15 +44,15 @@ class ThreadGroup:
 
 @pytest.mark.parametrize("wl,qi,batch", [("goal4_pentagon_10box", 2, 64), ("goal3_tallest_10box", 5, 256),
                                          ("clutter64", 0, 128)])
-@pytest.mark.parametrize("packed", ["", "1"])
-def test_two_rank_plan_equals_single(oracle_lib, wl, qi, batch, packed, monkeypatch):
-    """packed "1": the ranks' connect launches are work-compacted (k_edges_packed)."""
+@pytest.mark.parametrize("packed,world", [("", 2), ("1", 2), ("", 4)])
+def test_two_rank_plan_equals_single(oracle_lib, wl, qi, batch, packed, world, monkeypatch):
+    """World 2 and 4 (ranks as threads on one GPU); packed "1": the ranks' connect
+    launches are work-compacted (k_edges_packed)."""
     if packed:
         monkeypatch.setenv("RBE_EDGE_PACKED", packed)
     q = json.load(open(os.path.join(GOLD, "workloads", wl + ".json")))["queries"][qi]
     sc = scenes.Scene.from_json(q["scene"])
     p = _abi.make_params(seed=13, batch=batch, n_waypoints=150, timeout_s=60)
-    world = 2
     g = ThreadGroup(world, 8 * (batch // world + 4))
     ctxs = []
     for r in range(world):

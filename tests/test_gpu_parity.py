@@ -262,3 +262,48 @@ def test_plan_invalid_start_goal(gpu_ctx, oracle_lib):
     ok[7:] = np.float32(0.04)
     _, st = gpu_ctx.plan(ok, bad, model.Q_LO, model.Q_HI, p)
     assert st == _abi.STATUS_INVALID_GOAL
+
+
+def _hand_built_cases(oracle_lib):
+    """SURVEY.md §4 item 2 on the GPU: capsule end touching / missing a box face and
+    a yawed box corner (±2e-4 m), a closed grasp with the exemption on / partial /
+    off, the base against the plane with and without the 1 cm raise."""
+    import franka_np as F
+    o = oracle_lib.OracleScene()
+    caps = o.fk_capsules(model.SAFE_HOME)
+    a, b = caps[9]
+    end = b if b[1] > a[1] else a
+    r, h = 0.04, 0.02
+    home = model.SAFE_HOME.copy()
+    home[7:] = np.float32(0.04)
+    cases = []
+    for gap in (2e-4, -2e-4):
+        cases.append(([((float(end[0]), float(end[1] + r + h + gap), float(end[2])), (h, h, h), 0.0)],
+                      (0.0, 0.0, 0.01), -1, _abi.ATTACH_EXEMPT_MASK, model.SAFE_HOME, 1 if gap > 0 else 0))
+        cases.append(([((float(end[0]), float(end[1] + r + h * np.sqrt(2) + gap), float(end[2])), (h, h, h),
+                        np.pi / 4)], (0.0, 0.0, 0.01), -1, _abi.ATTACH_EXEMPT_MASK, model.SAFE_HOME,
+                      1 if gap > 0 else 0))
+    q = model.SAFE_HOME.copy()
+    q[7:] = 0.0
+    R, p = F.hand_pose(q, model.BASE_POS)
+    c = p + R @ np.array([0, 0, 0.0584 + 0.03])
+    grasp = [(tuple(map(float, c)), (0.02, 0.02, 0.02), 0.0)]
+    cases += [(grasp, (0.0, 0.0, 0.01), -1, _abi.ATTACH_EXEMPT_MASK, q, 0),
+              (grasp, (0.0, 0.0, 0.01), 0, _abi.ATTACH_EXEMPT_MASK, q, 1),
+              (grasp, (0.0, 0.0, 0.01), 0, 1 << 9, q, 0),
+              ([], (0.0, 0.0, 0.0), -1, _abi.ATTACH_EXEMPT_MASK, home, 0),
+              ([], (0.0, 0.0, 0.01), -1, _abi.ATTACH_EXEMPT_MASK, home, 1)]
+    return cases
+
+
+def test_hand_built_collision_cases(gpu_ctx, oracle_lib):
+    for boxes, base, att, mask, q, expect in _hand_built_cases(oracle_lib):
+        o = oracle_lib.OracleScene()
+        o.set_scene(boxes, 0.0, base)
+        o.set_attached(att, mask)
+        gpu_ctx.set_scene(boxes, 0.0, base)
+        gpu_ctx.set_attached(att, mask)
+        qq = np.asarray(q, dtype=np.float32)[None, :]
+        assert o.check_states(qq)[0] == expect
+        assert gpu_ctx.check_states(qq)[0] == expect
+        assert sorted(gpu_ctx.contacts(np.asarray(q, dtype=np.float64))) == sorted(o.contacts(q))

@@ -169,3 +169,16 @@ def test_kernel_exemption_equals_rule_on_contacts(oracle_lib):
         assert bool(sc.check_states(q)[0]) == _reference_rule(pairs, 0)
         n_checked += bool(con)
     assert n_checked > 20
+
+
+def test_base_vs_ground_plane(oracle_lib):
+    """The link0 capsule reaches the plane z = 0 unless the base is raised 1 cm as
+    the reference does (scenes.py:29-34); SURVEY.md §4 item 2."""
+    sc = oracle_lib.OracleScene()
+    home = model.SAFE_HOME.copy()
+    home[7:] = np.float32(0.04)
+    sc.set_scene([], 0.0, (0.0, 0.0, 0.0))
+    assert sc.check_states(home)[0] == 0
+    assert {l for l, o in sc.contacts(home)} == {0}
+    sc.set_scene([], 0.0, (0.0, 0.0, 0.01))
+    assert sc.check_states(home)[0] == 1

@@ -748,7 +748,93 @@ __device__ __forceinline__ void finalize_one(int* status, int added, int64_t TA,
     }
 }
 
-// where a solution path goes and how its shortcut candidates are emitted
+// ---------------------------------------------------------------------------
+// path simplification (DESIGN.md §4.5; oracle/rbe_oracle.c simplify_path)
+// ---------------------------------------------------------------------------
+// A fixed program of k_simp steps (one block) alternating with gated edge launches
+// (device count ss->nedges): each step applies the previous stage's edge results
+// and prepares the next stage's candidate edges. Stages: REDUCE (greedy
+// farthest-valid shortcut over all vertex pairs) and SMOOTH (one pass of OMPL
+// smoothBSpline: subdivide, then for every original interior vertex i the checks
+// valid(P[i-1]), motion(P[i-1] -> t), motion(t -> P[i+1]) of its corner cut t).
+// Rounds (ROUND_BEGIN .. ROUND_END) keep their result only if the path got shorter.
+enum : int {
+    OP_BEGIN = 1, OP_APPLY_REDUCE = 2, OP_APPLY_SMOOTH = 4, OP_ROUND_END = 8, OP_ROUND_BEGIN = 16,
+    OP_PREP_REDUCE = 32, OP_PREP_SMOOTH = 64, OP_OUT = 128, OP_STATUS = 256
+};
+constexpr int SIMPLIFY_ROUNDS = 2, SMOOTH_STEPS = 3;
+
+struct SimpState {
+    int n;          // states in P
+    int on;         // device simplification of this path (0 < level, n_raw <= dev_max <= SPMAX)
+    int done;       // nothing changes any more in this call
+    int stop;       // this round's smoothing stopped (a pass changed nothing)
+    int nprev;      // states at the round start
+    int nedges;     // candidate edges of the pending stage
+    int ncand;      // smoothing candidates of the pending stage
+    int changed;
+    long long edges_total;
+    double len0, min_change;
+    double P[SPMAX * NQ];
+    double Pprev[SPMAX * NQ];
+    double Q[SPMAX * NQ];          // subdivision scratch
+    double T[(SPMAX / 2) * NQ];    // corner cuts of the smoothing candidates
+};
+
+// compact index of shortcut (i, j), j >= i + 2, of an n-state path (row-major)
+__device__ __forceinline__ int pair_index(int i, int j, int n) { return i * (n - 2) - i * (i - 1) / 2 + (j - i - 2); }
+
+__device__ __forceinline__ double path_length(const double* P, int n) {
+    double L = 0.0;
+    for (int i = 0; i + 1 < n; ++i) L = L + sqrt(dist2(P + i * NQ, P + (i + 1) * NQ));
+    return L;
+}
+
+__device__ __forceinline__ void emit_edge(int e, const double* a, const double* b, double res, double* efrom,
+                                          double* eto, int* nd, uint8_t* valid) {
+    for (int d = 0; d < NQ; ++d) {
+        efrom[(int64_t)e * NQ + d] = a[d];
+        eto[(int64_t)e * NQ + d] = b[d];
+    }
+    nd[e] = segment_count(a, b, res);
+    valid[e] = 1;
+}
+
+// OP_BEGIN (block-cooperative): the raw path -> P, state reset
+__device__ void simp_begin(int level, int dev_max, const double* __restrict__ raw, const PlanIO* io,
+                           SimpState* ss) {
+    if (threadIdx.x == 0) {
+        const int n = io->n_raw;
+        ss->on = level > 0 && n >= 0 && n <= dev_max;
+        ss->n = ss->on ? n : 0;
+        ss->done = !(ss->on && n >= 3);
+        ss->stop = 0;
+        ss->nedges = 0;
+        ss->edges_total = 0;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < ss->n * NQ; k += blockDim.x) ss->P[k] = raw[k];
+    __syncthreads();
+}
+
+// OP_PREP_REDUCE (block-cooperative): every shortcut (i, j >= i + 2) of P
+__device__ void simp_prep_reduce(double res, SimpState* ss, double* efrom, double* eto, int* nd, uint8_t* valid) {
+    const int n = ss->n;
+    const bool on = !ss->done && n >= 3;
+    if (on)
+        for (int e = threadIdx.x; e < n * n; e += blockDim.x) {
+            const int i = e / n, j = e - i * n;
+            if (j >= i + 2) emit_edge(pair_index(i, j, n), ss->P + i * NQ, ss->P + j * NQ, res, efrom, eto, nd, valid);
+        }
+    if (threadIdx.x == 0) {
+        ss->nedges = on ? (n - 1) * (n - 2) / 2 : 0;
+        ss->edges_total += ss->nedges;
+    }
+    __syncthreads();
+}
+
+// where a solution path goes, and the first simplification step (OP_BEGIN, and
+// OP_PREP_REDUCE when `prep_reduce`) that an iteration's last kernel runs itself
 struct PathArgs {
     const double* S;      // start tree
     const int32_t* Spar;
@@ -756,6 +842,13 @@ struct PathArgs {
     const int32_t* Gpar;
     double* out;          // raw path, `cap` states
     int cap;
+    SimpState* ss;        // simplification state (nullptr: no simplification step)
+    int level, dev_max, prep_reduce;
+    double res;
+    double* efrom;        // candidate edge records
+    double* eto;
+    int* nd;
+    uint8_t* valid;
 };
 
 
@@ -792,6 +885,10 @@ __device__ void iteration_tail(int* status, int added, int64_t TA, int a_start, 
     }
     __syncthreads();
     if (sn != -2) build_path(pa, sn, gn, io);
+    if (pa.ss) {   // (build_path's lane-0 writes are ordered by simp_begin's barrier)
+        simp_begin(pa.level, pa.dev_max, pa.out, io, pa.ss);
+        if (pa.prep_reduce) simp_prep_reduce(pa.res, pa.ss, pa.efrom, pa.eto, pa.nd, pa.valid);
+    }
 }
 
 __global__ void k_finalize(int* status, const int32_t* __restrict__ inclL, int64_t TA, int a_start,
@@ -911,78 +1008,13 @@ __global__ void k_path(PathArgs pa, int32_t s_node, int32_t g_node, PlanIO* io) 
     build_path(pa, s_node, g_node, io);
 }
 
-// ---------------------------------------------------------------------------
-// path simplification (DESIGN.md §4.5; oracle/rbe_oracle.c simplify_path)
-// ---------------------------------------------------------------------------
-// A fixed program of k_simp steps (one block) alternating with gated edge launches
-// (device count ss->nedges): each step applies the previous stage's edge results
-// and prepares the next stage's candidate edges. Stages: REDUCE (greedy
-// farthest-valid shortcut over all vertex pairs) and SMOOTH (one pass of OMPL
-// smoothBSpline: subdivide, then for every original interior vertex i the checks
-// valid(P[i-1]), motion(P[i-1] -> t), motion(t -> P[i+1]) of its corner cut t).
-// Rounds (ROUND_BEGIN .. ROUND_END) keep their result only if the path got shorter.
-enum : int {
-    OP_BEGIN = 1, OP_APPLY_REDUCE = 2, OP_APPLY_SMOOTH = 4, OP_ROUND_END = 8, OP_ROUND_BEGIN = 16,
-    OP_PREP_REDUCE = 32, OP_PREP_SMOOTH = 64, OP_OUT = 128, OP_STATUS = 256
-};
-constexpr int SIMPLIFY_ROUNDS = 2, SMOOTH_STEPS = 3;
-
-struct SimpState {
-    int n;          // states in P
-    int on;         // device simplification of this path (0 < level, n_raw <= dev_max <= SPMAX)
-    int done;       // nothing changes any more in this call
-    int stop;       // this round's smoothing stopped (a pass changed nothing)
-    int nprev;      // states at the round start
-    int nedges;     // candidate edges of the pending stage
-    int ncand;      // smoothing candidates of the pending stage
-    int changed;
-    long long edges_total;
-    double len0, min_change;
-    double P[SPMAX * NQ];
-    double Pprev[SPMAX * NQ];
-    double Q[SPMAX * NQ];          // subdivision scratch
-    double T[(SPMAX / 2) * NQ];    // corner cuts of the smoothing candidates
-};
-
-// compact index of shortcut (i, j), j >= i + 2, of an n-state path (row-major)
-__device__ __forceinline__ int pair_index(int i, int j, int n) { return i * (n - 2) - i * (i - 1) / 2 + (j - i - 2); }
-
-__device__ __forceinline__ double path_length(const double* P, int n) {
-    double L = 0.0;
-    for (int i = 0; i + 1 < n; ++i) L = L + sqrt(dist2(P + i * NQ, P + (i + 1) * NQ));
-    return L;
-}
-
-__device__ __forceinline__ void emit_edge(int e, const double* a, const double* b, double res, double* efrom,
-                                          double* eto, int* nd, uint8_t* valid) {
-    for (int d = 0; d < NQ; ++d) {
-        efrom[(int64_t)e * NQ + d] = a[d];
-        eto[(int64_t)e * NQ + d] = b[d];
-    }
-    nd[e] = segment_count(a, b, res);
-    valid[e] = 1;
-}
-
 __global__ __launch_bounds__(256) void k_simp(int ops, int level, int dev_max, double res,
                                               const double* __restrict__ raw,
                                               PlanIO* io, SimpState* ss, double* efrom, double* eto, int* nd,
                                               uint8_t* valid, const unsigned long long* __restrict__ counter,
                                               PlanIO* hio, int seq) {
     const int tid = threadIdx.x, nt = blockDim.x;
-    if (ops & OP_BEGIN) {
-        if (tid == 0) {
-            const int n = io->n_raw;
-            ss->on = level > 0 && n >= 0 && n <= dev_max;
-            ss->n = ss->on ? n : 0;
-            ss->done = !(ss->on && n >= 3);
-            ss->stop = 0;
-            ss->nedges = 0;
-            ss->edges_total = 0;
-        }
-        __syncthreads();
-        for (int k = tid; k < ss->n * NQ; k += nt) ss->P[k] = raw[k];
-        __syncthreads();
-    }
+    if (ops & OP_BEGIN) simp_begin(level, dev_max, raw, io, ss);
     if (ops & OP_APPLY_REDUCE) {
         if (tid == 0 && !ss->done && ss->nedges > 0) {   // greedy walk, in place (writes trail reads)
             const int n = ss->n;
@@ -1047,17 +1079,7 @@ __global__ __launch_bounds__(256) void k_simp(int ops, int level, int dev_max, d
             for (int k = tid; k < ss->n * NQ; k += nt) ss->Pprev[k] = ss->P[k];
         __syncthreads();
     }
-    if (ops & OP_PREP_REDUCE) {
-        const int n = ss->n;
-        const bool on = !ss->done && n >= 3;
-        if (on)
-            for (int e = tid; e < n * n; e += nt) {
-                const int i = e / n, j = e - i * n;
-                if (j >= i + 2) emit_edge(pair_index(i, j, n), ss->P + i * NQ, ss->P + j * NQ, res, efrom, eto, nd, valid);
-            }
-        if (tid == 0) ss->nedges = on ? (n - 1) * (n - 2) / 2 : 0;
-        __syncthreads();
-    }
+    if (ops & OP_PREP_REDUCE) simp_prep_reduce(res, ss, efrom, eto, nd, valid);
     if (ops & OP_PREP_SMOOTH) {
         const bool on = !ss->done && !ss->stop;
         if (on) {   // PathGeometric::subdivide
@@ -1098,7 +1120,7 @@ __global__ __launch_bounds__(256) void k_simp(int ops, int level, int dev_max, d
         }
         __syncthreads();
     }
-    if ((ops & (OP_PREP_REDUCE | OP_PREP_SMOOTH)) && tid == 0) ss->edges_total += ss->nedges;
+    if ((ops & OP_PREP_SMOOTH) && tid == 0) ss->edges_total += ss->nedges;
     if (ops & (OP_OUT | OP_STATUS)) {
         // a status publication carries the output too once nothing is left to do
         const int n_raw = io->n_raw;

@@ -650,15 +650,21 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     int dev_max = SPMAX;
     if (const char* e = std::getenv("RBE_SIMPLIFY_DEVICE_MAX"))
         if (*e) dev_max = std::max(0, std::min(SPMAX, std::atoi(e)));
-    auto run_program = [&](size_t from, size_t to, int seq) {
+    // first_in_kernel: step `from`'s OP_BEGIN / OP_PREP_REDUCE already ran in the
+    // iteration's last kernel (PathArgs.ss), only its edge launch and any other
+    // ops of that step remain
+    auto run_program = [&](size_t from, size_t to, int seq, bool first_in_kernel) {
         for (size_t k = from; k < to; ++k) {
             int ops = prog[k];
+            if (first_in_kernel && k == from) ops &= ~(OP_BEGIN | OP_PREP_REDUCE);
             if (k + 1 == to) ops |= (ops & OP_OUT) ? 0 : OP_STATUS;
-            hipLaunchKernelGGL(k_simp, dim3(1), dim3(256), 0, c->stream, ops, level, dev_max, p.resolution,
-                               (const double*)c->path.p, io, c->simp.p, c->efrom.p, c->eto.p, c->nd.p, c->valid.p,
-                               (const unsigned long long*)c->counter.p, h, k + 1 == to ? seq : 0);
-            HIP_TRY(hipGetLastError());
-            if (ops & (OP_PREP_REDUCE | OP_PREP_SMOOTH))
+            if (ops) {
+                hipLaunchKernelGGL(k_simp, dim3(1), dim3(256), 0, c->stream, ops, level, dev_max, p.resolution,
+                                   (const double*)c->path.p, io, c->simp.p, c->efrom.p, c->eto.p, c->nd.p,
+                                   c->valid.p, (const unsigned long long*)c->counter.p, h, k + 1 == to ? seq : 0);
+                HIP_TRY(hipGetLastError());
+            }
+            if (prog[k] & (OP_PREP_REDUCE | OP_PREP_SMOOTH))
                 launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, (int64_t)(SPMAX - 1) * (SPMAX - 2) / 2, kfull, 0,
                              c->valid.p, 1, nullptr, c->stream, &c->simp.p->nedges, 1, 2048);
         }
@@ -670,6 +676,15 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     pa.Gpar = c->tree[1].par.p;
     pa.out = c->path.p;
     pa.cap = PATH_CAP;
+    pa.ss = c->simp.p;            // single-rank iterations run OP_BEGIN (+ OP_PREP_REDUCE) in their tail
+    pa.level = level;
+    pa.dev_max = dev_max;
+    pa.prep_reduce = (prog[0] & OP_PREP_REDUCE) ? 1 : 0;
+    pa.res = p.resolution;
+    pa.efrom = c->efrom.p;
+    pa.eto = c->eto.p;
+    pa.nd = c->nd.p;
+    pa.valid = c->valid.p;
 
     Bounds bd;
     for (int i = 0; i < NQ; ++i) { bd.lo[i] = lo[i]; bd.hi[i] = hi[i]; }
@@ -712,7 +727,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             else RP_ITER_SMALL(4);
 #undef RP_ITER_SMALL
             HIP_TRY(hipGetLastError());
-            run_program(0, tail_steps, seq);
+            run_program(0, tail_steps, seq, true);
             wait_seq(c, seq);
             if (!sg_known) {
                 if (const int code = endpoint_status(h->status[ST_SG])) return endpoint_fail(code);
@@ -794,7 +809,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             }
             // the first simplification steps run every iteration (empty unless this
             // one solved), so a solving iteration needs no extra host round trip
-            run_program(0, tail_steps, seq);
+            run_program(0, tail_steps, seq, true);
             wait_seq(c, seq);
             if (!sg_known) {
                 if (const int code = endpoint_status(h->status[ST_SG])) return endpoint_fail(code);
@@ -927,7 +942,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     const size_t from = tail_ran ? tail_steps : 0;
     if (from < prog.size() && !(tail_ran && h->out)) {
         const int seq = ++c->seq;
-        run_program(from, prog.size(), seq);
+        run_program(from, prog.size(), seq, false);
         wait_seq(c, seq);
     }
     const int n_raw = h->n_raw;

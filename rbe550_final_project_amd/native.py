@@ -156,7 +156,9 @@ class Context:
         goal = np.ascontiguousarray(goal, dtype=np.float64)
         lo = np.ascontiguousarray(lo, dtype=np.float64)
         hi = np.ascontiguousarray(hi, dtype=np.float64)
-        out = np.zeros((path_cap, _abi.NQ), dtype=np.float64)
+        out = getattr(self, "_plan_out", None)   # reused output buffer (no per-call allocation)
+        if out is None or len(out) < path_cap:
+            out = self._plan_out = np.empty((path_cap, _abi.NQ), dtype=np.float64)
         n = C.c_int32(0)
         status = C.c_int32(0)
         self._check(load().rp_plan(self._h, _ptr(start), _ptr(goal), _ptr(lo), _ptr(hi), C.byref(params),

@@ -280,7 +280,9 @@ def main():
                 extra = {}
                 t4, s4, st4 = run_plans(ctx, load_workload(wname), batch, 0, group, batch_min=batch,
                                         tree_capacity=cap, stats_out=extra)
+                it = max(1, int(extra.get("iterations", 0)))
                 extra = {"batch_min": batch, "exchange_ms": round(extra.get("exchange_ms", 0.0), 3),
+                         "exchange_ms_per_iteration": round(extra.get("exchange_ms", 0.0) / it, 4),
                          "iterations": int(extra.get("iterations", 0)), "samples": int(extra.get("samples", 0))}
                 plan[key] = plan_record(t4, s4, st4, batch, dev, distributed, extra)
             except Exception as ex:

@@ -562,7 +562,9 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
             struct Rec { float v[16]; };
             const Rec rec = *reinterpret_cast<const Rec*>(sc->box[j]);
             const float* bx = rec.v;
-            const bool cand = near_cl & !((__float_as_uint(bx[14]) >> C) & 1u) & !aabb_disjoint(u, bx + 8, bx + 11);
+            const bool exempt = (__float_as_uint(bx[14]) >> C) & 1u;
+            const bool apart = aabb_disjoint(u, bx + 8, bx + 11);   // both evaluated: no branch
+            const bool cand = near_cl && !exempt && !apart;
 #else
             const float* bx = sc->box[j];
             const bool cand = near_cl && !((__float_as_uint(bx[14]) >> C) & 1u) && !aabb_disjoint(u, bx + 8, bx + 11);

@@ -405,22 +405,10 @@ __device__ __forceinline__ bool pairs_ending_at(const Capsules& k) {
 constexpr int QCAP = RP_QCAP;   // items per queue; drained once more than QCAP-64 are pending
 
 struct WaveQ {
-    float ss[QCAP][13];   // self pair: a1 b1 a2 b2 (12), owner lane | pair << 8
+    float ss[QCAP][15];   // self pair: a1 b1 a2 b2 (12), owner lane | pair << 8, r_i, r_j
     float sb[QCAP][11];   // capsule-box: pa pb (box frame) h (9), r^2, owner lane
     int hit[64];          // per-lane collision found by a drained item
 };
-
-// radii of each self pair: r_i, r_j (read by pair id when a queue item is drained)
-struct PairRadii { float r[NPAIR][2]; };
-constexpr PairRadii make_pair_radii() {
-    PairRadii t{};
-    for (int p = 0; p < NPAIR; ++p) {
-        t.r[p][0] = CAP_GEOM[PAIRS[p][0]][6];
-        t.r[p][1] = CAP_GEOM[PAIRS[p][1]][6];
-    }
-    return t;
-}
-__device__ constexpr PairRadii PAIR_RADII = make_pair_radii();
 
 __device__ __forceinline__ int rank_in(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -469,8 +457,9 @@ __device__ RP_DRAIN_ATTR void drain_ss(S& s) {
         const V3 a1 = {it[0], it[1], it[2]}, b1 = {it[3], it[4], it[5]};
         const V3 a2 = {it[6], it[7], it[8]}, b2 = {it[9], it[10], it[11]};
         const int tag = __float_as_int(it[12]);
-        const int p = tag >> 8;
-        const float ri = PAIR_RADII.r[p][0], rj = PAIR_RADII.r[p][1];
+        // radii travel with the item (a table lookup by the lane's pair id was a
+        // global load with a full wait in every drain pass)
+        const float ri = it[13], rj = it[14];
         // the oracle's exact decision: AABB reject, then segment distance
         const Aabb u = capsule_aabb(a1, b1, ri);
         const Aabb v = capsule_aabb(a2, b2, rj);
@@ -557,7 +546,6 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
         if (!__any(near_cl)) continue;
         const int j0 = __float_as_int(cr[3]), nj = __float_as_int(cr[7]);
         for (int j = j0; j < j0 + nj; ++j) {
-#ifndef RP_OPT_BOXLOAD
             // the whole 64-B record in one scalar load; branch-free candidate test
             struct Rec { float v[16]; };
             const Rec rec = *reinterpret_cast<const Rec*>(sc->box[j]);
@@ -565,10 +553,6 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
             const bool exempt = (__float_as_uint(bx[14]) >> C) & 1u;
             const bool apart = aabb_disjoint(u, bx + 8, bx + 11);   // both evaluated: no branch
             const bool cand = near_cl && !exempt && !apart;
-#else
-            const float* bx = sc->box[j];
-            const bool cand = near_cl && !((__float_as_uint(bx[14]) >> C) & 1u) && !aabb_disjoint(u, bx + 8, bx + 11);
-#endif
             const unsigned long long m = __ballot(cand);
             if (!m) continue;
             if (cand) enqueue_sb<C>(k, bx, r, s, m);
@@ -597,15 +581,21 @@ constexpr float sphere_radius() {
     return (float)((double)CAP_GEOM[C][6] + 0.5 * csqrt(dx * dx + dy * dy + dz * dz) + 1e-4);
 }
 
-template <int P, class S>
-__device__ __forceinline__ void pair_queued(const Capsules& k, S& s) {
+// sphere prefilter of self pair P (exact reject, see sphere_radius)
+template <int P>
+__device__ __forceinline__ bool pair_sphere(const Capsules& k) {
     constexpr int I = PAIRS[P][0], J = PAIRS[P][1];
     constexpr float RS = sphere_radius<I>() + sphere_radius<J>();
     const V3 d = {(k.a[I].x + k.b[I].x) - (k.a[J].x + k.b[J].x), (k.a[I].y + k.b[I].y) - (k.a[J].y + k.b[J].y),
                   (k.a[I].z + k.b[I].z) - (k.a[J].z + k.b[J].z)};
     // |centre_I - centre_J| <= RS  <=>  |2 centre_I - 2 centre_J|^2 <= (2 RS)^2
-    const bool cand = dot3(d, d) <= (2.0f * RS) * (2.0f * RS);
-    const unsigned long long m = __ballot(cand);
+    return dot3(d, d) <= (2.0f * RS) * (2.0f * RS);
+}
+
+// queue the candidates of pair P (wave-uniform call)
+template <int P, class S>
+__device__ __forceinline__ void pair_enqueue(const Capsules& k, S& s, bool cand, unsigned long long m) {
+    constexpr int I = PAIRS[P][0], J = PAIRS[P][1];
     if (!m) return;
     if (cand) {
         float* it = s.Q->ss[s.nss + rank_in(m)];
@@ -614,19 +604,46 @@ __device__ __forceinline__ void pair_queued(const Capsules& k, S& s) {
         it[6] = k.a[J].x; it[7] = k.a[J].y; it[8] = k.a[J].z;
         it[9] = k.b[J].x; it[10] = k.b[J].y; it[11] = k.b[J].z;
         it[12] = __int_as_float(s.lane | (P << 8));
+        it[13] = CAP_GEOM[I][6];
+        it[14] = CAP_GEOM[J][6];
     }
     s.nss += __popcll(m);
     if (s.nss > QCAP - 64) drain_ss(s);
 }
 
-template <int J, int P = 0, class S>
+constexpr bool pairs_in_chain_order() {
+    for (int P = 0; P < NPAIR; ++P)
+        if (PAIRS[P][0] >= PAIRS[P][1]) return false;
+    return true;
+}
+// a pair is complete (both capsules placed) when its second capsule is
+static_assert(pairs_in_chain_order(), "self pair out of chain order");
+
+// the self pairs whose second capsule is J, in PAIRS order
+struct PairList { int n; int p[NPAIR]; };
+template <int J>
+constexpr PairList pairs_ending() {
+    PairList l{};
+    for (int P = 0; P < NPAIR; ++P)
+        if (PAIRS[P][1] == J) l.p[l.n++] = P;
+    return l;
+}
+
+template <int J, int T, class S>
+__device__ __forceinline__ void pairs_each(const Capsules& k, S& s) {
+    constexpr PairList L = pairs_ending<J>();
+    if constexpr (T < L.n) {
+        const bool cand = pair_sphere<L.p[T]>(k);
+        pair_enqueue<L.p[T]>(k, s, cand, __ballot(cand));
+        pairs_each<J, T + 1, S>(k, s);
+    }
+}
+
+template <int J, class S>
 __device__ __forceinline__ void pairs_queued(const Capsules& k, S& s) {
-    if constexpr (P < NPAIR) {
-        if constexpr (PAIRS[P][1] == J) {
-            static_assert(PAIRS[P][0] < J, "self pair out of chain order");
-            pair_queued<P>(k, s);
-        }
-        pairs_queued<J, P + 1>(k, s);
+    constexpr PairList L = pairs_ending<J>();
+    if constexpr (L.n > 0) {
+        pairs_each<J, 0, S>(k, s);
     }
 }
 

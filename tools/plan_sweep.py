@@ -1,0 +1,56 @@
+"""Plan wall time of a workload over a sweep of batch schedules (batch, batch_min):
+median / total per-query wall ms, iterations and states checked (1 GPU).
+Usage: python tools/plan_sweep.py [workload] [batch] [batch_min ...]"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from rbe550_final_project_amd import _abi, model, scenes  # noqa: E402
+from rbe550_final_project_amd.native import Context  # noqa: E402
+
+
+def run(ctx, wl, batch, bmin, seed0):
+    walls, iters, states, solved = [], 0, 0, 0
+    for i, q in enumerate(wl["queries"]):
+        sc = scenes.Scene.from_json(q["scene"])
+        ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+        ctx.set_attached(q["attached"])
+        p = _abi.make_params(seed=seed0 + i, batch=batch, batch_min=bmin, n_waypoints=150, timeout_s=10.0)
+        t0 = time.perf_counter()
+        _, st = ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+        walls.append(1e3 * (time.perf_counter() - t0))
+        s = ctx.stats()
+        iters += s["iterations"]
+        states += s["states_checked"]
+        solved += st in (_abi.STATUS_EXACT, _abi.STATUS_APPROXIMATE)
+    return walls, iters, states, solved
+
+
+def main():
+    name = sys.argv[1] if len(sys.argv) > 1 else "goal3_tallest_10box"
+    batch = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+    bmins = [int(x) for x in sys.argv[3:]] or [32, 64, 128, 256, 512]
+    wl = json.load(open(os.path.join(ROOT, "tests", "golden", "workloads", name + ".json")))
+    ctx = Context(0, model.robot_desc())
+    run(ctx, wl, batch, bmins[0], 100)   # warm-up
+    for bmin in bmins:
+        allw, it, stt, sv = [], 0, 0, 0
+        for seed0 in (0, 1000, 2000):
+            w, i, s, k = run(ctx, wl, batch, bmin, seed0)
+            allw += w
+            it += i
+            stt += s
+            sv += k
+        n = len(allw)
+        print(f"{name} batch {batch} batch_min {bmin:5d}: median {np.median(allw):.3f} ms  mean {np.mean(allw):.3f}  "
+              f"p90 {np.percentile(allw, 90):.3f}  iters/query {it / n:.2f}  states/query {stt / n:.0f}  solved {sv}/{n}",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

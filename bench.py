@@ -67,15 +67,17 @@ def pmc_traffic(n_states):
         return None
 
 
-def run_plans(ctx, wl, batch, seed, group, batch_min=0, tree_capacity=0, stats_out=None):
-    """Wall time of every query of a workload (ms), plus aggregate states checked."""
+def run_plans(ctx, wl, batch, seed, group, batch_min=0, tree_capacity=0, stats_out=None, straight_first=True):
+    """Wall time of every query of a workload (ms), plus aggregate states checked.
+    straight_first=False forces RRT-Connect on every query (the product default
+    first checks the straight edge start -> goal)."""
     times, states, statuses = [], 0, []
     for i, q in enumerate(wl["queries"]):
         sc = scenes.Scene.from_json(q["scene"])
         ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
         ctx.set_attached(q["attached"])
         p = _abi.make_params(seed=seed + i, batch=batch, batch_min=batch_min, n_waypoints=150, timeout_s=10.0,
-                             tree_capacity=tree_capacity)
+                             tree_capacity=tree_capacity, straight_first=straight_first)
         if group is not None:
             dist.barrier()
         t0 = time.perf_counter()
@@ -156,7 +158,7 @@ def cpu_baseline(scene, n_states, threads, chunk=1 << 24):
     return n_states / dt, dt
 
 
-def cpu_plan_baseline(wl, seed):
+def cpu_plan_baseline(wl, seed, straight_first=True):
     from oracle.oracle import OracleScene
     o = OracleScene()
     times = []
@@ -164,7 +166,7 @@ def cpu_plan_baseline(wl, seed):
         sc = scenes.Scene.from_json(q["scene"])
         o.set_scene(sc.boxes, sc.plane_z, sc.base)
         o.set_attached(q["attached"])
-        p = _abi.make_params(seed=seed + i, batch=1, n_waypoints=150, timeout_s=10.0)
+        p = _abi.make_params(seed=seed + i, batch=1, n_waypoints=150, timeout_s=10.0, straight_first=straight_first)
         t0 = time.perf_counter()
         o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
         times.append(1e3 * (time.perf_counter() - t0))
@@ -271,7 +273,12 @@ def main():
                 group = Group(ctx, max(args.plan_batch, C4_BATCH), local)
             run_plans(ctx, {"queries": wl["queries"][:2]}, args.plan_batch, 100, group)   # warm-up
             times, pstates, st = run_plans(ctx, wl, args.plan_batch, 0, group)
-            plan = plan_record(times, pstates, st, args.plan_batch, dev, distributed)
+            plan = plan_record(times, pstates, st, args.plan_batch, dev, distributed,
+                               {"mode": "product default: straight edge first, then RRT-Connect"})
+            # the same queries with RRT-Connect forced (straight_first off)
+            t3, s3, st3 = run_plans(ctx, wl, args.plan_batch, 0, group, straight_first=False)
+            plan["C3_rrt"] = plan_record(t3, s3, st3, args.plan_batch, dev, distributed,
+                                         {"mode": "RRT-Connect forced (straight_first off)"})
         except Exception as ex:  # report, keep the primary metric
             plan = {"error": repr(ex)[:300]}
         for key, wname, batch, cap in (("C4_pentagon", "goal4_pentagon_10box", C4_BATCH, 1 << 24),
@@ -279,9 +286,9 @@ def main():
             try:
                 extra = {}
                 t4, s4, st4 = run_plans(ctx, load_workload(wname), batch, 0, group, batch_min=batch,
-                                        tree_capacity=cap, stats_out=extra)
+                                        tree_capacity=cap, stats_out=extra, straight_first=False)
                 it = max(1, int(extra.get("iterations", 0)))
-                extra = {"batch_min": batch, "exchange_ms": round(extra.get("exchange_ms", 0.0), 3),
+                extra = {"mode": "RRT-Connect forced (straight_first off)", "batch_min": batch, "exchange_ms": round(extra.get("exchange_ms", 0.0), 3),
                          "exchange_ms_per_iteration": round(extra.get("exchange_ms", 0.0) / it, 4),
                          "iterations": int(extra.get("iterations", 0)), "samples": int(extra.get("samples", 0))}
                 plan[key] = plan_record(t4, s4, st4, batch, dev, distributed, extra)
@@ -306,10 +313,12 @@ def main():
             sample = 1 << 27   # ~8-10 s of oracle work on 16 cores
             rate, dt = cpu_baseline(scene, sample, threads)
             ptimes = cpu_plan_baseline(wl, 0)
+            rtimes = cpu_plan_baseline(wl, 0, straight_first=False)
             cpu = {"value": round(rate, 1), "unit": "states/s", "cores": threads, "kind": "port",
                    "sample": f"{sample} uniform states, goal3 10-box scene, OpenMP CPU oracle ({dt:.1f} s)",
                    "plan_total_ms": round(sum(ptimes), 3), "plan_median_ms": round(float(np.median(ptimes)), 3),
-                   "plan_sample": "21 goal3 queries, sequential RRT-Connect (batch 1), 1 core"}
+                   "plan_sample": "21 goal3 queries, straight edge first then sequential RRT-Connect (batch 1), 1 core",
+                   "plan_rrt_total_ms": round(sum(rtimes), 3), "plan_rrt_median_ms": round(float(np.median(rtimes)), 3)}
         except Exception as ex:
             cpu = {"error": repr(ex)[:300]}
 

@@ -117,6 +117,11 @@ typedef struct rp_plan_params {
                                structure (shortcuts + B-spline rounds);
                                2 = vertex shortcuts only                                */
     int64_t tree_capacity;  /* nodes per tree, default 1<<22                                */
+    int32_t straight_first; /* 0 (default) = with simplification on, check the straight edge
+                               start -> goal first and return it when valid (the path the
+                               shortcut stage would reduce any solution to); < 0 = always
+                               run RRT-Connect; ignored when simplify == 0               */
+    int32_t reserved;       /* 0                                                            */
 } rp_plan_params;
 
 /* rp_ik parameters (defaults follow Genesis inverse_kinematics). Zero / negative

@@ -777,6 +777,29 @@ int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], co
     }
     st.states_checked += 2;
 
+    /* straight-first (rp_plan_params.straight_first, rp_lib.hip plan_impl): with
+     * simplification on, a valid straight edge start -> goal is the path REDUCE's
+     * greedy farthest-valid walk would shorten any solution to, so it is checked
+     * first and returned when valid */
+    if (p.simplify > 0 && p.straight_first >= 0) {
+        st.edges_checked++;
+        if (edge_valid(s, start, goal, 0, p.resolution, &st.states_checked)) {
+            double raw2[2 * NQ];
+            memcpy(raw2, start, sizeof(double) * NQ);
+            memcpy(raw2 + NQ, goal, sizeof(double) * NQ);
+            int m = (p.n_waypoints > 0) ? ro_interpolate(raw2, 2, p.n_waypoints, path_out, path_cap)
+                                        : (2 <= path_cap ? (memcpy(path_out, raw2, sizeof raw2), 2) : -1);
+            st.start_tree_size = st.goal_tree_size = 1;
+            st.path_states_raw = st.path_states_simplified = 2;
+            st.total_ms = 1e3 * (now_s() - t_begin);
+            if (stats) *stats = st;
+            if (m < 0) return RP_ERR_CAPACITY;
+            *n_out = m;
+            *status_out = RP_STATUS_EXACT;
+            return RP_OK;
+        }
+    }
+
     tree_t T[2];
     if (!tree_init(&T[0], p.tree_capacity) || !tree_init(&T[1], p.tree_capacity)) return RP_ERR_CAPACITY;
     tree_add(&T[0], start, -1);

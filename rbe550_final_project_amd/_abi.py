@@ -36,7 +36,8 @@ class Box(C.Structure):
 class PlanParams(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("batch", C.c_int64), ("batch_min", C.c_int64), ("range", C.c_double),
                 ("resolution", C.c_double), ("timeout_s", C.c_double), ("max_iters", C.c_int64),
-                ("n_waypoints", C.c_int32), ("simplify", C.c_int32), ("tree_capacity", C.c_int64)]
+                ("n_waypoints", C.c_int32), ("simplify", C.c_int32), ("tree_capacity", C.c_int64),
+                ("straight_first", C.c_int32), ("reserved", C.c_int32)]
 
 
 class IkParams(C.Structure):
@@ -81,7 +82,7 @@ def make_boxes(boxes):
 
 
 def make_params(seed=0, batch=4096, range_=0.0, resolution=0.0, timeout_s=5.0, max_iters=0, batch_min=0,
-                n_waypoints=100, simplify=True, tree_capacity=0):
+                n_waypoints=100, simplify=True, tree_capacity=0, straight_first=True):
     p = PlanParams()
     p.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     p.batch = int(batch)
@@ -93,4 +94,5 @@ def make_params(seed=0, batch=4096, range_=0.0, resolution=0.0, timeout_s=5.0, m
     p.n_waypoints = int(n_waypoints or 0)
     p.simplify = 1 if simplify else 0
     p.tree_capacity = int(tree_capacity)
+    p.straight_first = 0 if straight_first else -1   # 0 = default (on with simplification)
     return p

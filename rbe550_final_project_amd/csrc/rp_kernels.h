@@ -353,6 +353,56 @@ __device__ __forceinline__ void publish_seq(PlanIO* hio, int seq) {
     __hip_atomic_store(&hio->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// Straight-first check in one launch: lane 0 = start, lane 1 = goal, lanes
+// 2..nd = the interior slots 1..nd-1 of start -> goal (checkMotion mode 0, the
+// states k_edges would build: interp(start, goal, slot / nd) rounded to float32).
+// Blocks OR their failures into sync[0] (bit 0 start, 1 goal, 2 interior); the
+// last block to finish (sync[1] counts them) publishes the flags as bits 0 / 8 /
+// 16 of status[ST_SG] with the number of states checked, then resets sync.
+struct Endpoints { double start[NQ]; double goal[NQ]; };
+template <int NCL>
+__global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_straight(Endpoints ep, double res,
+                                                                    const DevScene* __restrict__ sc,
+                                                                    unsigned* sync, PlanIO* hio, int seq) {
+    __shared__ WaveQ wq;
+    __shared__ int last;
+    const int nd = segment_count(ep.start, ep.goal, res);
+    const int64_t lanes = nd >= 1 ? (int64_t)nd + 1 : 2;
+    const int64_t idx = (int64_t)blockIdx.x * VBLOCK + threadIdx.x;
+    unsigned bad = 0;
+    if (idx < lanes) {
+        double st[NQ];
+        if (idx < 2) {
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) st[k] = idx == 0 ? ep.start[k] : ep.goal[k];
+        } else {
+            interp(ep.start, ep.goal, (double)(idx - 1) / (double)nd, st);
+        }
+        float qq[NQ];
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) qq[k] = (float)st[k];
+        if (state_collides<NCL>(qq, sc, wq)) bad = idx == 0 ? 1u : idx == 1 ? 2u : 4u;
+    }
+    // wave OR, then one atomic per block (a block is one wave)
+    const unsigned long long b1 = __ballot(bad & 1u), b2 = __ballot(bad & 2u), b4 = __ballot(bad & 4u);
+    if (threadIdx.x == 0) {
+        const unsigned wbad = (b1 ? 1u : 0u) | (b2 ? 2u : 0u) | (b4 ? 4u : 0u);
+        if (wbad) atomicOr(&sync[0], wbad);
+        __threadfence();
+        last = atomicAdd(&sync[1], 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && threadIdx.x == 0) {
+        __threadfence();
+        const unsigned f = atomicOr(&sync[0], 0u);
+        hio->status[ST_SG] = ((f & 1u) ? 0 : 1) | ((f & 2u) ? 0 : 0x100) | ((f & 6u) ? 0 : 0x10000);
+        hio->counter = (unsigned long long)lanes;
+        sync[0] = 0;
+        sync[1] = 0;
+        publish_seq(hio, seq);
+    }
+}
+
 // rp_plan prologue (one block): tree roots, float32 copies of start / goal, counters
 // (replaces per-field host->device copies). sg_edge >= 0: start and goal also
 // become zero-length edges at sg_edge and sg_edge + stride of the first extension

@@ -105,6 +105,7 @@ struct rp_ctx {
     DevBuf<uint8_t> eval;
     DevBuf<int> scalar;                  // small device scalars
     DevBuf<unsigned long long> counter;
+    DevBuf<unsigned> sync;               // k_straight: failure bits, finished blocks (kept zeroed)
 
     // planner workspace
     Tree tree[2];
@@ -563,6 +564,10 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     c->mine.ensure(PMAX + 1);
     c->scalar.ensure(16);
     c->counter.ensure(COUNTER_SLOTS);
+    if (!c->sync.p) {
+        c->sync.ensure(2);
+        HIP_TRY(hipMemsetAsync(c->sync.p, 0, 2 * sizeof(unsigned), c->stream));
+    }
     c->io.ensure(1);
     c->simp.ensure(1);
     if (!c->h_io) {
@@ -603,18 +608,12 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         return packed_mode >= 0 ? packed_mode == 1 : n_edges * (int64_t)kmax >= ((int64_t)1 << 20);
     };
     const bool spec0 = speculate && p.batch_min <= FUSE_MAX;
-    const int64_t sg_edge = (world == 1 && !oob) ? (spec0 ? p.batch_min * G : p.batch_min) : -1;
-    const int sg_stride = spec0 ? G : 1;
-    {
-        PlanRoots roots;
-        for (int i = 0; i < NQ; ++i) { roots.start[i] = start[i]; roots.goal[i] = goal[i]; }
-        hipLaunchKernelGGL(k_plan_init, dim3(1), dim3(64), 0, c->stream, roots, c->tree[0].q.p, c->tree[0].par.p,
-                           c->tree[0].cand.p, c->tree[1].q.p, c->tree[1].par.p, c->tree[1].cand.p, c->q32.p,
-                           c->counter.p, io, sg_edge, sg_stride, c->efrom.p, c->eto.p, c->nd.p, c->valid.p,
-                           c->gfail.p);
-        HIP_TRY(hipGetLastError());
-        for (auto& t : c->tree) t.n = 1;
-    }
+    const int level = p.simplify < 0 ? 0 : p.simplify > 2 ? 1 : p.simplify;
+    // straight-first (rp_plan_params.straight_first): with simplification on, a valid
+    // straight edge start -> goal is the path the shortcut stage (REDUCE's greedy
+    // farthest-valid walk from the start) would reduce any solution to, so it is
+    // checked first: one edge launch with the start / goal checks, one read-back
+    const bool straight = level >= 1 && p.straight_first >= 0 && !oob;
     // OMPL's PlannerInputStates: bounds and validity of start, then goal
     auto endpoint_status = [&](int sg) {
         if (out_of_bounds(start, lo, hi) || !(sg & 0xff)) return (int)RP_STATUS_INVALID_START;
@@ -628,21 +627,81 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         *status_out = code;
         return RP_OK;
     };
+    bool sg_known = false;
+    int64_t straight_states = 0;
+    if (straight) {
+        // one launch (k_straight): start, goal and the interior of start -> goal,
+        // flags published into the host mirror
+        Endpoints ep;
+        for (int i = 0; i < NQ; ++i) { ep.start[i] = start[i]; ep.goal[i] = goal[i]; }
+        const int nd = (int)std::ceil(std::sqrt(h_dist2(start, goal)) / p.resolution);
+        const unsigned nb = blocks_for(nd >= 1 ? nd + 1 : 2, VBLOCK) + 1;   // + 1: device nd may round up
+        const int seq = ++c->seq;
+#define RP_STRAIGHT(N) hipLaunchKernelGGL(k_straight<N>, dim3(nb), dim3(VBLOCK), 0, c->stream, ep, p.resolution, \
+                                          c->d_scene, c->sync.p, h, seq)
+        switch (ncl_bucket(c->scene)) {
+            case NCL_GRID: RP_STRAIGHT(NCL_GRID); break;
+            case 0: RP_STRAIGHT(0); break;
+            case 1: RP_STRAIGHT(1); break;
+            case 2: RP_STRAIGHT(2); break;
+            case 4: RP_STRAIGHT(4); break;
+            default: RP_STRAIGHT(8); break;
+        }
+#undef RP_STRAIGHT
+        HIP_TRY(hipGetLastError());
+        wait_seq(c, seq);
+        const int sgw = h->status[ST_SG];
+        if (const int code = endpoint_status(sgw & 0xffff)) return endpoint_fail(code);
+        sg_known = true;
+        straight_states = (int64_t)h->counter;
+        c->stats.edges_checked = 3;
+        if (sgw & 0xff0000) {
+            std::vector<double> raw(start, start + NQ);
+            raw.insert(raw.end(), goal, goal + NQ);
+            c->stats.states_checked = straight_states;
+            c->stats.start_tree_size = 1;
+            c->stats.goal_tree_size = 1;
+            c->stats.path_states_raw = 2;
+            c->stats.path_states_simplified = 2;
+            if (p.n_waypoints > 0) raw = interpolate_path(raw, p.n_waypoints);
+            const int m = (int)(raw.size() / NQ);
+            if (m > path_cap) {
+                c->err = "path_cap too small";
+                return RP_ERR_CAPACITY;
+            }
+            std::memcpy(path_out, raw.data(), sizeof(double) * NQ * m);
+            *n_out = m;
+            *status_out = RP_STATUS_EXACT;
+            c->stats.total_ms = 1e3 * (now_s() - t_begin);
+            return RP_OK;
+        }
+    }
+    int64_t sg_edge = (!straight && world == 1 && !oob) ? (spec0 ? p.batch_min * G : p.batch_min) : -1;
+    const int sg_stride = spec0 ? G : 1;
+    {
+        PlanRoots roots;
+        for (int i = 0; i < NQ; ++i) { roots.start[i] = start[i]; roots.goal[i] = goal[i]; }
+        hipLaunchKernelGGL(k_plan_init, dim3(1), dim3(64), 0, c->stream, roots, c->tree[0].q.p, c->tree[0].par.p,
+                           c->tree[0].cand.p, c->tree[1].q.p, c->tree[1].par.p, c->tree[1].cand.p, c->q32.p,
+                           c->counter.p, io, sg_edge, sg_stride, c->efrom.p, c->eto.p, c->nd.p, c->valid.p,
+                           c->gfail.p);
+        HIP_TRY(hipGetLastError());
+        for (auto& t : c->tree) t.n = 1;
+    }
     auto check_endpoints_now = [&]() {
         launch_validity(c, c->q32.p, 2, (uint8_t*)(status + ST_SG), c->stream);
         read_status();
         return endpoint_status(h->status[ST_SG]);
     };
-    bool sg_known = false;
-    if (sg_edge < 0) {
+    if (sg_edge < 0 && !sg_known) {
         if (const int code = check_endpoints_now()) return endpoint_fail(code);
         sg_known = true;
     }
-    // start / goal count as 2 checked states (in the edge counter when they ride along)
-    c->stats.states_checked = sg_edge < 0 ? 2 : 0;
+    // start / goal count as 2 checked states (in the edge counter when they ride along
+    // or when the straight-first launch checked them)
+    c->stats.states_checked = straight ? straight_states : sg_edge < 0 ? 2 : 0;
     // simplification program steps [from, to) (rp_kernels.h k_simp); the last one
     // publishes `seq` (with the output record when it is the program's end)
-    const int level = p.simplify < 0 ? 0 : p.simplify > 2 ? 1 : p.simplify;
     const std::vector<int> prog = simplify_program(level);
     const size_t tail_steps = level == 1 ? 2 : prog.size();   // run inside every single-rank iteration
     // raw paths longer than dev_max states are simplified host-driven (same
@@ -1075,6 +1134,10 @@ int rp_create(rp_ctx** out, int device, const rp_robot_desc* robot) {
         c->scene.plane_z = 0.0f;
         c->scene.n_boxes = 0;
         c->counter.ensure(COUNTER_SLOTS);
+    if (!c->sync.p) {
+        c->sync.ensure(2);
+        HIP_TRY(hipMemsetAsync(c->sync.p, 0, 2 * sizeof(unsigned), c->stream));
+    }
         c->scalar.ensure(16);
         upload_scene(c);
     } catch (const HipError& e) {

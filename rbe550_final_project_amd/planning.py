@@ -64,12 +64,15 @@ def _logger():
     return _log
 
 
-_CONFIG = {"seed": None, "batch": None, "device": None, "tree_capacity": None}
+_CONFIG = {"seed": None, "batch": None, "device": None, "tree_capacity": None, "straight_first": None}
 _QUERY_COUNTER = [0]
 
 
-def configure(seed=None, batch=None, device=None, tree_capacity=None):
-    """Set planner options without changing plan_path's signature."""
+def configure(seed=None, batch=None, device=None, tree_capacity=None, straight_first=None):
+    """Set planner options without changing plan_path's signature.
+
+    straight_first: with smooth_path, try the straight edge start -> goal before
+    RRT-Connect (default on; env RBE_PLANNER_STRAIGHT=0 turns it off)."""
     if seed is not None:
         _CONFIG["seed"] = int(seed)
         _QUERY_COUNTER[0] = 0
@@ -79,6 +82,14 @@ def configure(seed=None, batch=None, device=None, tree_capacity=None):
         _CONFIG["device"] = int(device)
     if tree_capacity is not None:
         _CONFIG["tree_capacity"] = int(tree_capacity)
+    if straight_first is not None:
+        _CONFIG["straight_first"] = bool(straight_first)
+
+
+def _straight_first():
+    if _CONFIG["straight_first"] is not None:
+        return _CONFIG["straight_first"]
+    return os.environ.get("RBE_PLANNER_STRAIGHT", "1") not in ("0", "false", "False", "")
 
 
 def _next_seed():
@@ -270,7 +281,8 @@ class PlannerInterface:
 
         params = _abi.make_params(seed=_next_seed(), batch=_batch(), timeout_s=float(timeout),
                                   n_waypoints=int(num_waypoints) if num_waypoints else 0,
-                                  simplify=bool(smooth_path), tree_capacity=_CONFIG["tree_capacity"] or 0)
+                                  simplify=bool(smooth_path), tree_capacity=_CONFIG["tree_capacity"] or 0,
+                                  straight_first=_straight_first())
         cap = max(4096, int(num_waypoints or 0) + 16)
         path, status = ctx.plan(qpos_start, qpos_goal, lo, hi, params, path_cap=cap)
         self.last_status = status

@@ -36,7 +36,7 @@ def main():
         C.memmove(recv, gathered.ctypes.data, nbytes * world)
         return 0
 
-    p = _abi.make_params(seed=seed, batch=batch, n_waypoints=150, timeout_s=60)
+    p = _abi.make_params(seed=seed, batch=batch, n_waypoints=150, timeout_s=60, straight_first=False)
     path, st, _ = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p, rank=rank, world=world,
                          allgather=allgather)
     np.save(out, path)

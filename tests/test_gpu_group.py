@@ -52,7 +52,7 @@ def test_two_rank_plan_equals_single(oracle_lib, wl, qi, batch, packed, world, m
         monkeypatch.setenv("RBE_EDGE_PACKED", packed)
     q = json.load(open(os.path.join(GOLD, "workloads", wl + ".json")))["queries"][qi]
     sc = scenes.Scene.from_json(q["scene"])
-    p = _abi.make_params(seed=13, batch=batch, n_waypoints=150, timeout_s=60)
+    p = _abi.make_params(seed=13, batch=batch, n_waypoints=150, timeout_s=60, straight_first=False)
     g = ThreadGroup(world, 8 * (batch // world + 4))
     ctxs = []
     for r in range(world):

@@ -156,7 +156,7 @@ def test_plan_parity(gpu_ctx, oracle_lib, wl, qi, batch, seed, batch_min, specul
     q = _wl(wl)["queries"][qi]
     sc = scenes.Scene.from_json(q["scene"])
     o = _both(gpu_ctx, oracle_lib, sc, q["attached"])
-    p = _abi.make_params(seed=seed, batch=batch, batch_min=batch_min, n_waypoints=150, timeout_s=60)
+    p = _abi.make_params(seed=seed, batch=batch, batch_min=batch_min, n_waypoints=150, timeout_s=60, straight_first=False)
     ref, st_ref, stats_ref = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
     path, st = gpu_ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
     gst = gpu_ctx.stats()
@@ -178,7 +178,7 @@ def test_plan_parity_packed_edges(gpu_ctx, oracle_lib, wl, qi, batch, seed, batc
     q = _wl(wl)["queries"][qi]
     sc = scenes.Scene.from_json(q["scene"])
     o = _both(gpu_ctx, oracle_lib, sc, q["attached"])
-    p = _abi.make_params(seed=seed, batch=batch, batch_min=batch_min, n_waypoints=150, timeout_s=60)
+    p = _abi.make_params(seed=seed, batch=batch, batch_min=batch_min, n_waypoints=150, timeout_s=60, straight_first=False)
     ref, st_ref, stats_ref = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
     path, st = gpu_ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
     assert st == st_ref == _abi.STATUS_EXACT
@@ -199,7 +199,7 @@ def test_plan_parity_hard_iterations(gpu_ctx, oracle_lib, simplify, rng, dev_max
     q = _wl("goal4_pentagon_10box")["queries"][8]
     sc = scenes.Scene.from_json(q["scene"])
     o = _both(gpu_ctx, oracle_lib, sc, q["attached"])
-    p = _abi.make_params(seed=21, batch=256, range_=rng, n_waypoints=0, timeout_s=120)
+    p = _abi.make_params(seed=21, batch=256, range_=rng, n_waypoints=0, timeout_s=120, straight_first=False)
     p.simplify = simplify
     ref, st_ref, s_ref = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
     path, st = gpu_ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
@@ -223,7 +223,7 @@ def test_plan_parity_smoothing(gpu_ctx, oracle_lib, wl, qi, dev_max, monkeypatch
     o = _both(gpu_ctx, oracle_lib, sc, q["attached"])
     lens = {}
     for level in (2, 1):
-        p = _abi.make_params(seed=qi, batch=64, range_=0.15, n_waypoints=0, timeout_s=120)
+        p = _abi.make_params(seed=qi, batch=64, range_=0.15, n_waypoints=0, timeout_s=120, straight_first=False)
         p.simplify = level
         ref, st_ref, _ = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
         path, st = gpu_ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
@@ -241,7 +241,7 @@ def test_plan_parity_approximate(gpu_ctx, oracle_lib, max_iters, simplify):
     sc = scenes.Scene(boxes=WALLS)
     o = _both(gpu_ctx, oracle_lib, sc)
     start, goal = walled_query()
-    p = _abi.make_params(seed=1, batch=64, max_iters=max_iters, range_=0.3, timeout_s=60, n_waypoints=100)
+    p = _abi.make_params(seed=1, batch=64, max_iters=max_iters, range_=0.3, timeout_s=60, n_waypoints=100, straight_first=False)
     p.simplify = simplify
     ref, st_ref, s_ref = o.plan(start, goal, model.Q_LO, model.Q_HI, p)
     path, st = gpu_ctx.plan(start, goal, model.Q_LO, model.Q_HI, p)
@@ -253,7 +253,7 @@ def test_plan_parity_approximate(gpu_ctx, oracle_lib, max_iters, simplify):
 def test_plan_invalid_start_goal(gpu_ctx, oracle_lib):
     gpu_ctx.set_scene([])
     gpu_ctx.set_attached(-1)
-    p = _abi.make_params(seed=0, batch=64, max_iters=3)
+    p = _abi.make_params(seed=0, batch=64, max_iters=3, straight_first=False)
     bad = model.SAFE_HOME.copy()
     bad[7:] = 0.04
     _, st = gpu_ctx.plan(bad, model.SAFE_HOME, model.Q_LO, model.Q_HI, p)
@@ -307,3 +307,38 @@ def test_hand_built_collision_cases(gpu_ctx, oracle_lib):
         assert o.check_states(qq)[0] == expect
         assert gpu_ctx.check_states(qq)[0] == expect
         assert sorted(gpu_ctx.contacts(np.asarray(q, dtype=np.float64))) == sorted(o.contacts(q))
+
+
+@pytest.mark.parametrize("wl", ["goal3_tallest_10box", "goal4_pentagon_10box", "clutter64", "single_pick_place_5box"])
+def test_plan_parity_straight_first(gpu_ctx, oracle_lib, wl):
+    """Default plans (straight edge first): every query of the workload gives the
+    oracle's status, path and iteration count (straight edge valid: no iteration;
+    invalid: the RRT-Connect run)."""
+    for qi, q in enumerate(_wl(wl)["queries"]):
+        sc = scenes.Scene.from_json(q["scene"])
+        o = _both(gpu_ctx, oracle_lib, sc, q["attached"])
+        p = _abi.make_params(seed=qi, batch=4096, n_waypoints=150, timeout_s=60)
+        ref, st_ref, stats_ref = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+        path, st = gpu_ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+        assert st == st_ref == _abi.STATUS_EXACT, (wl, qi)
+        assert np.array_equal(path, ref), (wl, qi)
+        assert gpu_ctx.stats()["iterations"] == stats_ref["iterations"], (wl, qi)
+
+
+def test_plan_straight_first_endpoint_status(gpu_ctx, oracle_lib):
+    """Invalid start / goal are reported through the straight-first launch as by
+    the RRT path (planning.py PlannerInputStates semantics)."""
+    sc = SCENES["goal3"]
+    o = _both(gpu_ctx, oracle_lib, sc)
+    home = np.array(model.SAFE_HOME, dtype=np.float64)
+    home[7:] = 0.035       # inside the float32 finger bound
+    bad = home.copy()
+    bad[1] = 1.7           # shoulder down: the arm goes through the table
+    bad[3] = -0.2
+    assert o.check_states(home[None].astype(np.float32))[0]
+    assert not o.check_states(bad[None].astype(np.float32))[0]
+    p = _abi.make_params(seed=0, batch=256, n_waypoints=150, timeout_s=10)
+    for s, g, want in ((bad, home, _abi.STATUS_INVALID_START), (home, bad, _abi.STATUS_INVALID_GOAL)):
+        _, st_ref, _ = o.plan(s, g, model.Q_LO, model.Q_HI, p)
+        _, st = gpu_ctx.plan(s, g, model.Q_LO, model.Q_HI, p)
+        assert st == st_ref == want

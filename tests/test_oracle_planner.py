@@ -49,7 +49,7 @@ def test_plan_deterministic_and_solves(oracle_lib):
     o = oracle_lib.OracleScene()
     for q in wl["queries"][:4]:
         _scene(o, q)
-        p = _abi.make_params(seed=3, batch=64, n_waypoints=150, timeout_s=30)
+        p = _abi.make_params(seed=3, batch=64, n_waypoints=150, timeout_s=30, straight_first=False)
         a, sa, st = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
         b, sb, _ = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
         assert sa == _abi.STATUS_EXACT and sb == sa
@@ -63,7 +63,7 @@ def test_plan_deterministic_and_solves(oracle_lib):
 def test_invalid_start_goal_status(oracle_lib):
     o = oracle_lib.OracleScene()
     o.set_scene([])
-    p = _abi.make_params(seed=0, batch=16, max_iters=4)
+    p = _abi.make_params(seed=0, batch=16, max_iters=4, straight_first=False)
     bad = model.SAFE_HOME.copy()
     bad[7:] = 0.04                # float64 0.04 > float32 limit: out of bounds (README.md:101-111)
     _, st, _ = o.plan(bad, model.SAFE_HOME, model.Q_LO, model.Q_HI, p)
@@ -102,7 +102,7 @@ def test_approximate_on_iteration_cap(oracle_lib):
     assert o.check_states(np.stack([start, goal]).astype(np.float32)).all()
     for it in (1, 4):
         p_ = _abi.make_params(seed=1, batch=64, max_iters=it, range_=0.3, timeout_s=60, n_waypoints=0,
-                              simplify=False)
+                              simplify=False, straight_first=False)
         path, st, stats = o.plan(start, goal, model.Q_LO, model.Q_HI, p_)
         assert st == _abi.STATUS_APPROXIMATE and stats["iterations"] == it
         assert np.array_equal(path[0], start)
@@ -133,7 +133,7 @@ def test_world_size_independence_gloo(oracle_lib, tmp_path, qi):
     q = wl["queries"][qi]
     o = oracle_lib.OracleScene()
     _scene(o, q)
-    p = _abi.make_params(seed=seed, batch=batch, n_waypoints=150, timeout_s=60)
+    p = _abi.make_params(seed=seed, batch=batch, n_waypoints=150, timeout_s=60, straight_first=False)
     ref, st, _ = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
     r0, r1 = _run_two_ranks(str(tmp_path), batch, seed, qi)
     assert np.array_equal(r0, ref) and np.array_equal(r1, ref)
@@ -153,10 +153,61 @@ def test_oracle_simplification_levels(oracle_lib):
     o.set_attached(q["attached"])
     lens = {}
     for level in (0, 2, 1):
-        p = _abi.make_params(seed=0, batch=64, range_=0.15, n_waypoints=0, timeout_s=60)
+        p = _abi.make_params(seed=0, batch=64, range_=0.15, n_waypoints=0, timeout_s=60, straight_first=False)
         p.simplify = level
         path, st, _ = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
         assert st == _abi.STATUS_EXACT
         assert np.allclose(path[0], q["start"]) and np.allclose(path[-1], q["goal"])
         lens[level] = float(np.sum(np.linalg.norm(np.diff(path, axis=0), axis=1)))
     assert lens[1] < lens[2] < lens[0]
+
+
+def test_straight_first_returns_the_straight_edge(oracle_lib):
+    """Default plans (simplification on) check the straight edge start -> goal first:
+    when it is valid the result is OMPL interpolate([start, goal]) with no RRT
+    iteration; that is the path REDUCE would shorten any solution to."""
+    o = oracle_lib.OracleScene()
+    res = 0.01 * model.max_extent()
+    n_straight = 0
+    for name in ("goal3_tallest_10box", "goal4_pentagon_10box"):
+        for q in _load(name)["queries"]:
+            _scene(o, q)
+            direct = bool(o.check_edges(np.array([q["start"]]), np.array([q["goal"]]), res)[0])
+            p = _abi.make_params(seed=7, batch=64, n_waypoints=150, timeout_s=30)
+            path, st, stats = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+            assert st == _abi.STATUS_EXACT
+            if direct:
+                n_straight += 1
+                assert stats["iterations"] == 0 and stats["path_states_raw"] == 2
+                want = oracle_lib.interpolate(np.array([q["start"], q["goal"]]), 150)
+                assert np.array_equal(path, want)
+            else:
+                assert stats["iterations"] >= 1
+    assert n_straight >= 40   # 20 of 21 goal3 and 25 of 25 pentagon queries
+
+
+def test_straight_first_falls_back_to_the_same_rrt(oracle_lib):
+    """An invalid straight edge leaves the RRT-Connect run unchanged (it draws no
+    samples): same path and trees as with straight_first off."""
+    q = _load("clutter64")["queries"][0]
+    o = oracle_lib.OracleScene()
+    _scene(o, q)
+    out = []
+    for sf in (True, False):
+        p = _abi.make_params(seed=2, batch=1024, n_waypoints=150, timeout_s=60, straight_first=sf)
+        out.append(o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p))
+    (pa, sa, ta), (pb, sb, tb) = out
+    assert sa == sb == _abi.STATUS_EXACT and np.array_equal(pa, pb)
+    assert (ta["iterations"], ta["start_tree_size"], ta["goal_tree_size"]) == \
+        (tb["iterations"], tb["start_tree_size"], tb["goal_tree_size"])
+    assert ta["iterations"] >= 1
+
+
+def test_straight_first_off_without_simplification(oracle_lib):
+    """smooth_path=False returns the raw RRT path: no straight-first shortcut."""
+    q = _load("goal3_tallest_10box")["queries"][2]
+    o = oracle_lib.OracleScene()
+    _scene(o, q)
+    p = _abi.make_params(seed=3, batch=64, n_waypoints=0, timeout_s=30, simplify=False)
+    _, st, stats = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+    assert st == _abi.STATUS_EXACT and stats["iterations"] >= 1

@@ -154,36 +154,48 @@ __global__ void k_edge_slots(const int* __restrict__ nd, int64_t n_edges, const 
     slots[e] = v;
 }
 
-// incl = inclusive scan of slots: item t belongs to the edge e with
-// incl[e-1] <= t < incl[e]. Grid-stride over the items (the grid is fixed, the
-// item count lives on the device); per 64-item step lane 0 binary-searches the
-// first edge, the lanes then step forward over the (few) edges the step spans.
+// chunk_first[c] = the edge holding item 64 c (incl = inclusive scan of the slot
+// counts: item t belongs to the edge e with incl[e-1] <= t < incl[e])
+__global__ void k_chunk_first(const int32_t* __restrict__ incl, int64_t n_edges, int32_t* __restrict__ chunk_first) {
+    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= n_edges) return;
+    const int64_t lo = e > 0 ? incl[e - 1] : 0, hi = incl[e];
+    for (int64_t c = (lo + VBLOCK - 1) / VBLOCK; c * VBLOCK < hi; ++c) chunk_first[c] = (int32_t)e;
+}
+
+// Grid-stride over the items (the grid is fixed, the item count lives on the
+// device), 64 per pass: the pass's first edge comes from chunk_first, then the
+// lanes map its 64 items to edges through LDS (each of the next 64 edges writes
+// its index into the item slots it covers; empty edges cover none, so a pass may
+// take another round of 64 edges).
 template <int NCL>
 __global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_edges_packed(
     const double* __restrict__ from, const double* __restrict__ to, const int* __restrict__ nd, int64_t n_edges,
     int mode, uint8_t* valid, int group, int* gfail, unsigned long long* counter, const DevScene* __restrict__ sc,
-    const int32_t* __restrict__ incl) {
+    const int32_t* __restrict__ incl, const int32_t* __restrict__ chunk_first) {
     __shared__ WaveQ wq;
-    __shared__ int64_t e_first;
+    __shared__ int32_t e_of[VBLOCK];
     if (n_edges <= 0) return;
     const int64_t total = incl[n_edges - 1];
+    const int lane = threadIdx.x;
     for (int64_t base = (int64_t)blockIdx.x * VBLOCK; base < total; base += (int64_t)gridDim.x * VBLOCK) {
-        if (threadIdx.x == 0) {   // first e with incl[e] > base
-            int64_t lo = 0, hi = n_edges - 1;
-            while (lo < hi) {
-                const int64_t mid = (lo + hi) >> 1;
-                if (incl[mid] > base) hi = mid;
-                else lo = mid + 1;
+        const int64_t bend = min(base + VBLOCK, total);
+        for (int64_t e0 = chunk_first[base / VBLOCK];; e0 += VBLOCK) {
+            const int64_t ej = e0 + lane;
+            if (ej < n_edges) {
+                const int64_t lo = ej > 0 ? incl[ej - 1] : 0, hi = incl[ej];
+                for (int64_t t = max(lo, base); t < min(hi, bend); ++t) e_of[t - base] = (int32_t)ej;
             }
-            e_first = lo;
+            const int64_t last = min(e0 + VBLOCK, n_edges) - 1;   // this round's last edge
+            if (last + 1 >= n_edges || incl[last] >= bend) break;
         }
         __syncthreads();
-        const int64_t t = base + threadIdx.x;
+        const int64_t t = base + lane;
         bool run = false;
-        int64_t e = e_first;
+        int64_t e = 0;
         int slot = 0, nde = 0, emode = mode;
         if (t < total) {
-            while (incl[e] <= t) ++e;
+            e = e_of[lane];
             slot = (int)(t - (e > 0 ? (int64_t)incl[e - 1] : 0));
             nde = nd[e];
             if (mode == 2) {

@@ -114,7 +114,7 @@ struct rp_ctx {
     DevBuf<uint8_t> valid;
     DevBuf<int32_t> near_, res, acc, incl, yv, mv, rec, Lv, chain_end, mine;
     DevBuf<int> gfail;
-    DevBuf<int32_t> eslot, eincl;        // work-compacted edge launches
+    DevBuf<int32_t> eslot, eincl, echunk;   // work-compacted edge launches
     DevBuf<char> cub_tmp;
     DevBuf<double> path;                 // raw solution path (PATH_CAP states)
     DevBuf<PlanIO> io;                   // iteration status + output record (rp_kernels.h)
@@ -138,7 +138,7 @@ struct rp_ctx {
         scalar.release(); counter.release(); efrom.release(); eto.release(); nd.release(); valid.release();
         near_.release(); res.release(); acc.release(); incl.release(); yv.release(); mv.release();
         rec.release(); Lv.release(); chain_end.release(); mine.release(); gfail.release();
-        eslot.release(); eincl.release();
+        eslot.release(); eincl.release(); echunk.release();
         cub_tmp.release(); path.release(); io.release(); simp.release(); partial.release();
         if (h_io) (void)hipHostFree(h_io);
         if (d_scene) (void)hipFree(d_scene);
@@ -220,9 +220,13 @@ void launch_edges_packed(rp_ctx* c, const double* from, const double* to, const 
     hipLaunchKernelGGL(k_edge_slots, dim3(blocks_for(n, 256)), dim3(256), 0, s, nd, n, dcount, per_item, c->eslot.p);
     HIP_TRY(hipGetLastError());
     scan_incl(c, c->eslot.p, c->eincl.p, n);
+    c->echunk.ensure(blocks_for(n * (int64_t)kmax, VBLOCK) + 1);
+    hipLaunchKernelGGL(k_chunk_first, dim3(blocks_for(n, 256)), dim3(256), 0, s, (const int32_t*)c->eincl.p, n,
+                       c->echunk.p);
     const dim3 g(std::min<unsigned>(blocks_for(n * (int64_t)kmax, VBLOCK), 8192u)), b(VBLOCK);
 #define RP_EDGESP(N) hipLaunchKernelGGL(k_edges_packed<N>, g, b, 0, s, from, to, nd, n, mode, valid, group, gfail, \
-                                        c->counter.p, c->d_scene, (const int32_t*)c->eincl.p)
+                                        c->counter.p, c->d_scene, (const int32_t*)c->eincl.p,   \
+                                        (const int32_t*)c->echunk.p)
     switch (ncl_bucket(c->scene)) {
         case NCL_GRID: RP_EDGESP(NCL_GRID); break;
         case 0: RP_EDGESP(0); break;

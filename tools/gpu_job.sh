@@ -24,7 +24,7 @@ for s in "$@"; do
     ab) step ab 600 python tools/variant_bench.py build/variants/*.so && step ab_clutter 600 python tools/variant_bench.py --scene clutter64 build/variants/*.so ;;
     ptrace) step ptrace 600 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/ptrace -o pt -- python tools/plan_trace.py && step plantime 300 python tools/plan_trace.py ;;
     gridab) step gridab 600 python tools/grid_ab.py ;;
-    ptrace4) step ptrace4 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ptrace4 -o pt -- python tools/plan_trace.py goal4_pentagon_10box 262144 full ;;
+    ptrace4) step ptrace4 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ptrace4 -o pt -- python tools/plan_trace.py goal4_pentagon_10box 262144 full && python tools/trace_summary.py gpurun_out/ptrace4/pt_kernel_trace.csv > gpurun_out/ptrace4_summary.txt && step ptrace5 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ptrace5 -o pt -- python tools/plan_trace.py clutter64 131072 full && python tools/trace_summary.py gpurun_out/ptrace5/pt_kernel_trace.csv > gpurun_out/ptrace5_summary.txt ;;
     rates) step rates 600 python tools/scene_rates.py ;;
     sweep) step sweep 600 python tools/plan_sweep.py goal3_tallest_10box 4096 32 64 128 256 512 && step sweep4 600 python tools/plan_sweep.py goal4_pentagon_10box 4096 32 64 128 256 512 ;;
     planab) for v in build/variants/*.so; do step planab_$(basename $v .so) 300 python tools/plan_bench.py $v goal4_pentagon_10box 262144 full; done ;;

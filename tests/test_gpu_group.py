@@ -44,15 +44,16 @@ class ThreadGroup:
 
 @pytest.mark.parametrize("wl,qi,batch", [("goal4_pentagon_10box", 2, 64), ("goal3_tallest_10box", 5, 256),
                                          ("clutter64", 0, 128)])
-@pytest.mark.parametrize("packed,world", [("", 2), ("1", 2), ("", 4)])
-def test_two_rank_plan_equals_single(oracle_lib, wl, qi, batch, packed, world, monkeypatch):
+@pytest.mark.parametrize("packed,world,straight", [("", 2, False), ("1", 2, False), ("", 4, False), ("", 2, True)])
+def test_two_rank_plan_equals_single(oracle_lib, wl, qi, batch, packed, world, straight, monkeypatch):
     """World 2 and 4 (ranks as threads on one GPU); packed "1": the ranks' connect
-    launches are work-compacted (k_edges_packed)."""
+    launches are work-compacted (k_edges_packed); straight: the product default
+    (straight edge first: every rank decides alone, no exchange when it is valid)."""
     if packed:
         monkeypatch.setenv("RBE_EDGE_PACKED", packed)
     q = json.load(open(os.path.join(GOLD, "workloads", wl + ".json")))["queries"][qi]
     sc = scenes.Scene.from_json(q["scene"])
-    p = _abi.make_params(seed=13, batch=batch, n_waypoints=150, timeout_s=60, straight_first=False)
+    p = _abi.make_params(seed=13, batch=batch, n_waypoints=150, timeout_s=60, straight_first=straight)
     g = ThreadGroup(world, 8 * (batch // world + 4))
     ctxs = []
     for r in range(world):
@@ -78,7 +79,7 @@ def test_two_rank_plan_equals_single(oracle_lib, wl, qi, batch, packed, world, m
     o.set_scene(sc.boxes, sc.plane_z, sc.base)
     o.set_attached(q["attached"])
     ref_cpu, st_cpu, _ = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
-    assert g.calls >= 2
+    assert g.calls >= (0 if straight else 2)
     for path, status in out:
         assert status == st == st_cpu == _abi.STATUS_EXACT
         assert np.array_equal(path, ref) and np.array_equal(path, ref_cpu)

@@ -39,11 +39,16 @@ __global__ __launch_bounds__(VBLOCK, RP_VALIDITY_WAVES) void k_validity(const fl
                                                                        uint8_t* __restrict__ flags,
                                                                        const DevScene* __restrict__ sc) {
     __shared__ WaveQ wq;
+    RP_STAMP(0);
     const int64_t i = (int64_t)blockIdx.x * VBLOCK + threadIdx.x;
     if (i >= n) return;
     float qq[NQ];
 #pragma unroll
     for (int k = 0; k < NQ; ++k) qq[k] = q[i * NQ + k];
+#ifdef RP_STAMPS
+    asm volatile("" ::"v"(qq[0]), "v"(qq[8]));
+    RP_STAMP(1);
+#endif
     flags[i] = state_collides<NCL>(qq, sc, wq) ? 0 : 1;
 }
 

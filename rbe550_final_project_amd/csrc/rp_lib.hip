@@ -1490,6 +1490,14 @@ int rp_ik(rp_ctx* c, int32_t n_targets, const double* pos, const double* quat, c
     RP_GUARD_END(c)
 }
 
+#ifdef RP_STAMPS
+// diagnostic builds: copy the k_validity wave stamps (STAMP_WAVES x STAMP_K) out
+int rp_debug_stamps(unsigned long long* out, int64_t n) {
+    if (n > (int64_t)STAMP_WAVES * STAMP_K) n = (int64_t)STAMP_WAVES * STAMP_K;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -1;
+}
+#endif
+
 // Numerics self-test (test-only entry, not in the public header's contract list):
 // device sqrt / div / ceil / f64->f32 of x[i] -> out[4*i..4*i+3].
 int rp_selftest_f64(rp_ctx* c, const double* x, int64_t n, double* out) {

@@ -24,6 +24,24 @@ namespace rp {
 
 struct V3 { float x, y, z; };
 
+#ifdef RP_STAMPS
+// in-kernel timestamps (diagnostic builds only): lane 0 of each k_validity wave
+// writes s_memtime at fixed points into g_stamps[wave][k] (vector store)
+constexpr int STAMP_WAVES = 65536, STAMP_K = 8;
+__device__ unsigned long long g_stamps[STAMP_WAVES * STAMP_K];
+__device__ __forceinline__ void stamp(int k) {
+    __builtin_amdgcn_sched_barrier(0);
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    const unsigned w = blockIdx.x;
+    if (w < STAMP_WAVES && __lane_id() == __builtin_amdgcn_readfirstlane(__lane_id())) g_stamps[w * STAMP_K + k] = t;
+}
+#define RP_STAMP(k) stamp(k)
+#else
+#define RP_STAMP(k)
+#endif
+
 // min / max / clamp as single instructions (v_min_f32, v_max_f32, v_med3_f32). The
 // oracle writes them as compares; for the finite operands here the two agree except
 // possibly in the sign of a zero result, which no later comparison or square sees.
@@ -653,6 +671,9 @@ struct QueuedVisit {
     QueueState<NCL> s;
     template <int C>
     __device__ __forceinline__ bool at(const Capsules& k) {
+        if constexpr (C == C_LINK4) RP_STAMP(2);
+        if constexpr (C == C_LINK6) RP_STAMP(3);
+        if constexpr (C == C_HAND) RP_STAMP(4);
         if (env_queued<C>(k, sc, s)) return true;
 #ifndef RP_ABLATE_SELF
         pairs_queued<C>(k, s);
@@ -680,8 +701,11 @@ __device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene
     Q.hit[v.s.lane] = 0;
     __builtin_amdgcn_wave_barrier();
     if (fk_walk(q, sc, k, v)) return true;
+    RP_STAMP(5);
     if (__any(v.s.nsb > 0)) drain_sb(v.s);
+    RP_STAMP(6);
     if (__any(v.s.nss > 0)) drain_ss(v.s);
+    RP_STAMP(7);
     return Q.hit[v.s.lane] != 0;
 }
 

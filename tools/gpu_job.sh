@@ -26,6 +26,7 @@ for s in "$@"; do
     gridab) step gridab 600 python tools/grid_ab.py ;;
     ptrace4) step ptrace4 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ptrace4 -o pt -- python tools/plan_trace.py goal4_pentagon_10box 262144 full && python tools/trace_summary.py gpurun_out/ptrace4/pt_kernel_trace.csv > gpurun_out/ptrace4_summary.txt && step ptrace5 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ptrace5 -o pt -- python tools/plan_trace.py clutter64 131072 full && python tools/trace_summary.py gpurun_out/ptrace5/pt_kernel_trace.csv > gpurun_out/ptrace5_summary.txt ;;
     rates) step rates 600 python tools/scene_rates.py ;;
+    stamps) step stamps 300 python tools/stamp_probe.py build/variants/lib_stamps.so ;;
     sweep) step sweep 600 python tools/plan_sweep.py goal3_tallest_10box 4096 32 64 128 256 512 && step sweep4 600 python tools/plan_sweep.py goal4_pentagon_10box 4096 32 64 128 256 512 ;;
     planab) for v in build/variants/*.so; do step planab_$(basename $v .so) 300 python tools/plan_bench.py $v goal4_pentagon_10box 262144 full; done ;;
     bench2) step bench2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --no-cpu --backend gloo ;;

@@ -275,6 +275,15 @@ def main():
             times, pstates, st = run_plans(ctx, wl, args.plan_batch, 0, group)
             plan = plan_record(times, pstates, st, args.plan_batch, dev, distributed,
                                {"mode": "product default: straight edge first, then RRT-Connect"})
+            # C1: goal1_scattered's 12 queries (BASELINE configs[0]; the reference runs
+            # it on the CPU), product default and RRT-forced
+            wl1 = load_workload("goal1_scattered_6box")
+            t1, s1, st1 = run_plans(ctx, wl1, args.plan_batch, 0, group)
+            plan["C1_goal1"] = plan_record(t1, s1, st1, args.plan_batch, dev, distributed,
+                                           {"mode": "product default: straight edge first, then RRT-Connect"})
+            t1, s1, st1 = run_plans(ctx, wl1, args.plan_batch, 0, group, straight_first=False)
+            plan["C1_goal1_rrt"] = plan_record(t1, s1, st1, args.plan_batch, dev, distributed,
+                                               {"mode": "RRT-Connect forced (straight_first off)"})
             # the same queries with RRT-Connect forced (straight_first off)
             t3, s3, st3 = run_plans(ctx, wl, args.plan_batch, 0, group, straight_first=False)
             plan["C3_rrt"] = plan_record(t3, s3, st3, args.plan_batch, dev, distributed,
@@ -314,11 +323,18 @@ def main():
             rate, dt = cpu_baseline(scene, sample, threads)
             ptimes = cpu_plan_baseline(wl, 0)
             rtimes = cpu_plan_baseline(wl, 0, straight_first=False)
+            wl1 = load_workload("goal1_scattered_6box")
+            g1 = cpu_plan_baseline(wl1, 0)
+            g1r = cpu_plan_baseline(wl1, 0, straight_first=False)
             cpu = {"value": round(rate, 1), "unit": "states/s", "cores": threads, "kind": "port",
                    "sample": f"{sample} uniform states, goal3 10-box scene, OpenMP CPU oracle ({dt:.1f} s)",
                    "plan_total_ms": round(sum(ptimes), 3), "plan_median_ms": round(float(np.median(ptimes)), 3),
                    "plan_sample": "21 goal3 queries, straight edge first then sequential RRT-Connect (batch 1), 1 core",
-                   "plan_rrt_total_ms": round(sum(rtimes), 3), "plan_rrt_median_ms": round(float(np.median(rtimes)), 3)}
+                   "plan_rrt_total_ms": round(sum(rtimes), 3), "plan_rrt_median_ms": round(float(np.median(rtimes)), 3),
+                   "C1_goal1": {"queries": len(g1), "total_ms": round(sum(g1), 3),
+                                "median_ms": round(float(np.median(g1)), 3),
+                                "rrt_total_ms": round(sum(g1r), 3), "rrt_median_ms": round(float(np.median(g1r)), 3),
+                                "sample": "goal1_scattered 12 queries (BASELINE configs[0]), CPU oracle, 1 core"}}
         except Exception as ex:
             cpu = {"error": repr(ex)[:300]}
 

@@ -127,6 +127,24 @@ def workload_single(seed=0):
     return {"name": "single_pick_place_5box", "config": 1, "queries": w.queries}
 
 
+def workload_goal1(seed=1):
+    """C1: goal1_scattered (code/goal1_scattered.py): two 3-block towers g-r-b and
+    m-y-c from the scattered 6-block scene (jitter seeded); the Pyperplan plan is
+    pick r, stack r on g, pick b, stack b on r, pick y, stack y on m, pick c, stack c
+    on y -> 4 x (approach, grasp, high approach) = 12 queries. Jitter seed 1: with
+    seed 0 block b lands at (0.68, 0.44), where no collision-free top-down grasp
+    approach exists for the capsule model."""
+    sc = scenes.goal1_scattered(seed)
+    w = World(sc, model.SAFE_HOME)
+    for blk, onto, level in (("r", "g", 1), ("b", "g", 2), ("y", "m", 1), ("c", "m", 2)):
+        base_xy = np.array(sc.boxes[sc.index(onto)][0][:2])
+        w.pick(blk)
+        final_center_z = 0.02 + level * scenes.BLOCK
+        w.place_high(blk, base_xy, final_center_z, GRASP_QUAT, f"stack {blk} on tower {onto}: high approach")
+        w.release_at(blk, (base_xy[0], base_xy[1], final_center_z), 0.0, GRASP_QUAT)
+    return {"name": "goal1_scattered_6box", "config": 0, "queries": w.queries}
+
+
 def workload_goal3(height=8):
     """C3: goal3_tallest (code/goal3_tallest.py:63-283): build order by distance to
     (0.50, 0.0), base = closest, stack the next 7 blocks on it -> 21 queries."""
@@ -192,7 +210,10 @@ def workload_clutter():
 
 def main():
     os.makedirs(OUT, exist_ok=True)
-    for fn in (workload_single, workload_goal3, workload_goal4, workload_clutter):
+    only = set(sys.argv[1:])
+    for fn in (workload_goal1, workload_single, workload_goal3, workload_goal4, workload_clutter):
+        if only and fn.__name__ not in only:
+            continue
         wl = fn()
         path = os.path.join(OUT, wl["name"] + ".json")
         with open(path, "w") as f:

@@ -140,7 +140,7 @@ def test_f64_device_numerics(gpu_ctx):
     assert np.array_equal(out[:, 3], x.astype(np.float32).astype(np.float64))
 
 
-PLAN_CASES = [("single_pick_place_5box", 0), ("single_pick_place_5box", 1), ("goal3_tallest_10box", 2),
+PLAN_CASES = [("goal1_scattered_6box", 7), ("single_pick_place_5box", 0), ("single_pick_place_5box", 1), ("goal3_tallest_10box", 2),
               ("goal3_tallest_10box", 5), ("goal4_pentagon_10box", 2), ("goal4_pentagon_10box", 14),
               ("clutter64", 0)]
 
@@ -309,7 +309,8 @@ def test_hand_built_collision_cases(gpu_ctx, oracle_lib):
         assert sorted(gpu_ctx.contacts(np.asarray(q, dtype=np.float64))) == sorted(o.contacts(q))
 
 
-@pytest.mark.parametrize("wl", ["goal3_tallest_10box", "goal4_pentagon_10box", "clutter64", "single_pick_place_5box"])
+@pytest.mark.parametrize("wl", ["goal1_scattered_6box", "goal3_tallest_10box", "goal4_pentagon_10box", "clutter64",
+                                "single_pick_place_5box"])
 def test_plan_parity_straight_first(gpu_ctx, oracle_lib, wl):
     """Default plans (straight edge first): every query of the workload gives the
     oracle's status, path and iteration count (straight edge valid: no iteration;

@@ -169,7 +169,7 @@ def test_straight_first_returns_the_straight_edge(oracle_lib):
     o = oracle_lib.OracleScene()
     res = 0.01 * model.max_extent()
     n_straight = 0
-    for name in ("goal3_tallest_10box", "goal4_pentagon_10box"):
+    for name in ("goal1_scattered_6box", "goal3_tallest_10box", "goal4_pentagon_10box"):
         for q in _load(name)["queries"]:
             _scene(o, q)
             direct = bool(o.check_edges(np.array([q["start"]]), np.array([q["goal"]]), res)[0])
@@ -183,7 +183,7 @@ def test_straight_first_returns_the_straight_edge(oracle_lib):
                 assert np.array_equal(path, want)
             else:
                 assert stats["iterations"] >= 1
-    assert n_straight >= 40   # 20 of 21 goal3 and 25 of 25 pentagon queries
+    assert n_straight >= 57   # 12 of 12 goal1, 20 of 21 goal3 and 25 of 25 pentagon queries
 
 
 def test_straight_first_falls_back_to_the_same_rrt(oracle_lib):

@@ -21,7 +21,7 @@ for s in "$@"; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     benchq) step bench 300 python bench.py --steps 20 --no-cpu ;;
-    ab) step ab 600 python tools/variant_bench.py build/variants/*.so && step ab_clutter 600 python tools/variant_bench.py --scene clutter64 build/variants/*.so ;;
+    ab) step ab 600 python tools/variant_bench.py build/variants/*.so && step ab_clutter 600 python tools/variant_bench.py --scene clutter64 build/variants/*.so && step ab_small 600 python tools/variant_bench.py --states 65536 --iters 50 build/variants/*.so ;;
     ptrace) step ptrace 600 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/ptrace -o pt -- python tools/plan_trace.py && step plantime 300 python tools/plan_trace.py ;;
     gridab) step gridab 600 python tools/grid_ab.py ;;
     ptrace4) step ptrace4 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ptrace4 -o pt -- python tools/plan_trace.py goal4_pentagon_10box 262144 full && python tools/trace_summary.py gpurun_out/ptrace4/pt_kernel_trace.csv > gpurun_out/ptrace4_summary.txt && step ptrace5 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ptrace5 -o pt -- python tools/plan_trace.py clutter64 131072 full && python tools/trace_summary.py gpurun_out/ptrace5/pt_kernel_trace.csv > gpurun_out/ptrace5_summary.txt ;;

@@ -452,6 +452,7 @@ template <int NCL>
 struct QueueState {
     WaveQ* Q;
     int nss, nsb;     // wave-uniform item counts
+    bool in_limits;   // every state of the wave inside the joint limits (skip never pairs)
     int lane;
     float plane_z;
     ClusterRegs<NCL> cl;
@@ -651,8 +652,13 @@ template <int J, int T, class S>
 __device__ __forceinline__ void pairs_each(const Capsules& k, S& s) {
     constexpr PairList L = pairs_ending<J>();
     if constexpr (T < L.n) {
-        const bool cand = pair_sphere<L.p[T]>(k);
-        pair_enqueue<L.p[T]>(k, s, cand, __ballot(cand));
+#ifndef RP_NO_NEVER_PAIRS
+        if (!pair_never(L.p[T]) || !s.in_limits)
+#endif
+        {
+            const bool cand = pair_sphere<L.p[T]>(k);
+            pair_enqueue<L.p[T]>(k, s, cand, __ballot(cand));
+        }
         pairs_each<J, T + 1, S>(k, s);
     }
 }
@@ -696,6 +702,12 @@ __device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene
     v.s.nss = 0;
     v.s.nsb = 0;
     v.s.lane = (int)__lane_id();
+    {
+        bool in = true;
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) in = in && q[j] >= Q_LO_F[j] && q[j] <= Q_HI_F[j];
+        v.s.in_limits = !__any(!in);
+    }
     v.s.plane_z = sc->plane_z;
     v.s.cl.load(sc);
     Q.hit[v.s.lane] = 0;

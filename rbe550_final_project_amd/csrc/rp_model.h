@@ -35,6 +35,24 @@ constexpr int PAIRS[NPAIR][2] = {
     {C_LINK5B, C_HAND}, {C_LINK5B, C_LFINGER}, {C_LINK5B, C_RFINGER},
 };
 
+// Joint limits as float32 (model.py Q_LO / Q_HI: Genesis keeps q_limit in float32).
+constexpr float Q_LO_F[NQ] = {-2.8973f, -1.7628f, -2.8973f, -3.0718f, -2.8973f, -0.0175f, -2.8973f, 0.0f, 0.0f};
+constexpr float Q_HI_F[NQ] = {2.8973f, 1.7628f, 2.8973f, -0.0698f, 2.8973f, 3.7525f, 2.8973f, 0.04f, 0.04f};
+
+// Self pairs proven never to touch while every joint is inside [Q_LO_F, Q_HI_F]
+// (tools/prove_pairs.py: exact segment distance on a joint grid minus a Lipschitz
+// bound exceeds r_I + r_J + 1e-4 m; tests/golden/never_pairs_proof.json). A wave
+// whose states are all inside the limits skips them; any other wave tests them.
+constexpr int NEVER_PAIRS[][2] = {
+    {C_LINK2, C_LINK5A}, {C_LINK3, C_LINK6}, {C_LINK3, C_LINK7}, {C_LINK4, C_LINK7}, {C_LINK4, C_HAND},
+    {C_LINK4, C_LFINGER}, {C_LINK4, C_RFINGER}, {C_LINK5B, C_HAND}, {C_LINK5B, C_LFINGER}, {C_LINK5B, C_RFINGER},
+};
+constexpr bool pair_never(int p) {
+    for (const auto& n : NEVER_PAIRS)
+        if (n[0] == PAIRS[p][0] && n[1] == PAIRS[p][1]) return true;
+    return false;
+}
+
 // Capsule geometry (spec/franka_capsules.json): a(3), b(3), radius, in the link
 // frame. Compiled into the kernels (zero terms of the link->world transform fold
 // away, no scalar loads); rp_create rejects a descriptor with other numbers.

@@ -343,3 +343,25 @@ def test_plan_straight_first_endpoint_status(gpu_ctx, oracle_lib):
         _, st_ref, _ = o.plan(s, g, model.Q_LO, model.Q_HI, p)
         _, st = gpu_ctx.plan(s, g, model.Q_LO, model.Q_HI, p)
         assert st == st_ref == want
+
+
+@pytest.mark.parametrize("name", ["empty", "goal3", "clutter64"])
+@pytest.mark.parametrize("mode", ["wide", "one_per_wave"])
+def test_validity_flags_outside_joint_limits(gpu_ctx, oracle_lib, name, mode):
+    """Waves with states outside the joint limits test the never pairs (rp_model.h
+    NEVER_PAIRS) that in-limit waves skip: flags stay bit-exact either way. "wide":
+    states from the limits widened by 0.6 rad / 0.02 m; "one_per_wave": one
+    out-of-limit state in every 64."""
+    sc = SCENES[name]
+    o = _both(gpu_ctx, oracle_lib, sc)
+    rng = np.random.default_rng(17)
+    n = 1 << 17
+    pad = np.array([0.6] * 7 + [0.02] * 2)
+    if mode == "wide":
+        q = (model.Q_LO - pad + (model.Q_HI - model.Q_LO + 2 * pad) * rng.random((n, 9))).astype(np.float32)
+    else:
+        q = _uniform(n, 17)
+        q[::64] = (model.Q_HI + pad * rng.random((n // 64, 9))).astype(np.float32)
+    g = gpu_ctx.check_states(q)
+    c = o.check_states(q)
+    assert np.array_equal(g, c), f"{(g != c).sum()} flags differ"

@@ -147,7 +147,6 @@ __device__ __forceinline__ void place(Capsules& k, const Frame& f) {
     k.a[C] = xform_c<C, 0>(f);
     k.b[C] = xform_c<C, 3>(f);
 }
-
 // Franka Panda forward kinematics (MJCF bodies of
 // panda.xml that Genesis loads at code/scenes.py:85) -> world capsule endpoints.
 // After each capsule is placed, v.template at<C>(k) runs; a true return stops the
@@ -652,10 +651,10 @@ template <int J, int T, class S>
 __device__ __forceinline__ void pairs_each(const Capsules& k, S& s) {
     constexpr PairList L = pairs_ending<J>();
     if constexpr (T < L.n) {
-#ifndef RP_NO_NEVER_PAIRS
-        if (!pair_never(L.p[T]) || !s.in_limits)
-#endif
-        {
+        // never pairs are left out of the walk (their first capsule then dies early,
+        // which lowers the register peak); waves with a state outside the joint
+        // limits test them afterwards (never_pairs_outside_limits)
+        if constexpr (!pair_never(L.p[T])) {
             const bool cand = pair_sphere<L.p[T]>(k);
             pair_enqueue<L.p[T]>(k, s, cand, __ballot(cand));
         }
@@ -688,6 +687,27 @@ struct QueuedVisit {
     }
 };
 
+// the never pairs (rp_model.h NEVER_PAIRS) of a wave with a state outside the joint
+// limits, where their proof does not hold: the capsules are placed again (a second
+// FK walk, rare) and the pairs queued as in the walk
+template <int P = 0, class S>
+__device__ __forceinline__ void never_pairs_each(const Capsules& k, S& s) {
+    if constexpr (P < NPAIR) {
+        if constexpr (pair_never(P)) {
+            const bool cand = pair_sphere<P>(k);
+            pair_enqueue<P>(k, s, cand, __ballot(cand));
+        }
+        never_pairs_each<P + 1>(k, s);
+    }
+}
+template <class S>
+__device__ __forceinline__ void never_pairs_outside_limits(const float q[NQ], const DevScene* __restrict__ sc,
+                                                                     S& s) {
+    Capsules k;
+    fk_capsules(q, sc, k);
+    never_pairs_each(k, s);
+}
+
 // true if the state collides with the plane, a (non-exempt) box, or itself: the OR
 // over every test. Plane tests decide at once (a colliding lane stops walking);
 // box and self narrow phases are queued and drained wave-compacted. Every lane of
@@ -713,6 +733,7 @@ __device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene
     Q.hit[v.s.lane] = 0;
     __builtin_amdgcn_wave_barrier();
     if (fk_walk(q, sc, k, v)) return true;
+    if (!v.s.in_limits) never_pairs_outside_limits(q, sc, v.s);
     RP_STAMP(5);
     if (__any(v.s.nsb > 0)) drain_sb(v.s);
     RP_STAMP(6);

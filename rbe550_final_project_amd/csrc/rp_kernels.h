@@ -15,14 +15,19 @@
 namespace rp {
 
 constexpr int VBLOCK = 64;      // validity / edge block size: one wave (its LDS = its queue)
-// waves per SIMD requested from the register allocator: 4 holds k_validity at 128
-// VGPRs (4 waves/SIMD, no spills; measured +2 % goal3, +22 % clutter64 over letting
-// it take 130 and drop to 3); the edge kernel would spill at 4 and stays free
+// waves per SIMD requested from the register allocator. k_validity on cluster
+// scenes: 5 (96 VGPRs, 3 spilled in a cold path; needs the 8160-B queue of
+// QCAP 76 — 20 one-wave workgroups per CU): +4.5 % goal3 over 4 waves. Grid scenes
+// keep 4 (their broad phase spills at 96). The edge kernels: 4 (was uncapped at
+// 136 VGPRs = 3 waves): C4 262k-sample plans -12 %; 5 spills.
 #ifndef RP_VALIDITY_WAVES
-#define RP_VALIDITY_WAVES 4
+#define RP_VALIDITY_WAVES 5
+#endif
+#ifndef RP_VALIDITY_WAVES_GRID
+#define RP_VALIDITY_WAVES_GRID 4
 #endif
 #ifndef RP_EDGE_WAVES
-#define RP_EDGE_WAVES 1
+#define RP_EDGE_WAVES 4
 #endif
 constexpr int NNBLOCK = 256;    // NN block size
 constexpr int NNTILE = 256;     // tree nodes per LDS tile (256 x 72 B = 18 KiB)
@@ -35,7 +40,7 @@ constexpr int NNTILE = 256;     // tree nodes per LDS tile (256 x 72 B = 18 KiB)
 // narrow-phase queue (rp_math.h WaveQ). The scene record is read with wave-uniform
 // scalar loads (measured faster than staging it in LDS: 10.74 vs 10.52 G states/s).
 template <int NCL>
-__global__ __launch_bounds__(VBLOCK, RP_VALIDITY_WAVES) void k_validity(const float* __restrict__ q, int64_t n,
+__global__ __launch_bounds__(VBLOCK, NCL == NCL_GRID ? RP_VALIDITY_WAVES_GRID : RP_VALIDITY_WAVES) void k_validity(const float* __restrict__ q, int64_t n,
                                                                        uint8_t* __restrict__ flags,
                                                                        const DevScene* __restrict__ sc) {
     __shared__ WaveQ wq;

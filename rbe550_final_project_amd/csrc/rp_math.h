@@ -412,14 +412,15 @@ __device__ __forceinline__ bool pairs_ending_at(const Capsules& k) {
 // needs it: with ~35 self pairs and per-lane candidate rates of 0.1-7 %, a wave
 // ran ~11 narrow phases although a lane needs ~0.4 on average. Instead, a lane
 // whose broad phase passes appends the candidate (endpoints already in the box /
-// world frame) to a per-wave LDS queue; when the queue holds >= 64 items, or at
-// the end of the chain, the active lanes drain it together, one item per lane.
+// world frame) to a per-wave LDS queue; when the next batch would overflow it, the
+// active lanes pop one full pass of items (one per lane), and at the end of the
+// chain they drain the rest.
 // The set of tests and their arithmetic are unchanged, so results are identical.
 // All queue operations sit in wave-uniform control flow (ballot + mbcnt).
 #ifndef RP_QCAP
-#define RP_QCAP 96
+#define RP_QCAP 76
 #endif
-constexpr int QCAP = RP_QCAP;   // items per queue; drained once more than QCAP-64 are pending
+constexpr int QCAP = RP_QCAP;   // items per queue (WaveQ = 76 x 104 B + 256 B = 8160 B: 20 waves per CU)
 
 struct WaveQ {
     float ss[QCAP][15];   // self pair: a1 b1 a2 b2 (12), owner lane | pair << 8, r_i, r_j
@@ -489,6 +490,69 @@ __device__ RP_DRAIN_ATTR void drain_ss(S& s) {
     s.nss = 0;
 }
 
+// Pop-one-pass drains (RP_DRAIN_POP): a queue is drained only when the next
+// enqueue would overflow it, and then by exactly one pass over its top items (one
+// per active lane), so mid-walk passes run full; the walk's end drains the rest.
+// Room is guaranteed: a batch has at most as many items as there are active lanes.
+#ifndef RP_DRAIN_POP
+#define RP_DRAIN_POP 1
+#endif
+template <class S>
+__device__ __forceinline__ void pop_ss(S& s) {
+    const unsigned long long act = __ballot(1);
+    const int nact = __popcll(act), r = rank_in(act);
+    const int take = s.nss < nact ? s.nss : nact;
+    __builtin_amdgcn_wave_barrier();
+    if (r < take) {
+        const float* it = s.Q->ss[s.nss - 1 - r];
+        const V3 a1 = {it[0], it[1], it[2]}, b1 = {it[3], it[4], it[5]};
+        const V3 a2 = {it[6], it[7], it[8]}, b2 = {it[9], it[10], it[11]};
+        const int tag = __float_as_int(it[12]);
+        const float ri = it[13], rj = it[14];
+        const Aabb u = capsule_aabb(a1, b1, ri);
+        const Aabb v = capsule_aabb(a2, b2, rj);
+        if (!aabb_disjoint2(u, v)) {
+            const float rr = ri + rj;
+            if (segment_segment_dist2(a1, b1, a2, b2) <= rr * rr) s.Q->hit[tag & 63] = 1;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    s.nss -= take;
+}
+template <class S>
+__device__ __forceinline__ void pop_sb(S& s) {
+    const unsigned long long act = __ballot(1);
+    const int nact = __popcll(act), r = rank_in(act);
+    const int take = s.nsb < nact ? s.nsb : nact;
+    __builtin_amdgcn_wave_barrier();
+    if (r < take) {
+        const float* it = s.Q->sb[s.nsb - 1 - r];
+        const V3 pa = {it[0], it[1], it[2]}, pb = {it[3], it[4], it[5]}, h = {it[6], it[7], it[8]};
+        if (segment_box_dist2(pa, pb, h) <= it[9]) s.Q->hit[__float_as_int(it[10])] = 1;
+    }
+    __builtin_amdgcn_wave_barrier();
+    s.nsb -= take;
+}
+// make room for a batch of c items / the old policy's check after it (wave-uniform)
+template <class S>
+__device__ __forceinline__ void room_ss(S& s, int c) {
+#if RP_DRAIN_POP
+    if (s.nss + c > QCAP) pop_ss(s);
+#endif
+}
+template <class S>
+__device__ __forceinline__ void room_sb(S& s, int c) {
+#if RP_DRAIN_POP
+    if (s.nsb + c > QCAP) pop_sb(s);
+#endif
+}
+template <class S>
+__device__ __forceinline__ void after_ss(S& s) {
+#if !RP_DRAIN_POP
+    if (s.nss > QCAP - 64) drain_ss(s);
+#endif
+}
+
 template <class S>
 __device__ RP_DRAIN_ATTR void drain_sb(S& s) {
     const unsigned long long act = __ballot(1);
@@ -504,6 +568,12 @@ __device__ RP_DRAIN_ATTR void drain_sb(S& s) {
     }
     __builtin_amdgcn_wave_barrier();
     s.nsb = 0;
+}
+template <class S>
+__device__ __forceinline__ void after_sb(S& s) {
+#if !RP_DRAIN_POP
+    if (s.nsb > QCAP - 64) drain_sb(s);
+#endif
 }
 
 // queue item of capsule C vs box record bx (box frame segment, half extents, r^2)
@@ -551,9 +621,10 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
             }
             const unsigned long long bm = __ballot(cand);
             if (!bm) continue;
+            room_sb(s, __popcll(bm));
             if (cand) enqueue_sb<C>(k, bx, r, s, bm);
             s.nsb += __popcll(bm);
-            if (s.nsb > QCAP - 64) drain_sb(s);
+            after_sb(s);
         }
         return false;
     }
@@ -573,9 +644,10 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
             const bool cand = near_cl && !exempt && !apart;
             const unsigned long long m = __ballot(cand);
             if (!m) continue;
+            room_sb(s, __popcll(m));
             if (cand) enqueue_sb<C>(k, bx, r, s, m);
             s.nsb += __popcll(m);
-            if (s.nsb > QCAP - 64) drain_sb(s);
+            after_sb(s);
         }
     }
     return false;
@@ -615,6 +687,7 @@ template <int P, class S>
 __device__ __forceinline__ void pair_enqueue(const Capsules& k, S& s, bool cand, unsigned long long m) {
     constexpr int I = PAIRS[P][0], J = PAIRS[P][1];
     if (!m) return;
+    room_ss(s, __popcll(m));
     if (cand) {
         float* it = s.Q->ss[s.nss + rank_in(m)];
         it[0] = k.a[I].x; it[1] = k.a[I].y; it[2] = k.a[I].z;
@@ -626,7 +699,7 @@ __device__ __forceinline__ void pair_enqueue(const Capsules& k, S& s, bool cand,
         it[14] = CAP_GEOM[J][6];
     }
     s.nss += __popcll(m);
-    if (s.nss > QCAP - 64) drain_ss(s);
+    after_ss(s);
 }
 
 constexpr bool pairs_in_chain_order() {

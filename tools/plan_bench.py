@@ -27,7 +27,7 @@ def main():
             ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
             ctx.set_attached(q["attached"])
             p = _abi.make_params(seed=i, batch=batch, batch_min=batch_min, n_waypoints=150, timeout_s=10.0,
-                                 tree_capacity=1 << 24)
+                                 tree_capacity=1 << 24, straight_first=False)
             t0 = time.perf_counter()
             ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
             t.append(1e3 * (time.perf_counter() - t0))

@@ -251,11 +251,15 @@ __global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_edges_packed(
 __global__ void k_edge_prep(const double* __restrict__ from, const double* __restrict__ to, int64_t n,
                             double res, int* nd, uint8_t* valid, int* kmax) {
     const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= n) return;
-    const int c = segment_count(from + e * NQ, to + e * NQ, res);
-    nd[e] = c;
-    valid[e] = 1;
-    atomicMax(kmax, c > 1 ? c : 1);
+    int v = 0;
+    if (e < n) {
+        const int c = segment_count(from + e * NQ, to + e * NQ, res);
+        nd[e] = c;
+        valid[e] = 1;
+        v = c > 1 ? c : 1;
+    }
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));   // wave max: one atomic per wave
+    if ((threadIdx.x & 63) == 0 && v > 0) atomicMax(kmax, v);
 }
 
 // ---------------------------------------------------------------------------
@@ -778,28 +782,33 @@ __global__ void k_conn_append(const int32_t* __restrict__ rec, const int32_t* __
                               const double* __restrict__ chain_nodes, const int32_t* __restrict__ m) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (status) n = min(n, (int64_t)status[ST_NACC]);
-    if (t >= n) return;
-    const int L = rec[2 * t + 1];
-    const int64_t off = TB + incl[t] - L;
-    if (!chain_nodes) {
-        if (conn_append_one(t, rec[2 * t], L, off, A, TA0, Bt, Bpar, Bcand, range, cmax, a_start, Acand,
-                            chain_end))
-            atomicMin(first_reached, (int)t);
-        return;
+    bool reached = false;
+    if (t < n) {
+        const int L = rec[2 * t + 1];
+        const int64_t off = TB + incl[t] - L;
+        if (!chain_nodes) {
+            reached = conn_append_one(t, rec[2 * t], L, off, A, TA0, Bt, Bpar, Bcand, range, cmax, a_start, Acand,
+                                      chain_end);
+        } else {
+            int32_t par = rec[2 * t];
+            for (int s = 0; s < L; ++s) {
+                const double* cs = chain_nodes + (t * cmax + s) * NQ;
+                for (int d = 0; d < NQ; ++d) Bt[(off + s) * NQ + d] = cs[d];
+                Bpar[off + s] = par;
+                Bcand[off + s] = 0;
+                par = (int32_t)(off + s);
+            }
+            const int mk = m[t];
+            reached = L == (mk & CHAIN_LEN) && (mk & CHAIN_REACHES);
+            chain_end[t] = L > 0 ? par : -1;
+            if (!reached && a_start) Acand[TA0 + t] = 1;
+        }
     }
-    int32_t par = rec[2 * t];
-    for (int s = 0; s < L; ++s) {
-        const double* cs = chain_nodes + (t * cmax + s) * NQ;
-        for (int d = 0; d < NQ; ++d) Bt[(off + s) * NQ + d] = cs[d];
-        Bpar[off + s] = par;
-        Bcand[off + s] = 0;
-        par = (int32_t)(off + s);
-    }
-    const int mk = m[t];
-    const bool reached = L == (mk & CHAIN_LEN) && (mk & CHAIN_REACHES);
-    chain_end[t] = L > 0 ? par : -1;
-    if (!reached && a_start) Acand[TA0 + t] = 1;
-    if (reached) atomicMin(first_reached, (int)t);
+    // first REACHED target: one atomic per wave (its lowest reached lane), not per
+    // lane — every lane's atomic on the one word queued in a single L2 channel
+    const unsigned long long b = __ballot(reached);
+    const int lane = (int)(threadIdx.x & 63);
+    if (b && lane == 0) atomicMin(first_reached, (int)(t + __builtin_ctzll(b)));
 }
 
 // end of an iteration (single lane): nodes added to tree B; on success the join

@@ -1,0 +1,103 @@
+"""GPU edge cases of the C-ABI (SURVEY.md §4 style: empty and ragged inputs, maximum
+sizes, degenerate edges and plans, argument errors), each against the CPU oracle."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from rbe550_final_project_amd import _abi, model, scenes
+from rbe550_final_project_amd.native import NativeError, load
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(gpu_ctx, oracle_lib, sc, attached=-1):
+    o = oracle_lib.OracleScene()
+    o.set_scene(sc.boxes, sc.plane_z, sc.base)
+    o.set_attached(attached)
+    gpu_ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+    gpu_ctx.set_attached(attached)
+    return o
+
+
+@pytest.mark.parametrize("n", [0, 1, 63, 65, 127, 1000, 4097])
+def test_ragged_state_counts(gpu_ctx, oracle_lib, n):
+    """State counts that are not multiples of the 64-lane wave (and zero)."""
+    o = _pair(gpu_ctx, oracle_lib, scenes.goal3_tallest())
+    rng = np.random.default_rng(n)
+    q = (model.Q_LO + (model.Q_HI - model.Q_LO) * rng.random((n, 9))).astype(np.float32)
+    g = gpu_ctx.check_states(q)
+    assert g.shape == (n,)
+    assert np.array_equal(g, o.check_states(q))
+
+
+def test_max_boxes_scene(gpu_ctx, oracle_lib):
+    """64 boxes (MAX_BOXES) with yaw and an attached box: flags bit-exact."""
+    rng = np.random.default_rng(64)
+    boxes = [(tuple(rng.uniform([0.2, -0.6, 0.02], [0.9, 0.6, 0.7])), tuple(rng.uniform(0.01, 0.06, 3)),
+              float(rng.uniform(-np.pi, np.pi))) for i in range(64)]
+    sc = scenes.Scene(boxes=boxes)
+    o = _pair(gpu_ctx, oracle_lib, sc, attached=5)
+    q = (model.Q_LO + (model.Q_HI - model.Q_LO) * np.random.default_rng(1).random((50000, 9))).astype(np.float32)
+    assert np.array_equal(gpu_ctx.check_states(q), o.check_states(q))
+
+
+def test_too_many_boxes_rejected(gpu_ctx):
+    boxes = [((0.5, 0.0, 0.02 + 0.05 * i), (0.02, 0.02, 0.02), 0.0) for i in range(65)]
+    with pytest.raises(NativeError):
+        gpu_ctx.set_scene(boxes)
+
+
+def test_zero_length_and_long_edges(gpu_ctx, oracle_lib):
+    """Zero-length edges (only the endpoint is checked) and bound-to-bound edges
+    (the longest in the space): edge flags bit-exact."""
+    o = _pair(gpu_ctx, oracle_lib, scenes.goal3_tallest())
+    rng = np.random.default_rng(3)
+    a = model.Q_LO + (model.Q_HI - model.Q_LO) * rng.random((300, 9))
+    b = a.copy()
+    b[100:200] = model.Q_LO + (model.Q_HI - model.Q_LO) * rng.random((100, 9))
+    b[200:] = np.where(rng.random((100, 9)) < 0.5, model.Q_LO, model.Q_HI)
+    a[200:] = np.where(b[200:] == model.Q_LO, model.Q_HI, model.Q_LO)
+    res = 0.01 * model.max_extent()
+    assert np.array_equal(gpu_ctx.check_edges(a, b, res), o.check_edges(a, b, res))
+    assert np.array_equal(gpu_ctx.check_edges(a[:0], b[:0], res), np.zeros(0, np.uint8))
+
+
+@pytest.mark.parametrize("straight", [True, False])
+def test_plan_start_equals_goal(gpu_ctx, oracle_lib, straight):
+    """start == goal: an exact solution with the oracle's path."""
+    o = _pair(gpu_ctx, oracle_lib, scenes.goal3_tallest())
+    s = np.array(model.SAFE_HOME)
+    s[7:] = 0.035
+    p = _abi.make_params(seed=4, batch=64, n_waypoints=150, timeout_s=10, straight_first=straight)
+    ref, st_ref, _ = o.plan(s, s, model.Q_LO, model.Q_HI, p)
+    path, st = gpu_ctx.plan(s, s, model.Q_LO, model.Q_HI, p)
+    assert st == st_ref == _abi.STATUS_EXACT
+    assert np.array_equal(path, ref) and len(path) == 150
+
+
+def test_plan_out_of_bounds_goal(gpu_ctx, oracle_lib):
+    """A goal outside the bounds is INVALID_GOAL (OMPL PlannerInputStates), with and
+    without the straight-first check."""
+    o = _pair(gpu_ctx, oracle_lib, scenes.goal3_tallest())
+    s = np.array(model.SAFE_HOME)
+    s[7:] = 0.035
+    g = s.copy()
+    g[0] = model.Q_HI[0] + 0.1
+    for straight in (True, False):
+        p = _abi.make_params(seed=1, batch=64, n_waypoints=150, timeout_s=10, straight_first=straight)
+        st_gpu = gpu_ctx.plan(s, g, model.Q_LO, model.Q_HI, p)[1]
+        st_cpu = o.plan(s, g, model.Q_LO, model.Q_HI, p)[1]
+        assert st_gpu == st_cpu == _abi.STATUS_INVALID_GOAL
+
+
+def test_argument_errors(gpu_ctx):
+    """Negative counts and null buffers return errors, not crashes."""
+    L = load()
+    out = (C.c_uint8 * 4)()
+    assert L.rp_check_states(gpu_ctx._h, None, -1, out) < 0
+    assert L.rp_check_states(gpu_ctx._h, None, 4, out) < 0
+    assert L.rp_check_edges(gpu_ctx._h, None, None, 4, 0.1, out) < 0
+    n, st = C.c_int32(0), C.c_int32(0)
+    p = _abi.make_params()
+    assert L.rp_plan(gpu_ctx._h, None, None, None, None, C.byref(p), None, 0, C.byref(n), C.byref(st)) < 0

@@ -458,45 +458,11 @@ struct QueueState {
     ClusterRegs<NCL> cl;
 };
 
-#ifdef RP_OPT_DRAIN_NOINLINE
-#define RP_DRAIN_ATTR __attribute__((noinline))
-#else
-#define RP_DRAIN_ATTR __forceinline__
-#endif
-template <class S>
-__device__ RP_DRAIN_ATTR void drain_ss(S& s) {
-    const unsigned long long act = __ballot(1);
-    const int nact = __popcll(act), r = rank_in(act);
-    __builtin_amdgcn_wave_barrier();
-#ifdef RP_ABLATE_DRAIN
-    s.nss = 0;
-#endif
-    for (int i = r; i < s.nss; i += nact) {
-        const float* it = s.Q->ss[i];
-        const V3 a1 = {it[0], it[1], it[2]}, b1 = {it[3], it[4], it[5]};
-        const V3 a2 = {it[6], it[7], it[8]}, b2 = {it[9], it[10], it[11]};
-        const int tag = __float_as_int(it[12]);
-        // radii travel with the item (a table lookup by the lane's pair id was a
-        // global load with a full wait in every drain pass)
-        const float ri = it[13], rj = it[14];
-        // the oracle's exact decision: AABB reject, then segment distance
-        const Aabb u = capsule_aabb(a1, b1, ri);
-        const Aabb v = capsule_aabb(a2, b2, rj);
-        if (aabb_disjoint2(u, v)) continue;
-        const float rr = ri + rj;
-        if (segment_segment_dist2(a1, b1, a2, b2) <= rr * rr) s.Q->hit[tag & 63] = 1;
-    }
-    __builtin_amdgcn_wave_barrier();
-    s.nss = 0;
-}
-
-// Pop-one-pass drains (RP_DRAIN_POP): a queue is drained only when the next
-// enqueue would overflow it, and then by exactly one pass over its top items (one
-// per active lane), so mid-walk passes run full; the walk's end drains the rest.
-// Room is guaranteed: a batch has at most as many items as there are active lanes.
-#ifndef RP_DRAIN_POP
-#define RP_DRAIN_POP 1
-#endif
+// Drains pop: a queue is drained only when the next enqueue would overflow it, and
+// then by exactly one pass over its top items (one per active lane), so mid-walk
+// passes run full; the walk's end pops until empty. Room is guaranteed: a batch has
+// at most as many items as there are active lanes. (Draining whenever more than
+// QCAP - 64 items were pending ran more, emptier passes and needed a larger queue.)
 template <class S>
 __device__ __forceinline__ void pop_ss(S& s) {
     const unsigned long long act = __ballot(1);
@@ -533,47 +499,14 @@ __device__ __forceinline__ void pop_sb(S& s) {
     __builtin_amdgcn_wave_barrier();
     s.nsb -= take;
 }
-// make room for a batch of c items / the old policy's check after it (wave-uniform)
+// make room for a batch of c items (wave-uniform)
 template <class S>
 __device__ __forceinline__ void room_ss(S& s, int c) {
-#if RP_DRAIN_POP
     if (s.nss + c > QCAP) pop_ss(s);
-#endif
 }
 template <class S>
 __device__ __forceinline__ void room_sb(S& s, int c) {
-#if RP_DRAIN_POP
     if (s.nsb + c > QCAP) pop_sb(s);
-#endif
-}
-template <class S>
-__device__ __forceinline__ void after_ss(S& s) {
-#if !RP_DRAIN_POP
-    if (s.nss > QCAP - 64) drain_ss(s);
-#endif
-}
-
-template <class S>
-__device__ RP_DRAIN_ATTR void drain_sb(S& s) {
-    const unsigned long long act = __ballot(1);
-    const int nact = __popcll(act), r = rank_in(act);
-    __builtin_amdgcn_wave_barrier();
-#ifdef RP_ABLATE_DRAIN
-    s.nsb = 0;
-#endif
-    for (int i = r; i < s.nsb; i += nact) {
-        const float* it = s.Q->sb[i];
-        const V3 pa = {it[0], it[1], it[2]}, pb = {it[3], it[4], it[5]}, h = {it[6], it[7], it[8]};
-        if (segment_box_dist2(pa, pb, h) <= it[9]) s.Q->hit[__float_as_int(it[10])] = 1;
-    }
-    __builtin_amdgcn_wave_barrier();
-    s.nsb = 0;
-}
-template <class S>
-__device__ __forceinline__ void after_sb(S& s) {
-#if !RP_DRAIN_POP
-    if (s.nsb > QCAP - 64) drain_sb(s);
-#endif
 }
 
 // queue item of capsule C vs box record bx (box frame segment, half extents, r^2)
@@ -624,7 +557,6 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
             room_sb(s, __popcll(bm));
             if (cand) enqueue_sb<C>(k, bx, r, s, bm);
             s.nsb += __popcll(bm);
-            after_sb(s);
         }
         return false;
     }
@@ -647,7 +579,6 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
             room_sb(s, __popcll(m));
             if (cand) enqueue_sb<C>(k, bx, r, s, m);
             s.nsb += __popcll(m);
-            after_sb(s);
         }
     }
     return false;
@@ -699,7 +630,6 @@ __device__ __forceinline__ void pair_enqueue(const Capsules& k, S& s, bool cand,
         it[14] = CAP_GEOM[J][6];
     }
     s.nss += __popcll(m);
-    after_ss(s);
 }
 
 constexpr bool pairs_in_chain_order() {
@@ -808,9 +738,9 @@ __device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene
     if (fk_walk(q, sc, k, v)) return true;
     if (!v.s.in_limits) never_pairs_outside_limits(q, sc, v.s);
     RP_STAMP(5);
-    if (__any(v.s.nsb > 0)) drain_sb(v.s);
+    while (v.s.nsb > 0) pop_sb(v.s);
     RP_STAMP(6);
-    if (__any(v.s.nss > 0)) drain_ss(v.s);
+    while (v.s.nss > 0) pop_ss(v.s);
     RP_STAMP(7);
     return Q.hit[v.s.lane] != 0;
 }

@@ -15,16 +15,17 @@ triangle inequality), for the finger slide 1. The pair is proven "never" when
     python tools/prove_pairs.py [grid_scale]   -> JSON on stdout
 """
 import json
+import os
 import re
 import sys
 
 import numpy as np
 
-sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 from rbe550_final_project_amd import model  # noqa: E402
 
-SRC = open(__import__("os").path.join(__import__("os").path.dirname(__import__("os").path.dirname(
-    __import__("os").path.abspath(__file__))), "rbe550_final_project_amd", "csrc", "rp_model.h")).read()
+SRC = open(os.path.join(ROOT, "rbe550_final_project_amd", "csrc", "rp_model.h")).read()
 G = np.array([[float(x.rstrip("f")) for x in r.split(",")]
               for r in re.findall(r"\{(-?[\d.]+f?(?:, -?[\d.]+f?){6})\},\s*// \w+", SRC)])
 NAMES = ["link0", "link1", "link2", "link3", "link4", "link5a", "link5b", "link6", "link7", "hand", "lfinger",

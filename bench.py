@@ -33,6 +33,7 @@ METRIC = "states-checked/sec + plan wall-time, 7-DOF arm/10 blocks, 1/2/4/8 GPU"
 VALU_PEAK_TFLOPS = 157.3     # MI355X FP32 vector peak (MI355X_MICROARCH.md chip table)
 HBM_PEAK_GBPS = 8000.0       # spec
 BYTES_PER_STATE = 9 * 4 + 1  # 9 x fp32 in, 1 B flag out
+C2_BATCH = 65536             # BASELINE C2: 64k-sample batch
 C4_BATCH = 262144            # BASELINE C4: 256k-sample iterations
 C5_BATCH = 131072            # BASELINE C5: 131,072-sample iterations (2^20 budget)
 
@@ -284,6 +285,17 @@ def main():
             t1, s1, st1 = run_plans(ctx, wl1, args.plan_batch, 0, group, straight_first=False)
             plan["C1_goal1_rrt"] = plan_record(t1, s1, st1, args.plan_batch, dev, distributed,
                                                {"mode": "RRT-Connect forced (straight_first off)"})
+            # C2: the single pick -> place segment (2 queries, 5 boxes) with 65,536-sample
+            # iterations over 10 seeds (BASELINE configs[1]: median of 20 plans)
+            wl2 = load_workload("single_pick_place_5box")
+            wl2x = {"queries": wl2["queries"] * 10}
+            t2, s2, st2 = run_plans(ctx, wl2x, C2_BATCH, 0, group)
+            plan["C2_single_64k"] = plan_record(t2, s2, st2, C2_BATCH, dev, distributed,
+                                                {"mode": "product default: straight edge first, then RRT-Connect"})
+            t2, s2, st2 = run_plans(ctx, wl2x, C2_BATCH, 0, group, batch_min=C2_BATCH, straight_first=False)
+            plan["C2_single_64k_rrt"] = plan_record(t2, s2, st2, C2_BATCH, dev, distributed,
+                                                    {"mode": "RRT-Connect forced, 65,536-sample iterations",
+                                                     "batch_min": C2_BATCH})
             # the same queries with RRT-Connect forced (straight_first off)
             t3, s3, st3 = run_plans(ctx, wl, args.plan_batch, 0, group, straight_first=False)
             plan["C3_rrt"] = plan_record(t3, s3, st3, args.plan_batch, dev, distributed,

@@ -39,7 +39,7 @@ constexpr int NNTILE = 256;     // tree nodes per LDS tile (256 x 72 B = 18 KiB)
 // One lane per state; one wave per workgroup, whose LDS holds the wave's
 // narrow-phase queue (rp_math.h WaveQ). The scene record is read with wave-uniform
 // scalar loads (measured faster than staging it in LDS: 10.74 vs 10.52 G states/s).
-template <int NCL>
+template <int NCL, bool BF = false>
 __global__ __launch_bounds__(VBLOCK, NCL == NCL_GRID ? RP_VALIDITY_WAVES_GRID : RP_VALIDITY_WAVES) void k_validity(const float* __restrict__ q, int64_t n,
                                                                        uint8_t* __restrict__ flags,
                                                                        const DevScene* __restrict__ sc) {
@@ -54,7 +54,7 @@ __global__ __launch_bounds__(VBLOCK, NCL == NCL_GRID ? RP_VALIDITY_WAVES_GRID : 
     asm volatile("" ::"v"(qq[0]), "v"(qq[8]));
     RP_STAMP(1);
 #endif
-    flags[i] = state_collides<NCL>(qq, sc, wq) ? 0 : 1;
+    flags[i] = state_collides<NCL, BF>(qq, sc, wq) ? 0 : 1;
 }
 
 // ---------------------------------------------------------------------------

@@ -160,17 +160,31 @@ int ncl_bucket(const DevScene& sc) {
     return sc.grid ? NCL_GRID : n <= 0 ? 0 : n == 1 ? 1 : n == 2 ? 2 : n <= 4 ? 4 : 8;
 }
 
+// base_fixed: the scene's robot base is rp_math.h BASE_FIXED (the reference's), so
+// the kernels with the base folded in apply
+bool base_fixed(const DevScene& sc) {
+    return sc.base[0] == BASE_FIXED[0] && sc.base[1] == BASE_FIXED[1] && sc.base[2] == BASE_FIXED[2];
+}
+
+template <bool BF>
+void launch_validity_bf(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, hipStream_t s) {
+    const dim3 g(blocks_for(n, VBLOCK)), b(VBLOCK);
+#define RP_VAL(N) hipLaunchKernelGGL((k_validity<N, BF>), g, b, 0, s, q, n, flags, c->d_scene)
+    switch (ncl_bucket(c->scene)) {
+        case NCL_GRID: RP_VAL(NCL_GRID); break;
+        case 0: RP_VAL(0); break;
+        case 1: RP_VAL(1); break;
+        case 2: RP_VAL(2); break;
+        case 4: RP_VAL(4); break;
+        default: RP_VAL(8); break;
+    }
+#undef RP_VAL
+}
+
 void launch_validity(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, hipStream_t s) {
     if (n <= 0) return;
-    const dim3 g(blocks_for(n, VBLOCK)), b(VBLOCK);
-    switch (ncl_bucket(c->scene)) {
-        case NCL_GRID: hipLaunchKernelGGL(k_validity<NCL_GRID>, g, b, 0, s, q, n, flags, c->d_scene); break;
-        case 0: hipLaunchKernelGGL(k_validity<0>, g, b, 0, s, q, n, flags, c->d_scene); break;
-        case 1: hipLaunchKernelGGL(k_validity<1>, g, b, 0, s, q, n, flags, c->d_scene); break;
-        case 2: hipLaunchKernelGGL(k_validity<2>, g, b, 0, s, q, n, flags, c->d_scene); break;
-        case 4: hipLaunchKernelGGL(k_validity<4>, g, b, 0, s, q, n, flags, c->d_scene); break;
-        default: hipLaunchKernelGGL(k_validity<8>, g, b, 0, s, q, n, flags, c->d_scene); break;
-    }
+    if (base_fixed(c->scene)) launch_validity_bf<true>(c, q, n, flags, s);
+    else launch_validity_bf<false>(c, q, n, flags, s);
     HIP_TRY(hipGetLastError());
 }
 

@@ -152,14 +152,20 @@ __device__ __forceinline__ void place(Capsules& k, const Frame& f) {
 // After each capsule is placed, v.template at<C>(k) runs; a true return stops the
 // walk (a collision found: the rest of the chain is not needed). Capsules whose
 // last use has passed are dead, so their registers are reused.
-template <class Visit>
+// BF (base fixed): the robot base is the reference's (0, 0, 0.01) (scenes.py:29-34),
+// a compile-time constant, so everything that depends on the base alone (link0 and
+// link1's capsules, the shoulder position) folds into literals and takes no
+// registers; the values are the ones the runtime base gives
+constexpr float BASE_FIXED[3] = {0.0f, 0.0f, 0.01f};
+template <class Visit, bool BF = false>
 __device__ __forceinline__ bool fk_walk(const float q[NQ], const DevScene* __restrict__ sc, Capsules& k,
                                         Visit& v) {
     Frame f;
     f.c0 = {1.0f, 0.0f, 0.0f};
     f.c1 = {0.0f, 1.0f, 0.0f};
     f.c2 = {0.0f, 0.0f, 1.0f};
-    f.p = {sc->base[0], sc->base[1], sc->base[2]};
+    if constexpr (BF) f.p = {BASE_FIXED[0], BASE_FIXED[1], BASE_FIXED[2]};
+    else f.p = {sc->base[0], sc->base[1], sc->base[2]};
     place<C_LINK0>(k, f);
     if (v.template at<C_LINK0>(k)) return true;
     shift(f.p, 0.333f, f.c2);               // link1: pos (0,0,0.333), joint 1
@@ -716,7 +722,7 @@ __device__ __forceinline__ void never_pairs_outside_limits(const float q[NQ], co
 // box and self narrow phases are queued and drained wave-compacted. Every lane of
 // the wave that is still running must call this at the same point. NCL >= the
 // scene's cluster count (rp_lib.hip picks the instantiation).
-template <int NCL>
+template <int NCL, bool BF = false>
 __device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene* __restrict__ sc, WaveQ& Q) {
     Capsules k;
     QueuedVisit<NCL> v;
@@ -735,7 +741,7 @@ __device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene
     v.s.cl.load(sc);
     Q.hit[v.s.lane] = 0;
     __builtin_amdgcn_wave_barrier();
-    if (fk_walk(q, sc, k, v)) return true;
+    if (fk_walk<QueuedVisit<NCL>, BF>(q, sc, k, v)) return true;
     if (!v.s.in_limits) never_pairs_outside_limits(q, sc, v.s);
     RP_STAMP(5);
     while (v.s.nsb > 0) pop_sb(v.s);

@@ -101,3 +101,22 @@ def test_argument_errors(gpu_ctx):
     n, st = C.c_int32(0), C.c_int32(0)
     p = _abi.make_params()
     assert L.rp_plan(gpu_ctx._h, None, None, None, None, C.byref(p), None, 0, C.byref(n), C.byref(st)) < 0
+
+
+@pytest.mark.parametrize("base", [(0.0, 0.0, 0.01), (0.02, -0.03, 0.01), (0.0, 0.0, 0.0), (0.0, 0.0, 0.0100001)])
+@pytest.mark.parametrize("name", ["goal3", "clutter64"])
+def test_validity_robot_base(gpu_ctx, oracle_lib, base, name):
+    """The reference's base (0, 0, 0.01) runs kernels with the base folded in as a
+    constant (rp_math.h BASE_FIXED); any other base the general ones: flags
+    bit-exact for both."""
+    import json
+    import os
+    if name == "goal3":
+        sc = scenes.goal3_tallest()
+    else:
+        gold = os.path.join(os.path.dirname(__file__), "golden", "workloads", "clutter64.json")
+        sc = scenes.Scene.from_json(json.load(open(gold))["queries"][0]["scene"])
+    sc.base = base
+    o = _pair(gpu_ctx, oracle_lib, sc)
+    q = (model.Q_LO + (model.Q_HI - model.Q_LO) * np.random.default_rng(8).random((1 << 17, 9))).astype(np.float32)
+    assert np.array_equal(gpu_ctx.check_states(q), o.check_states(q))

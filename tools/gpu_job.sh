@@ -29,6 +29,7 @@ for s in "$@"; do
     stamps) step stamps 300 python tools/stamp_probe.py build/variants/lib_stamps.so ;;
     sweep) step sweep 600 python tools/plan_sweep.py goal3_tallest_10box 4096 32 64 128 256 512 && step sweep4 600 python tools/plan_sweep.py goal4_pentagon_10box 4096 32 64 128 256 512 ;;
     planab) for v in build/variants/*.so; do step planab_$(basename $v .so) 300 python tools/plan_bench.py $v goal4_pentagon_10box 262144 full; done ;;
+    planab3) for v in build/variants/*.so; do step planab3_$(basename $v .so) 300 python tools/plan_bench.py $v goal3_tallest_10box 4096; done ;;
     bench2) step bench2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --no-cpu --backend gloo ;;
     lat) step lat 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/lat -o lt -- python tools/latency_probe.py && python tools/latency_probe.py --summarize gpurun_out/lat/lt_kernel_trace.csv > gpurun_out/lat_summary.txt ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o kt -- python bench.py --steps 20 --no-cpu --no-plan --no-configs ;;

@@ -41,7 +41,7 @@ except Exception:  # pragma: no cover - Genesis is absent in CI
     gs = None
 
 from . import _abi, model, scenes
-from .native import Context
+from .native import Context, NativeError
 
 _log = logging.getLogger("rbe550_final_project_amd.planning")
 
@@ -284,9 +284,16 @@ class PlannerInterface:
                                   simplify=bool(smooth_path), tree_capacity=_CONFIG["tree_capacity"] or 0,
                                   straight_first=_straight_first())
         cap = max(4096, int(num_waypoints or 0) + 16)
-        path, status = ctx.plan(qpos_start, qpos_goal, lo, hi, params, path_cap=cap)
+        try:
+            path, status = ctx.plan(qpos_start, qpos_goal, lo, hi, params, path_cap=cap)
+            self.last_stats = ctx.stats()
+        except NativeError as ex:
+            # the reference never raises on a failed plan (planning.py:190-202):
+            # a library error (capacity, HIP) is reported and planning "fails"
+            _logger().warning(f"MI355X planner error: {ex}")
+            path, status = None, _abi.STATUS_NONE
+            self.last_stats = None
         self.last_status = status
-        self.last_stats = ctx.stats()
 
         waypoints = []
         if status in (_abi.STATUS_EXACT, _abi.STATUS_APPROXIMATE):
@@ -326,9 +333,11 @@ class PlannerInterface:
 
     # -- single-state validity (planning.py:209-219) ------------------------------
     def _is_ompl_state_valid(self, state):
+        """planning.py:209-219: checked against the live scene (box poses and the
+        attached object as they are now), like the reference's set_qpos +
+        detect_collision on every call."""
         q = np.asarray([float(state[i]) for i in range(_abi.NQ)], dtype=np.float32)
-        if self._ctx is None:
-            self._sync_scene()
+        self._sync_scene()
         return bool(self._context().check_states(q)[0])
 
     def collision_with_attached_object(self, collision_pairs):

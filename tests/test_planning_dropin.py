@@ -125,3 +125,50 @@ def test_inverse_kinematics_then_plan():
     wps = pi.plan_path(qpos_goal=qg, num_waypoints=150, timeout=10.0)
     assert len(wps) == 150
     assert pi.inverse_kinematics([3.0, 0.0, 0.5], [0.0, 1.0, 0.0, 0.0]) is None
+
+
+class _FakeContext:
+    """Stands in for native.Context (CPU test of planning.py's host logic only)."""
+
+    def __init__(self, *a, **k):
+        self.scenes = []
+        self.attached = []
+
+    def set_scene(self, boxes, plane_z, base):
+        self.scenes.append([tuple(map(tuple, b[:2])) + (b[2],) for b in boxes])
+
+    def set_attached(self, idx):
+        self.attached.append(idx)
+
+    def check_states(self, q):
+        return np.ones(len(np.asarray(q).reshape(-1, 9)), dtype=np.uint8)
+
+    def plan(self, *a, **k):
+        raise NativeError("rp_plan failed (-5): path_cap too small")
+
+    def stats(self):
+        return {}
+
+
+def test_native_error_in_plan_returns_empty_and_restores(monkeypatch):
+    """A library error inside rp_plan (capacity, HIP) becomes the reference's
+    failure contract: [] + a warning, qpos restored (planning.py:190-205)."""
+    monkeypatch.setattr(planning, "Context", _FakeContext)
+    pi, sc = _mk([((0.65, 0.0, 0.02), (0.02, 0.02, 0.02), 0.0)])
+    q0 = sc.robot.q.clone()
+    assert pi.plan_path(model.SAFE_HOME, num_waypoints=150) == []
+    assert pi.last_status == 0 and pi.last_stats is None
+    assert torch.equal(sc.robot.set_calls[-1], q0)
+
+
+def test_state_validity_uses_live_scene(monkeypatch):
+    """_is_ompl_state_valid checks against the scene as it is now (the reference
+    runs detect_collision on the live simulation, planning.py:209-219): a box moved
+    after the last plan_path is seen by the next check."""
+    monkeypatch.setattr(planning, "Context", _FakeContext)
+    pi, sc = _mk([((0.65, 0.0, 0.02), (0.02, 0.02, 0.02), 0.0)])
+    assert pi._is_ompl_state_valid(model.SAFE_HOME) is True
+    sc.entities[1].set_pos((0.40, 0.2, 0.02))
+    assert pi._is_ompl_state_valid(model.SAFE_HOME) is True
+    seen = pi._ctx.scenes
+    assert len(seen) == 2 and abs(seen[0][0][0][0] - 0.65) < 1e-6 and abs(seen[1][0][0][0] - 0.40) < 1e-6

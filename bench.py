@@ -267,11 +267,14 @@ def main():
     # N > 1 (RCCL all-gather per phase)
     plan = None
     if not args.no_plan:
+        # the rank group is built outside the per-workload error handling: at N > 1 a
+        # plan number without the group would be a single-rank number, so a failure
+        # here ends the run (non-zero exit) instead of being reported as N-GPU
         group = None
+        if distributed:
+            from rbe550_final_project_amd.distributed import Group
+            group = Group(ctx, transport="host" if args.backend == "gloo" else "rccl")
         try:
-            if distributed:
-                from rbe550_final_project_amd.distributed import Group
-                group = Group(ctx, max(args.plan_batch, C4_BATCH), local)
             run_plans(ctx, {"queries": wl["queries"][:2]}, args.plan_batch, 100, group)   # warm-up
             times, pstates, st = run_plans(ctx, wl, args.plan_batch, 0, group)
             plan = plan_record(times, pstates, st, args.plan_batch, dev, distributed,

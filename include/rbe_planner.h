@@ -63,7 +63,7 @@ enum {
     RP_ERR_DEVICE = -2,     /* no gfx950 device / HIP runtime error                 */
     RP_ERR_STATE = -3,      /* call out of order (e.g. rp_plan before rp_set_scene) */
     RP_ERR_CAPACITY = -4,   /* tree / path capacity exceeded                        */
-    RP_ERR_EXCHANGE = -5    /* group all-gather callback failed                     */
+    RP_ERR_EXCHANGE = -5    /* group all-gather (callback or RCCL) failed            */
 };
 
 /* Plan status (OMPL PlannerStatus analogue; planning.py:190-202 treats EXACT and
@@ -151,15 +151,19 @@ typedef struct rp_stats {
     double solve_ms;            /* wall time of the solve loop                       */
     double simplify_ms;
     double total_ms;            /* wall time of the whole rp_plan call               */
-    double exchange_ms;         /* time inside the group all-gather callback         */
+    double exchange_ms;         /* group all-gather time (RCCL: stream events; host
+                                   transport: the callback)                          */
 } rp_stats;
 
 typedef struct rp_ctx rp_ctx;
 
-/* All-gather callback used by a rank group: gather `bytes_per_rank` bytes from
- * every rank's send buffer into recv (rank-major). Buffers are the ones registered
- * with rp_group_init (device memory). Return 0 on success. */
-typedef int (*rp_allgather_fn)(void* user, int64_t bytes_per_rank);
+/* Host-transport all-gather used by a rank group (rp_group_init): gather
+ * `bytes_per_rank` bytes of every rank's `send` into `recv` (rank-major). Both are
+ * pinned host buffers owned by the library, valid for the duration of the call.
+ * Return 0 on success. */
+typedef int (*rp_allgather_fn)(void* user, const void* send, void* recv, int64_t bytes_per_rank);
+
+#define RP_RCCL_ID_BYTES 128    /* ncclUniqueId */
 
 /* Library identity: returns a static string ("librbe_mi355x <version> gfx950"). */
 const char* rp_version(void);
@@ -167,7 +171,11 @@ const char* rp_version(void);
 /* Fill `out` with the built-in Franka Panda capsule model (spec/franka_capsules.json). */
 int rp_default_robot(rp_robot_desc* out);
 
-/* Create a context on HIP device `device` (>= 0). `robot` may be NULL (default model). */
+/* Create a context on HIP device `device` (>= 0). `robot` may be NULL (default model).
+ * The capsule geometry is compiled into the kernels (spec/franka_capsules.json, the
+ * constants fold into the instruction stream), so a non-NULL `robot` must equal
+ * rp_default_robot()'s description field for field; any other model is RP_ERR_ARG.
+ * The parameter lets a caller assert the model it was built against. */
 int rp_create(rp_ctx** out, int device, const rp_robot_desc* robot);
 void rp_destroy(rp_ctx* ctx);
 
@@ -199,6 +207,9 @@ int rp_check_states_device(rp_ctx* ctx, const float* q_dev, int64_t n, uint8_t* 
  * (qa is assumed valid). out[i] = 1 if the motion is valid. */
 int rp_check_edges(rp_ctx* ctx, const double* qa, const double* qb, int64_t n,
                    double resolution, uint8_t* out);
+/* Device-buffer variant, fully asynchronous on `stream` (NULL: the context stream):
+ * no host read-back; it uses the context's edge scratch, so calls in flight on
+ * different streams must be ordered by the caller. */
 int rp_check_edges_device(rp_ctx* ctx, const double* qa_dev, const double* qb_dev, int64_t n,
                           double resolution, uint8_t* out_dev, void* stream);
 
@@ -225,13 +236,26 @@ int rp_ik(rp_ctx* ctx, int32_t n_targets, const double* pos, const double* quat,
           const double lo[RP_NQ], const double hi[RP_NQ], const rp_ik_params* params, double* q_out,
           int32_t* status_out);
 
-/* Data-parallel rank group. Each rank (one process per GPU) owns one context; the
- * caller allocates `send`/`recv` device buffers of `cap_bytes` and cap_bytes*world
- * bytes and supplies an all-gather over them (torch.distributed over RCCL). After
- * this call rp_plan shards every iteration's samples and connect targets across the
- * group; the plan result is identical for every world size. world = 1 disables. */
-int rp_group_init(rp_ctx* ctx, int32_t rank, int32_t world, void* send_dev, void* recv_dev,
-                  int64_t cap_bytes, rp_allgather_fn fn, void* user);
+/* Data-parallel rank group (DESIGN.md §4 "Multi-GPU"; the reference is one process,
+ * code/planning.py:121-122). Each rank (one process per GPU) owns one context. Every
+ * RRT-Connect iteration then shards its samples across the group: each rank runs the
+ * nearest-node searches, steering and edge checks of its slice and packs one
+ * 12-byte record per sample; ONE all-gather of the records per iteration lets every
+ * rank append the same nodes, so the trees (and the plan) are identical for every
+ * world size and equal to the single-rank result.
+ *
+ * rp_group_init_rccl: the all-gather is an RCCL ncclAllGather on the context stream
+ * (xGMI between the GPUs of a node), no host synchronisation besides the
+ * iteration's status wait. `id` comes from rp_group_rccl_unique_id on rank 0,
+ * broadcast by the caller; every rank must call it (it is collective). Ranks must
+ * be on distinct GPUs.
+ * rp_group_init: host transport: the records go through library-owned pinned host
+ * buffers and `fn` (e.g. torch.distributed gloo); for ranks sharing a GPU and CPU
+ * rehearsals. world = 1 (fn may be NULL) returns the context to single-rank
+ * planning. */
+int rp_group_init(rp_ctx* ctx, int32_t rank, int32_t world, rp_allgather_fn fn, void* user);
+int rp_group_rccl_unique_id(uint8_t id_out[RP_RCCL_ID_BYTES]);
+int rp_group_init_rccl(rp_ctx* ctx, int32_t rank, int32_t world, const uint8_t id[RP_RCCL_ID_BYTES]);
 
 int rp_get_stats(rp_ctx* ctx, rp_stats* out);
 

@@ -641,6 +641,9 @@ static int walk(const tree_t* t, int32_t node, double* out, int cap) {
  * the segment-interior shortcut points of shortcutPath. Rounds repeat while the
  * path gets shorter. Level 1 = all of it, level 2 = the shortcut only. */
 #define SIMPLIFY_MAXN 1024
+/* batched RRT loops run OpenMP over samples / targets from this many on (the
+ * sequential B = 1 CPU baseline stays single-threaded) */
+#define OMP_MIN_ITEMS 512
 #define SIMPLIFY_ROUNDS 2
 #define SMOOTH_STEPS 3
 #define SMOOTH_MAX 256   /* a smoothing round runs only if 8n - 7 <= SMOOTH_MAX */
@@ -832,7 +835,10 @@ int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], co
         const int64_t TA = A->n, TB = Bt->n;
         const uint64_t g0 = gbase;
         const int64_t per = B / world;
-        /* extension: my slice of the batch */
+        /* extension: my slice of the batch (samples are independent: OpenMP over
+         * them for large batches, same results as the serial loop) */
+        int64_t ext_states = 0;
+#pragma omp parallel for schedule(dynamic, 64) reduction(+ : ext_states) if (per >= OMP_MIN_ITEMS)
         for (int64_t k = 0; k < per; ++k) {
             const int64_t i = rank * per + k;
             double qr[NQ], qn[NQ];
@@ -840,11 +846,12 @@ int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], co
             sample_state(p.seed, g0 + (uint64_t)i, lo, hi, qr);
             int32_t nn = nearest(A, TA, qr);
             steer(A->q + NQ * nn, qr, p.range, qn, &reach);
-            int ok = a_start ? edge_valid(s, A->q + NQ * nn, qn, 0, p.resolution, &st.states_checked)
-                             : edge_valid(s, qn, A->q + NQ * nn, 1, p.resolution, &st.states_checked);
-            st.edges_checked++;
+            int ok = a_start ? edge_valid(s, A->q + NQ * nn, qn, 0, p.resolution, &ext_states)
+                             : edge_valid(s, qn, A->q + NQ * nn, 1, p.resolution, &ext_states);
             mine[k] = ok ? nn : -1;
         }
+        st.states_checked += ext_states;
+        st.edges_checked += per;
         if (world > 1) {
             double te = now_s();
             mine[per] = tflag;
@@ -870,29 +877,35 @@ int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], co
             tnode[nacc++] = tree_add(A, qn, res[i]);
         }
         st.samples += B;
-        /* connect: my slice of the accepted targets */
+        /* connect: my slice of the accepted targets (independent: OpenMP) */
         const int64_t pt = (nacc + world - 1) / world;
+        int64_t con_states = 0, con_edges = 0;
+#pragma omp parallel for schedule(dynamic, 16) reduction(+ : con_states, con_edges) if (pt >= OMP_MIN_ITEMS)
         for (int64_t k = 0; k < pt; ++k) {
             const int64_t t = rank * pt + k;
             tmine[2 * k] = -1;
             tmine[2 * k + 1] = 0;
             if (t >= nacc) continue;
+            double (*ch)[NQ] = (double(*)[NQ])malloc(sizeof(double) * NQ * cmax);
             const double* x = A->q + NQ * tnode[t];
             int32_t y = nearest(Bt, TB, x);
             int reach;
-            int m = build_chain(Bt->q + NQ * y, x, p.range, chain, cmax, &reach);
+            int m = build_chain(Bt->q + NQ * y, x, p.range, ch, cmax, &reach);
             int L = 0;
             for (int c = 0; c < m; ++c) {
-                const double* from = c == 0 ? Bt->q + NQ * y : chain[c - 1];
-                int ok = a_start ? edge_valid(s, chain[c], from, 1, p.resolution, &st.states_checked)
-                                 : edge_valid(s, from, chain[c], 0, p.resolution, &st.states_checked);
-                st.edges_checked++;
+                const double* from = c == 0 ? Bt->q + NQ * y : ch[c - 1];
+                int ok = a_start ? edge_valid(s, ch[c], from, 1, p.resolution, &con_states)
+                                 : edge_valid(s, from, ch[c], 0, p.resolution, &con_states);
+                con_edges++;
                 if (!ok) break;
                 ++L;
             }
+            free(ch);
             tmine[2 * k] = y;
             tmine[2 * k + 1] = L;
         }
+        st.states_checked += con_states;
+        st.edges_checked += con_edges;
         if (world > 1) {
             double te = now_s();
             if (fn(user, tmine, trec, (int64_t)(sizeof(int32_t) * 2 * pt))) { solved = -1; break; }

@@ -25,6 +25,9 @@ HEADERS.append(os.path.join(os.path.dirname(_HERE), "include", "rbe_planner.h"))
 DEVICE_FLAGS = ["-Xarch_device", "-fno-honor-nans", "-Xarch_device", "-mno-amdgpu-ieee", "-fno-slp-vectorize"]
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
          "-fno-fast-math", "-Wall", "-Wno-unused-result"] + DEVICE_FLAGS
+# RCCL (rank-group all-gather on the context stream, rp_group_init_rccl); when torch
+# is loaded first its bundled librccl.so.1 (same SONAME) satisfies the dependency
+LIBS = ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
 
 
 def hipcc():
@@ -44,7 +47,7 @@ def up_to_date():
 def build(force=False, verbose=True):
     if not force and up_to_date():
         return OUT
-    cmd = [hipcc()] + FLAGS + ["-o", OUT, SRC]
+    cmd = [hipcc()] + FLAGS + ["-o", OUT, SRC] + LIBS
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

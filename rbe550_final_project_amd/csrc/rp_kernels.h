@@ -90,11 +90,14 @@ __global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_edges(const double* _
                                                   int kmax, int mode, uint8_t* valid, int group,
                                                   int* gfail, unsigned long long* counter,
                                                   const DevScene* __restrict__ sc,
-                                                  const int* __restrict__ dcount, int per_item) {
+                                                  const int* __restrict__ dcount, int per_item,
+                                                  const int* __restrict__ dkmax) {
     __shared__ WaveQ wq;
-    // device-side edge count (planner iterations: dcount = accepted targets); the
-    // grid may be smaller than the work (gated launches): grid-stride over it
+    // device-side edge count (planner iterations: dcount = accepted targets) and
+    // slot count (rp_check_edges_device: k_edge_prep's max); the grid may be
+    // smaller than the work (gated launches): grid-stride over it
     if (dcount) n_edges = min(n_edges, (int64_t)dcount[0] * per_item);
+    if (dkmax) kmax = *dkmax;
     const int64_t total = n_edges * kmax;
     for (int64_t base = (int64_t)blockIdx.x * VBLOCK; base < total; base += (int64_t)gridDim.x * VBLOCK) {
         const int64_t idx = base + threadIdx.x;
@@ -356,7 +359,7 @@ __global__ void k_flag(const int32_t* __restrict__ v, int64_t n, int32_t* __rest
 // to the other tree, [2] first REACHED target (INT_MAX: none), [3] start-side and
 // [4] goal-side join nodes of the solution, [5] start / goal validity flags (bytes
 // 0 and 1, written by the first validity launch of rp_plan).
-enum { ST_NACC = 0, ST_ADDED = 1, ST_FIRST = 2, ST_SNODE = 3, ST_GNODE = 4, ST_SG = 5, ST_WORDS = 8 };
+enum { ST_NACC = 0, ST_ADDED = 1, ST_FIRST = 2, ST_SNODE = 3, ST_GNODE = 4, ST_SG = 5, ST_STOP = 6, ST_WORDS = 8 };
 
 // I/O record of one rp_plan call. The device copy holds the live status; a
 // pinned, host-coherent mirror receives what the host needs (status after every
@@ -1084,9 +1087,160 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
     iteration_tail(status, totalB, TA, a_start, Apar, Bpar, chain_end, pa, io);
 }
 
-// solution path for host-chosen join nodes (approximate solutions, rank groups)
+// solution path for host-chosen join nodes (approximate solutions)
 __global__ void k_path(PathArgs pa, int32_t s_node, int32_t g_node, PlanIO* io) {
     build_path(pa, s_node, g_node, io);
+}
+
+// ---------------------------------------------------------------------------
+// rank groups (DESIGN.md §4 "Multi-GPU"): ONE exchange per iteration
+// ---------------------------------------------------------------------------
+// Every rank runs the speculative front (k_ext_conn_nn + one prefix-group edge
+// launch) on its slice [rank * per, (rank + 1) * per) of the iteration's samples
+// and packs one GREC-int32 record per sample; the records of all ranks are
+// all-gathered (RCCL on the stream, or the host transport) into a rank-major
+// buffer of `world` slots of GREC * per + 1 words (the last word of a slot: that
+// rank's timeout vote). Every rank then appends the same nodes in global sample
+// order, recomputing them from the records (Philox sample + steer; chain steers),
+// so the replicated trees stay bit-identical and equal to the world-1 trees.
+// record: [0] nearest node of the accepted extension, or -1; [1] y = nearest node
+// of the other tree; [2] L (valid chain steps) | CHAIN_REACHES if the chain's last
+// valid step lands on the new node
+constexpr int GREC = 3;
+
+__global__ void k_group_pack(const int* __restrict__ gfail, const int32_t* __restrict__ near,
+                             const int32_t* __restrict__ y, const int32_t* __restrict__ m, int64_t per, int tflag,
+                             int32_t* __restrict__ rec) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k == 0) rec[GREC * per] = tflag;
+    if (k >= per) return;
+    const int g = gfail[k];
+    const int mk = m[k];
+    const int L = g > 0 ? min(g - 1, mk & CHAIN_LEN) : -1;   // -1: extension rejected
+    const bool reached = L >= 0 && L == (mk & CHAIN_LEN) && (mk & CHAIN_REACHES);
+    rec[GREC * k] = L >= 0 ? near[k] : -1;
+    rec[GREC * k + 1] = y[k];
+    rec[GREC * k + 2] = L >= 0 ? (L | (reached ? CHAIN_REACHES : 0)) : 0;
+}
+
+struct GroupRecs {
+    const int32_t* rbuf;   // world slots, rank-major
+    int64_t per;           // samples per rank
+    int world;
+    __device__ __forceinline__ int64_t slot() const { return GREC * per + 1; }
+    __device__ __forceinline__ const int32_t* rec(int64_t i) const {   // global sample i
+        const int64_t r = i / per;
+        return rbuf + r * slot() + GREC * (i - r * per);
+    }
+    // any rank timed out: the iteration is discarded on every rank (the oracle's vote)
+    __device__ __forceinline__ bool stop() const {
+        bool s = false;
+        for (int r = 0; r < world; ++r) s |= rbuf[r * slot() + GREC * per] != 0;
+        return s;
+    }
+};
+
+// one accepted sample: extension node at TA + t, its valid chain prefix at off
+__device__ __forceinline__ bool group_append_one(int64_t i, const int32_t* rc, int64_t t, int64_t off, uint64_t seed,
+                                                 uint64_t g0, const Bounds& bd, double range, int cmax, double* A,
+                                                 int32_t* Apar, uint8_t* Acand, int64_t TA, double* Bt, int32_t* Bpar,
+                                                 uint8_t* Bcand, int a_start, int32_t* chain_end) {
+    ext_append_one(i, rc[0], TA + t, seed, g0, bd, range, A, Apar, Acand);
+    return conn_append_one(t, rc[1], rc[2] & CHAIN_LEN, off, A, TA, Bt, Bpar, Bcand, range, cmax, a_start, Acand,
+                           chain_end);
+}
+
+// batches <= FUSE_MAX: vote + scans + appends + iteration tail in one block
+template <int ITEMS>
+__global__ __launch_bounds__(FUSE_THREADS) void k_group_accept_small(
+    GroupRecs gr, int64_t B, uint64_t seed, uint64_t g0, Bounds bd, double range, int cmax, double* A,
+    int32_t* Apar, uint8_t* Acand, int64_t TA, double* Bt, int32_t* Bpar, uint8_t* Bcand, int64_t TB, int a_start,
+    int32_t* chain_end, int* status, PathArgs pa, PlanIO* io) {
+    __shared__ int lds[FUSE_THREADS / 64 + 1];
+    __shared__ int first;
+    const bool stop = gr.stop();
+    const int64_t k0 = (int64_t)threadIdx.x * ITEMS;
+    int L[ITEMS];
+    int na = 0, nl = 0;
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+        const int64_t i = k0 + r;
+        L[r] = -1;
+        if (!stop && i < B) {
+            const int32_t* rc = gr.rec(i);
+            if (rc[0] >= 0) L[r] = rc[2] & CHAIN_LEN;
+        }
+        na += L[r] >= 0;
+        nl += L[r] > 0 ? L[r] : 0;
+    }
+    int totalA, totalB;
+    const int exA = block_scan_excl(na, lds, &totalA);
+    const int exB = block_scan_excl(nl, lds, &totalB);
+    if (threadIdx.x == 0) first = 0x7fffffff;
+    __syncthreads();
+    int t = exA;
+    int64_t off = TB + exB;
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+        if (L[r] < 0) continue;
+        const int64_t i = k0 + r;
+        if (group_append_one(i, gr.rec(i), t, off, seed, g0, bd, range, cmax, A, Apar, Acand, TA, Bt, Bpar, Bcand,
+                             a_start, chain_end))
+            atomicMin(&first, t);
+        off += L[r];
+        ++t;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        status[ST_NACC] = totalA;
+        status[ST_FIRST] = first;
+        status[ST_STOP] = stop ? 1 : 0;
+    }
+    iteration_tail(status, totalB, TA, a_start, Apar, Bpar, chain_end, pa, io);
+}
+
+// large batches: per-sample counts (accepted << 40 | chain nodes), an inclusive
+// scan (hipCUB, u64), the appends, then a one-block finalize
+constexpr int GCOUNT_SHIFT = 40;
+__global__ void k_group_counts(GroupRecs gr, int64_t B, unsigned long long* __restrict__ cnt, int* status) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool stop = gr.stop();
+    if (i == 0) {
+        status[ST_FIRST] = 0x7fffffff;
+        status[ST_STOP] = stop ? 1 : 0;
+    }
+    if (i >= B) return;
+    unsigned long long v = 0;
+    if (!stop) {
+        const int32_t* rc = gr.rec(i);
+        if (rc[0] >= 0) v = (1ull << GCOUNT_SHIFT) | (unsigned long long)(rc[2] & CHAIN_LEN);
+    }
+    cnt[i] = v;
+}
+
+__global__ void k_group_append(GroupRecs gr, const unsigned long long* __restrict__ incl, int64_t B, uint64_t seed,
+                               uint64_t g0, Bounds bd, double range, int cmax, double* A, int32_t* Apar,
+                               uint8_t* Acand, int64_t TA, double* Bt, int32_t* Bpar, uint8_t* Bcand, int64_t TB,
+                               int a_start, int32_t* chain_end, int* status) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= B || status[ST_STOP]) return;
+    const int32_t* rc = gr.rec(i);
+    if (rc[0] < 0) return;
+    const int L = rc[2] & CHAIN_LEN;
+    const unsigned long long v = incl[i];
+    const int64_t t = (int64_t)(v >> GCOUNT_SHIFT) - 1;
+    const int64_t off = TB + (int64_t)(v & ((1ull << GCOUNT_SHIFT) - 1)) - L;
+    if (group_append_one(i, rc, t, off, seed, g0, bd, range, cmax, A, Apar, Acand, TA, Bt, Bpar, Bcand, a_start,
+                         chain_end))
+        atomicMin(&status[ST_FIRST], (int)t);   // a reached chain solves: rare, one atomic each
+}
+
+__global__ void k_group_finalize(const unsigned long long* __restrict__ incl, int64_t B, int* status, int64_t TA,
+                                 int a_start, const int32_t* __restrict__ Apar, const int32_t* __restrict__ Bpar,
+                                 const int32_t* __restrict__ chain_end, PathArgs pa, PlanIO* io) {
+    const unsigned long long v = (B > 0 && !status[ST_STOP]) ? incl[B - 1] : 0ull;
+    if (threadIdx.x == 0) status[ST_NACC] = (int)(v >> GCOUNT_SHIFT);
+    iteration_tail(status, (int)(v & ((1ull << GCOUNT_SHIFT) - 1)), TA, a_start, Apar, Bpar, chain_end, pa, io);
 }
 
 __global__ __launch_bounds__(256) void k_simp(int ops, int level, int dev_max, double res,

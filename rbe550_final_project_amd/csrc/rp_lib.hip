@@ -5,6 +5,7 @@
 // There is no CPU execution path: every validity evaluation runs on the GPU.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <array>
@@ -71,6 +72,19 @@ struct DevBuf {
 
 inline unsigned blocks_for(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
+enum { TR_NONE = 0, TR_HOST = 1, TR_RCCL = 2 };   // rank-group transports
+
+#define NCCL_TRY(x)                                                                              \
+    do {                                                                                         \
+        ncclResult_t r_ = (x);                                                                   \
+        if (r_ != ncclSuccess) {                                                                 \
+            char b_[512];                                                                        \
+            snprintf(b_, sizeof b_, "%s failed: %s (%s:%d)", #x, ncclGetErrorString(r_), __FILE__, \
+                     __LINE__);                                                                  \
+            throw HipError{b_};                                                                  \
+        }                                                                                        \
+    } while (0)
+
 constexpr int PATH_CAP = 1 << 16;   // states of a raw solution path (device buffer)
 constexpr int GRID_MIN_BOXES = 16;  // scenes with more boxes use the axis-grid broad phase
 
@@ -123,13 +137,37 @@ struct rp_ctx {
     int seq = 0;                         // last publication number awaited on h_io
     DevBuf<DI> partial;
 
-    // rank group
+    // rank group (DESIGN.md §4 "Multi-GPU"): one all-gather of sample records per
+    // iteration, on the context stream (RCCL) or through pinned host buffers and a
+    // caller callback (host transport: gloo rehearsals, ranks sharing one GPU)
     int rank = 0, world = 1;
-    void* g_send = nullptr;
-    void* g_recv = nullptr;
-    int64_t g_cap = 0;
+    int transport = 0;                   // TR_NONE / TR_HOST / TR_RCCL
     rp_allgather_fn g_fn = nullptr;
     void* g_user = nullptr;
+    ncclComm_t comm = nullptr;
+    DevBuf<int32_t> g_send, g_recv;      // this rank's records, every rank's (rank-major)
+    int32_t* h_send = nullptr;           // host transport staging (pinned)
+    int32_t* h_recv = nullptr;
+    int64_t h_cap = 0;                   // int32 words per rank slot in the staging
+    DevBuf<unsigned long long> g_cnt, g_incl;
+    hipEvent_t gx0 = nullptr, gx1 = nullptr;
+
+    void free_staging() {
+        if (h_send) (void)hipHostFree(h_send);
+        if (h_recv) (void)hipHostFree(h_recv);
+        h_send = h_recv = nullptr;
+        h_cap = 0;
+    }
+    void leave_group() {
+        if (comm) (void)ncclCommDestroy(comm);
+        comm = nullptr;
+        free_staging();
+        rank = 0;
+        world = 1;
+        transport = 0;
+        g_fn = nullptr;
+        g_user = nullptr;
+    }
 
     ~rp_ctx() {
         (void)hipSetDevice(device);
@@ -140,6 +178,10 @@ struct rp_ctx {
         rec.release(); Lv.release(); chain_end.release(); mine.release(); gfail.release();
         eslot.release(); eincl.release(); echunk.release();
         cub_tmp.release(); path.release(); io.release(); simp.release(); partial.release();
+        g_send.release(); g_recv.release(); g_cnt.release(); g_incl.release();
+        leave_group();
+        if (gx0) (void)hipEventDestroy(gx0);
+        if (gx1) (void)hipEventDestroy(gx1);
         if (h_io) (void)hipHostFree(h_io);
         if (d_scene) (void)hipFree(d_scene);
         if (ev0) (void)hipEventDestroy(ev0);
@@ -190,14 +232,14 @@ void launch_validity(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, hipSt
 
 void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd, int64_t n, int kmax,
                   int mode, uint8_t* valid, int group, int* gfail, hipStream_t s, const int* dcount = nullptr,
-                  int per_item = 1, unsigned max_blocks = 0) {
+                  int per_item = 1, unsigned max_blocks = 0, const int* dkmax = nullptr) {
     if (n <= 0) return;
-    const int64_t threads = n * (int64_t)kmax;
+    const int64_t threads = n * (int64_t)kmax;   // (dkmax: kmax is only the grid's size hint)
     unsigned nb = blocks_for(threads, VBLOCK);
     if (max_blocks && nb > max_blocks) nb = max_blocks;   // grid-stride (gated launches)
     const dim3 g(nb), b(VBLOCK);
 #define RP_EDGES(N) hipLaunchKernelGGL(k_edges<N>, g, b, 0, s, from, to, nd, n, kmax, mode, valid, group, gfail, \
-                                       c->counter.p, c->d_scene, dcount, per_item)
+                                       c->counter.p, c->d_scene, dcount, per_item, dkmax)
     switch (ncl_bucket(c->scene)) {
         case NCL_GRID: RP_EDGES(NCL_GRID); break;
         case 0: RP_EDGES(0); break;
@@ -271,14 +313,39 @@ int64_t read_counter(rp_ctx* c) {
     return (int64_t)s;
 }
 
-// all-gather `bytes` from dev buffer src into the group's recv buffer
-void exchange(rp_ctx* c, const void* src, int64_t bytes) {
-    if (bytes > c->g_cap) throw HipError{"group exchange buffer too small"};
-    HIP_TRY(hipMemcpyAsync(c->g_send, src, bytes, hipMemcpyDeviceToDevice, c->stream));
+// scan of u64 (hipCUB) on the context stream
+void scan_incl_u64(rp_ctx* c, const unsigned long long* in, unsigned long long* out, int64_t n) {
+    if (n <= 0) return;
+    size_t bytes = 0;
+    HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, bytes, in, out, (int)n, c->stream));
+    c->cub_tmp.ensure(bytes + 16);
+    HIP_TRY(hipcub::DeviceScan::InclusiveSum(c->cub_tmp.p, bytes, in, out, (int)n, c->stream));
+}
+
+// All-gather `words` int32 of g_send from every rank into g_recv (rank-major).
+// RCCL: enqueued on the context stream, no host wait (its time is read from two
+// events after the iteration's one host wait). Host transport: the records go
+// through pinned host buffers and the caller's callback (one stream wait).
+void group_exchange(rp_ctx* c, int64_t words) {
+    const size_t bytes = sizeof(int32_t) * (size_t)words;
+    if (c->transport == TR_RCCL) {
+        HIP_TRY(hipEventRecord(c->gx0, c->stream));
+        NCCL_TRY(ncclAllGather(c->g_send.p, c->g_recv.p, (size_t)words, ncclInt32, c->comm, c->stream));
+        HIP_TRY(hipEventRecord(c->gx1, c->stream));
+        return;
+    }
+    if (words > c->h_cap) {
+        c->free_staging();
+        HIP_TRY(hipHostMalloc((void**)&c->h_send, bytes, hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc((void**)&c->h_recv, bytes * c->world, hipHostMallocDefault));
+        c->h_cap = words;
+    }
+    HIP_TRY(hipMemcpyAsync(c->h_send, c->g_send.p, bytes, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     const double t0 = now_s();
-    if (c->g_fn(c->g_user, bytes) != 0) throw HipError{"group all-gather callback failed"};
+    if (c->g_fn(c->g_user, c->h_send, c->h_recv, (int64_t)bytes) != 0) throw HipError{"group all-gather callback failed"};
     c->stats.exchange_ms += 1e3 * (now_s() - t0);
+    HIP_TRY(hipMemcpyAsync(c->g_recv.p, c->h_recv, bytes * c->world, hipMemcpyHostToDevice, c->stream));
 }
 
 void upload_scene(rp_ctx* c) {
@@ -554,6 +621,11 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     const int kmax = (int)std::ceil(p.range / p.resolution) + 2;
     const int kfull = (int)std::ceil(max_extent / p.resolution) + 2;   // any in-bounds edge
     const int64_t BMAX = p.batch, PMAX = BMAX / world;
+    // rank groups (and RBE_PLAN_GROUPED=1 at world 1, the same iteration without an
+    // exchange) run the one-exchange speculative iteration at every batch size
+    bool grouped = c->transport != TR_NONE;
+    if (const char* e = std::getenv("RBE_PLAN_GROUPED"))
+        if (*e && world == 1 && std::atoi(e) != 0) grouped = true;
 
     // workspace
     const int64_t cap = p.tree_capacity;
@@ -564,7 +636,8 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         t.n = 0;
     }
     const int64_t ne = std::max<int64_t>({PMAX + 2, ((BMAX + world - 1) / world) * cmax, (int64_t)SPMAX * SPMAX / 2,
-                                          (std::min<int64_t>(BMAX, FUSE_MAX) + 2) * (cmax + 1)});
+                                          (std::min<int64_t>(BMAX, FUSE_MAX) + 2) * (cmax + 1),
+                                          grouped ? PMAX * (cmax + 1) : 0});
     c->efrom.ensure(ne * NQ);
     c->eto.ensure(ne * NQ);
     c->nd.ensure(ne);
@@ -580,6 +653,12 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     c->chain_end.ensure(BMAX);
     c->gfail.ensure(std::max<int64_t>(BMAX, FUSE_MAX + 2));
     c->mine.ensure(PMAX + 1);
+    if (grouped) {
+        c->g_send.ensure((size_t)GREC * PMAX + 1);
+        c->g_recv.ensure((size_t)world * (GREC * PMAX + 1));
+        c->g_cnt.ensure(BMAX);
+        c->g_incl.ensure(BMAX);
+    }
     c->scalar.ensure(16);
     c->counter.ensure(COUNTER_SLOTS);
     if (!c->sync.p) {
@@ -613,7 +692,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     // single-rank iterations of <= FUSE_MAX samples run speculatively (extension
     // and connect edges in one launch, k_ext_conn_nn); RBE_PLAN_SPECULATE=0 keeps
     // the two-phase iteration (same trees; the parity tests run both)
-    bool speculate = world == 1;
+    bool speculate = !grouped;
     if (const char* e = std::getenv("RBE_PLAN_SPECULATE"))
         if (*e) speculate = speculate && std::atoi(e) != 0;
     const int G = cmax + 1;   // edges per sample in a speculative launch
@@ -694,7 +773,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             return RP_OK;
         }
     }
-    int64_t sg_edge = (!straight && world == 1 && !oob) ? (spec0 ? p.batch_min * G : p.batch_min) : -1;
+    int64_t sg_edge = (!straight && !grouped && !oob) ? (spec0 ? p.batch_min * G : p.batch_min) : -1;
     const int sg_stride = spec0 ? G : 1;
     {
         PlanRoots roots;
@@ -773,7 +852,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     for (; iter < p.max_iters; ++iter, gbase += (uint64_t)B, B = std::min(BMAX, 2 * B)) {
         const int64_t per = B / world;
         const int tflag = (now_s() - t_solve) >= p.timeout_s;
-        if (world == 1 && tflag) break;
+        if (!grouped && tflag) break;   // (a group votes through its exchange)
         const int a_start = (iter % 2) == 0;
         Tree& A = c->tree[a_start ? 0 : 1];
         Tree& Bt = c->tree[a_start ? 1 : 0];
@@ -783,6 +862,72 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
 
         const int64_t sg = (iter == 0) ? sg_edge : -1;   // start / goal ride along
         c->stats.samples += B;
+        if (grouped) {
+            // ---- rank group: the speculative front on my slice, ONE all-gather of
+            // sample records, every rank appends the same nodes, one host round trip
+            const int seq = ++c->seq;
+            const int64_t slot = (int64_t)GREC * per + 1;
+            hipLaunchKernelGGL(k_ext_conn_nn, dim3(blocks_for(per, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
+                               Bt.q.p, TB, p.seed, g0 + (uint64_t)rank * (uint64_t)per, per, bd, p.range,
+                               p.resolution, cmax, a_start, c->efrom.p, c->eto.p, c->nd.p, c->valid.p, c->gfail.p,
+                               c->near_.p, c->yv.p, c->mv.p);
+            HIP_TRY(hipGetLastError());
+            if (packed(per * G))
+                launch_edges_packed(c, c->efrom.p, c->eto.p, c->nd.p, per * G, kmax, 2, c->valid.p, G, c->gfail.p,
+                                    c->stream, nullptr, 1);
+            else
+                launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, per * G, kmax, 2, c->valid.p, G, c->gfail.p,
+                             c->stream);
+            // without a transport (world 1) the records go straight to the gathered buffer
+            int32_t* own = c->transport == TR_NONE ? c->g_recv.p : c->g_send.p;
+            hipLaunchKernelGGL(k_group_pack, dim3(blocks_for(per, 256)), dim3(256), 0, c->stream,
+                               (const int*)c->gfail.p, (const int32_t*)c->near_.p, (const int32_t*)c->yv.p,
+                               (const int32_t*)c->mv.p, per, tflag, own);
+            HIP_TRY(hipGetLastError());
+            if (c->transport != TR_NONE) group_exchange(c, slot);
+            GroupRecs gr{c->g_recv.p, per, world};
+            if (B <= FUSE_MAX) {
+#define RP_GROUP_SMALL(IT)                                                                                          \
+    hipLaunchKernelGGL(k_group_accept_small<IT>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, gr, B, p.seed, g0, bd,  \
+                       p.range, cmax, A.q.p, A.par.p, A.cand.p, TA, Bt.q.p, Bt.par.p, Bt.cand.p, TB, a_start,      \
+                       c->chain_end.p, status, pa, io)
+                if (B <= FUSE_THREADS) RP_GROUP_SMALL(1);
+                else RP_GROUP_SMALL(4);
+#undef RP_GROUP_SMALL
+            } else {
+                hipLaunchKernelGGL(k_group_counts, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, gr, B,
+                                   c->g_cnt.p, status);
+                scan_incl_u64(c, c->g_cnt.p, c->g_incl.p, B);
+                hipLaunchKernelGGL(k_group_append, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, gr,
+                                   (const unsigned long long*)c->g_incl.p, B, p.seed, g0, bd, p.range, cmax, A.q.p,
+                                   A.par.p, A.cand.p, TA, Bt.q.p, Bt.par.p, Bt.cand.p, TB, a_start, c->chain_end.p,
+                                   status);
+                hipLaunchKernelGGL(k_group_finalize, dim3(1), dim3(256), 0, c->stream,
+                                   (const unsigned long long*)c->g_incl.p, B, status, TA, a_start,
+                                   (const int32_t*)A.par.p, (const int32_t*)Bt.par.p, (const int32_t*)c->chain_end.p,
+                                   pa, io);
+            }
+            HIP_TRY(hipGetLastError());
+            run_program(0, tail_steps, seq, true);
+            wait_seq(c, seq);
+            if (c->transport == TR_RCCL) {
+                float ms = 0.0f;
+                if (hipEventElapsedTime(&ms, c->gx0, c->gx1) == hipSuccess) c->stats.exchange_ms += ms;
+            }
+            const int* st = h->status;
+            if (st[ST_STOP]) break;   // some rank timed out: all leave at this iteration
+            A.n = TA + st[ST_NACC];
+            Bt.n = TB + st[ST_ADDED];
+            c->stats.edges_checked += per * G;
+            if (st[ST_FIRST] != INT_MAX) {
+                solved = 1;
+                s_node = st[ST_SNODE];
+                g_node = st[ST_GNODE];
+                ++iter;
+                break;
+            }
+            continue;
+        }
         if (speculate && B <= FUSE_MAX) {
             // ---- single rank, speculative: one NN kernel (both trees), one edge
             // launch, one accept kernel, the first simplification steps (no-ops
@@ -824,7 +969,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             continue;
         }
 
-        // ---- extension: my slice of the samples
+        // ---- single rank, two-phase (large batches, or RBE_PLAN_SPECULATE=0)
         hipLaunchKernelGGL(k_ext_nn, dim3(blocks_for(per, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA, p.seed,
                            g0, (int64_t)rank * per, per, bd, p.range, p.resolution, a_start, c->efrom.p, c->eto.p,
                            c->nd.p, c->valid.p, c->near_.p);
@@ -833,9 +978,9 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                      1, nullptr, c->stream);
         c->stats.edges_checked += per;
 
-        if (world == 1) {
-            // ---- single rank, two-phase: device-side counts, one host round trip
-            // per iteration; batches <= FUSE_MAX use the single-block accept kernels
+        {
+            // device-side counts, one host round trip per iteration; batches
+            // <= FUSE_MAX use the single-block accept kernels
             const bool fused = B <= FUSE_MAX;
             const int seq = ++c->seq;
             if (fused) {
@@ -906,76 +1051,6 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             continue;
         }
 
-        // ---- rank group: host-visible counts (the exchange is a host callback)
-        hipLaunchKernelGGL(k_ext_result, dim3(blocks_for(per, 256)), dim3(256), 0, c->stream, c->valid.p,
-                           c->near_.p, per, c->mine.p);
-        HIP_TRY(hipMemcpyAsync(c->mine.p + per, &tflag, sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
-        exchange(c, c->mine.p, sizeof(int32_t) * (per + 1));
-        HIP_TRY(hipMemsetAsync(c->scalar.p, 0, sizeof(int), c->stream));
-        hipLaunchKernelGGL(k_ext_unpack, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream,
-                           (const int32_t*)c->g_recv, per, world, c->res.p, c->scalar.p);
-        HIP_TRY(hipGetLastError());
-        if (read_scalar(c, c->scalar.p)) break;  // some rank timed out
-        hipLaunchKernelGGL(k_flag, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->res.p, B, c->acc.p);
-        scan_incl(c, c->acc.p, c->incl.p, B);
-        hipLaunchKernelGGL(k_ext_append, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->res.p, c->incl.p, B,
-                           p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA, (int*)nullptr,
-                           (const uint8_t*)nullptr, (int64_t)-1, 1);
-        HIP_TRY(hipGetLastError());
-        const int32_t nacc = read_scalar(c, c->incl.p + (B - 1));
-        A.n = TA + nacc;
-        if (nacc == 0) continue;
-
-        const int64_t pt = (nacc + world - 1) / world;
-        const int64_t t0 = (int64_t)rank * pt;
-        const int64_t nmine = std::max<int64_t>(0, std::min<int64_t>(pt, nacc - t0));
-        if (nmine > 0) {
-            hipLaunchKernelGGL(k_conn_nn, dim3(blocks_for(nmine, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
-                               t0, nmine, Bt.q.p, TB, p.range, p.resolution, cmax, a_start, c->efrom.p, c->eto.p,
-                               c->nd.p, c->valid.p, c->gfail.p, c->yv.p, c->mv.p, (const int*)nullptr);
-            HIP_TRY(hipGetLastError());
-            if (packed(nmine * cmax))
-                launch_edges_packed(c, c->efrom.p, c->eto.p, c->nd.p, nmine * cmax, kmax, a_start ? 1 : 0,
-                                    c->valid.p, cmax, c->gfail.p, c->stream, nullptr, 1);
-            else
-                launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, nmine * cmax, kmax, a_start ? 1 : 0, c->valid.p,
-                             cmax, c->gfail.p, c->stream);
-        }
-        hipLaunchKernelGGL(k_conn_record, dim3(blocks_for(pt, 256)), dim3(256), 0, c->stream, c->yv.p, c->mv.p,
-                           c->gfail.p, nmine, pt, c->rec.p);
-        HIP_TRY(hipGetLastError());
-        exchange(c, c->rec.p, sizeof(int32_t) * 2 * pt);
-        const int32_t* rec = (const int32_t*)c->g_recv;
-        hipLaunchKernelGGL(k_conn_len, dim3(blocks_for(nacc, 256)), dim3(256), 0, c->stream, rec, (int64_t)nacc,
-                           c->Lv.p);
-        scan_incl(c, c->Lv.p, c->incl.p, nacc);
-        const int big = INT_MAX;
-        HIP_TRY(hipMemcpyAsync(c->scalar.p, &big, sizeof(int), hipMemcpyHostToDevice, c->stream));
-        hipLaunchKernelGGL(k_conn_append, dim3(blocks_for(nacc, 256)), dim3(256), 0, c->stream, rec, c->incl.p,
-                           (int64_t)nacc, A.q.p, TA, Bt.q.p, Bt.par.p, Bt.cand.p, TB, p.range, cmax, a_start,
-                           A.cand.p, c->scalar.p, c->chain_end.p, (const int*)nullptr, (const double*)nullptr,
-                           (const int32_t*)nullptr);
-        HIP_TRY(hipGetLastError());
-        int32_t hdr[2];
-        HIP_TRY(hipMemcpyAsync(&hdr[0], c->incl.p + (nacc - 1), sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipMemcpyAsync(&hdr[1], c->scalar.p, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        c->stats.edges_checked += nmine * cmax;
-        Bt.n = TB + hdr[0];
-        const int fr = hdr[1];
-        if (fr != INT_MAX) {
-            solved = 1;
-            const int32_t end = read_scalar(c, c->chain_end.p + fr);
-            if (a_start) {
-                s_node = read_scalar(c, A.par.p + (TA + fr));
-                g_node = end;
-            } else {
-                s_node = read_scalar(c, Bt.par.p + end);
-                g_node = (int32_t)(TA + fr);
-            }
-            ++iter;
-            break;
-        }
     }
     if (!sg_known) {   // the loop ran no iteration
         if (const int code = check_endpoints_now()) return endpoint_fail(code);
@@ -1011,7 +1086,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     // the rest of the simplification program on the device (a solving single-rank
     // iteration has run its first steps); the output record lands in the host mirror
     const double t_simp = now_s();
-    const bool tail_ran = world == 1 && solved;
+    const bool tail_ran = solved;   // the solving iteration's last kernel built the path
     if (!tail_ran) {
         hipLaunchKernelGGL(k_path, dim3(1), dim3(64), 0, c->stream, pa, s_node, g_node, io);
         HIP_TRY(hipGetLastError());
@@ -1368,10 +1443,9 @@ int rp_check_edges_device(rp_ctx* c, const double* qa, const double* qb, int64_t
     hipLaunchKernelGGL(k_edge_prep, dim3(blocks_for(n, 256)), dim3(256), 0, s, qa, qb, n, res, c->end_nd.p, out,
                        c->scalar.p);
     HIP_TRY(hipGetLastError());
-    int kmax = 0;
-    HIP_TRY(hipMemcpyAsync(&kmax, c->scalar.p, sizeof(int), hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
-    launch_edges(c, qa, qb, c->end_nd.p, n, kmax, 0, out, 1, nullptr, s);
+    // fully asynchronous: the slot count (the longest edge's) stays on the device and
+    // a fixed grid strides over n x kmax (no host read-back, no stream wait)
+    launch_edges(c, qa, qb, c->end_nd.p, n, 16, 0, out, 1, nullptr, s, nullptr, 1, 8192, c->scalar.p);
     return RP_OK;
     RP_GUARD_END(c)
 }
@@ -1410,18 +1484,50 @@ int rp_plan(rp_ctx* c, const double start[RP_NQ], const double goal[RP_NQ], cons
     RP_GUARD_END(c)
 }
 
-int rp_group_init(rp_ctx* c, int32_t rank, int32_t world, void* send, void* recv, int64_t cap, rp_allgather_fn fn,
-                  void* user) {
-    if (!c || world < 1 || rank < 0 || rank >= world) return RP_ERR_ARG;
-    if (world > 1 && (!send || !recv || cap <= 0 || !fn)) return RP_ERR_ARG;
+int rp_group_init(rp_ctx* c, int32_t rank, int32_t world, rp_allgather_fn fn, void* user) {
+    if (!c || world < 1 || rank < 0 || rank >= world || (world > 1 && !fn)) return RP_ERR_ARG;
+    RP_GUARD_BEGIN
+    HIP_TRY(hipSetDevice(c->device));
+    c->leave_group();
+    if (fn) {
+        c->rank = rank;
+        c->world = world;
+        c->transport = TR_HOST;
+        c->g_fn = fn;
+        c->g_user = user;
+    }
+    return RP_OK;
+    RP_GUARD_END(c)
+}
+
+int rp_group_rccl_unique_id(uint8_t out[RP_RCCL_ID_BYTES]) {
+    if (!out) return RP_ERR_ARG;
+    static_assert(sizeof(ncclUniqueId) == RP_RCCL_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId id;
+    const ncclResult_t r = ncclGetUniqueId(&id);
+    if (r != ncclSuccess) {
+        g_create_error = std::string("ncclGetUniqueId failed: ") + ncclGetErrorString(r);
+        return RP_ERR_EXCHANGE;
+    }
+    std::memcpy(out, &id, sizeof id);
+    return RP_OK;
+}
+
+int rp_group_init_rccl(rp_ctx* c, int32_t rank, int32_t world, const uint8_t id[RP_RCCL_ID_BYTES]) {
+    if (!c || !id || world < 1 || rank < 0 || rank >= world) return RP_ERR_ARG;
+    RP_GUARD_BEGIN
+    HIP_TRY(hipSetDevice(c->device));
+    c->leave_group();
+    ncclUniqueId uid;
+    std::memcpy(&uid, id, sizeof uid);
+    NCCL_TRY(ncclCommInitRank(&c->comm, world, uid, rank));   // collective: every rank calls it
+    if (!c->gx0) HIP_TRY(hipEventCreate(&c->gx0));
+    if (!c->gx1) HIP_TRY(hipEventCreate(&c->gx1));
     c->rank = rank;
     c->world = world;
-    c->g_send = send;
-    c->g_recv = recv;
-    c->g_cap = cap;
-    c->g_fn = fn;
-    c->g_user = user;
+    c->transport = TR_RCCL;
     return RP_OK;
+    RP_GUARD_END(c)
 }
 
 int rp_get_stats(rp_ctx* c, rp_stats* out) {

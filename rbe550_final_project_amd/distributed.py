@@ -1,43 +1,48 @@
-"""Rank group for the data-parallel planner: one process per GPU, torch.distributed
-over RCCL (backend "nccl") on xGMI.
+"""Rank group for the data-parallel planner: one process per GPU.
 
-Each RRT-Connect iteration shards its samples (and then its connect targets) across
-the ranks; the per-sample results — one int32 (nearest node or -1) per sample, two
-int32 (nearest node, valid steps) per connect target — are all-gathered so every
-rank appends the same nodes in global sample order and the replicated trees stay
-bit-identical. Messages are small (4 B per sample): the exchange
-is latency-bound, one all-gather per phase.
+Each RRT-Connect iteration shards its samples across the ranks (rank r takes
+samples [r * B/world, (r + 1) * B/world) of the global Philox stream); every rank
+runs nearest-node search, steering, the extension edge and the connect chain of
+its slice on its GPU, then ONE all-gather per iteration exchanges a 12-byte record
+per sample (accepted extension's nearest node or -1, the other tree's nearest node,
+valid chain steps | reached) so every rank appends the same nodes in global sample
+order: the replicated trees stay bit-identical and the plan equals the world-1
+plan (DESIGN.md §4 "Multi-GPU").
+
+Transports (inside librbe_mi355x.so):
+  rccl  ncclAllGather on the planner's stream over xGMI; the group's id is made by
+        rank 0 and broadcast with torch.distributed (backend "nccl" = RCCL).
+  host  the records pass through pinned host buffers and a torch.distributed
+        all-gather on CPU tensors (backend "gloo"): ranks sharing one GPU, CPU
+        rehearsals.
 """
 import torch
 import torch.distributed as dist
 
+from . import native
+
 
 class Group:
-    def __init__(self, ctx, batch, device):
+    def __init__(self, ctx, transport=None):
         self.rank = dist.get_rank()
         self.world = dist.get_world_size()
-        per = (batch + self.world - 1) // self.world
-        self.cap = 8 * (per + 4)
-        dev = torch.device("cuda", device)
-        self.send = torch.zeros(self.cap, dtype=torch.uint8, device=dev)
-        self.recv = torch.zeros(self.cap * self.world, dtype=torch.uint8, device=dev)
+        if transport is None:
+            transport = "rccl" if dist.get_backend() == "nccl" else "host"
+        if transport not in ("rccl", "host"):
+            raise ValueError(f"unknown transport {transport!r}")
+        self.transport = transport
         self.calls = 0
-
-        staged = dist.get_backend() != "nccl"   # gloo: exchange through host memory
-
-        def allgather(nbytes):
-            self.calls += 1
-            if staged:
-                out = torch.empty(nbytes * self.world, dtype=torch.uint8)
-                dist.all_gather_into_tensor(out, self.send[:nbytes].cpu())
-                self.recv[: nbytes * self.world].copy_(out)
-            else:
-                dist.all_gather_into_tensor(self.recv[: nbytes * self.world], self.send[:nbytes])
-            torch.cuda.synchronize(dev)
-
-        ctx.group_init(self.rank, self.world, self.send.data_ptr(), self.recv.data_ptr(), self.cap, allgather)
         self.ctx = ctx
+        if transport == "rccl":
+            obj = [native.rccl_unique_id() if self.rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            ctx.group_init_rccl(self.rank, self.world, obj[0])
+        else:
+            def allgather(send, recv):
+                self.calls += 1
+                dist.all_gather_into_tensor(torch.from_numpy(recv), torch.from_numpy(send))
+            ctx.group_init(self.rank, self.world, allgather)
 
     def leave(self):
         """Back to single-rank planning on this context."""
-        self.ctx.group_init(0, 1, 0, 0, 0, None)
+        self.ctx.group_leave()

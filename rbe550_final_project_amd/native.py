@@ -18,10 +18,12 @@ LIB_PATH = os.path.join(_HERE, LIB_NAME)
 # every symbol include/rbe_planner.h declares
 EXPORTS = ("rp_version", "rp_default_robot", "rp_create", "rp_destroy", "rp_set_scene", "rp_set_attached",
            "rp_check_states", "rp_check_states_device", "rp_check_edges", "rp_check_edges_device",
-           "rp_state_contacts", "rp_plan", "rp_group_init", "rp_get_stats", "rp_last_error",
-           "rp_last_kernel_ms", "rp_selftest_f64", "rp_ik")
+           "rp_state_contacts", "rp_plan", "rp_group_init", "rp_group_rccl_unique_id", "rp_group_init_rccl",
+           "rp_get_stats", "rp_last_error", "rp_last_kernel_ms", "rp_selftest_f64", "rp_ik")
 
-ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64)
+# rp_allgather_fn(user, send, recv, bytes_per_rank): library-owned pinned host buffers
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64)
+RCCL_ID_BYTES = 128
 
 _lib = None
 
@@ -53,7 +55,9 @@ def load():
     L.rp_check_edges_device.argtypes = [vp, vp, vp, i64, f64, vp, vp]
     L.rp_state_contacts.argtypes = [vp, vp, vp, i32]
     L.rp_plan.argtypes = [vp, vp, vp, vp, vp, C.POINTER(_abi.PlanParams), vp, i32, C.POINTER(i32), C.POINTER(i32)]
-    L.rp_group_init.argtypes = [vp, i32, i32, vp, vp, i64, vp, vp]
+    L.rp_group_init.argtypes = [vp, i32, i32, vp, vp]
+    L.rp_group_rccl_unique_id.argtypes = [vp]
+    L.rp_group_init_rccl.argtypes = [vp, i32, i32, vp]
     L.rp_get_stats.argtypes = [vp, C.POINTER(_abi.Stats)]
     L.rp_last_error.argtypes = [vp]
     L.rp_last_error.restype = C.c_char_p
@@ -66,6 +70,15 @@ def load():
 
 def _ptr(a):
     return a.ctypes.data_as(C.c_void_p)
+
+
+def rccl_unique_id():
+    """ncclGetUniqueId (rank 0 of an RCCL rank group; broadcast it to the others)."""
+    buf = (C.c_uint8 * RCCL_ID_BYTES)()
+    rc = load().rp_group_rccl_unique_id(buf)
+    if rc != 0:
+        raise NativeError(f"rp_group_rccl_unique_id failed ({rc}): {load().rp_last_error(None).decode()}")
+    return bytes(buf)
 
 
 def default_robot():
@@ -188,22 +201,35 @@ class Context:
         return st.as_dict()
 
     # -- rank group ----------------------------------------------------------
-    def group_init(self, rank, world, send_ptr, recv_ptr, cap_bytes, allgather):
-        """allgather(bytes_per_rank) -> None; gathers send[:bytes] of every rank into recv.
-        world == 1 (allgather None) returns the context to single-rank planning."""
-        if allgather is None:
-            self._cb = None
-            self._check(load().rp_group_init(self._h, 0, 1, None, None, 0, None, None), "rp_group_init")
-            return
+    def group_init(self, rank, world, allgather):
+        """Host transport: allgather(send, recv) gathers the uint8 array `send` of
+        every rank into `recv` (rank-major, world * len(send) bytes); both are numpy
+        views of library-owned pinned host buffers, valid during the call."""
+        if allgather is None or world == 1:
+            return self.group_leave()
 
-        def _cb(_user, nbytes):
+        def _cb(_user, send_p, recv_p, nbytes):
             try:
-                allgather(int(nbytes))
+                n = int(nbytes)
+                send = np.ctypeslib.as_array((C.c_uint8 * n).from_address(send_p))
+                recv = np.ctypeslib.as_array((C.c_uint8 * (n * int(world))).from_address(recv_p))
+                allgather(send, recv)
                 return 0
             except Exception:  # never let a Python exception cross into C
                 import traceback
                 traceback.print_exc()
                 return 1
         self._cb = ALLGATHER_FN(_cb)
-        self._check(load().rp_group_init(self._h, int(rank), int(world), C.c_void_p(send_ptr), C.c_void_p(recv_ptr),
-                                         int(cap_bytes), C.cast(self._cb, C.c_void_p), None), "rp_group_init")
+        self._check(load().rp_group_init(self._h, int(rank), int(world), C.cast(self._cb, C.c_void_p), None),
+                    "rp_group_init")
+
+    def group_init_rccl(self, rank, world, unique_id):
+        """RCCL transport (ncclAllGather on the context stream); collective over the
+        group, ranks on distinct GPUs. unique_id: rccl_unique_id() of rank 0."""
+        uid = (C.c_uint8 * RCCL_ID_BYTES).from_buffer_copy(bytes(unique_id))
+        self._check(load().rp_group_init_rccl(self._h, int(rank), int(world), uid), "rp_group_init_rccl")
+
+    def group_leave(self):
+        """Back to single-rank planning."""
+        self._check(load().rp_group_init(self._h, 0, 1, None, None), "rp_group_init")
+        self._cb = None

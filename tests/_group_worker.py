@@ -1,0 +1,59 @@
+"""One rank of tests/test_gpu_group_procs.py: a fresh process with torch.distributed
+(gloo) and the product rank group (distributed.Group, host transport) on GPU 0,
+shared with the other rank. Plans the cases, then rank 0 leaves the group and
+plans them again at world 1. Writes <out>.<rank>.npz."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from rbe550_final_project_amd import _abi, model, scenes  # noqa: E402
+from rbe550_final_project_amd.distributed import Group  # noqa: E402
+from rbe550_final_project_amd.native import Context  # noqa: E402
+
+
+def main():
+    rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
+    cases = json.loads(sys.argv[5])
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ctx = Context(device=0, robot=model.robot_desc())
+    grp = Group(ctx)
+    assert grp.transport == "host"
+    res = {}
+
+    def run(tag):
+        for c in cases:
+            q = json.load(open(os.path.join(ROOT, "tests", "golden", "workloads", c["workload"] + ".json")))
+            q = q["queries"][c["query"]]
+            sc = scenes.Scene.from_json(q["scene"])
+            ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+            ctx.set_attached(q["attached"])
+            p = _abi.make_params(seed=c["seed"], batch=c["batch"], batch_min=c.get("batch_min", 0), n_waypoints=150,
+                                 timeout_s=3600.0, straight_first=False, tree_capacity=1 << 23,
+                                 max_iters=c.get("max_iters", 0))
+            path, st = ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+            s = ctx.stats()
+            res[f"{tag}/{c['name']}/path"] = path
+            res[f"{tag}/{c['name']}/info"] = np.array([st, s["iterations"], s["start_tree_size"], s["goal_tree_size"]])
+
+    run("group")
+    calls = grp.calls
+    dist.barrier()
+    if rank == 0:
+        grp.leave()
+        run("single")
+    res["calls"] = np.array([calls])
+    np.savez(f"{out}.{rank}.npz", **res)
+    ctx.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

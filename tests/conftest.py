@@ -11,6 +11,15 @@ for p in (ROOT, os.path.join(ROOT, "tools")):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU; calls the HIP library")
+    config.addinivalue_line("markers", "spawns_gpu_procs: starts GPU processes; runs before this process "
+                                       "touches the GPU")
+
+
+def pytest_collection_modifyitems(config, items):
+    """Tests that start GPU processes run first: no process is ever started from a
+    pytest process that has already initialised the GPU."""
+    first = [i for i in items if i.get_closest_marker("spawns_gpu_procs")]
+    items[:] = first + [i for i in items if not i.get_closest_marker("spawns_gpu_procs")]
 
 
 @pytest.fixture(scope="session")

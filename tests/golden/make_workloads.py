@@ -208,10 +208,63 @@ def workload_clutter():
     return {"name": "clutter64", "config": 4, "queries": w.queries}
 
 
+def _well(cx, cy, half_in, z_top, t=0.01):
+    """4 walls (half thickness t) around a square opening of half width half_in."""
+    h = z_top / 2
+    return [((cx + half_in + t, cy, h), (t, half_in + 2 * t, h), 0.0),
+            ((cx - half_in - t, cy, h), (t, half_in + 2 * t, h), 0.0),
+            ((cx, cy + half_in + t, h), (half_in, t, h), 0.0),
+            ((cx, cy - half_in - t, h), (half_in, t, h), 0.0)]
+
+
+def _roof(cx, cy, half_in, z, hole, t=0.01):
+    """4 plates covering the well's square top except a centred square hole."""
+    a, c = (half_in + hole) / 2, (half_in - hole) / 2
+    return [((cx + a, cy, z), (c, half_in, t), 0.0), ((cx - a, cy, z), (c, half_in, t), 0.0),
+            ((cx, cy + a, z), (hole, c, t), 0.0), ((cx, cy - a, z), (hole, c, t), 0.0)]
+
+
+WELL = {"center": (0.55, 0.0), "half": 0.13, "wall_top": 0.225, "roof_z": 0.235, "hole": 0.078, "hand_z": 0.20}
+
+
+def workload_clutter_well():
+    """C5, hard: the goal puts the hand into a covered well (8 boxes: 4 walls + a
+    roof with a 15.6 cm square hole, the wrist just above it), the remaining 56 of
+    the 64 boxes are clutter64 boxes away from the well; start = the clutter64
+    start. Only a narrow threading motion through the hole reaches the goal, so
+    RRT-Connect at 131,072-sample iterations grows trees of ~10^5 nodes over
+    several iterations (tests/test_gpu_configs.py, bench.py C5)."""
+    start = model.SAFE_HOME.copy()
+    start[0] = 1.0
+    start[7:] = 0.039
+    w = World(scenes.Scene(), model.SAFE_HOME)
+    cx, cy = WELL["center"]
+    goal = w.ik(np.array([cx, cy, WELL["hand_z"]]), GRASP_QUAT, OPEN)
+    fixed = _well(cx, cy, WELL["half"], WELL["wall_top"]) + _roof(cx, cy, WELL["half"], WELL["roof_z"], WELL["hole"])
+    orc = OracleScene()
+
+    def keep(box):
+        c = box[0]
+        if abs(c[0] - cx) < 0.25 and abs(c[1] - cy) < 0.25:
+            return False
+        orc.set_scene([box])
+        return bool(orc.check_states(np.stack([start, goal]).astype(np.float32)).all())
+
+    sc = scenes.clutter64(seed=0x64B1, n=64 - len(fixed), keep_clear=keep)
+    for i, b in enumerate(fixed):
+        sc.boxes.append(b)
+        sc.names.append(f"well{i}")
+        sc.entity_idx.append(len(sc.names))
+    w = World(sc, start)
+    w.query("clutter: into the covered well", goal)
+    return {"name": "clutter64_well", "config": 4, "queries": w.queries}
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     only = set(sys.argv[1:])
-    for fn in (workload_goal1, workload_single, workload_goal3, workload_goal4, workload_clutter):
+    for fn in (workload_goal1, workload_single, workload_goal3, workload_goal4, workload_clutter,
+               workload_clutter_well):
         if only and fn.__name__ not in only:
             continue
         wl = fn()

@@ -1,0 +1,83 @@
+"""GPU plans at the BASELINE configs' own batch sizes, bit for bit against the
+oracle's golden plans (tests/golden/plans_configured.npz, made by
+tests/golden/make_plan_fixtures.py):
+
+  C2  65,536-sample iterations (single pick -> place, 5 boxes)
+  C4  262,144-sample iterations (pentagon, yawed boxes)
+  C5  131,072-sample iterations: clutter64, and the covered-well query whose
+      trees reach 10^5 - 3 x 10^5 nodes over 3 - 8 iterations (nearest-node
+      search over large trees; seed 0 spends the whole 2^20-sample budget and
+      returns the APPROXIMATE path)
+
+each through the single-rank iteration (two-phase at these sizes), the
+one-exchange group iteration at world 1 (RBE_PLAN_GROUPED=1), and the RCCL
+transport at world 1 (ncclAllGather on the planner stream). Tolerance in the
+tests: 1e-5 rad (north_star); the measured difference is 0."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from rbe550_final_project_amd import _abi, model, native, scenes
+from rbe550_final_project_amd.native import Context
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+FIX = np.load(os.path.join(GOLD, "plans_configured.npz"))
+META = json.loads(str(FIX["meta"]))
+TOL = 1e-5
+
+
+def _case(name):
+    m = META[name]
+    q = json.load(open(os.path.join(GOLD, "workloads", m["workload"] + ".json")))["queries"][m["query"]]
+    p = _abi.make_params(seed=m["seed"], batch=m["batch"], batch_min=m["batch"], n_waypoints=150, timeout_s=3600.0,
+                         straight_first=False, tree_capacity=1 << 23, max_iters=m["max_iters"])
+    return m, q, p
+
+
+def _check(ctx, name):
+    m, q, p = _case(name)
+    sc = scenes.Scene.from_json(q["scene"])
+    ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+    ctx.set_attached(q["attached"])
+    path, st = ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+    s = ctx.stats()
+    ref = FIX[name]
+    assert st == m["status"], (name, st, m["status"])
+    assert s["iterations"] == m["iterations"], (name, s["iterations"], m)
+    assert (s["start_tree_size"], s["goal_tree_size"]) == (m["start_tree"], m["goal_tree"]), (name, s, m)
+    assert path.shape == ref.shape == (150, 9)
+    assert np.max(np.abs(path - ref)) <= TOL
+    assert np.array_equal(path, ref)
+    return s
+
+
+@pytest.mark.parametrize("name", sorted(META))
+def test_configured_batch_plan_equals_oracle(gpu_ctx, name):
+    s = _check(gpu_ctx, name)
+    assert s["samples"] == META[name]["iterations"] * META[name]["batch"]
+
+
+@pytest.mark.parametrize("name", ["C2_q0_s0", "C4_q0", "C5_clutter64", "C5_well_s4", "C5_well_s0"])
+def test_configured_batch_group_iteration_world1(gpu_ctx, name, monkeypatch):
+    """The rank-group iteration (speculative front + record exchange + multi-block
+    accept) at world 1 without a transport: same plans."""
+    monkeypatch.setenv("RBE_PLAN_GROUPED", "1")
+    _check(gpu_ctx, name)
+
+
+@pytest.mark.parametrize("name", ["C2_q1_s1", "C5_well_s4"])
+def test_rccl_transport_world1(name):
+    """The RCCL transport end to end on one GPU (a 1-rank communicator: the
+    records go through ncclAllGather on the planner stream)."""
+    ctx = Context(device=0, robot=model.robot_desc())
+    try:
+        ctx.group_init_rccl(0, 1, native.rccl_unique_id())
+        s = _check(ctx, name)
+        assert s["exchange_ms"] > 0.0
+        ctx.group_leave()
+        _check(ctx, name)
+    finally:
+        ctx.close()

@@ -135,6 +135,7 @@ struct rp_ctx {
     DevBuf<SimpState> simp;              // device path simplification state
     PlanIO* h_io = nullptr;              // its pinned host mirror
     int seq = 0;                         // last publication number awaited on h_io
+    double watchdog_s = 120.0;           // wait_seq gives up on a stream busy this long
     DevBuf<DI> partial;
 
     // rank group (DESIGN.md §4 "Multi-GPU"): one all-gather of sample records per
@@ -252,6 +253,25 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
     HIP_TRY(hipGetLastError());
 }
 
+// Diagnostic (RBE_DEBUG_SYNC=1): wait for the stream after a launch, at most 10 s,
+// and name the launch that did not finish.
+void debug_wait(rp_ctx* c, const char* label) {
+    static const bool on = std::getenv("RBE_DEBUG_SYNC") != nullptr;
+    if (!on) return;
+    const double t0 = now_s();
+    for (;;) {
+        const hipError_t e = hipStreamQuery(c->stream);
+        if (e == hipSuccess) break;
+        if (e != hipErrorNotReady) HIP_TRY(e);
+        if (now_s() - t0 > 10.0) {
+            fprintf(stderr, "[rbe debug] stream stuck after %s\n", label);
+            fflush(stderr);
+            throw HipError{std::string("stream stuck after ") + label};
+        }
+    }
+    fprintf(stderr, "[rbe debug] ok %s (%.3f ms)\n", label, 1e3 * (now_s() - t0));
+}
+
 // Work-compacted edge check (rp_kernels.h k_edges_packed) for large launches:
 // slot counts, their scan, then a fixed grid striding over the real items.
 void launch_edges_packed(rp_ctx* c, const double* from, const double* to, const int* nd, int64_t n, int kmax,
@@ -275,10 +295,13 @@ void launch_edges_packed(rp_ctx* c, const double* from, const double* to, const 
     c->eincl.ensure(n);
     hipLaunchKernelGGL(k_edge_slots, dim3(blocks_for(n, 256)), dim3(256), 0, s, nd, n, dcount, per_item, c->eslot.p);
     HIP_TRY(hipGetLastError());
+    debug_wait(c, "k_edge_slots");
     scan_incl(c, c->eslot.p, c->eincl.p, n);
+    debug_wait(c, "slot scan");
     c->echunk.ensure(blocks_for(n * (int64_t)kmax, VBLOCK) + 1);
     hipLaunchKernelGGL(k_chunk_first, dim3(blocks_for(n, 256)), dim3(256), 0, s, (const int32_t*)c->eincl.p, n,
                        c->echunk.p);
+    debug_wait(c, "k_chunk_first");
     const dim3 g(std::min<unsigned>(blocks_for(n * (int64_t)kmax, VBLOCK), 8192u)), b(VBLOCK);
 #define RP_EDGESP(N) hipLaunchKernelGGL(k_edges_packed<N>, g, b, 0, s, from, to, nd, n, mode, valid, group, gfail, \
                                         c->counter.p, c->d_scene, (const int32_t*)c->eincl.p,   \
@@ -565,6 +588,7 @@ bool out_of_bounds(const double* q, const double* lo, const double* hi) {
 // or finished-without-publishing stream turns into an error instead of a hang.
 void wait_seq(rp_ctx* c, int seq) {
     const volatile int* f = &c->h_io->seq;
+    double t0 = -1.0;
     for (uint64_t spin = 1;; ++spin) {
         if (*f == seq) break;
         if ((spin & 4095) == 0) {
@@ -574,6 +598,15 @@ void wait_seq(rp_ctx* c, int seq) {
                 throw HipError{"plan status was not published"};
             }
             if (e != hipErrorNotReady) HIP_TRY(e);
+            // watchdog: a stream that stays busy this long is reported, not waited on
+            const double now = now_s();
+            if (t0 < 0) t0 = now;
+            if (now - t0 > c->watchdog_s) {
+                char b[256];
+                snprintf(b, sizeof b, "plan stream still busy after %.0f s (awaiting status %d, mirror at %d)",
+                         now - t0, seq, *f);
+                throw HipError{b};
+            }
         }
 #if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
         __builtin_ia32_pause();
@@ -601,6 +634,10 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     for (int i = 0; i < NQ; ++i) ext2 += (hi[i] - lo[i]) * (hi[i] - lo[i]);
     const double max_extent = std::sqrt(ext2);
     rp_plan_params p = *pp;
+    // wait watchdog: well past any iteration (RBE_WAIT_WATCHDOG_S overrides)
+    c->watchdog_s = 120.0;
+    if (const char* e = std::getenv("RBE_WAIT_WATCHDOG_S"))
+        if (*e) c->watchdog_s = std::max(1.0, std::atof(e));
     if (p.batch <= 0) p.batch = 4096;
     if (p.range <= 0) p.range = 0.2 * max_extent;
     if (p.resolution <= 0) p.resolution = 0.01 * max_extent;
@@ -651,7 +688,9 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     c->rec.ensure(2 * (BMAX + world));
     c->Lv.ensure(BMAX);
     c->chain_end.ensure(BMAX);
-    c->gfail.ensure(std::max<int64_t>(BMAX, FUSE_MAX + 2));
+    // + 2: k_plan_init marks the start / goal edges' groups at batch_min and
+    // batch_min + 1 (two-phase: batch_min = BMAX at the configured sizes)
+    c->gfail.ensure(std::max<int64_t>(BMAX, FUSE_MAX) + 2);
     c->mine.ensure(PMAX + 1);
     if (grouped) {
         c->g_send.ensure((size_t)GREC * PMAX + 1);
@@ -970,12 +1009,15 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         }
 
         // ---- single rank, two-phase (large batches, or RBE_PLAN_SPECULATE=0)
+        debug_wait(c, "iteration start");
         hipLaunchKernelGGL(k_ext_nn, dim3(blocks_for(per, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA, p.seed,
                            g0, (int64_t)rank * per, per, bd, p.range, p.resolution, a_start, c->efrom.p, c->eto.p,
                            c->nd.p, c->valid.p, c->near_.p);
         HIP_TRY(hipGetLastError());
+        debug_wait(c, "k_ext_nn");
         launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, per + (sg >= 0 ? 2 : 0), kmax, a_start ? 0 : 1, c->valid.p,
                      1, nullptr, c->stream);
+        debug_wait(c, "ext edges");
         c->stats.edges_checked += per;
 
         {
@@ -1000,16 +1042,19 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                                    c->incl.p, B, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA, status,
                                    (const uint8_t*)c->valid.p, sg, sg_stride);
             }
+            debug_wait(c, "ext accept");
             hipLaunchKernelGGL(k_conn_nn, dim3(blocks_for(B, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
                                (int64_t)0, B, Bt.q.p, TB, p.range, p.resolution, cmax, a_start, c->efrom.p,
                                c->eto.p, c->nd.p, c->valid.p, c->gfail.p, c->yv.p, c->mv.p, (const int*)status);
             HIP_TRY(hipGetLastError());
+            debug_wait(c, "k_conn_nn");
             if (packed(B * cmax))
                 launch_edges_packed(c, c->efrom.p, c->eto.p, c->nd.p, B * cmax, kmax, a_start ? 1 : 0, c->valid.p,
                                     cmax, c->gfail.p, c->stream, status, cmax);
             else
                 launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, B * cmax, kmax, a_start ? 1 : 0, c->valid.p, cmax,
                              c->gfail.p, c->stream, status, cmax);
+            debug_wait(c, "conn edges");
             if (fused) {
 #define RP_CONN_SMALL(IT)                                                                                        \
     hipLaunchKernelGGL(k_conn_accept_small<IT>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, c->yv.p, c->mv.p,      \

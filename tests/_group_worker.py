@@ -2,9 +2,11 @@
 (gloo) and the product rank group (distributed.Group, host transport) on GPU 0,
 shared with the other rank. Plans the cases, then rank 0 leaves the group and
 plans them again at world 1. Writes <out>.<rank>.npz."""
+import faulthandler
 import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -20,10 +22,26 @@ from rbe550_final_project_amd.native import Context  # noqa: E402
 def main():
     rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
     cases = json.loads(sys.argv[5])
+    # progress lines (on the GPU box: under gpurun_out/, which its hang detector watches)
+    logdir = os.path.join(os.environ["GRAFT_REPO_ROOT"], "gpurun_out") if os.environ.get("GRAFT_REPO_ROOT") else None
+    logf = open(os.path.join(logdir, f"group_worker.{rank}.log"), "a") if logdir and os.path.isdir(logdir) else None
+
+    t0 = time.time()
+
+    def log(msg):
+        line = f"[rank {rank} {time.time() - t0:7.2f}s] {msg}"
+        print(line, flush=True)
+        if logf:
+            logf.write(line + "\n")
+            logf.flush()
+    faulthandler.dump_traceback_later(150, exit=True)
+    log("start")
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    log("process group up")
     ctx = Context(device=0, robot=model.robot_desc())
     grp = Group(ctx)
+    log("rank group up")
     assert grp.transport == "host"
     res = {}
 
@@ -37,22 +55,37 @@ def main():
             p = _abi.make_params(seed=c["seed"], batch=c["batch"], batch_min=c.get("batch_min", 0), n_waypoints=150,
                                  timeout_s=3600.0, straight_first=False, tree_capacity=1 << 23,
                                  max_iters=c.get("max_iters", 0))
+            log(f"{tag} {c['name']} ...")
             path, st = ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
             s = ctx.stats()
+            log(f"{tag} {c['name']} status {st} iterations {s['iterations']} trees {s['start_tree_size']} "
+                f"{s['goal_tree_size']} {s['total_ms']:.1f} ms (exchange {s['exchange_ms']:.1f} ms)")
             res[f"{tag}/{c['name']}/path"] = path
             res[f"{tag}/{c['name']}/info"] = np.array([st, s["iterations"], s["start_tree_size"], s["goal_tree_size"]])
 
+    order = os.environ.get("RBE_WORKER_ORDER", "group_first")
+    if order == "single_first" and rank == 0:
+        grp.leave()
+        run("single")
+        grp = Group(ctx)
+    dist.barrier()
     run("group")
     calls = grp.calls
     dist.barrier()
-    if rank == 0:
+    if rank == 0 and order != "single_first":
         grp.leave()
         run("single")
     res["calls"] = np.array([calls])
     np.savez(f"{out}.{rank}.npz", **res)
+    if os.environ.get("RBE_WORKER_KEEP"):
+        log("final barrier (context kept)")
+        dist.barrier()
+    log("closing")
     ctx.close()
+    log("closed, final barrier")
     dist.barrier()
     dist.destroy_process_group()
+    log("end")
 
 
 if __name__ == "__main__":

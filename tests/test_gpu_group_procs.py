@@ -44,13 +44,15 @@ def _free_port():
 def test_two_process_group_plans_equal_world1_and_oracle(tmp_path, oracle_lib):
     out = str(tmp_path / "res")
     port = str(_free_port())
+    env = dict(os.environ, RBE_WAIT_WATCHDOG_S="30")
     procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "_group_worker.py"), str(r), "2", port, out,
-                               json.dumps(CASES)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+                               json.dumps(CASES)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                              env=env)
              for r in range(2)]
     logs = []
     for pr in procs:
         try:
-            logs.append(pr.communicate(timeout=420)[0])
+            logs.append(pr.communicate(timeout=160)[0])
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()

@@ -16,7 +16,8 @@ step() {  # step <name> <timeout_s> <cmd...>
 }
 for s in "$@"; do
   case $s in
-    tests) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    tests) step pytest_gpu 1000 python -u -m pytest tests -m gpu -x -v --timeout 500 --timeout-method thread ;;
+    gtests) step pytest_gpu_cfg 600 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_group.py -m gpu -x -v --timeout 300 --timeout-method thread && step pytest_gpu_procs 600 python -u -m pytest tests/test_gpu_group_procs.py -m gpu -x -v --timeout 170 --timeout-method thread ;;
     alltests) step pytest_all 1200 python -m pytest tests -q -x ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;

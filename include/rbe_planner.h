@@ -155,6 +155,19 @@ typedef struct rp_stats {
                                    transport: the callback)                          */
 } rp_stats;
 
+/* Kernel profile of the last rp_plan (rp_set_profiling on): HIP events around every
+ * nearest-node launch and every edge-validity launch, on the planner stream. The
+ * work counts are algorithmic: nn_pairs = (query, tree node) distance evaluations;
+ * edge_states = validity evaluations executed by the edge launches. */
+typedef struct rp_profile {
+    int64_t nn_launches;
+    double nn_ms;
+    double nn_pairs;
+    int64_t edge_launches;
+    double edge_ms;
+    int64_t edge_states;
+} rp_profile;
+
 typedef struct rp_ctx rp_ctx;
 
 /* Host-transport all-gather used by a rank group (rp_group_init): gather
@@ -258,6 +271,11 @@ int rp_group_rccl_unique_id(uint8_t id_out[RP_RCCL_ID_BYTES]);
 int rp_group_init_rccl(rp_ctx* ctx, int32_t rank, int32_t world, const uint8_t id[RP_RCCL_ID_BYTES]);
 
 int rp_get_stats(rp_ctx* ctx, rp_stats* out);
+
+/* Per-kernel-class timing of rp_plan (measurement runs; off by default: the events
+ * cost a few microseconds per iteration). rp_get_profile returns the last plan's. */
+int rp_set_profiling(rp_ctx* ctx, int32_t on);
+int rp_get_profile(rp_ctx* ctx, rp_profile* out);
 
 /* Last error text for this context (or for a failed rp_create when ctx is NULL). */
 const char* rp_last_error(rp_ctx* ctx);

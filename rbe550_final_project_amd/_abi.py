@@ -70,6 +70,14 @@ class Stats(C.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class Profile(C.Structure):
+    _fields_ = [("nn_launches", C.c_int64), ("nn_ms", C.c_double), ("nn_pairs", C.c_double),
+                ("edge_launches", C.c_int64), ("edge_ms", C.c_double), ("edge_states", C.c_int64)]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
 def make_boxes(boxes):
     """boxes: iterable of (center(3), half(3), yaw) -> ctypes array."""
     boxes = list(boxes)

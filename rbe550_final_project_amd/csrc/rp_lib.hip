@@ -134,6 +134,13 @@ struct rp_ctx {
     DevBuf<PlanIO> io;                   // iteration status + output record (rp_kernels.h)
     DevBuf<SimpState> simp;              // device path simplification state
     PlanIO* h_io = nullptr;              // its pinned host mirror
+    // kernel profile (rp_set_profiling): event pairs around NN and edge launches
+    bool profiling = false;
+    bool in_plan = false;
+    rp_profile prof{};
+    std::vector<hipEvent_t> pev;         // pool: pev[2i], pev[2i+1] = launch i
+    std::vector<int> pkind;              // launch i: 0 = NN, 1 = edges
+    size_t pused = 0;
     int seq = 0;                         // last publication number awaited on h_io
     double watchdog_s = 120.0;           // wait_seq gives up on a stream busy this long
     DevBuf<DI> partial;
@@ -181,6 +188,7 @@ struct rp_ctx {
         cub_tmp.release(); path.release(); io.release(); simp.release(); partial.release();
         g_send.release(); g_recv.release(); g_cnt.release(); g_incl.release();
         leave_group();
+        for (hipEvent_t e : pev) (void)hipEventDestroy(e);
         if (gx0) (void)hipEventDestroy(gx0);
         if (gx1) (void)hipEventDestroy(gx1);
         if (h_io) (void)hipHostFree(h_io);
@@ -196,6 +204,39 @@ namespace {
 // ---------------------------------------------------------------------------
 // launch helpers
 // ---------------------------------------------------------------------------
+
+// kernel profile: record a start event (returns the launch slot, -1 when off), then
+// the end event with the launch's class; summed after the plan's last wait
+int prof_begin(rp_ctx* c, hipStream_t s) {
+    if (!c->profiling || !c->in_plan) return -1;
+    const size_t i = c->pused++;
+    if (2 * i + 2 > c->pev.size()) {
+        for (int k = 0; k < 2; ++k) {
+            hipEvent_t e;
+            HIP_TRY(hipEventCreate(&e));
+            c->pev.push_back(e);
+        }
+        c->pkind.push_back(0);
+    }
+    HIP_TRY(hipEventRecord(c->pev[2 * i], s));
+    return (int)i;
+}
+void prof_end(rp_ctx* c, int slot, int kind, hipStream_t s) {
+    if (slot < 0) return;
+    HIP_TRY(hipEventRecord(c->pev[2 * slot + 1], s));
+    c->pkind[slot] = kind;
+    if (kind == 0) ++c->prof.nn_launches;
+    else ++c->prof.edge_launches;
+}
+void prof_collect(rp_ctx* c) {
+    for (size_t i = 0; i < c->pused; ++i) {
+        HIP_TRY(hipEventSynchronize(c->pev[2 * i + 1]));
+        float ms = 0.0f;
+        HIP_TRY(hipEventElapsedTime(&ms, c->pev[2 * i], c->pev[2 * i + 1]));
+        (c->pkind[i] == 0 ? c->prof.nn_ms : c->prof.edge_ms) += ms;
+    }
+    c->pused = 0;
+}
 
 // kernel instantiation: axis grid, or the cluster count (cluster AABBs in registers)
 int ncl_bucket(const DevScene& sc) {
@@ -239,6 +280,7 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
     unsigned nb = blocks_for(threads, VBLOCK);
     if (max_blocks && nb > max_blocks) nb = max_blocks;   // grid-stride (gated launches)
     const dim3 g(nb), b(VBLOCK);
+    const int ps = prof_begin(c, s);
 #define RP_EDGES(N) hipLaunchKernelGGL(k_edges<N>, g, b, 0, s, from, to, nd, n, kmax, mode, valid, group, gfail, \
                                        c->counter.p, c->d_scene, dcount, per_item, dkmax)
     switch (ncl_bucket(c->scene)) {
@@ -251,6 +293,7 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
     }
 #undef RP_EDGES
     HIP_TRY(hipGetLastError());
+    prof_end(c, ps, 1, s);
 }
 
 // Diagnostic (RBE_DEBUG_SYNC=1): wait for the stream after a launch, at most 10 s,
@@ -291,6 +334,7 @@ void launch_edges_packed(rp_ctx* c, const double* from, const double* to, const 
                          int mode, uint8_t* valid, int group, int* gfail, hipStream_t s, const int* dcount,
                          int per_item) {
     if (n <= 0) return;
+    const int ps = prof_begin(c, s);   // (slot counts + scan + chunk map + the check)
     c->eslot.ensure(n);
     c->eincl.ensure(n);
     hipLaunchKernelGGL(k_edge_slots, dim3(blocks_for(n, 256)), dim3(256), 0, s, nd, n, dcount, per_item, c->eslot.p);
@@ -316,6 +360,7 @@ void launch_edges_packed(rp_ctx* c, const double* from, const double* to, const 
     }
 #undef RP_EDGESP
     HIP_TRY(hipGetLastError());
+    prof_end(c, ps, 1, s);
 }
 
 template <typename T>
@@ -906,11 +951,14 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             // sample records, every rank appends the same nodes, one host round trip
             const int seq = ++c->seq;
             const int64_t slot = (int64_t)GREC * per + 1;
+            const int pn = prof_begin(c, c->stream);
             hipLaunchKernelGGL(k_ext_conn_nn, dim3(blocks_for(per, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
                                Bt.q.p, TB, p.seed, g0 + (uint64_t)rank * (uint64_t)per, per, bd, p.range,
                                p.resolution, cmax, a_start, c->efrom.p, c->eto.p, c->nd.p, c->valid.p, c->gfail.p,
                                c->near_.p, c->yv.p, c->mv.p);
             HIP_TRY(hipGetLastError());
+            prof_end(c, pn, 0, c->stream);
+            c->prof.nn_pairs += (double)per * (double)(TA + TB);
             if (packed(per * G))
                 launch_edges_packed(c, c->efrom.p, c->eto.p, c->nd.p, per * G, kmax, 2, c->valid.p, G, c->gfail.p,
                                     c->stream, nullptr, 1);
@@ -972,10 +1020,13 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             // launch, one accept kernel, the first simplification steps (no-ops
             // until a path exists), one host round trip
             const int seq = ++c->seq;
+            const int pn = prof_begin(c, c->stream);
             hipLaunchKernelGGL(k_ext_conn_nn, dim3(blocks_for(B, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
                                Bt.q.p, TB, p.seed, g0, B, bd, p.range, p.resolution, cmax, a_start, c->efrom.p,
                                c->eto.p, c->nd.p, c->valid.p, c->gfail.p, c->near_.p, c->yv.p, c->mv.p);
             HIP_TRY(hipGetLastError());
+            prof_end(c, pn, 0, c->stream);
+            c->prof.nn_pairs += (double)B * (double)(TA + TB);
             launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, (B + (sg >= 0 ? 2 : 0)) * G, kmax, 2, c->valid.p, G,
                          c->gfail.p, c->stream);
 #define RP_ITER_SMALL(IT)                                                                                           \
@@ -1010,10 +1061,13 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
 
         // ---- single rank, two-phase (large batches, or RBE_PLAN_SPECULATE=0)
         debug_wait(c, "iteration start");
+        const int pn1 = prof_begin(c, c->stream);
         hipLaunchKernelGGL(k_ext_nn, dim3(blocks_for(per, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA, p.seed,
                            g0, (int64_t)rank * per, per, bd, p.range, p.resolution, a_start, c->efrom.p, c->eto.p,
                            c->nd.p, c->valid.p, c->near_.p);
         HIP_TRY(hipGetLastError());
+        prof_end(c, pn1, 0, c->stream);
+        c->prof.nn_pairs += (double)per * (double)TA;
         debug_wait(c, "k_ext_nn");
         launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, per + (sg >= 0 ? 2 : 0), kmax, a_start ? 0 : 1, c->valid.p,
                      1, nullptr, c->stream);
@@ -1043,10 +1097,12 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                                    (const uint8_t*)c->valid.p, sg, sg_stride);
             }
             debug_wait(c, "ext accept");
+            const int pn2 = prof_begin(c, c->stream);
             hipLaunchKernelGGL(k_conn_nn, dim3(blocks_for(B, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
                                (int64_t)0, B, Bt.q.p, TB, p.range, p.resolution, cmax, a_start, c->efrom.p,
                                c->eto.p, c->nd.p, c->valid.p, c->gfail.p, c->yv.p, c->mv.p, (const int*)status);
             HIP_TRY(hipGetLastError());
+            prof_end(c, pn2, 0, c->stream);
             debug_wait(c, "k_conn_nn");
             if (packed(B * cmax))
                 launch_edges_packed(c, c->efrom.p, c->eto.p, c->nd.p, B * cmax, kmax, a_start ? 1 : 0, c->valid.p,
@@ -1086,6 +1142,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             A.n = TA + st[ST_NACC];
             Bt.n = TB + st[ST_ADDED];
             c->stats.edges_checked += (int64_t)st[ST_NACC] * cmax;
+            c->prof.nn_pairs += (double)st[ST_NACC] * (double)TB;   // k_conn_nn: accepted targets x tree B
             if (st[ST_FIRST] != INT_MAX) {
                 solved = 1;
                 s_node = st[ST_SNODE];
@@ -1525,8 +1582,36 @@ int rp_plan(rp_ctx* c, const double start[RP_NQ], const double goal[RP_NQ], cons
         return RP_ERR_ARG;
     RP_GUARD_BEGIN
     HIP_TRY(hipSetDevice(c->device));
-    return plan_impl(c, start, goal, lo, hi, params, path_out, path_cap, n_out, status_out);
+    c->prof = rp_profile{};
+    c->pused = 0;
+    c->in_plan = true;
+    int rc;
+    try {
+        rc = plan_impl(c, start, goal, lo, hi, params, path_out, path_cap, n_out, status_out);
+    } catch (...) {
+        c->in_plan = false;
+        c->pused = 0;
+        throw;
+    }
+    c->in_plan = false;
+    if (c->profiling) {
+        prof_collect(c);
+        c->prof.edge_states = c->stats.states_checked;
+    }
+    return rc;
     RP_GUARD_END(c)
+}
+
+int rp_set_profiling(rp_ctx* c, int32_t on) {
+    if (!c) return RP_ERR_ARG;
+    c->profiling = on != 0;
+    return RP_OK;
+}
+
+int rp_get_profile(rp_ctx* c, rp_profile* out) {
+    if (!c || !out) return RP_ERR_ARG;
+    *out = c->prof;
+    return RP_OK;
 }
 
 int rp_group_init(rp_ctx* c, int32_t rank, int32_t world, rp_allgather_fn fn, void* user) {

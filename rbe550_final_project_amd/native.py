@@ -19,7 +19,8 @@ LIB_PATH = os.path.join(_HERE, LIB_NAME)
 EXPORTS = ("rp_version", "rp_default_robot", "rp_create", "rp_destroy", "rp_set_scene", "rp_set_attached",
            "rp_check_states", "rp_check_states_device", "rp_check_edges", "rp_check_edges_device",
            "rp_state_contacts", "rp_plan", "rp_group_init", "rp_group_rccl_unique_id", "rp_group_init_rccl",
-           "rp_get_stats", "rp_last_error", "rp_last_kernel_ms", "rp_selftest_f64", "rp_ik")
+           "rp_get_stats", "rp_last_error", "rp_last_kernel_ms", "rp_selftest_f64", "rp_ik", "rp_set_profiling",
+           "rp_get_profile")
 
 # rp_allgather_fn(user, send, recv, bytes_per_rank): library-owned pinned host buffers
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64)
@@ -59,6 +60,8 @@ def load():
     L.rp_group_rccl_unique_id.argtypes = [vp]
     L.rp_group_init_rccl.argtypes = [vp, i32, i32, vp]
     L.rp_get_stats.argtypes = [vp, C.POINTER(_abi.Stats)]
+    L.rp_set_profiling.argtypes = [vp, i32]
+    L.rp_get_profile.argtypes = [vp, C.POINTER(_abi.Profile)]
     L.rp_last_error.argtypes = [vp]
     L.rp_last_error.restype = C.c_char_p
     L.rp_last_kernel_ms.argtypes = [vp, C.POINTER(f64)]
@@ -194,6 +197,15 @@ class Context:
         self._check(load().rp_ik(self._h, n, _ptr(pos), _ptr(quat), _ptr(init), _ptr(lo), _ptr(hi), C.byref(p),
                                  _ptr(q), _ptr(st)), "rp_ik")
         return q, st
+
+    def set_profiling(self, on=True):
+        self._check(load().rp_set_profiling(self._h, 1 if on else 0), "rp_set_profiling")
+
+    def profile(self):
+        """Kernel-class timing of the last plan (rp_get_profile)."""
+        pr = _abi.Profile()
+        self._check(load().rp_get_profile(self._h, C.byref(pr)), "rp_get_profile")
+        return pr.as_dict()
 
     def stats(self):
         st = _abi.Stats()

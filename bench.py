@@ -30,22 +30,41 @@ from rbe550_final_project_amd import _abi, model, scenes  # noqa: E402
 from rbe550_final_project_amd.native import Context  # noqa: E402
 
 METRIC = "states-checked/sec + plan wall-time, 7-DOF arm/10 blocks, 1/2/4/8 GPU"
-VALU_PEAK_TFLOPS = 157.3     # MI355X FP32 vector peak (MI355X_MICROARCH.md chip table)
-HBM_PEAK_GBPS = 8000.0       # spec
-BYTES_PER_STATE = 9 * 4 + 1  # 9 x fp32 in, 1 B flag out
+ROOF = json.load(open(os.path.join(ROOT, "bench", "roofline.json")))   # frozen constants
+VALU_PEAK_TFLOPS = ROOF["peaks"]["fp32_vector_tflops"]
+FP64_PEAK_TFLOPS = ROOF["peaks"]["fp64_vector_tflops"]
+HBM_PEAK_GBPS = ROOF["peaks"]["hbm_gbps"]
+BYTES_PER_STATE = ROOF["state_check"]["bytes"]     # 9 x fp32 in, 1 B flag out
+BYTES_PER_EDGE = ROOF["edge_check"]["bytes"]
+NN_FLOP_PER_PAIR = ROOF["nearest_node"]["flop"]
 C2_BATCH = 65536             # BASELINE C2: 64k-sample batch
 C4_BATCH = 262144            # BASELINE C4: 256k-sample iterations
 C5_BATCH = 131072            # BASELINE C5: 131,072-sample iterations (2^20 budget)
 
 
 def flops_per_state(n_boxes):
-    """Algorithmic FP32 work of one full (collision-free) state check in
-    rp_math.h, counted from the source: FK 818 (7 x [sincos 26 +
-    Rz 18], 10 frame shifts x 6, hand Rz 18, 24 capsule endpoints x 18); capsule
-    AABBs + plane 12 x 13 = 156; box broad phase 6 compares per capsule-box pair;
-    self broad phase 6 compares x 35 pairs = 210. Narrow phases (only for
-    overlapping AABBs) are not counted."""
-    return 818 + 156 + 72 * n_boxes + 210
+    """Algorithmic FP32 work of one full (collision-free) state check, from
+    bench/roofline.json (counted from rp_math.h)."""
+    f = ROOF["state_check"]["flop"]
+    return f["fk"] + f["capsule_aabb_and_plane"] + f["box_broad_phase_per_box"] * n_boxes + f["self_broad_phase"]
+
+
+def host_info():
+    """The host the CPU baseline ran on: the threads it may use and the machine."""
+    model_name = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model_name = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count()
+    return {"nproc": os.cpu_count(), "affinity": affinity, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "cpu_model": model_name}
 
 
 def load_workload(name):
@@ -63,12 +82,16 @@ def pmc_traffic(n_states):
         d = json.load(open(path))
         if int(d.get("states_per_launch", -1)) != int(n_states):
             return None
+        from rbe550_final_project_amd.build import validity_source_hash
+        if d.get("source_hash") != validity_source_hash():
+            return None   # measured on another build of k_validity: stale
         return float(d["hbm_bytes_per_launch"])
     except Exception:
         return None
 
 
-def run_plans(ctx, wl, batch, seed, group, batch_min=0, tree_capacity=0, stats_out=None, straight_first=True):
+def run_plans(ctx, wl, batch, seed, group, batch_min=0, tree_capacity=0, stats_out=None, straight_first=True,
+              max_iters=0):
     """Wall time of every query of a workload (ms), plus aggregate states checked.
     straight_first=False forces RRT-Connect on every query (the product default
     first checks the straight edge start -> goal)."""
@@ -78,7 +101,7 @@ def run_plans(ctx, wl, batch, seed, group, batch_min=0, tree_capacity=0, stats_o
         ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
         ctx.set_attached(q["attached"])
         p = _abi.make_params(seed=seed + i, batch=batch, batch_min=batch_min, n_waypoints=150, timeout_s=10.0,
-                             tree_capacity=tree_capacity, straight_first=straight_first)
+                             tree_capacity=tree_capacity, straight_first=straight_first, max_iters=max_iters)
         if group is not None:
             dist.barrier()
         t0 = time.perf_counter()
@@ -159,19 +182,68 @@ def cpu_baseline(scene, n_states, threads, chunk=1 << 24):
     return n_states / dt, dt
 
 
-def cpu_plan_baseline(wl, seed, straight_first=True):
+def cpu_plan_baseline(wl, seed, straight_first=True, timeout_s=10.0, batch=1):
+    """The reference's CPU planner class: RRT-Connect one sample at a time (OMPL's
+    loop, batch 1) in the CPU oracle on one core, per query, with the reference's
+    per-query budget (motion_primitives.py:144: timeout=10.0)."""
     from oracle.oracle import OracleScene
     o = OracleScene()
-    times = []
+    times, statuses = [], []
     for i, q in enumerate(wl["queries"]):
         sc = scenes.Scene.from_json(q["scene"])
         o.set_scene(sc.boxes, sc.plane_z, sc.base)
         o.set_attached(q["attached"])
-        p = _abi.make_params(seed=seed + i, batch=1, n_waypoints=150, timeout_s=10.0, straight_first=straight_first)
+        p = _abi.make_params(seed=seed + i, batch=batch, n_waypoints=150, timeout_s=timeout_s,
+                             straight_first=straight_first)
         t0 = time.perf_counter()
-        o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+        _, st, _ = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
         times.append(1e3 * (time.perf_counter() - t0))
-    return times
+        statuses.append(st)
+    return times, statuses
+
+
+def cpu_plan_record(times, statuses, sample):
+    return {"queries": len(times), "total_ms": round(sum(times), 3), "median_ms": round(float(np.median(times)), 3),
+            "max_ms": round(float(np.max(times)), 3),
+            "exact": int(sum(s == _abi.STATUS_EXACT for s in statuses)),
+            "approximate": int(sum(s == _abi.STATUS_APPROXIMATE for s in statuses)), "sample": sample}
+
+
+def well_profile(ctx, seeds=(2, 3, 4, 0)):
+    """C5 covered-well plans (131,072-sample iterations, up to the 2^20 budget) with
+    the kernel-class profile on: the nearest-node and edge-launch rooflines on trees
+    of 10^5 - 3 x 10^5 nodes (rp_get_profile: HIP events on the planner stream)."""
+    wl = load_workload("clutter64_well")
+    q = wl["queries"][0]
+    sc = scenes.Scene.from_json(q["scene"])
+    ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+    ctx.set_attached(q["attached"])
+    ctx.set_profiling(True)
+    tot = {"nn_ms": 0.0, "nn_pairs": 0.0, "edge_ms": 0.0, "edge_states": 0, "nn_launches": 0, "edge_launches": 0}
+    try:
+        for seed in seeds:
+            p = _abi.make_params(seed=seed, batch=C5_BATCH, batch_min=C5_BATCH, n_waypoints=150, timeout_s=60.0,
+                                 straight_first=False, tree_capacity=1 << 23, max_iters=8)
+            ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+            pr = ctx.profile()
+            for k in tot:
+                tot[k] += pr[k]
+    finally:
+        ctx.set_profiling(False)
+    nn_tf = tot["nn_pairs"] * NN_FLOP_PER_PAIR / (tot["nn_ms"] * 1e-3) / 1e12
+    fps = flops_per_state(len(sc.boxes))
+    ed_tf = tot["edge_states"] * fps / (tot["edge_ms"] * 1e-3) / 1e12
+    sample = f"C5 covered-well plans, seeds {list(seeds)}, 131,072-sample iterations (trees up to 3.3e5 nodes)"
+    return ({"bound": "fp64", "achieved": round(nn_tf, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+             "frac": round(nn_tf / FP64_PEAK_TFLOPS, 4), "kernel": "k_ext_nn/k_conn_nn/k_ext_conn_nn",
+             "launches": tot["nn_launches"], "kernel_ms": round(tot["nn_ms"], 3), "pairs": tot["nn_pairs"],
+             "flop_per_pair": NN_FLOP_PER_PAIR, "sample": sample},
+            {"bound": "valu", "achieved": round(ed_tf, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+             "frac": round(ed_tf / VALU_PEAK_TFLOPS, 4), "kernel": "k_edges/k_edges_packed",
+             "launches": tot["edge_launches"], "kernel_ms": round(tot["edge_ms"], 3),
+             "states": int(tot["edge_states"]),
+             "states_per_sec": round(tot["edge_states"] / (tot["edge_ms"] * 1e-3), 1),
+             "flop_per_state": fps, "sample": sample})
 
 
 def main():
@@ -305,19 +377,43 @@ def main():
                                          {"mode": "RRT-Connect forced (straight_first off)"})
         except Exception as ex:  # report, keep the primary metric
             plan = {"error": repr(ex)[:300]}
-        for key, wname, batch, cap in (("C4_pentagon", "goal4_pentagon_10box", C4_BATCH, 1 << 24),
-                                       ("C5_clutter64", "clutter64", C5_BATCH, 1 << 23)):
+        # configured-batch workloads: C4 (262,144-sample iterations) and C5
+        # (131,072-sample iterations: clutter64, and the covered well, whose trees
+        # grow to 10^5 - 3 x 10^5 nodes over up to 8 iterations = the 2^20 budget);
+        # "_sched": the product's batch schedule (256 samples first, doubling to the
+        # configured batch) on the same queries
+        well = load_workload("clutter64_well")
+        wellx = {"queries": well["queries"] * 4}
+        for key, wl_c, batch, bmin, seeds_from, max_iters in (
+                ("C4_pentagon", load_workload("goal4_pentagon_10box"), C4_BATCH, C4_BATCH, 0, 0),
+                ("C4_pentagon_sched", load_workload("goal4_pentagon_10box"), C4_BATCH, 0, 0, 0),
+                ("C5_clutter64", load_workload("clutter64"), C5_BATCH, C5_BATCH, 0, 0),
+                ("C5_well", wellx, C5_BATCH, C5_BATCH, 1, 8),
+                ("C5_well_sched", wellx, C5_BATCH, 0, 1, 8)):
             try:
                 extra = {}
-                t4, s4, st4 = run_plans(ctx, load_workload(wname), batch, 0, group, batch_min=batch,
-                                        tree_capacity=cap, stats_out=extra, straight_first=False)
+                tq, sq, stq = run_plans(ctx, wl_c, batch, seeds_from, group, batch_min=bmin, tree_capacity=1 << 23,
+                                        stats_out=extra, straight_first=False, max_iters=max_iters)
                 it = max(1, int(extra.get("iterations", 0)))
-                extra = {"mode": "RRT-Connect forced (straight_first off)", "batch_min": batch, "exchange_ms": round(extra.get("exchange_ms", 0.0), 3),
+                extra = {"mode": "RRT-Connect forced (straight_first off)", "batch_min": bmin or 256,
+                         "exchange_ms": round(extra.get("exchange_ms", 0.0), 3),
                          "exchange_ms_per_iteration": round(extra.get("exchange_ms", 0.0) / it, 4),
-                         "iterations": int(extra.get("iterations", 0)), "samples": int(extra.get("samples", 0))}
-                plan[key] = plan_record(t4, s4, st4, batch, dev, distributed, extra)
+                         "iterations": int(extra.get("iterations", 0)), "samples": int(extra.get("samples", 0)),
+                         "max_iters": max_iters or None}
+                plan[key] = plan_record(tq, sq, stq, batch, dev, distributed, extra)
             except Exception as ex:
                 plan[key] = {"error": repr(ex)[:300]}
+
+    # ---- nearest-node and edge-launch rooflines on large trees (this rank, no group)
+    rooflines_plan = None
+    if not args.no_plan and rank == 0 and not distributed:
+        try:
+            nn_roof, edge_roof = well_profile(ctx)
+            rooflines_plan = {"nearest_node": nn_roof, "edges": edge_roof}
+        except Exception as ex:
+            rooflines_plan = {"error": repr(ex)[:300]}
+    ctx.set_scene(scene.boxes, scene.plane_z, scene.base)
+    ctx.set_attached(-1)
 
     flop = flops_per_state(len(scene.boxes))
     achieved_tflops = n * flop / (kernel_ms * 1e-3) / 1e12
@@ -333,23 +429,38 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         try:
-            threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+            hi = host_info()
+            # the box's CPU share for one GPU is OMP_NUM_THREADS (16 on the GPU pool);
+            # the whole machine's count is recorded beside it (host.nproc)
+            threads = args.cpu_threads or int(hi["omp_num_threads"] or 0) or (hi["affinity"] or 1)
             sample = 1 << 27   # ~8-10 s of oracle work on 16 cores
             rate, dt = cpu_baseline(scene, sample, threads)
-            ptimes = cpu_plan_baseline(wl, 0)
-            rtimes = cpu_plan_baseline(wl, 0, straight_first=False)
-            wl1 = load_workload("goal1_scattered_6box")
-            g1 = cpu_plan_baseline(wl1, 0)
-            g1r = cpu_plan_baseline(wl1, 0, straight_first=False)
+            rate1, dt1 = cpu_baseline(scene, 1 << 22, 1)      # one core: the per-core rate
             cpu = {"value": round(rate, 1), "unit": "states/s", "cores": threads, "kind": "port",
                    "sample": f"{sample} uniform states, goal3 10-box scene, OpenMP CPU oracle ({dt:.1f} s)",
-                   "plan_total_ms": round(sum(ptimes), 3), "plan_median_ms": round(float(np.median(ptimes)), 3),
-                   "plan_sample": "21 goal3 queries, straight edge first then sequential RRT-Connect (batch 1), 1 core",
-                   "plan_rrt_total_ms": round(sum(rtimes), 3), "plan_rrt_median_ms": round(float(np.median(rtimes)), 3),
-                   "C1_goal1": {"queries": len(g1), "total_ms": round(sum(g1), 3),
-                                "median_ms": round(float(np.median(g1)), 3),
-                                "rrt_total_ms": round(sum(g1r), 3), "rrt_median_ms": round(float(np.median(g1r)), 3),
-                                "sample": "goal1_scattered 12 queries (BASELINE configs[0]), CPU oracle, 1 core"}}
+                   "per_core": round(rate1, 1), "per_core_sample": f"{1 << 22} states on 1 thread ({dt1:.1f} s)",
+                   "host": hi}
+            # plan wall-time of the reference's CPU planner class (sequential
+            # RRT-Connect, batch 1, one core, 10 s budget per query)
+            plans = {}
+            for key, wname, sf, reps in (("C1_goal1", "goal1_scattered_6box", True, 1),
+                                         ("C1_goal1_rrt", "goal1_scattered_6box", False, 1),
+                                         ("C3", "goal3_tallest_10box", True, 1),
+                                         ("C3_rrt", "goal3_tallest_10box", False, 1),
+                                         ("C2_rrt", "single_pick_place_5box", False, 10),
+                                         ("C4_rrt", "goal4_pentagon_10box", False, 1),
+                                         ("C5_clutter64_rrt", "clutter64", False, 1),
+                                         ("C5_well_rrt", "clutter64_well", False, 1)):
+                w = load_workload(wname)
+                w = {"queries": w["queries"] * reps}
+                t, stc = cpu_plan_baseline(w, 0, straight_first=sf)
+                plans[key] = cpu_plan_record(t, stc, f"{wname}: {'straight edge first, then ' if sf else ''}"
+                                                     "sequential RRT-Connect (batch 1), CPU oracle, 1 core, "
+                                                     "10 s budget per query")
+            cpu["plans"] = plans
+            # legacy keys (round 1 records)
+            cpu["plan_total_ms"], cpu["plan_median_ms"] = plans["C3"]["total_ms"], plans["C3"]["median_ms"]
+            cpu["plan_rrt_total_ms"], cpu["plan_rrt_median_ms"] = plans["C3_rrt"]["total_ms"], plans["C3_rrt"]["median_ms"]
         except Exception as ex:
             cpu = {"error": repr(ex)[:300]}
 
@@ -362,7 +473,8 @@ def main():
                "config": {"workload": "C3 goal3_tallest 10-block scene: validity batch per GPU + 21-query plan",
                           "states_per_gpu": n, "global_batch": n * world, "parallelism": f"dp{world}",
                           "valid_fraction": round(valid_frac, 4)},
-               "plan_wall": plan, "per_config": per_config, "roofline": roofline, "cpu_baseline": cpu}
+               "plan_wall": plan, "per_config": per_config, "roofline": roofline,
+               "rooflines_plan": rooflines_plan, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
     ctx.close()
     if distributed:

@@ -30,6 +30,18 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp
 LIBS = ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
 
 
+def validity_source_hash():
+    """Hash of what k_validity's machine code is made from (rp_math.h, rp_model.h,
+    the compiler flags): PMC measurements of that kernel (profiles/pmc_validity.json)
+    carry it, and bench.py uses them only while it still matches."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in ("rp_math.h", "rp_model.h"):
+        h.update(open(os.path.join(_HERE, "csrc", f), "rb").read())
+    h.update(" ".join(FLAGS).encode())
+    return h.hexdigest()[:16]
+
+
 def hipcc():
     for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
         if c and (os.path.exists(c) or c == "hipcc"):

@@ -10,7 +10,9 @@ import json
 import sys
 
 sys.path.insert(0, __file__.rsplit("/", 1)[0])
+sys.path.insert(0, __file__.rsplit("/", 2)[0])
 from pmc_summary import load  # noqa: E402
+from rbe550_final_project_amd.build import validity_source_hash  # noqa: E402
 
 
 def main():
@@ -23,7 +25,7 @@ def main():
          "write_size_kb": w["WRITE_SIZE"], "read_bytes_per_launch": read_b, "write_bytes_per_launch": write_b,
          "hbm_bytes_per_launch": read_b + write_b, "algorithmic_bytes_per_launch": 37 * n,
          "correction": "read = 2 x FETCH_SIZE (gfx950 half-count of wide streaming reads), write = WRITE_SIZE",
-         "dispatch_meta": meta}
+         "dispatch_meta": meta, "source_hash": validity_source_hash()}
     json.dump(d, open(out, "w"), indent=1)
     print(json.dumps(d, indent=1))
 

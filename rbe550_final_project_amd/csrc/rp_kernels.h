@@ -432,6 +432,125 @@ __global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_straight(Endpoints ep
     }
 }
 
+// validity of n states, GL lanes per state (small batches: the start / goal checks,
+// diagnostics, small API calls)
+template <int GL, bool BF>
+__global__ __launch_bounds__(64) void k_validity_ml(const float* __restrict__ q, int64_t n,
+                                                   uint8_t* __restrict__ flags, const DevScene* __restrict__ sc) {
+    constexpr int SPW = 64 / GL;
+    __shared__ CapsLds caps[SPW];
+    const int64_t i = (int64_t)blockIdx.x * SPW + threadIdx.x / GL;
+    const bool run = i < n;
+    float qq[NQ];
+    const float* src = q + (run ? i : 0) * NQ;
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) qq[k] = src[k];
+    const bool col = state_collides_ml<GL, BF>(qq, run, sc, caps);
+    if (run && (threadIdx.x & (GL - 1)) == 0) flags[i] = col ? 0 : 1;
+}
+
+// ---- low-latency variants (rp_math.h state_collides_ml): GL lanes per state, for
+// launches that cannot fill the chip; same flags, same counters (one per state).
+template <int GL, bool BF>
+__global__ __launch_bounds__(64) void k_straight_ml(Endpoints ep, double res, const DevScene* __restrict__ sc,
+                                                   unsigned* sync, PlanIO* hio, int seq) {
+    constexpr int SPW = 64 / GL;   // states per wave (= block)
+    __shared__ CapsLds caps[SPW];
+    __shared__ int last;
+    const int nd = segment_count(ep.start, ep.goal, res);
+    const int64_t states = nd >= 1 ? (int64_t)nd + 1 : 2;
+    const int64_t idx = (int64_t)blockIdx.x * SPW + threadIdx.x / GL;
+    const bool run = idx < states;
+    double st[NQ];
+    if (idx < 2 || !run) {
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) st[k] = idx == 1 ? ep.goal[k] : ep.start[k];
+    } else {
+        interp(ep.start, ep.goal, (double)(idx - 1) / (double)nd, st);
+    }
+    float qq[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) qq[k] = (float)st[k];
+    const bool col = state_collides_ml<GL, BF>(qq, run, sc, caps);
+    const unsigned bad = (run && col) ? (idx == 0 ? 1u : idx == 1 ? 2u : 4u) : 0u;
+    const unsigned long long b1 = __ballot(bad & 1u), b2 = __ballot(bad & 2u), b4 = __ballot(bad & 4u);
+    if (threadIdx.x == 0) {
+        const unsigned wbad = (b1 ? 1u : 0u) | (b2 ? 2u : 0u) | (b4 ? 4u : 0u);
+        if (wbad) atomicOr(&sync[0], wbad);
+        __threadfence();
+        last = atomicAdd(&sync[1], 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && threadIdx.x == 0) {
+        __threadfence();
+        const unsigned f = atomicOr(&sync[0], 0u);
+        hio->status[ST_SG] = ((f & 1u) ? 0 : 1) | ((f & 2u) ? 0 : 0x100) | ((f & 6u) ? 0 : 0x10000);
+        hio->counter = (unsigned long long)states;
+        sync[0] = 0;
+        sync[1] = 0;
+        publish_seq(hio, seq);
+    }
+}
+
+// k_edges with GL lanes per (edge, slot) item; grid-stride over the items
+template <int GL, bool BF>
+__global__ __launch_bounds__(64) void k_edges_ml(const double* __restrict__ from, const double* __restrict__ to,
+                                                const int* __restrict__ nd, int64_t n_edges, int kmax, int mode,
+                                                uint8_t* valid, int group, int* gfail, unsigned long long* counter,
+                                                const DevScene* __restrict__ sc, const int* __restrict__ dcount,
+                                                int per_item, const int* __restrict__ dkmax) {
+    constexpr int SPW = 64 / GL;
+    __shared__ CapsLds caps[SPW];
+    if (dcount) n_edges = min(n_edges, (int64_t)dcount[0] * per_item);
+    if (dkmax) kmax = *dkmax;
+    const int64_t total = n_edges * kmax;
+    const int gl = (int)(threadIdx.x & (GL - 1));
+    for (int64_t base = (int64_t)blockIdx.x * SPW; base < total; base += (int64_t)gridDim.x * SPW) {
+        const int64_t idx = base + threadIdx.x / GL;
+        const int64_t e = idx / kmax;
+        const int slot = (int)(idx - e * kmax);
+        bool run = false;
+        int nde = -1;
+        int emode = mode;
+        if (e < n_edges) {
+            nde = nd[e];
+            if (mode == 2 && nde >= 0) {
+                emode = (nde & ND_FROM) ? 1 : 0;
+                nde &= ~ND_FROM;
+            }
+            const int slots = nde > 1 ? nde : 1;
+            run = nde >= 0 && slot < slots && valid[e] != 0;
+            if (run && gfail) {
+                const int g = (int)(e / group), s = (int)(e - (int64_t)g * group);
+                run = gfail[g] > s;
+            }
+        }
+        count_states(counter, __ballot(run && gl == 0));
+        if (!__any(run)) continue;
+        double st[NQ];
+        const double* a = from + (run ? e : 0) * NQ;
+        const double* b = to + (run ? e : 0) * NQ;
+        if (slot == 0 || !run) {
+            const double* ep = emode ? a : b;
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) st[k] = ep[k];
+        } else {
+            interp(a, b, (double)slot / (double)nde, st);
+        }
+        float qq[NQ];
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) qq[k] = (float)st[k];
+        const bool col = state_collides_ml<GL, BF>(qq, run, sc, caps);
+        if (run && col && gl == 0) {
+            valid[e] = 0;
+            if (gfail) {
+                const int g = (int)(e / group), s = (int)(e - (int64_t)g * group);
+                atomicMin(&gfail[g], s);
+            }
+        }
+    }
+}
+
 // rp_plan prologue (one block): tree roots, float32 copies of start / goal, counters
 // (replaces per-field host->device copies). sg_edge >= 0: start and goal also
 // become zero-length edges at sg_edge and sg_edge + stride of the first extension

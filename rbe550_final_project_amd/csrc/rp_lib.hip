@@ -265,18 +265,80 @@ void launch_validity_bf(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, hi
 #undef RP_VAL
 }
 
+int ml_lanes(int64_t states);
+
 void launch_validity(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, hipStream_t s) {
     if (n <= 0) return;
-    if (base_fixed(c->scene)) launch_validity_bf<true>(c, q, n, flags, s);
-    else launch_validity_bf<false>(c, q, n, flags, s);
+    if (const int gl = ml_lanes(n); gl > 1) {   // small batches: GL lanes per state
+        const bool bf = base_fixed(c->scene);
+#define RP_VML(G)                                                                                               \
+    do {                                                                                                        \
+        const unsigned nb = blocks_for(n, 64 / G);                                                              \
+        if (bf) hipLaunchKernelGGL((k_validity_ml<G, true>), dim3(nb), dim3(64), 0, s, q, n, flags, c->d_scene); \
+        else hipLaunchKernelGGL((k_validity_ml<G, false>), dim3(nb), dim3(64), 0, s, q, n, flags, c->d_scene);  \
+    } while (0)
+        switch (gl) {
+            case 8: RP_VML(8); break;
+            case 16: RP_VML(16); break;
+            case 32: RP_VML(32); break;
+            default: RP_VML(64); break;
+        }
+#undef RP_VML
+    } else if (base_fixed(c->scene)) {
+        launch_validity_bf<true>(c, q, n, flags, s);
+    } else {
+        launch_validity_bf<false>(c, q, n, flags, s);
+    }
     HIP_TRY(hipGetLastError());
+}
+
+// Lanes per state of the low-latency kernels (rp_math.h state_collides_ml) for a
+// launch of up to `states` states: the one-lane kernels leave small launches as
+// slow as one wave's dependency chain. 1 = the throughput kernels.
+// RBE_ML_LANES=1/8/16/32/64 forces a value (tests, A/B).
+int ml_lanes(int64_t states) {
+    const char* e = std::getenv("RBE_ML_LANES");
+    const int forced = (e && *e) ? std::atoi(e) : 0;
+    if (forced == 1 || forced == 8 || forced == 16 || forced == 32 || forced == 64) return forced;
+    if (states <= 1024) return 64;
+    if (states <= 8192) return 16;
+    if (states <= 65536) return 8;
+    return 1;
+}
+
+template <int GL>
+void launch_edges_ml(rp_ctx* c, const double* from, const double* to, const int* nd, int64_t n, int kmax, int mode,
+                     uint8_t* valid, int group, int* gfail, hipStream_t s, const int* dcount, int per_item,
+                     unsigned max_blocks, const int* dkmax) {
+    constexpr int SPW = 64 / GL;
+    unsigned nb = blocks_for(n * (int64_t)kmax, SPW);
+    nb = std::min<unsigned>(nb, max_blocks ? std::max(max_blocks, 4096u) : 16384u);
+    if (base_fixed(c->scene))
+        hipLaunchKernelGGL((k_edges_ml<GL, true>), dim3(nb), dim3(64), 0, s, from, to, nd, n, kmax, mode, valid, group,
+                           gfail, c->counter.p, c->d_scene, dcount, per_item, dkmax);
+    else
+        hipLaunchKernelGGL((k_edges_ml<GL, false>), dim3(nb), dim3(64), 0, s, from, to, nd, n, kmax, mode, valid,
+                           group, gfail, c->counter.p, c->d_scene, dcount, per_item, dkmax);
 }
 
 void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd, int64_t n, int kmax,
                   int mode, uint8_t* valid, int group, int* gfail, hipStream_t s, const int* dcount = nullptr,
-                  int per_item = 1, unsigned max_blocks = 0, const int* dkmax = nullptr) {
+                  int per_item = 1, unsigned max_blocks = 0, const int* dkmax = nullptr, int64_t expect = 0) {
     if (n <= 0) return;
     const int64_t threads = n * (int64_t)kmax;   // (dkmax: kmax is only the grid's size hint)
+    // expect: the states a gated launch (dcount) usually has, when far below its bound
+    if (const int gl = ml_lanes(expect > 0 ? expect : dkmax ? n * 32 : threads); gl > 1) {
+        const int ps = prof_begin(c, s);
+        switch (gl) {
+            case 8: launch_edges_ml<8>(c, from, to, nd, n, kmax, mode, valid, group, gfail, s, dcount, per_item, max_blocks, dkmax); break;
+            case 16: launch_edges_ml<16>(c, from, to, nd, n, kmax, mode, valid, group, gfail, s, dcount, per_item, max_blocks, dkmax); break;
+            case 32: launch_edges_ml<32>(c, from, to, nd, n, kmax, mode, valid, group, gfail, s, dcount, per_item, max_blocks, dkmax); break;
+            default: launch_edges_ml<64>(c, from, to, nd, n, kmax, mode, valid, group, gfail, s, dcount, per_item, max_blocks, dkmax); break;
+        }
+        HIP_TRY(hipGetLastError());
+        prof_end(c, ps, 1, s);
+        return;
+    }
     unsigned nb = blocks_for(threads, VBLOCK);
     if (max_blocks && nb > max_blocks) nb = max_blocks;   // grid-stride (gated launches)
     const dim3 g(nb), b(VBLOCK);
@@ -816,19 +878,40 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         Endpoints ep;
         for (int i = 0; i < NQ; ++i) { ep.start[i] = start[i]; ep.goal[i] = goal[i]; }
         const int nd = (int)std::ceil(std::sqrt(h_dist2(start, goal)) / p.resolution);
-        const unsigned nb = blocks_for(nd >= 1 ? nd + 1 : 2, VBLOCK) + 1;   // + 1: device nd may round up
+        const int64_t nst = nd >= 1 ? nd + 1 : 2;
         const int seq = ++c->seq;
+        const int gl = ml_lanes(nst);
+        if (gl > 1) {   // low-latency: GL lanes per state
+            const bool bf = base_fixed(c->scene);
+#define RP_STRAIGHT_ML(G)                                                                                          \
+    do {                                                                                                           \
+        const unsigned nbm = blocks_for(nst, 64 / G) + 1;                                                          \
+        if (bf) hipLaunchKernelGGL((k_straight_ml<G, true>), dim3(nbm), dim3(64), 0, c->stream, ep, p.resolution,  \
+                                   c->d_scene, c->sync.p, h, seq);                                                 \
+        else hipLaunchKernelGGL((k_straight_ml<G, false>), dim3(nbm), dim3(64), 0, c->stream, ep, p.resolution,    \
+                                c->d_scene, c->sync.p, h, seq);                                                    \
+    } while (0)
+            switch (gl) {
+                case 8: RP_STRAIGHT_ML(8); break;
+                case 16: RP_STRAIGHT_ML(16); break;
+                case 32: RP_STRAIGHT_ML(32); break;
+                default: RP_STRAIGHT_ML(64); break;
+            }
+#undef RP_STRAIGHT_ML
+        } else {
+            const unsigned nb = blocks_for(nst, VBLOCK) + 1;   // + 1: device nd may round up
 #define RP_STRAIGHT(N) hipLaunchKernelGGL(k_straight<N>, dim3(nb), dim3(VBLOCK), 0, c->stream, ep, p.resolution, \
                                           c->d_scene, c->sync.p, h, seq)
-        switch (ncl_bucket(c->scene)) {
-            case NCL_GRID: RP_STRAIGHT(NCL_GRID); break;
-            case 0: RP_STRAIGHT(0); break;
-            case 1: RP_STRAIGHT(1); break;
-            case 2: RP_STRAIGHT(2); break;
-            case 4: RP_STRAIGHT(4); break;
-            default: RP_STRAIGHT(8); break;
-        }
+            switch (ncl_bucket(c->scene)) {
+                case NCL_GRID: RP_STRAIGHT(NCL_GRID); break;
+                case 0: RP_STRAIGHT(0); break;
+                case 1: RP_STRAIGHT(1); break;
+                case 2: RP_STRAIGHT(2); break;
+                case 4: RP_STRAIGHT(4); break;
+                default: RP_STRAIGHT(8); break;
+            }
 #undef RP_STRAIGHT
+        }
         HIP_TRY(hipGetLastError());
         wait_seq(c, seq);
         const int sgw = h->status[ST_SG];
@@ -905,8 +988,9 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                 HIP_TRY(hipGetLastError());
             }
             if (prog[k] & (OP_PREP_REDUCE | OP_PREP_SMOOTH))
+                // candidates: up to SPMAX^2 / 2 edges, usually a few dozen (short raw paths)
                 launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, (int64_t)(SPMAX - 1) * (SPMAX - 2) / 2, kfull, 0,
-                             c->valid.p, 1, nullptr, c->stream, &c->simp.p->nedges, 1, 2048);
+                             c->valid.p, 1, nullptr, c->stream, &c->simp.p->nedges, 1, 2048, nullptr, 4096);
         }
     };
     PathArgs pa;

@@ -157,9 +157,20 @@ __device__ __forceinline__ void place(Capsules& k, const Frame& f) {
 // link1's capsules, the shoulder position) folds into literals and takes no
 // registers; the values are the ones the runtime base gives
 constexpr float BASE_FIXED[3] = {0.0f, 0.0f, 0.01f};
-template <class Visit, bool BF = false>
-__device__ __forceinline__ bool fk_walk(const float q[NQ], const DevScene* __restrict__ sc, Capsules& k,
-                                        Visit& v) {
+// joint angle source of the walk: sin / cos of joint i from q (rp_sincos), or
+// precomputed values (the low-latency kernels compute the 7 in parallel lanes;
+// the same function of q, so the same bits)
+struct JointsQ {
+    const float* q;
+    __device__ __forceinline__ void rot(Frame& f, int i) const { rot_z(f, q[i]); }
+};
+struct JointsSC {
+    float s[7], c[7];
+    __device__ __forceinline__ void rot(Frame& f, int i) const { rot_sc(f, s[i], c[i]); }
+};
+template <class Visit, bool BF = false, class J = JointsQ>
+__device__ __forceinline__ bool fk_walk_j(const float q[NQ], const J& jt, const DevScene* __restrict__ sc,
+                                          Capsules& k, Visit& v) {
     Frame f;
     f.c0 = {1.0f, 0.0f, 0.0f};
     f.c1 = {0.0f, 1.0f, 0.0f};
@@ -169,38 +180,38 @@ __device__ __forceinline__ bool fk_walk(const float q[NQ], const DevScene* __res
     place<C_LINK0>(k, f);
     if (v.template at<C_LINK0>(k)) return true;
     shift(f.p, 0.333f, f.c2);               // link1: pos (0,0,0.333), joint 1
-    rot_z(f, q[0]);
+    jt.rot(f, 0);
     place<C_LINK1>(k, f);
     if (v.template at<C_LINK1>(k)) return true;
     rot_xm(f);                              // link2: quat (1,-1,0,0) = Rx(-90), joint 2
-    rot_z(f, q[1]);
+    jt.rot(f, 1);
     place<C_LINK2>(k, f);
     if (v.template at<C_LINK2>(k)) return true;
     shift(f.p, -0.316f, f.c1);              // link3: pos (0,-0.316,0), Rx(+90), joint 3
     rot_xp(f);
-    rot_z(f, q[2]);
+    jt.rot(f, 2);
     place<C_LINK3>(k, f);
     if (v.template at<C_LINK3>(k)) return true;
     shift(f.p, 0.0825f, f.c0);              // link4: pos (0.0825,0,0), Rx(+90), joint 4
     rot_xp(f);
-    rot_z(f, q[3]);
+    jt.rot(f, 3);
     place<C_LINK4>(k, f);
     if (v.template at<C_LINK4>(k)) return true;
     shift(f.p, -0.0825f, f.c0);             // link5: pos (-0.0825,0.384,0), Rx(-90), joint 5
     shift(f.p, 0.384f, f.c1);
     rot_xm(f);
-    rot_z(f, q[4]);
+    jt.rot(f, 4);
     place<C_LINK5A>(k, f);
     if (v.template at<C_LINK5A>(k)) return true;
     place<C_LINK5B>(k, f);
     if (v.template at<C_LINK5B>(k)) return true;
     rot_xp(f);                              // link6: Rx(+90), joint 6
-    rot_z(f, q[5]);
+    jt.rot(f, 5);
     place<C_LINK6>(k, f);
     if (v.template at<C_LINK6>(k)) return true;
     shift(f.p, 0.088f, f.c0);               // link7: pos (0.088,0,0), Rx(+90), joint 7
     rot_xp(f);
-    rot_z(f, q[6]);
+    jt.rot(f, 6);
     place<C_LINK7>(k, f);
     if (v.template at<C_LINK7>(k)) return true;
     shift(f.p, 0.107f, f.c2);               // hand: pos (0,0,0.107), Rz(-45deg)
@@ -221,6 +232,12 @@ __device__ __forceinline__ bool fk_walk(const float q[NQ], const DevScene* __res
         if (v.template at<C_RFINGER>(k)) return true;
     }
     return false;
+}
+template <class Visit, bool BF = false>
+__device__ __forceinline__ bool fk_walk(const float q[NQ], const DevScene* __restrict__ sc, Capsules& k,
+                                        Visit& v) {
+    const JointsQ jt{q};
+    return fk_walk_j<Visit, BF>(q, jt, sc, k, v);
 }
 
 struct NoVisit {
@@ -749,6 +766,119 @@ __device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene
     while (v.s.nss > 0) pop_ss(v.s);
     RP_STAMP(7);
     return Q.hit[v.s.lane] != 0;
+}
+
+// ---------------------------------------------------------------------------
+// Low-latency state check: GL lanes per state (DESIGN.md §5 "latency kernels")
+// ---------------------------------------------------------------------------
+// A launch too small to fill the chip (a straight edge; the few thousand edges of a
+// small RRT iteration; the simplification's candidate edges) is as slow as one
+// wave's dependency chain when one lane owns a state (~20k cycles, FK + 12 capsule
+// walks + 35 pairs in sequence). Here a group of GL lanes shares a state: the 7
+// joint sin/cos are computed by 7 lanes at once and exchanged, every lane then walks
+// the (short) FK chain, lane 0 of the group stores the 12 capsules in LDS, and the
+// group's lanes split the tests — unit u < NPAIR is self pair u, unit NPAIR + c*nb + j
+// is capsule c vs box j — with the oracle's test arithmetic (plain per-box AABB, no
+// cluster / grid / sphere prefilters, every self pair): the state collides iff the
+// plane test or any unit hits (group OR). Same flags as state_collides.
+struct CapsLds { float v[NCAP][6]; };   // a.xyz, b.xyz of each capsule (world)
+__constant__ int ML_PAIR_I[NPAIR] = {
+#define RP_PI(p) PAIRS[p][0]
+    RP_PI(0), RP_PI(1), RP_PI(2), RP_PI(3), RP_PI(4), RP_PI(5), RP_PI(6), RP_PI(7), RP_PI(8), RP_PI(9),
+    RP_PI(10), RP_PI(11), RP_PI(12), RP_PI(13), RP_PI(14), RP_PI(15), RP_PI(16), RP_PI(17), RP_PI(18), RP_PI(19),
+    RP_PI(20), RP_PI(21), RP_PI(22), RP_PI(23), RP_PI(24), RP_PI(25), RP_PI(26), RP_PI(27), RP_PI(28), RP_PI(29),
+    RP_PI(30), RP_PI(31), RP_PI(32), RP_PI(33), RP_PI(34)
+#undef RP_PI
+};
+__constant__ int ML_PAIR_J[NPAIR] = {
+#define RP_PJ(p) PAIRS[p][1]
+    RP_PJ(0), RP_PJ(1), RP_PJ(2), RP_PJ(3), RP_PJ(4), RP_PJ(5), RP_PJ(6), RP_PJ(7), RP_PJ(8), RP_PJ(9),
+    RP_PJ(10), RP_PJ(11), RP_PJ(12), RP_PJ(13), RP_PJ(14), RP_PJ(15), RP_PJ(16), RP_PJ(17), RP_PJ(18), RP_PJ(19),
+    RP_PJ(20), RP_PJ(21), RP_PJ(22), RP_PJ(23), RP_PJ(24), RP_PJ(25), RP_PJ(26), RP_PJ(27), RP_PJ(28), RP_PJ(29),
+    RP_PJ(30), RP_PJ(31), RP_PJ(32), RP_PJ(33), RP_PJ(34)
+#undef RP_PJ
+};
+__constant__ float ML_RADIUS[NCAP] = {CAP_GEOM[0][6], CAP_GEOM[1][6], CAP_GEOM[2][6], CAP_GEOM[3][6],
+                                      CAP_GEOM[4][6], CAP_GEOM[5][6], CAP_GEOM[6][6], CAP_GEOM[7][6],
+                                      CAP_GEOM[8][6], CAP_GEOM[9][6], CAP_GEOM[10][6], CAP_GEOM[11][6]};
+
+struct NoVisitPlane {   // plane test only, in the walk (every lane, registers)
+    float plane_z;
+    template <int C>
+    __device__ __forceinline__ bool at(const Capsules& k) {
+        constexpr float r = CAP_GEOM[C][6];
+        return fminr(k.a[C].z, k.b[C].z) - r <= plane_z;   // capsule_aabb(...).lo.z <= plane
+    }
+};
+
+// Every lane of the wave calls it (wave-uniform control flow); `run`: this lane's
+// group has a state. Returns the group's verdict on every lane of the group.
+template <int GL, bool BF = false>
+__device__ __forceinline__ bool state_collides_ml(const float q[NQ], bool run, const DevScene* __restrict__ sc,
+                                                  CapsLds* caps) {
+    static_assert(GL >= 8 && GL <= 64 && (GL & (GL - 1)) == 0, "group of 8..64 lanes");
+    const int lane = (int)__lane_id();
+    const int gl = lane & (GL - 1), base = lane & ~(GL - 1);
+    CapsLds& cs = caps[lane / GL];
+    // joint sin / cos: lane gl < 7 of the group computes joint gl's
+    float sj, cj;
+    rp_sincos(q[gl < 7 ? gl : 0], &sj, &cj);
+    JointsSC jt;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+        jt.s[i] = __shfl(sj, base + i, 64);
+        jt.c[i] = __shfl(cj, base + i, 64);
+    }
+    Capsules k;
+    NoVisitPlane pv{sc->plane_z};
+    bool hit = run && fk_walk_j<NoVisitPlane, BF>(q, jt, sc, k, pv);
+    if (!__any(run && !hit)) return hit;   // every state decided by the plane (or idle)
+    if (gl == 0) {
+#pragma unroll
+        for (int c = 0; c < NCAP; ++c) {
+            cs.v[c][0] = k.a[c].x; cs.v[c][1] = k.a[c].y; cs.v[c][2] = k.a[c].z;
+            cs.v[c][3] = k.b[c].x; cs.v[c][4] = k.b[c].y; cs.v[c][5] = k.b[c].z;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const int nb = sc->n_boxes;
+    const int units = NPAIR + NCAP * nb;
+    const bool active = run && !hit;   // uniform within the group
+    for (int u0 = 0; u0 < units; u0 += GL) {
+        const int u = u0 + gl;
+        bool h = false;
+        if (active && u < units) {
+            if (u < NPAIR) {
+                const int i = ML_PAIR_I[u], j = ML_PAIR_J[u];
+                const float* pi = cs.v[i];
+                const float* pj = cs.v[j];
+                const V3 a1 = {pi[0], pi[1], pi[2]}, b1 = {pi[3], pi[4], pi[5]};
+                const V3 a2 = {pj[0], pj[1], pj[2]}, b2 = {pj[3], pj[4], pj[5]};
+                const float ri = ML_RADIUS[i], rj = ML_RADIUS[j];
+                if (!aabb_disjoint2(capsule_aabb(a1, b1, ri), capsule_aabb(a2, b2, rj))) {
+                    const float rr = ri + rj;
+                    h = segment_segment_dist2(a1, b1, a2, b2) <= rr * rr;
+                }
+            } else {
+                const int w = u - NPAIR;
+                const int c = w / nb, j = w - c * nb;
+                const float* bx = sc->box[j];
+                if (!((__float_as_uint(bx[14]) >> c) & 1u)) {
+                    const float* pc = cs.v[c];
+                    const V3 a = {pc[0], pc[1], pc[2]}, b = {pc[3], pc[4], pc[5]};
+                    const float r = ML_RADIUS[c];
+                    if (!aabb_disjoint(capsule_aabb(a, b, r), bx + 8, bx + 11)) h = capsule_box_narrow(a, b, r, bx);
+                }
+            }
+        }
+        constexpr unsigned long long GMASK = GL == 64 ? ~0ull : ((1ull << (GL & 63)) - 1);
+        const unsigned long long m = __ballot(h);
+        hit = hit || ((m >> base) & GMASK) != 0;
+        if (!__any(active && !hit)) break;   // every group decided
+    }
+    __builtin_amdgcn_wave_barrier();   // the LDS capsules are reused by the next state
+    return hit;
 }
 
 }  // namespace rp

@@ -439,13 +439,15 @@ __global__ __launch_bounds__(64) void k_validity_ml(const float* __restrict__ q,
                                                    uint8_t* __restrict__ flags, const DevScene* __restrict__ sc) {
     constexpr int SPW = 64 / GL;
     __shared__ CapsLds caps[SPW];
+    __shared__ SceneLds scl;
+    scene_to_lds(sc, scl);
     const int64_t i = (int64_t)blockIdx.x * SPW + threadIdx.x / GL;
     const bool run = i < n;
     float qq[NQ];
     const float* src = q + (run ? i : 0) * NQ;
 #pragma unroll
     for (int k = 0; k < NQ; ++k) qq[k] = src[k];
-    const bool col = state_collides_ml<GL, BF>(qq, run, sc, caps);
+    const bool col = state_collides_ml<GL, BF>(qq, run, scl, caps);
     if (run && (threadIdx.x & (GL - 1)) == 0) flags[i] = col ? 0 : 1;
 }
 
@@ -456,7 +458,9 @@ __global__ __launch_bounds__(64) void k_straight_ml(Endpoints ep, double res, co
                                                    unsigned* sync, PlanIO* hio, int seq) {
     constexpr int SPW = 64 / GL;   // states per wave (= block)
     __shared__ CapsLds caps[SPW];
+    __shared__ SceneLds scl;
     __shared__ int last;
+    scene_to_lds(sc, scl);
     const int nd = segment_count(ep.start, ep.goal, res);
     const int64_t states = nd >= 1 ? (int64_t)nd + 1 : 2;
     const int64_t idx = (int64_t)blockIdx.x * SPW + threadIdx.x / GL;
@@ -471,7 +475,7 @@ __global__ __launch_bounds__(64) void k_straight_ml(Endpoints ep, double res, co
     float qq[NQ];
 #pragma unroll
     for (int k = 0; k < NQ; ++k) qq[k] = (float)st[k];
-    const bool col = state_collides_ml<GL, BF>(qq, run, sc, caps);
+    const bool col = state_collides_ml<GL, BF>(qq, run, scl, caps);
     const unsigned bad = (run && col) ? (idx == 0 ? 1u : idx == 1 ? 2u : 4u) : 0u;
     const unsigned long long b1 = __ballot(bad & 1u), b2 = __ballot(bad & 2u), b4 = __ballot(bad & 4u);
     if (threadIdx.x == 0) {
@@ -501,6 +505,8 @@ __global__ __launch_bounds__(64) void k_edges_ml(const double* __restrict__ from
                                                 int per_item, const int* __restrict__ dkmax) {
     constexpr int SPW = 64 / GL;
     __shared__ CapsLds caps[SPW];
+    __shared__ SceneLds scl;
+    scene_to_lds(sc, scl);
     if (dcount) n_edges = min(n_edges, (int64_t)dcount[0] * per_item);
     if (dkmax) kmax = *dkmax;
     const int64_t total = n_edges * kmax;
@@ -509,44 +515,39 @@ __global__ __launch_bounds__(64) void k_edges_ml(const double* __restrict__ from
         const int64_t idx = base + threadIdx.x / GL;
         const int64_t e = idx / kmax;
         const int slot = (int)(idx - e * kmax);
-        bool run = false;
-        int nde = -1;
+        // the edge's words and endpoints loaded together (no dependent round trips)
+        const bool in = e < n_edges;
+        const int64_t ec = in ? e : 0;
+        const int g = (int)(ec / group), gs = (int)(ec - (int64_t)g * group);
+        int nde = nd[ec];
+        const bool ok = valid[ec] != 0;
+        const int gf = gfail ? gfail[g] : 0x7fffffff;
+        double a[NQ], b[NQ];
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) { a[k] = from[ec * NQ + k]; b[k] = to[ec * NQ + k]; }
         int emode = mode;
-        if (e < n_edges) {
-            nde = nd[e];
-            if (mode == 2 && nde >= 0) {
-                emode = (nde & ND_FROM) ? 1 : 0;
-                nde &= ~ND_FROM;
-            }
-            const int slots = nde > 1 ? nde : 1;
-            run = nde >= 0 && slot < slots && valid[e] != 0;
-            if (run && gfail) {
-                const int g = (int)(e / group), s = (int)(e - (int64_t)g * group);
-                run = gfail[g] > s;
-            }
+        if (mode == 2 && nde >= 0) {
+            emode = (nde & ND_FROM) ? 1 : 0;
+            nde &= ~ND_FROM;
         }
+        const int slots = nde > 1 ? nde : 1;
+        const bool run = in && nde >= 0 && slot < slots && ok && gf > gs;
         count_states(counter, __ballot(run && gl == 0));
         if (!__any(run)) continue;
         double st[NQ];
-        const double* a = from + (run ? e : 0) * NQ;
-        const double* b = to + (run ? e : 0) * NQ;
         if (slot == 0 || !run) {
-            const double* ep = emode ? a : b;
 #pragma unroll
-            for (int k = 0; k < NQ; ++k) st[k] = ep[k];
+            for (int k = 0; k < NQ; ++k) st[k] = emode ? a[k] : b[k];
         } else {
             interp(a, b, (double)slot / (double)nde, st);
         }
         float qq[NQ];
 #pragma unroll
         for (int k = 0; k < NQ; ++k) qq[k] = (float)st[k];
-        const bool col = state_collides_ml<GL, BF>(qq, run, sc, caps);
+        const bool col = state_collides_ml<GL, BF>(qq, run, scl, caps);
         if (run && col && gl == 0) {
             valid[e] = 0;
-            if (gfail) {
-                const int g = (int)(e / group), s = (int)(e - (int64_t)g * group);
-                atomicMin(&gfail[g], s);
-            }
+            if (gfail) atomicMin(&gfail[g], gs);
         }
     }
 }

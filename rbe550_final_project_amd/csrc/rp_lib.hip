@@ -265,11 +265,11 @@ void launch_validity_bf(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, hi
 #undef RP_VAL
 }
 
-int ml_lanes(int64_t states);
+int ml_lanes(int64_t states, bool edges);
 
 void launch_validity(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, hipStream_t s) {
     if (n <= 0) return;
-    if (const int gl = ml_lanes(n); gl > 1) {   // small batches: GL lanes per state
+    if (const int gl = ml_lanes(n, false); gl > 1) {   // small batches: GL lanes per state
         const bool bf = base_fixed(c->scene);
 #define RP_VML(G)                                                                                               \
     do {                                                                                                        \
@@ -296,12 +296,16 @@ void launch_validity(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, hipSt
 // launch of up to `states` states: the one-lane kernels leave small launches as
 // slow as one wave's dependency chain. 1 = the throughput kernels.
 // RBE_ML_LANES=1/8/16/32/64 forces a value (tests, A/B).
-int ml_lanes(int64_t states) {
+// Thresholds measured on MI355X (tools/ml_tune.py): a validity launch of dense
+// states gains below ~4k states; an edge launch's bound (edges x slots, mostly
+// idle lanes: short edges, finished chains) gains up to ~64k.
+int ml_lanes(int64_t states, bool edges) {
     const char* e = std::getenv("RBE_ML_LANES");
     const int forced = (e && *e) ? std::atoi(e) : 0;
     if (forced == 1 || forced == 8 || forced == 16 || forced == 32 || forced == 64) return forced;
-    if (states <= 1024) return 64;
-    if (states <= 8192) return 16;
+    if (!edges) return states <= 1024 ? 64 : states <= 4096 ? 32 : 1;
+    if (states <= 4096) return 64;
+    if (states <= 16384) return 16;
     if (states <= 65536) return 8;
     return 1;
 }
@@ -327,7 +331,7 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
     if (n <= 0) return;
     const int64_t threads = n * (int64_t)kmax;   // (dkmax: kmax is only the grid's size hint)
     // expect: the states a gated launch (dcount) usually has, when far below its bound
-    if (const int gl = ml_lanes(expect > 0 ? expect : dkmax ? n * 32 : threads); gl > 1) {
+    if (const int gl = ml_lanes(expect > 0 ? expect : dkmax ? n * 32 : threads, true); gl > 1) {
         const int ps = prof_begin(c, s);
         switch (gl) {
             case 8: launch_edges_ml<8>(c, from, to, nd, n, kmax, mode, valid, group, gfail, s, dcount, per_item, max_blocks, dkmax); break;
@@ -880,7 +884,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         const int nd = (int)std::ceil(std::sqrt(h_dist2(start, goal)) / p.resolution);
         const int64_t nst = nd >= 1 ? nd + 1 : 2;
         const int seq = ++c->seq;
-        const int gl = ml_lanes(nst);
+        const int gl = ml_lanes(nst, false);
         if (gl > 1) {   // low-latency: GL lanes per state
             const bool bf = base_fixed(c->scene);
 #define RP_STRAIGHT_ML(G)                                                                                          \

@@ -169,14 +169,14 @@ struct JointsSC {
     __device__ __forceinline__ void rot(Frame& f, int i) const { rot_sc(f, s[i], c[i]); }
 };
 template <class Visit, bool BF = false, class J = JointsQ>
-__device__ __forceinline__ bool fk_walk_j(const float q[NQ], const J& jt, const DevScene* __restrict__ sc,
-                                          Capsules& k, Visit& v) {
+__device__ __forceinline__ bool fk_walk_j(const float q[NQ], const J& jt, const float* base, Capsules& k,
+                                          Visit& v) {
     Frame f;
     f.c0 = {1.0f, 0.0f, 0.0f};
     f.c1 = {0.0f, 1.0f, 0.0f};
     f.c2 = {0.0f, 0.0f, 1.0f};
     if constexpr (BF) f.p = {BASE_FIXED[0], BASE_FIXED[1], BASE_FIXED[2]};
-    else f.p = {sc->base[0], sc->base[1], sc->base[2]};
+    else f.p = {base[0], base[1], base[2]};
     place<C_LINK0>(k, f);
     if (v.template at<C_LINK0>(k)) return true;
     shift(f.p, 0.333f, f.c2);               // link1: pos (0,0,0.333), joint 1
@@ -237,7 +237,7 @@ template <class Visit, bool BF = false>
 __device__ __forceinline__ bool fk_walk(const float q[NQ], const DevScene* __restrict__ sc, Capsules& k,
                                         Visit& v) {
     const JointsQ jt{q};
-    return fk_walk_j<Visit, BF>(q, jt, sc, k, v);
+    return fk_walk_j<Visit, BF>(q, jt, sc->base, k, v);
 }
 
 struct NoVisit {
@@ -781,7 +781,6 @@ __device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene
 // is capsule c vs box j — with the oracle's test arithmetic (plain per-box AABB, no
 // cluster / grid / sphere prefilters, every self pair): the state collides iff the
 // plane test or any unit hits (group OR). Same flags as state_collides.
-struct CapsLds { float v[NCAP][6]; };   // a.xyz, b.xyz of each capsule (world)
 __constant__ int ML_PAIR_I[NPAIR] = {
 #define RP_PI(p) PAIRS[p][0]
     RP_PI(0), RP_PI(1), RP_PI(2), RP_PI(3), RP_PI(4), RP_PI(5), RP_PI(6), RP_PI(7), RP_PI(8), RP_PI(9),
@@ -802,6 +801,37 @@ __constant__ float ML_RADIUS[NCAP] = {CAP_GEOM[0][6], CAP_GEOM[1][6], CAP_GEOM[2
                                       CAP_GEOM[4][6], CAP_GEOM[5][6], CAP_GEOM[6][6], CAP_GEOM[7][6],
                                       CAP_GEOM[8][6], CAP_GEOM[9][6], CAP_GEOM[10][6], CAP_GEOM[11][6]};
 
+struct CapsLds { float v[NCAP][6]; };   // a.xyz, b.xyz of each capsule (world)
+
+// The scene and the test tables in LDS: in these latency-bound kernels every
+// dependent global load is a round trip to another XCD's L2 or HBM (~1-2 us), so
+// the block loads all of it at once at its start (overlapping the FK chain) and
+// the test loop reads only LDS.
+struct SceneLds {
+    float box[MAX_BOXES][16];
+    int pi[NPAIR], pj[NPAIR];
+    float rad[NCAP];
+    float plane_z, base[3];
+    int nb;
+};
+// all 64 lanes of the (one-wave) block; no wait (state_collides_ml waits)
+__device__ __forceinline__ void scene_to_lds(const DevScene* __restrict__ sc, SceneLds& L) {
+    const int t = (int)threadIdx.x;
+    const float4* src = reinterpret_cast<const float4*>(&sc->box[0][0]);
+    float4* dst = reinterpret_cast<float4*>(&L.box[0][0]);
+#pragma unroll
+    for (int k = 0; k < MAX_BOXES * 4 / 64; ++k) dst[t + 64 * k] = src[t + 64 * k];
+    if (t < NPAIR) {
+        L.pi[t] = ML_PAIR_I[t];
+        L.pj[t] = ML_PAIR_J[t];
+    }
+    if (t < NCAP) L.rad[t] = ML_RADIUS[t];
+    if (t == 0) {
+        L.plane_z = sc->plane_z;
+        L.nb = sc->n_boxes;
+    }
+    if (t < 3) L.base[t] = sc->base[t];
+}
 struct NoVisitPlane {   // plane test only, in the walk (every lane, registers)
     float plane_z;
     template <int C>
@@ -814,7 +844,7 @@ struct NoVisitPlane {   // plane test only, in the walk (every lane, registers)
 // Every lane of the wave calls it (wave-uniform control flow); `run`: this lane's
 // group has a state. Returns the group's verdict on every lane of the group.
 template <int GL, bool BF = false>
-__device__ __forceinline__ bool state_collides_ml(const float q[NQ], bool run, const DevScene* __restrict__ sc,
+__device__ __forceinline__ bool state_collides_ml(const float q[NQ], bool run, const SceneLds& sc,
                                                   CapsLds* caps) {
     static_assert(GL >= 8 && GL <= 64 && (GL & (GL - 1)) == 0, "group of 8..64 lanes");
     const int lane = (int)__lane_id();
@@ -829,9 +859,10 @@ __device__ __forceinline__ bool state_collides_ml(const float q[NQ], bool run, c
         jt.s[i] = __shfl(sj, base + i, 64);
         jt.c[i] = __shfl(cj, base + i, 64);
     }
+    __syncthreads();   // the block's SceneLds (scene_to_lds, issued before the caller's state setup)
     Capsules k;
-    NoVisitPlane pv{sc->plane_z};
-    bool hit = run && fk_walk_j<NoVisitPlane, BF>(q, jt, sc, k, pv);
+    NoVisitPlane pv{sc.plane_z};
+    bool hit = run && fk_walk_j<NoVisitPlane, BF>(q, jt, sc.base, k, pv);
     if (!__any(run && !hit)) return hit;   // every state decided by the plane (or idle)
     if (gl == 0) {
 #pragma unroll
@@ -842,7 +873,7 @@ __device__ __forceinline__ bool state_collides_ml(const float q[NQ], bool run, c
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const int nb = sc->n_boxes;
+    const int nb = sc.nb;
     const int units = NPAIR + NCAP * nb;
     const bool active = run && !hit;   // uniform within the group
     for (int u0 = 0; u0 < units; u0 += GL) {
@@ -850,12 +881,12 @@ __device__ __forceinline__ bool state_collides_ml(const float q[NQ], bool run, c
         bool h = false;
         if (active && u < units) {
             if (u < NPAIR) {
-                const int i = ML_PAIR_I[u], j = ML_PAIR_J[u];
+                const int i = sc.pi[u], j = sc.pj[u];
                 const float* pi = cs.v[i];
                 const float* pj = cs.v[j];
                 const V3 a1 = {pi[0], pi[1], pi[2]}, b1 = {pi[3], pi[4], pi[5]};
                 const V3 a2 = {pj[0], pj[1], pj[2]}, b2 = {pj[3], pj[4], pj[5]};
-                const float ri = ML_RADIUS[i], rj = ML_RADIUS[j];
+                const float ri = sc.rad[i], rj = sc.rad[j];
                 if (!aabb_disjoint2(capsule_aabb(a1, b1, ri), capsule_aabb(a2, b2, rj))) {
                     const float rr = ri + rj;
                     h = segment_segment_dist2(a1, b1, a2, b2) <= rr * rr;
@@ -863,11 +894,11 @@ __device__ __forceinline__ bool state_collides_ml(const float q[NQ], bool run, c
             } else {
                 const int w = u - NPAIR;
                 const int c = w / nb, j = w - c * nb;
-                const float* bx = sc->box[j];
+                const float* bx = sc.box[j];
                 if (!((__float_as_uint(bx[14]) >> c) & 1u)) {
                     const float* pc = cs.v[c];
                     const V3 a = {pc[0], pc[1], pc[2]}, b = {pc[3], pc[4], pc[5]};
-                    const float r = ML_RADIUS[c];
+                    const float r = sc.rad[c];
                     if (!aabb_disjoint(capsule_aabb(a, b, r), bx + 8, bx + 11)) h = capsule_box_narrow(a, b, r, bx);
                 }
             }

@@ -292,6 +292,154 @@ __device__ __forceinline__ int32_t nn_tiled(const double* __restrict__ tree, int
 
 struct Bounds { double lo[NQ]; double hi[NQ]; };
 
+// ---- large trees: nearest node split over (query block, tree range) --------------
+// Brute force over T nodes for n queries is n x T distance evaluations (27 FP64
+// FLOP each). The fused kernels give each lane one query and stream the tree
+// through LDS: a node's 72 B come back to all 64 lanes for 27 f64 ops, so four
+// SIMDs sharing one LDS run it LDS-bound. Here a lane holds NN_QPT queries (one
+// LDS read of a node serves NN_QPT distances), and the tree is split into S ranges
+// (grid.y) so a few hundred query blocks still fill 256 CUs; each range keeps its
+// own (distance, index) minimum with the strict-< scan, and k_nn_reduce takes the
+// lexicographic minimum over the ranges — the sequential scan's result (lowest
+// index among equal distances), bit for bit.
+constexpr int NN_QPT = 4;
+struct DI2 { double d; int i; int pad; };
+enum : int { NNQ_SAMPLE = 0, NNQ_ROWS = 1, NNQ_STEER = 2 };
+struct NnQuery {
+    int kind;            // NNQ_SAMPLE: Philox sample g0 + i0 + k; NNQ_ROWS: A[TA0 + t0 + k];
+                         // NNQ_STEER: steer(A[near[k]], sample g0 + i0 + k)
+    uint64_t seed, g0;
+    int64_t i0;
+    Bounds bd;
+    double range;
+    const double* A;
+    int64_t TA0, t0;
+    const int32_t* near;
+    const int* status;   // NNQ_ROWS: n = min(n, status[ST_NACC] - t0) (device count)
+};
+__device__ __forceinline__ void nn_query(const NnQuery& Q, int64_t k, double x[NQ]) {
+    if (Q.kind == NNQ_ROWS) {
+        const double* xs = Q.A + (Q.TA0 + Q.t0 + k) * NQ;
+#pragma unroll
+        for (int d = 0; d < NQ; ++d) x[d] = xs[d];
+        return;
+    }
+    double qr[NQ];
+    sample_state(Q.seed, Q.g0 + (uint64_t)(Q.i0 + k), Q.bd.lo, Q.bd.hi, qr);
+    if (Q.kind == NNQ_SAMPLE) {
+#pragma unroll
+        for (int d = 0; d < NQ; ++d) x[d] = qr[d];
+        return;
+    }
+    steer(Q.A + (int64_t)Q.near[k] * NQ, qr, Q.range, x);
+}
+
+// f32 filter with a proven bound: for in-bounds states (|coordinate| <= 4) the f32
+// distance d32 = sum fma(e, e) of e = f32(y) - f32(x) satisfies
+// |d32 - d| <= 11u d + 48u sqrt(d) + 1e-12 (u = 2^-24: conversion, subtraction and
+// 9-term summation errors), d the exact squared distance. A node whose true d could
+// be <= the current exact best passes d32 <= thr(best) = best + nn_err(best) and
+// gets the exact f64 dist2 (the oracle's arithmetic) and the strict-< update; a node
+// failing it has d > best and cannot change the result. nn_err uses ~6x margins.
+__device__ __forceinline__ float nn_thr(double best) {
+    if (!(best < 1e30)) return __builtin_inff();
+    const double t = best + (4e-6 * best + 1.6e-5 * sqrt(best) + 1e-9);
+    return (float)(t * (1.0 + 1e-6));   // rounding to f32 stays above t
+}
+typedef float nnf2 __attribute__((ext_vector_type(2)));
+
+__global__ __launch_bounds__(NNBLOCK) void k_nn_part(NnQuery Q, int64_t n, const double* __restrict__ tree,
+                                                     int64_t T, int64_t chunk, DI2* __restrict__ part) {
+    static_assert(NN_QPT % 2 == 0, "queries in pairs (packed f32)");
+    __shared__ double tile[NNTILE * NQ];
+    __shared__ float tile32[NNTILE * NQ];
+    if (Q.status) n = min(n, (int64_t)Q.status[0] - Q.t0);   // ST_NACC
+    const int64_t q0 = (int64_t)blockIdx.x * NNBLOCK * NN_QPT;
+    if (q0 >= n) return;   // whole block idle (uniform)
+    const int64_t t_lo = (int64_t)blockIdx.y * chunk, t_hi = min(T, t_lo + chunk);
+    double x[NN_QPT][NQ], best[NN_QPT];
+    nnf2 x2[NN_QPT / 2][NQ];
+    float thr[NN_QPT];
+    int32_t bi[NN_QPT];
+#pragma unroll
+    for (int r = 0; r < NN_QPT; ++r) {
+        const int64_t k = q0 + threadIdx.x + (int64_t)r * NNBLOCK;
+        nn_query(Q, k < n ? k : 0, x[r]);
+        best[r] = __builtin_inf();
+        thr[r] = __builtin_inff();
+        bi[r] = -1;
+    }
+#pragma unroll
+    for (int r = 0; r < NN_QPT / 2; ++r)
+#pragma unroll
+        for (int d = 0; d < NQ; ++d) x2[r][d] = nnf2{(float)x[2 * r][d], (float)x[2 * r + 1][d]};
+    for (int64_t base = t_lo; base < t_hi; base += NNTILE) {
+        const int cnt = (int)((t_hi - base) < NNTILE ? (t_hi - base) : NNTILE);
+        __syncthreads();
+        const double* src = tree + base * NQ;
+        for (int k = threadIdx.x; k < cnt * NQ; k += NNBLOCK) {
+            const double v = src[k];
+            tile[k] = v;
+            tile32[k] = (float)v;
+        }
+        __syncthreads();
+        for (int j = 0; j < cnt; ++j) {
+            float y[NQ];
+#pragma unroll
+            for (int d = 0; d < NQ; ++d) y[d] = tile32[j * NQ + d];
+            bool need = false;
+            bool pass[NN_QPT];
+#pragma unroll
+            for (int r = 0; r < NN_QPT / 2; ++r) {
+                nnf2 acc = {0.0f, 0.0f};
+#pragma unroll
+                for (int d = 0; d < NQ; ++d) {
+                    const nnf2 e = nnf2{y[d], y[d]} - x2[r][d];
+                    acc = __builtin_elementwise_fma(e, e, acc);
+                }
+                pass[2 * r] = acc.x <= thr[2 * r];
+                pass[2 * r + 1] = acc.y <= thr[2 * r + 1];
+                need = need || pass[2 * r] || pass[2 * r + 1];
+            }
+            if (need) {   // rare past the first nodes: the exact f64 test
+                double yd[NQ];
+#pragma unroll
+                for (int d = 0; d < NQ; ++d) yd[d] = tile[j * NQ + d];
+#pragma unroll
+                for (int r = 0; r < NN_QPT; ++r) {
+                    if (!pass[r]) continue;
+                    const double dd = dist2(yd, x[r]);   // same operand order as nn_tiled / the oracle
+                    if (dd < best[r]) {
+                        best[r] = dd;
+                        bi[r] = (int32_t)(base + j);
+                        thr[r] = nn_thr(dd);
+                    }
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < NN_QPT; ++r) {
+        const int64_t k = q0 + threadIdx.x + (int64_t)r * NNBLOCK;
+        if (k < n) part[(int64_t)blockIdx.y * n + k] = DI2{best[r], bi[r], 0};
+    }
+}
+
+// lexicographic (distance, index) minimum over the S tree ranges -> out[k]
+__global__ void k_nn_reduce(const DI2* __restrict__ part, int64_t n, int S, const int* status, int64_t t0,
+                            int32_t* __restrict__ out) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (status) n = min(n, (int64_t)status[0] - t0);
+    if (k >= n) return;
+    double bd = __builtin_inf();
+    int bi = -1;
+    for (int s = 0; s < S; ++s) {
+        const DI2 v = part[(int64_t)s * n + k];
+        if (v.i >= 0 && (v.d < bd || (v.d == bd && v.i < bi))) { bd = v.d; bi = v.i; }
+    }
+    out[k] = bi;
+}
+
 // Extension step for samples [i0, i0 + n): sample, nearest node of tree A, steer,
 // edge record (a_start: near -> new, mode 0; goal tree: new -> near, mode 1).
 __global__ __launch_bounds__(NNBLOCK) void k_ext_nn(const double* __restrict__ A, int64_t TA,
@@ -299,13 +447,15 @@ __global__ __launch_bounds__(NNBLOCK) void k_ext_nn(const double* __restrict__ A
                                                     Bounds bd, double range, double res, int a_start,
                                                     double* __restrict__ efrom, double* __restrict__ eto,
                                                     int* __restrict__ nd, uint8_t* __restrict__ valid,
-                                                    int32_t* __restrict__ near_out) {
+                                                    int32_t* __restrict__ near_out,
+                                                    const int32_t* __restrict__ near_in) {
     __shared__ double tile[NNTILE * NQ];
     const int64_t k = (int64_t)blockIdx.x * NNBLOCK + threadIdx.x;
     const bool active = k < n;
     double qr[NQ];
     sample_state(seed, g0 + (uint64_t)(i0 + (active ? k : 0)), bd.lo, bd.hi, qr);
-    const int32_t nn = nn_tiled(A, TA, qr, active, tile);
+    // near_in: nearest nodes from the split search (k_nn_part + k_nn_reduce)
+    const int32_t nn = near_in ? (active ? near_in[k] : 0) : nn_tiled(A, TA, qr, active, tile);
     if (!active) return;
     double qn[NQ];
     const double* near = A + (int64_t)nn * NQ;
@@ -704,7 +854,8 @@ __global__ __launch_bounds__(NNBLOCK) void k_conn_nn(const double* __restrict__ 
                                                      double* __restrict__ efrom, double* __restrict__ eto,
                                                      int* __restrict__ nd, uint8_t* __restrict__ valid,
                                                      int* __restrict__ gfail, int32_t* __restrict__ yout,
-                                                     int32_t* __restrict__ mout, const int* __restrict__ status) {
+                                                     int32_t* __restrict__ mout, const int* __restrict__ status,
+                                                     const int32_t* __restrict__ y_in) {
     __shared__ double tile[NNTILE * NQ];
     if (status) n = min(n, (int64_t)status[ST_NACC] - t0);
     if ((int64_t)blockIdx.x * NNBLOCK >= n) return;   // whole block idle (uniform)
@@ -714,7 +865,7 @@ __global__ __launch_bounds__(NNBLOCK) void k_conn_nn(const double* __restrict__ 
     const double* xs = A + (TA0 + t0 + (active ? k : 0)) * NQ;
 #pragma unroll
     for (int d = 0; d < NQ; ++d) x[d] = xs[d];
-    const int32_t y = nn_tiled(Bt, TB, x, active, tile);
+    const int32_t y = y_in ? (active ? y_in[k] : 0) : nn_tiled(Bt, TB, x, active, tile);
     if (!active) return;
     double cur[NQ], nxt[NQ];
     const double* ys = Bt + (int64_t)y * NQ;
@@ -765,16 +916,19 @@ __global__ __launch_bounds__(NNBLOCK) void k_ext_conn_nn(const double* __restric
                                                          double* __restrict__ eto, int* __restrict__ nd,
                                                          uint8_t* __restrict__ valid, int* __restrict__ gfail,
                                                          int32_t* __restrict__ near_out, int32_t* __restrict__ yout,
-                                                         int32_t* __restrict__ mout) {
+                                                         int32_t* __restrict__ mout,
+                                                         const int32_t* __restrict__ near_in,
+                                                         const int32_t* __restrict__ y_in) {
     __shared__ double tile[NNTILE * NQ];
     const int64_t k = (int64_t)blockIdx.x * NNBLOCK + threadIdx.x;
     const bool active = k < n;
     double qr[NQ], x[NQ];
     sample_state(seed, g0 + (uint64_t)(active ? k : 0), bd.lo, bd.hi, qr);
-    const int32_t nn = nn_tiled(A, TA, qr, active, tile);
+    // near_in / y_in: nearest nodes from the split search (large trees)
+    const int32_t nn = near_in ? (active ? near_in[k] : 0) : nn_tiled(A, TA, qr, active, tile);
     const double* near = A + (int64_t)(nn >= 0 ? nn : 0) * NQ;
     steer(near, qr, range, x);
-    const int32_t y = nn_tiled(Bt, TB, x, active, tile);
+    const int32_t y = y_in ? (active ? y_in[k] : 0) : nn_tiled(Bt, TB, x, active, tile);
     if (!active) return;
     const int G = cmax + 1;
     int64_t e = k * G;

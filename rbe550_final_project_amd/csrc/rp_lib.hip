@@ -159,6 +159,7 @@ struct rp_ctx {
     int64_t h_cap = 0;                   // int32 words per rank slot in the staging
     DevBuf<unsigned long long> g_cnt, g_incl;
     hipEvent_t gx0 = nullptr, gx1 = nullptr;
+    DevBuf<DI2> nn_part;                 // split nearest-node search: (distance, index) per range
 
     void free_staging() {
         if (h_send) (void)hipHostFree(h_send);
@@ -186,7 +187,7 @@ struct rp_ctx {
         rec.release(); Lv.release(); chain_end.release(); mine.release(); gfail.release();
         eslot.release(); eincl.release(); echunk.release();
         cub_tmp.release(); path.release(); io.release(); simp.release(); partial.release();
-        g_send.release(); g_recv.release(); g_cnt.release(); g_incl.release();
+        g_send.release(); g_recv.release(); g_cnt.release(); g_incl.release(); nn_part.release();
         leave_group();
         for (hipEvent_t e : pev) (void)hipEventDestroy(e);
         if (gx0) (void)hipEventDestroy(gx0);
@@ -694,6 +695,34 @@ bool out_of_bounds(const double* q, const double* lo, const double* hi) {
     return false;
 }
 
+// Nearest nodes of n queries over a large tree by the split search (rp_kernels.h
+// k_nn_part + k_nn_reduce) into out[0..n); false (nothing launched) when n x T is
+// small enough for the fused kernels' own search. RBE_NN_SPLIT=0/1 forces it.
+bool nn_split(rp_ctx* c, const NnQuery& Q, int64_t n, const double* tree, int64_t T, int32_t* out,
+              bool force = false) {
+    if (n <= 0 || T <= 0) return false;
+    int mode = -1;
+    if (const char* e = std::getenv("RBE_NN_SPLIT"))
+        if (*e) mode = std::atoi(e) != 0;
+    if (mode == 0 || (mode < 0 && !force && (double)n * (double)T < (double)(1 << 24))) return false;
+    const int64_t per_block = (int64_t)NNBLOCK * NN_QPT;
+    const int64_t qblocks = (n + per_block - 1) / per_block;
+    const int64_t tiles = (T + NNTILE - 1) / NNTILE;
+    const int64_t want = std::max<int64_t>(1, (2048 + qblocks - 1) / qblocks);   // >= 2048 blocks
+    const int64_t S0 = std::min<int64_t>(want, tiles);
+    const int64_t chunk = ((tiles + S0 - 1) / S0) * NNTILE;
+    const int S = (int)((T + chunk - 1) / chunk);
+    c->nn_part.ensure((size_t)S * n);
+    const int ps = prof_begin(c, c->stream);
+    hipLaunchKernelGGL(k_nn_part, dim3((unsigned)qblocks, (unsigned)S), dim3(NNBLOCK), 0, c->stream, Q, n, tree, T,
+                       chunk, c->nn_part.p);
+    hipLaunchKernelGGL(k_nn_reduce, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream,
+                       (const DI2*)c->nn_part.p, n, S, Q.status, Q.t0, out);
+    HIP_TRY(hipGetLastError());
+    prof_end(c, ps, 0, c->stream);
+    return true;
+}
+
 // Wait for a kernel to publish `seq` into the host mirror (rp_kernels.h PlanIO).
 // Spins on the host-coherent word; polls the stream now and then so that a failed
 // or finished-without-publishing stream turns into an error instead of a hang.
@@ -1016,6 +1045,28 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
 
     Bounds bd;
     for (int i = 0; i < NQ; ++i) { bd.lo[i] = lo[i]; bd.hi[i] = hi[i]; }
+    // speculative fronts on large trees: nearest nodes by the split search (both
+    // searches; the second's queries are the steered new nodes, so it needs the
+    // first's result: a large second search forces the first)
+    Tree* spec_A = nullptr;
+    Tree* spec_B = nullptr;
+    auto spec_split = [&](uint64_t gs0, int64_t n, const int32_t*& nin, const int32_t*& yin) {
+        NnQuery q1{};
+        q1.kind = NNQ_SAMPLE;
+        q1.seed = p.seed;
+        q1.g0 = gs0;
+        q1.i0 = 0;
+        q1.bd = bd;
+        q1.range = p.range;
+        const bool big_b = (double)n * (double)spec_B->n >= (double)(1 << 24);
+        if (!nn_split(c, q1, n, spec_A->q.p, spec_A->n, c->near_.p, big_b)) return;
+        nin = c->near_.p;
+        NnQuery q2 = q1;
+        q2.kind = NNQ_STEER;
+        q2.A = spec_A->q.p;
+        q2.near = c->near_.p;
+        if (nn_split(c, q2, n, spec_B->q.p, spec_B->n, c->yv.p)) yin = c->yv.p;
+    };
     int solved = 0;
     int32_t s_node = -1, g_node = -1;
     const double t_solve = now_s();
@@ -1031,6 +1082,8 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         if (A.n + B > cap || Bt.n + B * cmax > cap) break;
         const int64_t TA = A.n, TB = Bt.n;
         const uint64_t g0 = gbase;
+        spec_A = &A;
+        spec_B = &Bt;
 
         const int64_t sg = (iter == 0) ? sg_edge : -1;   // start / goal ride along
         c->stats.samples += B;
@@ -1039,11 +1092,14 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             // sample records, every rank appends the same nodes, one host round trip
             const int seq = ++c->seq;
             const int64_t slot = (int64_t)GREC * per + 1;
+            const uint64_t gr0 = g0 + (uint64_t)rank * (uint64_t)per;
+            const int32_t *nin = nullptr, *yin = nullptr;
+            spec_split(gr0, per, nin, yin);
             const int pn = prof_begin(c, c->stream);
             hipLaunchKernelGGL(k_ext_conn_nn, dim3(blocks_for(per, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
-                               Bt.q.p, TB, p.seed, g0 + (uint64_t)rank * (uint64_t)per, per, bd, p.range,
+                               Bt.q.p, TB, p.seed, gr0, per, bd, p.range,
                                p.resolution, cmax, a_start, c->efrom.p, c->eto.p, c->nd.p, c->valid.p, c->gfail.p,
-                               c->near_.p, c->yv.p, c->mv.p);
+                               c->near_.p, c->yv.p, c->mv.p, nin, yin);
             HIP_TRY(hipGetLastError());
             prof_end(c, pn, 0, c->stream);
             c->prof.nn_pairs += (double)per * (double)(TA + TB);
@@ -1108,10 +1164,12 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             // launch, one accept kernel, the first simplification steps (no-ops
             // until a path exists), one host round trip
             const int seq = ++c->seq;
+            const int32_t *nin = nullptr, *yin = nullptr;
+            spec_split(g0, B, nin, yin);
             const int pn = prof_begin(c, c->stream);
             hipLaunchKernelGGL(k_ext_conn_nn, dim3(blocks_for(B, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
                                Bt.q.p, TB, p.seed, g0, B, bd, p.range, p.resolution, cmax, a_start, c->efrom.p,
-                               c->eto.p, c->nd.p, c->valid.p, c->gfail.p, c->near_.p, c->yv.p, c->mv.p);
+                               c->eto.p, c->nd.p, c->valid.p, c->gfail.p, c->near_.p, c->yv.p, c->mv.p, nin, yin);
             HIP_TRY(hipGetLastError());
             prof_end(c, pn, 0, c->stream);
             c->prof.nn_pairs += (double)B * (double)(TA + TB);
@@ -1149,10 +1207,17 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
 
         // ---- single rank, two-phase (large batches, or RBE_PLAN_SPECULATE=0)
         debug_wait(c, "iteration start");
+        NnQuery qe{};
+        qe.kind = NNQ_SAMPLE;
+        qe.seed = p.seed;
+        qe.g0 = g0;
+        qe.i0 = (int64_t)rank * per;
+        qe.bd = bd;
+        const bool esplit = nn_split(c, qe, per, A.q.p, TA, c->near_.p);
         const int pn1 = prof_begin(c, c->stream);
         hipLaunchKernelGGL(k_ext_nn, dim3(blocks_for(per, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA, p.seed,
                            g0, (int64_t)rank * per, per, bd, p.range, p.resolution, a_start, c->efrom.p, c->eto.p,
-                           c->nd.p, c->valid.p, c->near_.p);
+                           c->nd.p, c->valid.p, c->near_.p, esplit ? (const int32_t*)c->near_.p : nullptr);
         HIP_TRY(hipGetLastError());
         prof_end(c, pn1, 0, c->stream);
         c->prof.nn_pairs += (double)per * (double)TA;
@@ -1185,10 +1250,18 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                                    (const uint8_t*)c->valid.p, sg, sg_stride);
             }
             debug_wait(c, "ext accept");
+            NnQuery qc{};
+            qc.kind = NNQ_ROWS;
+            qc.A = A.q.p;
+            qc.TA0 = TA;
+            qc.t0 = 0;
+            qc.status = status;   // accepted extensions (ST_NACC), on the device
+            const bool csplit = nn_split(c, qc, B, Bt.q.p, TB, c->yv.p);
             const int pn2 = prof_begin(c, c->stream);
             hipLaunchKernelGGL(k_conn_nn, dim3(blocks_for(B, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
                                (int64_t)0, B, Bt.q.p, TB, p.range, p.resolution, cmax, a_start, c->efrom.p,
-                               c->eto.p, c->nd.p, c->valid.p, c->gfail.p, c->yv.p, c->mv.p, (const int*)status);
+                               c->eto.p, c->nd.p, c->valid.p, c->gfail.p, c->yv.p, c->mv.p, (const int*)status,
+                               csplit ? (const int32_t*)c->yv.p : nullptr);
             HIP_TRY(hipGetLastError());
             prof_end(c, pn2, 0, c->stream);
             debug_wait(c, "k_conn_nn");

@@ -81,3 +81,14 @@ def test_rccl_transport_world1(name):
         _check(ctx, name)
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("name,split", [("C2_q0_s1", "1"), ("C4_q5", "1"), ("C5_well_s4", "0"), ("C5_well_s2", "1")])
+@pytest.mark.parametrize("grouped", ["0", "1"])
+def test_nearest_node_split_forced(gpu_ctx, name, split, grouped, monkeypatch):
+    """The split nearest-node search (k_nn_part + k_nn_reduce: queries x tree ranges,
+    lexicographic (distance, index) minimum) forced on / off, through the two-phase
+    and the group iteration: same plans as the oracle."""
+    monkeypatch.setenv("RBE_NN_SPLIT", split)
+    monkeypatch.setenv("RBE_PLAN_GROUPED", grouped)
+    _check(gpu_ctx, name)

@@ -89,3 +89,19 @@ def test_plans_forced_lanes(gpu_ctx, oracle_lib, lanes, straight, monkeypatch):
         path, st = gpu_ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
         ref, st_ref, _ = orc.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
         assert st == st_ref == _abi.STATUS_EXACT and np.array_equal(path, ref), (name, qi, lanes, straight)
+
+
+@pytest.mark.parametrize("split", ["0", "1"])
+def test_plans_nn_split_small_trees(gpu_ctx, oracle_lib, split, monkeypatch):
+    """The split nearest-node search on small trees and batches (forced), both
+    iteration kinds (speculative <= 4096 samples, two-phase above)."""
+    monkeypatch.setenv("RBE_NN_SPLIT", split)
+    orc = oracle_lib.OracleScene()
+    for name, qi, batch, bmin in [("goal3_tallest_10box", 5, 256, 0), ("goal4_pentagon_10box", 20, 8192, 8192),
+                                  ("clutter64", 0, 2048, 0)]:
+        q = _setup(gpu_ctx, orc, name, qi)
+        p = _abi.make_params(seed=9, batch=batch, batch_min=bmin, n_waypoints=150, timeout_s=60,
+                             straight_first=False)
+        path, st = gpu_ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+        ref, st_ref, _ = orc.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+        assert st == st_ref == _abi.STATUS_EXACT and np.array_equal(path, ref), (name, qi, split)

@@ -150,11 +150,11 @@ def rate_on_scene(ctx, scene, q, n, flags, stream, steps):
     kernel's stream)."""
     ctx.set_scene(scene.boxes, scene.plane_z, scene.base)
     for _ in range(3):
-        ctx.check_states_device(q.data_ptr(), n, flags.data_ptr(), stream.cuda_stream)
+        ctx.check_states_device(q.data_ptr(), n, flags.data_ptr(), None)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(steps):
-        ctx.check_states_device(q.data_ptr(), n, flags.data_ptr(), stream.cuda_stream)
+        ctx.check_states_device(q.data_ptr(), n, flags.data_ptr(), None)
     e1.record(stream)
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / steps
@@ -258,7 +258,7 @@ def main():
     ap.add_argument("--no-configs", action="store_true", help="skip the C2/C4/C5 scene rates (profiling runs)")
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend: nccl (= RCCL, the product path) or gloo (rehearsal of N > 1 "
-                         "with several ranks on one GPU; exchanges staged through host memory)")
+                         "with several ranks on one GPU; records exchanged through a shared-memory segment)")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "0") or 0))
     args = ap.parse_args()
 
@@ -290,14 +290,15 @@ def main():
     q = lo + (hi - lo) * torch.rand((n, 9), generator=g, device=dev, dtype=torch.float32)
     q = q.contiguous()
     flags = torch.empty(n, dtype=torch.uint8, device=dev)
-    # a dedicated stream: the kernel is launched on it and the HIP events are
-    # recorded on it (the legacy default stream has handle 0, which the C-ABI
-    # reads as "the context's own stream")
-    stream = torch.cuda.Stream(dev)
+    # the kernel runs on the context's own stream and the HIP events are recorded on
+    # it (torch.cuda.ExternalStream over rp_get_stream): no extra hardware queue per
+    # rank (an extra torch stream per process slowed later plans 2x when ranks share
+    # a GPU, tools/share_probe.py)
+    stream = torch.cuda.ExternalStream(ctx.stream_handle(), device=dev)
     torch.cuda.synchronize(dev)
 
     def step():
-        ctx.check_states_device(q.data_ptr(), n, flags.data_ptr(), stream.cuda_stream)
+        ctx.check_states_device(q.data_ptr(), n, flags.data_ptr(), None)
 
     for _ in range(args.warmup):
         step()
@@ -345,7 +346,7 @@ def main():
         group = None
         if distributed:
             from rbe550_final_project_amd.distributed import Group
-            group = Group(ctx, transport="host" if args.backend == "gloo" else "rccl")
+            group = Group(ctx, transport="shm" if args.backend == "gloo" else "rccl")
         try:
             run_plans(ctx, {"queries": wl["queries"][:2]}, args.plan_batch, 100, group)   # warm-up
             times, pstates, st = run_plans(ctx, wl, args.plan_batch, 0, group)

@@ -267,6 +267,13 @@ int rp_ik(rp_ctx* ctx, int32_t n_targets, const double* pos, const double* quat,
  * rehearsals. world = 1 (fn may be NULL) returns the context to single-rank
  * planning. */
 int rp_group_init(rp_ctx* ctx, int32_t rank, int32_t world, rp_allgather_fn fn, void* user);
+/* rp_group_init_shm: shared-memory transport for ranks of ONE node (they may share a
+ * GPU): `base` / `bytes` is a host segment every rank has mapped (POSIX shared
+ * memory, zero-filled when created); the library registers it with HIP, the pack
+ * kernel writes this rank's records into it in place, the ranks meet at a spin
+ * barrier on per-rank sequence words in the segment, and the accept kernels read
+ * every rank's records from it (no copies, no callback). */
+int rp_group_init_shm(rp_ctx* ctx, int32_t rank, int32_t world, void* base, int64_t bytes);
 int rp_group_rccl_unique_id(uint8_t id_out[RP_RCCL_ID_BYTES]);
 int rp_group_init_rccl(rp_ctx* ctx, int32_t rank, int32_t world, const uint8_t id[RP_RCCL_ID_BYTES]);
 
@@ -279,6 +286,11 @@ int rp_get_profile(rp_ctx* ctx, rp_profile* out);
 
 /* Last error text for this context (or for a failed rp_create when ctx is NULL). */
 const char* rp_last_error(rp_ctx* ctx);
+
+/* The context's own HIP stream (hipStream_t; non-blocking). Callers record events on
+ * it (e.g. torch.cuda.ExternalStream) to time or order work against the planner's
+ * launches without opening another hardware queue. */
+int rp_get_stream(rp_ctx* ctx, void** stream_out);
 
 /* Kernel-level timing of the last rp_check_states_device call: average duration of
  * the validity kernel measured with HIP events on the context's stream (ms). */

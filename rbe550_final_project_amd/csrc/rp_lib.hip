@@ -72,7 +72,7 @@ struct DevBuf {
 
 inline unsigned blocks_for(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
 
-enum { TR_NONE = 0, TR_HOST = 1, TR_RCCL = 2 };   // rank-group transports
+enum { TR_NONE = 0, TR_HOST = 1, TR_RCCL = 2, TR_SHM = 3 };   // rank-group transports
 
 #define NCCL_TRY(x)                                                                              \
     do {                                                                                         \
@@ -159,6 +159,13 @@ struct rp_ctx {
     int64_t h_cap = 0;                   // int32 words per rank slot in the staging
     DevBuf<unsigned long long> g_cnt, g_incl;
     hipEvent_t gx0 = nullptr, gx1 = nullptr;
+    // shared-memory transport (ranks of one node sharing a host segment): per-rank
+    // sequence words, then two record regions (double buffer), registered so the
+    // kernels write / read the records in place
+    char* shm = nullptr;
+    char* shm_dev = nullptr;
+    int64_t shm_bytes = 0;
+    int64_t shm_k = 0;                   // exchanges done (lockstep on every rank)
     DevBuf<DI2> nn_part;                 // split nearest-node search: (distance, index) per range
 
     void free_staging() {
@@ -170,6 +177,9 @@ struct rp_ctx {
     void leave_group() {
         if (comm) (void)ncclCommDestroy(comm);
         comm = nullptr;
+        if (shm) (void)hipHostUnregister(shm);
+        shm = shm_dev = nullptr;
+        shm_bytes = shm_k = 0;
         free_staging();
         rank = 0;
         world = 1;
@@ -481,6 +491,34 @@ void group_exchange(rp_ctx* c, int64_t words) {
     if (c->g_fn(c->g_user, c->h_send, c->h_recv, (int64_t)bytes) != 0) throw HipError{"group all-gather callback failed"};
     c->stats.exchange_ms += 1e3 * (now_s() - t0);
     HIP_TRY(hipMemcpyAsync(c->g_recv.p, c->h_recv, bytes * c->world, hipMemcpyHostToDevice, c->stream));
+}
+
+// shared-memory transport layout: SHM_HDR bytes of per-rank sequence words (one
+// 64-B line each), then two regions of `region` bytes (exchange k uses region k & 1:
+// a rank writes region (k+2) & 1 only after every rank has arrived at exchange k+1,
+// i.e. finished reading exchange k's records)
+constexpr int64_t SHM_HDR = 64 * 64;
+inline int64_t shm_region(const rp_ctx* c) { return ((c->shm_bytes - SHM_HDR) / 2) & ~(int64_t)255; }
+// device pointer of this exchange's records (rank-major slots of `words` int32)
+int32_t* shm_records(rp_ctx* c, int64_t k, int64_t words) {
+    if (sizeof(int32_t) * words * c->world > shm_region(c)) throw HipError{"shared-memory transport segment too small"};
+    return reinterpret_cast<int32_t*>(c->shm_dev + SHM_HDR + (k & 1) * shm_region(c));
+}
+// after this rank's records are written (stream synchronised): publish arrival k
+// and wait for every rank's (acquire), bounded by the wait watchdog
+void shm_barrier(rp_ctx* c, int64_t k) {
+    volatile int64_t* seq = reinterpret_cast<volatile int64_t*>(c->shm);
+    __atomic_store_n(reinterpret_cast<int64_t*>(c->shm + 64 * c->rank), k, __ATOMIC_RELEASE);
+    const double t0 = now_s();
+    for (int r = 0; r < c->world; ++r) {
+        while (__atomic_load_n(reinterpret_cast<const int64_t*>(c->shm + 64 * r), __ATOMIC_ACQUIRE) < k) {
+            if (now_s() - t0 > c->watchdog_s) throw HipError{"shared-memory transport: a rank did not arrive"};
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+            __builtin_ia32_pause();
+#endif
+        }
+    }
+    (void)seq;
 }
 
 void upload_scene(rp_ctx* c) {
@@ -1110,13 +1148,27 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                 launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, per * G, kmax, 2, c->valid.p, G, c->gfail.p,
                              c->stream);
             // without a transport (world 1) the records go straight to the gathered buffer
+            int32_t* recs = c->g_recv.p;   // every rank's records, rank-major
             int32_t* own = c->transport == TR_NONE ? c->g_recv.p : c->g_send.p;
+            int64_t shm_k = 0;
+            if (c->transport == TR_SHM) {   // pack in place into the shared segment
+                shm_k = ++c->shm_k;
+                recs = shm_records(c, shm_k, slot);
+                own = recs + (int64_t)rank * slot;
+            }
             hipLaunchKernelGGL(k_group_pack, dim3(blocks_for(per, 256)), dim3(256), 0, c->stream,
                                (const int*)c->gfail.p, (const int32_t*)c->near_.p, (const int32_t*)c->yv.p,
                                (const int32_t*)c->mv.p, per, tflag, own);
             HIP_TRY(hipGetLastError());
-            if (c->transport != TR_NONE) group_exchange(c, slot);
-            GroupRecs gr{c->g_recv.p, per, world};
+            if (c->transport == TR_SHM) {
+                HIP_TRY(hipStreamSynchronize(c->stream));   // my records are in the segment
+                const double te = now_s();
+                shm_barrier(c, shm_k);
+                c->stats.exchange_ms += 1e3 * (now_s() - te);
+            } else if (c->transport != TR_NONE) {
+                group_exchange(c, slot);
+            }
+            GroupRecs gr{recs, per, world};
             if (B <= FUSE_MAX) {
 #define RP_GROUP_SMALL(IT)                                                                                          \
     hipLaunchKernelGGL(k_group_accept_small<IT>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, gr, B, p.seed, g0, bd,  \
@@ -1763,6 +1815,12 @@ int rp_plan(rp_ctx* c, const double start[RP_NQ], const double goal[RP_NQ], cons
     RP_GUARD_END(c)
 }
 
+int rp_get_stream(rp_ctx* c, void** out) {
+    if (!c || !out) return RP_ERR_ARG;
+    *out = (void*)c->stream;
+    return RP_OK;
+}
+
 int rp_set_profiling(rp_ctx* c, int32_t on) {
     if (!c) return RP_ERR_ARG;
     c->profiling = on != 0;
@@ -1787,6 +1845,31 @@ int rp_group_init(rp_ctx* c, int32_t rank, int32_t world, rp_allgather_fn fn, vo
         c->g_fn = fn;
         c->g_user = user;
     }
+    return RP_OK;
+    RP_GUARD_END(c)
+}
+
+int rp_group_init_shm(rp_ctx* c, int32_t rank, int32_t world, void* base, int64_t bytes) {
+    if (!c || !base || world < 1 || world > 64 || rank < 0 || rank >= world || bytes < SHM_HDR + 2 * 4096)
+        return RP_ERR_ARG;
+    RP_GUARD_BEGIN
+    HIP_TRY(hipSetDevice(c->device));
+    c->leave_group();
+    HIP_TRY(hipHostRegister(base, (size_t)bytes, hipHostRegisterMapped));
+    c->shm = static_cast<char*>(base);
+    void* dptr = nullptr;
+    const hipError_t e = hipHostGetDevicePointer(&dptr, base, 0);
+    if (e != hipSuccess) {
+        (void)hipHostUnregister(base);
+        c->shm = nullptr;
+        HIP_TRY(e);
+    }
+    c->shm_dev = static_cast<char*>(dptr);
+    c->shm_bytes = bytes;
+    c->shm_k = 0;
+    c->rank = rank;
+    c->world = world;
+    c->transport = TR_SHM;
     return RP_OK;
     RP_GUARD_END(c)
 }

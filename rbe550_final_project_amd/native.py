@@ -18,9 +18,9 @@ LIB_PATH = os.path.join(_HERE, LIB_NAME)
 # every symbol include/rbe_planner.h declares
 EXPORTS = ("rp_version", "rp_default_robot", "rp_create", "rp_destroy", "rp_set_scene", "rp_set_attached",
            "rp_check_states", "rp_check_states_device", "rp_check_edges", "rp_check_edges_device",
-           "rp_state_contacts", "rp_plan", "rp_group_init", "rp_group_rccl_unique_id", "rp_group_init_rccl",
+           "rp_state_contacts", "rp_plan", "rp_group_init", "rp_group_init_shm", "rp_group_rccl_unique_id", "rp_group_init_rccl",
            "rp_get_stats", "rp_last_error", "rp_last_kernel_ms", "rp_selftest_f64", "rp_ik", "rp_set_profiling",
-           "rp_get_profile")
+           "rp_get_profile", "rp_get_stream")
 
 # rp_allgather_fn(user, send, recv, bytes_per_rank): library-owned pinned host buffers
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64)
@@ -58,9 +58,11 @@ def load():
     L.rp_plan.argtypes = [vp, vp, vp, vp, vp, C.POINTER(_abi.PlanParams), vp, i32, C.POINTER(i32), C.POINTER(i32)]
     L.rp_group_init.argtypes = [vp, i32, i32, vp, vp]
     L.rp_group_rccl_unique_id.argtypes = [vp]
+    L.rp_group_init_shm.argtypes = [vp, i32, i32, vp, i64]
     L.rp_group_init_rccl.argtypes = [vp, i32, i32, vp]
     L.rp_get_stats.argtypes = [vp, C.POINTER(_abi.Stats)]
     L.rp_set_profiling.argtypes = [vp, i32]
+    L.rp_get_stream.argtypes = [vp, C.POINTER(vp)]
     L.rp_get_profile.argtypes = [vp, C.POINTER(_abi.Profile)]
     L.rp_last_error.argtypes = [vp]
     L.rp_last_error.restype = C.c_char_p
@@ -198,13 +200,19 @@ class Context:
                                  _ptr(q), _ptr(st)), "rp_ik")
         return q, st
 
+    def stream_handle(self):
+        """The context's hipStream_t (as an int), for events / ordering (rp_get_stream)."""
+        h = C.c_void_p()
+        self._check(load().rp_get_stream(self._h, C.byref(h)), "rp_get_stream")
+        return int(h.value or 0)
+
     def set_profiling(self, on=True):
         self._check(load().rp_set_profiling(self._h, 1 if on else 0), "rp_set_profiling")
 
     def profile(self):
         """Kernel-class timing of the last plan (rp_get_profile)."""
         pr = _abi.Profile()
-        self._check(load().rp_get_profile(self._h, C.byref(pr)), "rp_get_profile")
+        self._check(load().rp_get_profile(self._h, C.byref(pr)), "rp_get_profile", "rp_get_stream")
         return pr.as_dict()
 
     def stats(self):
@@ -240,6 +248,11 @@ class Context:
         group, ranks on distinct GPUs. unique_id: rccl_unique_id() of rank 0."""
         uid = (C.c_uint8 * RCCL_ID_BYTES).from_buffer_copy(bytes(unique_id))
         self._check(load().rp_group_init_rccl(self._h, int(rank), int(world), uid), "rp_group_init_rccl")
+
+    def group_init_shm(self, rank, world, address, nbytes):
+        """Shared-memory transport over a host segment mapped by every rank of the node."""
+        self._check(load().rp_group_init_shm(self._h, int(rank), int(world), C.c_void_p(address), int(nbytes)),
+                    "rp_group_init_shm")
 
     def group_leave(self):
         """Back to single-rank planning."""

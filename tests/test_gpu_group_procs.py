@@ -1,7 +1,7 @@
 """The product rank group end to end across PROCESSES: two fresh
 Python processes (tests/_group_worker.py) join torch.distributed (gloo), build
-distributed.Group on GPU 0 (shared; the host transport carries the record
-all-gather) and plan — a goal3 query at a 256-sample batch, and BASELINE C4 / C5
+distributed.Group on GPU 0 (shared; the shared-memory transport, or the host
+transport over gloo, carries the record exchange) and plan — a goal3 query at a 256-sample batch, and BASELINE C4 / C5
 queries at their configured 262,144 / 131,072-sample iterations (C5 covered well:
 3 iterations, trees of 1.5 x 10^5 nodes). Both ranks' plans must equal rank 0's
 world-1 plan, the golden oracle plans (tests/golden/plans_configured.npz) and, for
@@ -41,10 +41,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_two_process_group_plans_equal_world1_and_oracle(tmp_path, oracle_lib):
+@pytest.mark.parametrize("transport", ["shm", "host"])
+def test_two_process_group_plans_equal_world1_and_oracle(tmp_path, oracle_lib, transport):
     out = str(tmp_path / "res")
     port = str(_free_port())
-    env = dict(os.environ, RBE_WAIT_WATCHDOG_S="30")
+    env = dict(os.environ, RBE_WAIT_WATCHDOG_S="30", RBE_WORKER_TRANSPORT=transport)
     procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "_group_worker.py"), str(r), "2", port, out,
                                json.dumps(CASES)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
                               env=env)

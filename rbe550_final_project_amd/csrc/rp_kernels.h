@@ -302,7 +302,13 @@ struct Bounds { double lo[NQ]; double hi[NQ]; };
 // own (distance, index) minimum with the strict-< scan, and k_nn_reduce takes the
 // lexicographic minimum over the ranges — the sequential scan's result (lowest
 // index among equal distances), bit for bit.
-constexpr int NN_QPT = 4;
+#ifndef RP_NN_QPT
+#define RP_NN_QPT 4
+#endif
+#ifndef RP_NN_UNROLL
+#define RP_NN_UNROLL 1
+#endif
+constexpr int NN_QPT = RP_NN_QPT;
 struct DI2 { double d; int i; int pad; };
 enum : int { NNQ_SAMPLE = 0, NNQ_ROWS = 1, NNQ_STEER = 2 };
 struct NnQuery {
@@ -383,6 +389,7 @@ __global__ __launch_bounds__(NNBLOCK) void k_nn_part(NnQuery Q, int64_t n, const
             tile32[k] = (float)v;
         }
         __syncthreads();
+#pragma unroll RP_NN_UNROLL
         for (int j = 0; j < cnt; ++j) {
             float y[NQ];
 #pragma unroll

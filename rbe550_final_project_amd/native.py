@@ -13,7 +13,8 @@ from . import _abi
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_NAME = "librbe_mi355x.so"
-LIB_PATH = os.path.join(_HERE, LIB_NAME)
+# RBE_LIB_PATH: an A/B build of the same library (tools/build_variants.sh), dev only
+LIB_PATH = os.environ.get("RBE_LIB_PATH") or os.path.join(_HERE, LIB_NAME)
 
 # every symbol include/rbe_planner.h declares
 EXPORTS = ("rp_version", "rp_default_robot", "rp_create", "rp_destroy", "rp_set_scene", "rp_set_attached",
@@ -212,7 +213,7 @@ class Context:
     def profile(self):
         """Kernel-class timing of the last plan (rp_get_profile)."""
         pr = _abi.Profile()
-        self._check(load().rp_get_profile(self._h, C.byref(pr)), "rp_get_profile", "rp_get_stream")
+        self._check(load().rp_get_profile(self._h, C.byref(pr)), "rp_get_profile")
         return pr.as_dict()
 
     def stats(self):

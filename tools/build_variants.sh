@@ -6,7 +6,7 @@ mkdir -p build/variants
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -fno-fast-math -Xarch_device -fno-honor-nans -Xarch_device -mno-amdgpu-ieee -fno-slp-vectorize $flags \
-    -o build/variants/lib_$name.so rbe550_final_project_amd/csrc/rp_lib.hip &
+    -o build/variants/lib_$name.so rbe550_final_project_amd/csrc/rp_lib.hip -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib &
 done
 wait
 ls build/variants

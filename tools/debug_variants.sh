@@ -1,11 +1,4 @@
-PROBE_VALIDITY=1 PROBE_CTX_STREAM=1 timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29561 tools/share_probe.py > gpurun_out/share.log 2>&1; echo "rc=$?"; grep "world\|after" gpurun_out/share.log
-PROBE_TORCH_GPU=1 timeout -k 10 200 python -c "
-import os, sys, time, json; sys.path.insert(0, '.')
-import torch
-from rbe550_final_project_amd.native import Context
-torch.cuda.set_device(0); s1 = torch.cuda.Stream(); s2 = torch.cuda.Stream()
-x = torch.ones(10, device='cuda')
-with torch.cuda.stream(s1): y = x * 2
-with torch.cuda.stream(s2): z = x * 3
-torch.cuda.synchronize(); print('ok')
-" > gpurun_out/q.log 2>&1; echo "q rc=$?"
+for v in nn_base nn_u2 nn_u4 nn_q2 nn_q2u4 nn_base; do
+  RBE_LIB_PATH=build/variants/lib_$v.so timeout -k 10 120 python -u tools/c5_profile.py > gpurun_out/nnv_$v.log 2>&1 || { echo "$v failed"; exit 1; }
+  echo "$v: $(grep 'prof=1' gpurun_out/nnv_$v.log | sed 's/.*NN [0-9]* launches \([0-9.]*\) ms.* \([0-9.]*\) TF64.*/\1 ms \2 TF/' | tr '\n' ' ')"
+done

@@ -306,7 +306,7 @@ struct Bounds { double lo[NQ]; double hi[NQ]; };
 #define RP_NN_QPT 4
 #endif
 #ifndef RP_NN_UNROLL
-#define RP_NN_UNROLL 1
+#define RP_NN_UNROLL 4
 #endif
 constexpr int NN_QPT = RP_NN_QPT;
 struct DI2 { double d; int i; int pad; };
@@ -479,13 +479,6 @@ __global__ __launch_bounds__(NNBLOCK) void k_ext_nn(const double* __restrict__ A
     near_out[k] = nn;
 }
 
-// res[k] = near index if the extension edge is valid, else -1
-__global__ void k_ext_result(const uint8_t* __restrict__ valid, const int32_t* __restrict__ near, int64_t n,
-                             int32_t* __restrict__ res) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < n) res[k] = valid[k] ? near[k] : -1;
-}
-
 // world == 1: res[k] and its accept flag in one pass
 __global__ void k_ext_result_flag(const uint8_t* __restrict__ valid, const int32_t* __restrict__ near, int64_t n,
                                   int32_t* __restrict__ res, int32_t* __restrict__ acc) {
@@ -494,22 +487,6 @@ __global__ void k_ext_result_flag(const uint8_t* __restrict__ valid, const int32
     const int32_t v = valid[k] ? near[k] : -1;
     res[k] = v;
     acc[k] = v >= 0 ? 1 : 0;
-}
-
-// unpack the gathered extension records (rank-major, `per`+1 int32 per rank)
-__global__ void k_ext_unpack(const int32_t* __restrict__ rbuf, int64_t per, int world,
-                             int32_t* __restrict__ res, int* any_flag) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < per * world) {
-        const int64_t r = i / per, k = i - r * per;
-        res[i] = rbuf[r * (per + 1) + k];
-    }
-    if (i < world && rbuf[i * (per + 1) + per]) atomicOr(any_flag, 1);
-}
-
-__global__ void k_flag(const int32_t* __restrict__ v, int64_t n, int32_t* __restrict__ out) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = v[i] >= 0 ? 1 : 0;
 }
 
 // Iteration status record (device): [0] accepted extension nodes, [1] nodes added
@@ -984,21 +961,6 @@ __global__ __launch_bounds__(NNBLOCK) void k_ext_conn_nn(const double* __restric
     mout[k] = m | (reached ? CHAIN_REACHES : 0);
 }
 
-// per-target record (y, L) with L = leading valid steps
-__global__ void k_conn_record(const int32_t* __restrict__ y, const int32_t* __restrict__ m,
-                              const int* __restrict__ gfail, int64_t n, int64_t pt, int32_t* __restrict__ rec) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= pt) return;
-    if (k < n) {
-        rec[2 * k] = y[k];
-        const int mk = m[k] & CHAIN_LEN;
-        rec[2 * k + 1] = gfail[k] < mk ? gfail[k] : mk;
-    } else {
-        rec[2 * k] = -1;
-        rec[2 * k + 1] = 0;
-    }
-}
-
 // world == 1: record and L in one pass over the batch bound B (L = 0 past nacc)
 __global__ void k_conn_record_len(const int32_t* __restrict__ y, const int32_t* __restrict__ m,
                                   const int* __restrict__ gfail, const int* __restrict__ status, int64_t B,
@@ -1014,11 +976,6 @@ __global__ void k_conn_record_len(const int32_t* __restrict__ y, const int32_t* 
     } else {
         L[k] = 0;
     }
-}
-
-__global__ void k_conn_len(const int32_t* __restrict__ rec, int64_t n, int32_t* __restrict__ L) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < n) L[t] = rec[2 * t + 1];
 }
 
 // rebuild target t's chain from (y, L), append its first L nodes to tree B at

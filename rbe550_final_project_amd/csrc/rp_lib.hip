@@ -126,7 +126,7 @@ struct rp_ctx {
     DevBuf<double> efrom, eto;
     DevBuf<int> nd;
     DevBuf<uint8_t> valid;
-    DevBuf<int32_t> near_, res, acc, incl, yv, mv, rec, Lv, chain_end, mine;
+    DevBuf<int32_t> near_, res, acc, incl, yv, mv, rec, Lv, chain_end;
     DevBuf<int> gfail;
     DevBuf<int32_t> eslot, eincl, echunk;   // work-compacted edge launches
     DevBuf<char> cub_tmp;
@@ -194,7 +194,7 @@ struct rp_ctx {
         q32.release(); flags.release(); ea.release(); eb.release(); end_nd.release(); eval.release();
         scalar.release(); counter.release(); efrom.release(); eto.release(); nd.release(); valid.release();
         near_.release(); res.release(); acc.release(); incl.release(); yv.release(); mv.release();
-        rec.release(); Lv.release(); chain_end.release(); mine.release(); gfail.release();
+        rec.release(); Lv.release(); chain_end.release(); gfail.release();
         eslot.release(); eincl.release(); echunk.release();
         cub_tmp.release(); path.release(); io.release(); simp.release(); partial.release();
         g_send.release(); g_recv.release(); g_cnt.release(); g_incl.release(); nn_part.release();
@@ -869,7 +869,6 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     // + 2: k_plan_init marks the start / goal edges' groups at batch_min and
     // batch_min + 1 (two-phase: batch_min = BMAX at the configured sizes)
     c->gfail.ensure(std::max<int64_t>(BMAX, FUSE_MAX) + 2);
-    c->mine.ensure(PMAX + 1);
     if (grouped) {
         c->g_send.ensure((size_t)GREC * PMAX + 1);
         c->g_recv.ensure((size_t)world * (GREC * PMAX + 1));

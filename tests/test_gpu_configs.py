@@ -92,3 +92,18 @@ def test_nearest_node_split_forced(gpu_ctx, name, split, grouped, monkeypatch):
     monkeypatch.setenv("RBE_NN_SPLIT", split)
     monkeypatch.setenv("RBE_PLAN_GROUPED", grouped)
     _check(gpu_ctx, name)
+
+
+def test_kernel_profile_of_a_plan(gpu_ctx):
+    """rp_set_profiling / rp_get_profile (bench.py's nearest-node and edge rooflines):
+    the profiled plan is the same plan, and the profile counts its launches, time
+    and work."""
+    gpu_ctx.set_profiling(True)
+    try:
+        s = _check(gpu_ctx, "C5_well_s4")
+        pr = gpu_ctx.profile()
+    finally:
+        gpu_ctx.set_profiling(False)
+    assert pr["nn_launches"] >= META["C5_well_s4"]["iterations"] and pr["edge_launches"] > 0
+    assert pr["nn_ms"] > 0 and pr["edge_ms"] > 0 and pr["nn_pairs"] > 1e9
+    assert pr["edge_states"] == s["states_checked"]

@@ -396,7 +396,7 @@ def main():
                 tq, sq, stq = run_plans(ctx, wl_c, batch, seeds_from, group, batch_min=bmin, tree_capacity=1 << 23,
                                         stats_out=extra, straight_first=False, max_iters=max_iters)
                 it = max(1, int(extra.get("iterations", 0)))
-                extra = {"mode": "RRT-Connect forced (straight_first off)", "batch_min": bmin or 256,
+                extra = {"mode": "RRT-Connect forced (straight_first off)", "batch_min": bmin or 64,
                          "exchange_ms": round(extra.get("exchange_ms", 0.0), 3),
                          "exchange_ms_per_iteration": round(extra.get("exchange_ms", 0.0) / it, 4),
                          "iterations": int(extra.get("iterations", 0)), "samples": int(extra.get("samples", 0)),

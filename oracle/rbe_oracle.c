@@ -760,7 +760,7 @@ int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], co
     /* batch schedule: iteration k draws min(batch, batch_min << k) samples; the
      * global sample counter keeps running, so the schedule is part of the
      * algorithm's definition (same on every rank and on the GPU) */
-    if (p.batch_min <= 0) p.batch_min = p.batch < 256 ? p.batch : 256;
+    if (p.batch_min <= 0) p.batch_min = p.batch < 64 ? p.batch : 64;
     if (p.batch_min > p.batch) p.batch_min = p.batch;
     p.batch_min = ((p.batch_min + world - 1) / world) * world;
     const int cmax = (int)ceil(max_extent / p.range) + 1;

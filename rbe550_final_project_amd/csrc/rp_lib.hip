@@ -829,7 +829,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     }
     // batch schedule (mirrored by oracle/rbe_oracle.c ro_plan): iteration k draws
     // min(batch, batch_min << k) samples from a running global sample counter
-    if (p.batch_min <= 0) p.batch_min = std::min<int64_t>(p.batch, 256);
+    if (p.batch_min <= 0) p.batch_min = std::min<int64_t>(p.batch, 64);
     p.batch_min = std::min(p.batch_min, p.batch);
     p.batch_min = ((p.batch_min + world - 1) / world) * world;
     const int cmax = (int)std::ceil(max_extent / p.range) + 1;

@@ -20,7 +20,8 @@ def run(ctx, wl, batch, bmin, seed0):
         sc = scenes.Scene.from_json(q["scene"])
         ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
         ctx.set_attached(q["attached"])
-        p = _abi.make_params(seed=seed0 + i, batch=batch, batch_min=bmin, n_waypoints=150, timeout_s=10.0)
+        p = _abi.make_params(seed=seed0 + i, batch=batch, batch_min=bmin, n_waypoints=150, timeout_s=10.0,
+                             straight_first=os.environ.get("SWEEP_STRAIGHT", "1") == "1")
         t0 = time.perf_counter()
         _, st = ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
         walls.append(1e3 * (time.perf_counter() - t0))

@@ -1086,7 +1086,7 @@ enum : int {
 };
 constexpr int SIMPLIFY_ROUNDS = 2, SMOOTH_STEPS = 3;
 
-struct SimpState {
+struct SimpHead {
     int n;          // states in P
     int on;         // device simplification of this path (0 < level, n_raw <= dev_max <= SPMAX)
     int done;       // nothing changes any more in this call
@@ -1097,9 +1097,11 @@ struct SimpState {
     int changed;
     long long edges_total;
     double len0, min_change;
+};
+// between launches; k_simp keeps the head, P and T in LDS for the duration of a call
+struct SimpState : SimpHead {
     double P[SPMAX * NQ];
     double Pprev[SPMAX * NQ];
-    double Q[SPMAX * NQ];          // subdivision scratch
     double T[(SPMAX / 2) * NQ];    // corner cuts of the smoothing candidates
 };
 
@@ -1123,26 +1125,36 @@ __device__ __forceinline__ void emit_edge(int e, const double* a, const double* 
 }
 
 // OP_BEGIN (block-cooperative): the raw path -> P, state reset
-__device__ void simp_begin(int level, int dev_max, const double* __restrict__ raw, const PlanIO* io,
-                           SimpState* ss) {
+// n_known >= -1: the raw path's length as the caller (iteration_tail) already
+// holds it, block-uniform, with P already written when `p_ready`; else io->n_raw.
+// Returns the states in P (block-uniform, 0 when off).
+__device__ int simp_begin(int level, int dev_max, const double* __restrict__ raw, const PlanIO* io,
+                          SimpState* ss, int n_known = -3, bool p_ready = false) {
+    __shared__ int bn;
     if (threadIdx.x == 0) {
-        const int n = io->n_raw;
-        ss->on = level > 0 && n >= 0 && n <= dev_max;
-        ss->n = ss->on ? n : 0;
-        ss->done = !(ss->on && n >= 3);
+        const int n = n_known >= -1 ? n_known : io->n_raw;
+        const bool on = level > 0 && n >= 0 && n <= dev_max;
+        ss->on = on;
+        ss->n = bn = on ? n : 0;
+        ss->done = !(on && n >= 3);
         ss->stop = 0;
         ss->nedges = 0;
         ss->edges_total = 0;
     }
     __syncthreads();
-    for (int k = threadIdx.x; k < ss->n * NQ; k += blockDim.x) ss->P[k] = raw[k];
+    const int n = bn;
+    if (!p_ready)
+        for (int k = threadIdx.x; k < n * NQ; k += blockDim.x) ss->P[k] = raw[k];
     __syncthreads();
+    return n;
 }
 
 // OP_PREP_REDUCE (block-cooperative): every shortcut (i, j >= i + 2) of P
-__device__ void simp_prep_reduce(double res, SimpState* ss, double* efrom, double* eto, int* nd, uint8_t* valid) {
-    const int n = ss->n;
-    const bool on = !ss->done && n >= 3;
+// n_known >= 0: ss->n as the caller holds it (right after simp_begin: done = n < 3)
+__device__ void simp_prep_reduce(double res, SimpState* ss, double* efrom, double* eto, int* nd, uint8_t* valid,
+                                 int n_known = -1) {
+    const int n = n_known >= 0 ? n_known : ss->n;
+    const bool on = n_known >= 0 ? n >= 3 : !ss->done && n >= 3;
     if (on)
         for (int e = threadIdx.x; e < n * n; e += blockDim.x) {
             const int i = e / n, j = e - i * n;
@@ -1174,24 +1186,57 @@ struct PathArgs {
 };
 
 
-// solution path (lane 0): start branch root..s_node, then goal branch g_node..root
-// (g_node < 0: start branch only); io->n_raw = -1 if longer than cap.
-__device__ void build_path(const PathArgs& pa, int32_t s_node, int32_t g_node, PlanIO* io) {
-    if (threadIdx.x != 0) return;
-    int ns = 0, ng = 0;
-    for (int32_t v = s_node; v >= 0; v = pa.Spar[v]) ++ns;
-    for (int32_t v = g_node; v >= 0; v = pa.Gpar[v]) ++ng;
-    if (ns + ng > pa.cap) {
-        io->n_raw = -1;
-        return;
+// solution path: start branch root..s_node, then goal branch g_node..root (g_node
+// < 0: start branch only); io->n_raw = -1 if longer than cap. Block-cooperative:
+// the two parent chains are walked by lanes of different waves at once (a walk is
+// a chain of dependent loads), their node indices kept in LDS, and the states
+// copied by every lane, into pa.out and, when `also` (P of the simplification,
+// n <= also_max), there too. Returns n_raw (block-uniform).
+constexpr int PATH_LDS = 512;
+__device__ int build_path(const PathArgs& pa, int32_t s_node, int32_t g_node, PlanIO* io, double* also = nullptr,
+                          int also_max = -1) {
+    __shared__ int32_t sidx[PATH_LDS], gidx[PATH_LDS];
+    __shared__ int bns, bng;
+    const int tid = threadIdx.x;
+    const int gl = blockDim.x >= 128 ? 64 : 0;   // the goal walk's lane
+    if (tid == 0) {
+        int ns = 0;
+        for (int32_t v = s_node; v >= 0; v = pa.Spar[v], ++ns)
+            if (ns < PATH_LDS) sidx[ns] = v;
+        bns = ns;
     }
-    int i = ns - 1;
-    for (int32_t v = s_node; v >= 0; v = pa.Spar[v], --i)
-        for (int d = 0; d < NQ; ++d) pa.out[i * NQ + d] = pa.S[(int64_t)v * NQ + d];
-    i = ns;
-    for (int32_t v = g_node; v >= 0; v = pa.Gpar[v], ++i)
-        for (int d = 0; d < NQ; ++d) pa.out[i * NQ + d] = pa.G[(int64_t)v * NQ + d];
-    io->n_raw = ns + ng;
+    if (tid == gl) {
+        int ng = 0;
+        for (int32_t v = g_node; v >= 0; v = pa.Gpar[v], ++ng)
+            if (ng < PATH_LDS) gidx[ng] = v;
+        bng = ng;
+    }
+    __syncthreads();
+    const int ns = bns, ng = bng, n = ns + ng;
+    if (n > pa.cap) {
+        if (tid == 0) io->n_raw = -1;
+        return -1;
+    }
+    double* p2 = n <= also_max ? also : nullptr;
+    if (ns <= PATH_LDS && ng <= PATH_LDS) {
+        for (int k = tid; k < n * NQ; k += blockDim.x) {
+            const int i = k / NQ, d = k - i * NQ;
+            const double v = i < ns ? pa.S[(int64_t)sidx[ns - 1 - i] * NQ + d] : pa.G[(int64_t)gidx[i - ns] * NQ + d];
+            pa.out[k] = v;
+            if (p2) p2[k] = v;
+        }
+    } else if (tid == 0) {   // long paths: walk again
+        int i = ns - 1;
+        for (int32_t v = s_node; v >= 0; v = pa.Spar[v], --i)
+            for (int d = 0; d < NQ; ++d) pa.out[i * NQ + d] = pa.S[(int64_t)v * NQ + d];
+        i = ns;
+        for (int32_t v = g_node; v >= 0; v = pa.Gpar[v], ++i)
+            for (int d = 0; d < NQ; ++d) pa.out[i * NQ + d] = pa.G[(int64_t)v * NQ + d];
+        if (p2)
+            for (int k = 0; k < n * NQ; ++k) p2[k] = pa.out[k];
+    }
+    if (tid == 0) io->n_raw = n;
+    return n;
 }
 
 // block tail of the last kernel of an iteration: join nodes and, on success, the
@@ -1206,10 +1251,12 @@ __device__ void iteration_tail(int* status, int added, int64_t TA, int a_start, 
         gn = status[ST_GNODE];
     }
     __syncthreads();
-    if (sn != -2) build_path(pa, sn, gn, io);
-    if (pa.ss) {   // (build_path's lane-0 writes are ordered by simp_begin's barrier)
-        simp_begin(pa.level, pa.dev_max, pa.out, io, pa.ss);
-        if (pa.prep_reduce) simp_prep_reduce(pa.res, pa.ss, pa.efrom, pa.eto, pa.nd, pa.valid);
+    const int nr = sn != -2 ? build_path(pa, sn, gn, io, pa.ss ? pa.ss->P : nullptr,
+                                         pa.level > 0 ? pa.dev_max : -1)
+                            : -3;   // no solution: simp_begin reads io->n_raw
+    if (pa.ss) {   // (build_path's writes are ordered by simp_begin's barrier)
+        const int n = simp_begin(pa.level, pa.dev_max, pa.out, io, pa.ss, nr, nr >= 0);
+        if (pa.prep_reduce) simp_prep_reduce(pa.res, pa.ss, pa.efrom, pa.eto, pa.nd, pa.valid, n);
     }
 }
 
@@ -1481,101 +1528,193 @@ __global__ void k_group_finalize(const unsigned long long* __restrict__ incl, in
     iteration_tail(status, (int)(v & ((1ull << GCOUNT_SHIFT) - 1)), TA, a_start, Apar, Bpar, chain_end, pa, io);
 }
 
+// path length in OMPL's order (segment lengths summed from the start): the
+// segments in parallel, the sum by lane 0. All lanes call it; block-uniform result.
+__device__ double path_length_blk(const double* P, int n, double* seg) {
+    __shared__ double L;
+    for (int i = threadIdx.x; i + 1 < n; i += blockDim.x) seg[i] = sqrt(dist2(P + i * NQ, P + (i + 1) * NQ));
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int i = 0; i + 1 < n; ++i) t = t + seg[i];
+        L = t;
+    }
+    __syncthreads();
+    return L;
+}
+
+// One step of the simplification program (one block of 256). The step's inputs,
+// written by earlier launches, are fetched at once up front: the head, P, the
+// pending stage's edge flags and corner cuts, and what a publication needs (the
+// PlanIO status, the state counters); the ops then run on LDS, and the head and
+// P go back to `ss` at the end. (Each op's global round trips used to be serial.)
 __global__ __launch_bounds__(256) void k_simp(int ops, int level, int dev_max, double res,
                                               const double* __restrict__ raw,
                                               PlanIO* io, SimpState* ss, double* efrom, double* eto, int* nd,
                                               uint8_t* valid, const unsigned long long* __restrict__ counter,
                                               PlanIO* hio, int seq) {
+    __shared__ SimpHead h;
+    __shared__ double P[SPMAX * NQ], X[SPMAX * NQ];   // X: subdivision / gather scratch
+    __shared__ double T[(SPMAX / 2) * NQ];
+    __shared__ double seg[SPMAX];
+    __shared__ uint8_t vl[(SPMAX - 1) * (SPMAX - 2) / 2];
+    __shared__ short keep[SPMAX];
+    __shared__ int st[ST_WORDS], n_raw_s, mk;
+    __shared__ unsigned long long part[64];
     const int tid = threadIdx.x, nt = blockDim.x;
-    if (ops & OP_BEGIN) simp_begin(level, dev_max, raw, io, ss);
-    if (ops & OP_APPLY_REDUCE) {
-        if (tid == 0 && !ss->done && ss->nedges > 0) {   // greedy walk, in place (writes trail reads)
-            const int n = ss->n;
-            int m = 1, i = 0;
-            while (i < n - 1) {
-                int j = n - 1;
-                while (j > i + 1 && !valid[pair_index(i, j, n)]) --j;
-                for (int d = 0; d < NQ; ++d) ss->P[m * NQ + d] = ss->P[j * NQ + d];
-                ++m;
-                i = j;
+    const bool pub = (ops & (OP_OUT | OP_STATUS)) != 0;
+    // ---- fetch 1: head (wave 0), PlanIO words (wave 1), counter partials (wave 2)
+    if (tid == 0) h = *static_cast<const SimpHead*>(ss);
+    if (tid == 64) {
+        n_raw_s = io->n_raw;
+        if (pub)
+#pragma unroll
+            for (int w = 0; w < ST_WORDS; ++w) st[w] = io->status[w];
+    }
+    if (pub && tid >= 128 && tid < 192) {
+        unsigned long long v = 0;
+        for (int i = tid - 128; i < COUNTER_SLOTS; i += 64) v += counter[i];
+        part[tid - 128] = v;
+    }
+    __syncthreads();
+    if (ops & OP_BEGIN) {   // the raw path -> P, state reset
+        const int n = n_raw_s;
+        const bool on = level > 0 && n >= 0 && n <= dev_max;
+        __syncthreads();
+        if (tid == 0) {
+            h.on = on;
+            h.n = on ? n : 0;
+            h.done = !(on && n >= 3);
+            h.stop = 0;
+            h.nedges = 0;
+            h.edges_total = 0;
+        }
+        __syncthreads();
+    }
+    // ---- fetch 2: P, and the pending stage's results
+    {
+        const double* src = (ops & OP_BEGIN) ? raw : ss->P;
+        for (int k = tid; k < h.n * NQ; k += nt) P[k] = src[k];
+        const bool red = (ops & OP_APPLY_REDUCE) && !h.done && h.nedges > 0;
+        const bool smo = (ops & OP_APPLY_SMOOTH) && !h.done && !h.stop && h.nedges > 0;
+        if (red || smo)
+            for (int e = tid; e < h.nedges; e += nt) vl[e] = valid[e];
+        if (smo)
+            for (int k = tid; k < h.ncand * NQ; k += nt) T[k] = ss->T[k];
+    }
+    __syncthreads();
+    if (ops & OP_APPLY_REDUCE) {   // greedy farthest-valid walk (lane 0), then a gather
+        if (!h.done && h.nedges > 0) {
+            const int n = h.n;
+            if (tid == 0) {
+                int m = 1, i = 0;
+                keep[0] = 0;
+                while (i < n - 1) {
+                    int j = n - 1;
+                    while (j > i + 1 && !vl[pair_index(i, j, n)]) --j;
+                    keep[m++] = (short)j;
+                    i = j;
+                }
+                mk = m;
             }
-            ss->n = m;
+            __syncthreads();
+            const int m = mk;
+            for (int k = tid; k < m * NQ; k += nt) X[k] = P[keep[k / NQ] * NQ + k % NQ];
+            __syncthreads();
+            for (int k = tid; k < m * NQ; k += nt) P[k] = X[k];
+            if (tid == 0) h.n = m;
         }
         __syncthreads();
     }
     if (ops & OP_APPLY_SMOOTH) {
-        if (tid == 0) ss->changed = 0;
+        if (tid == 0) h.changed = 0;
         __syncthreads();
-        if (!ss->done && !ss->stop && ss->nedges > 0) {
-            for (int c = tid; c < ss->ncand; c += nt) {
-                if (!(valid[3 * c] && valid[3 * c + 1] && valid[3 * c + 2])) continue;
-                double* pi = ss->P + (2 * c + 2) * NQ;
-                const double* t = ss->T + c * NQ;
-                if (sqrt(dist2(pi, t)) > ss->min_change) {
+        if (!h.done && !h.stop && h.nedges > 0) {
+            for (int c = tid; c < h.ncand; c += nt) {
+                if (!(vl[3 * c] && vl[3 * c + 1] && vl[3 * c + 2])) continue;
+                double* pi = P + (2 * c + 2) * NQ;
+                const double* t = T + c * NQ;
+                if (sqrt(dist2(pi, t)) > h.min_change) {
                     for (int d = 0; d < NQ; ++d) pi[d] = t[d];
-                    atomicOr(&ss->changed, 1);
+                    atomicOr(&h.changed, 1);
                 }
             }
             __syncthreads();
-            if (tid == 0 && !ss->changed) ss->stop = 1;
+            if (tid == 0 && !h.changed) h.stop = 1;
         }
         __syncthreads();
     }
-    if (ops & OP_ROUND_END) {
-        __shared__ int rollback;
-        if (tid == 0) {
-            rollback = !ss->done && !(path_length(ss->P, ss->n) < ss->len0);
+    if (ops & OP_ROUND_END) {   // keep the round only if the path got shorter
+        if (!h.done) {
+            const bool rollback = !(path_length_blk(P, h.n, seg) < h.len0);
             if (rollback) {
-                ss->n = ss->nprev;
-                ss->done = 1;
+                const int np = h.nprev;
+                for (int k = tid; k < np * NQ; k += nt) P[k] = ss->Pprev[k];
+                __syncthreads();
+                if (tid == 0) {
+                    h.n = np;
+                    h.done = 1;
+                }
             }
         }
-        __syncthreads();
-        if (rollback)
-            for (int k = tid; k < ss->n * NQ; k += nt) ss->P[k] = ss->Pprev[k];
         __syncthreads();
     }
     if (ops & OP_ROUND_BEGIN) {
-        if (tid == 0 && !ss->done) {
-            const int n = ss->n;
+        if (!h.done) {
+            const int n = h.n;
             if (n < 3 || 8 * n - 7 > SPMAX) {
-                ss->done = 1;
+                __syncthreads();
+                if (tid == 0) h.done = 1;
             } else {
-                ss->nprev = n;
-                ss->len0 = path_length(ss->P, n);
-                ss->min_change = ss->len0 / 100.0;
-                ss->stop = 0;
+                const double L = path_length_blk(P, n, seg);
+                if (tid == 0) {
+                    h.nprev = n;
+                    h.len0 = L;
+                    h.min_change = L / 100.0;
+                    h.stop = 0;
+                }
+                for (int k = tid; k < n * NQ; k += nt) ss->Pprev[k] = P[k];
             }
         }
         __syncthreads();
-        if (!ss->done)
-            for (int k = tid; k < ss->n * NQ; k += nt) ss->Pprev[k] = ss->P[k];
+    }
+    if (ops & OP_PREP_REDUCE) {   // every shortcut (i, j >= i + 2) of P
+        const int n = h.n;
+        const bool on = !h.done && n >= 3;
+        if (on)
+            for (int e = tid; e < n * n; e += nt) {
+                const int i = e / n, j = e - i * n;
+                if (j >= i + 2) emit_edge(pair_index(i, j, n), P + i * NQ, P + j * NQ, res, efrom, eto, nd, valid);
+            }
+        __syncthreads();
+        if (tid == 0) {
+            h.nedges = on ? (n - 1) * (n - 2) / 2 : 0;
+            h.edges_total += h.nedges;
+        }
         __syncthreads();
     }
-    if (ops & OP_PREP_REDUCE) simp_prep_reduce(res, ss, efrom, eto, nd, valid);
     if (ops & OP_PREP_SMOOTH) {
-        const bool on = !ss->done && !ss->stop;
-        if (on) {   // PathGeometric::subdivide
-            const int n = ss->n;
+        if (!h.done && !h.stop) {   // PathGeometric::subdivide, then the corner cuts
+            const int n = h.n;
             for (int k = tid; k < 2 * n - 1; k += nt) {
-                double* q = ss->Q + k * NQ;
+                double* q = X + k * NQ;
                 if (k & 1) {
-                    interp(ss->P + (k / 2) * NQ, ss->P + (k / 2 + 1) * NQ, 0.5, q);
+                    interp(P + (k / 2) * NQ, P + (k / 2 + 1) * NQ, 0.5, q);
                 } else {
-                    for (int d = 0; d < NQ; ++d) q[d] = ss->P[(k / 2) * NQ + d];
+                    for (int d = 0; d < NQ; ++d) q[d] = P[(k / 2) * NQ + d];
                 }
             }
             __syncthreads();
-            for (int k = tid; k < (2 * n - 1) * NQ; k += nt) ss->P[k] = ss->Q[k];
+            for (int k = tid; k < (2 * n - 1) * NQ; k += nt) P[k] = X[k];
             __syncthreads();
             const int n2 = 2 * n - 1, ncand = (n2 - 3) / 2;
             for (int c = tid; c < ncand; c += nt) {
                 const int i = 2 * c + 2;
-                const double* a = ss->P + (i - 1) * NQ;
-                const double* b = ss->P + (i + 1) * NQ;
+                const double* a = P + (i - 1) * NQ;
+                const double* b = P + (i + 1) * NQ;
                 double t1[NQ], t2[NQ];
-                interp(a, ss->P + i * NQ, 0.5, t1);
-                interp(ss->P + i * NQ, b, 0.5, t2);
+                interp(a, P + i * NQ, 0.5, t1);
+                interp(P + i * NQ, b, 0.5, t2);
                 interp(t1, t2, 0.5, t1);
                 for (int d = 0; d < NQ; ++d) ss->T[c * NQ + d] = t1[d];
                 emit_edge(3 * c, a, a, res, efrom, eto, nd, valid);
@@ -1584,30 +1723,36 @@ __global__ __launch_bounds__(256) void k_simp(int ops, int level, int dev_max, d
             }
             __syncthreads();
             if (tid == 0) {
-                ss->n = n2;
-                ss->ncand = ncand;
-                ss->nedges = 3 * ncand;
+                h.n = n2;
+                h.ncand = ncand;
+                h.nedges = 3 * ncand;
             }
         } else if (tid == 0) {
-            ss->nedges = 0;
+            h.nedges = 0;
         }
+        if (tid == 0) h.edges_total += h.nedges;
         __syncthreads();
     }
-    if ((ops & OP_PREP_SMOOTH) && tid == 0) ss->edges_total += ss->nedges;
-    if (ops & (OP_OUT | OP_STATUS)) {
+    // ---- write back (the next launches read the head, P and the edge records)
+    if (tid == 0) *static_cast<SimpHead*>(ss) = h;
+    if (ops & (OP_BEGIN | OP_APPLY_REDUCE | OP_APPLY_SMOOTH | OP_ROUND_END | OP_PREP_SMOOTH))
+        for (int k = tid; k < h.n * NQ; k += nt) ss->P[k] = P[k];
+    if (pub) {
         // a status publication carries the output too once nothing is left to do
-        const int n_raw = io->n_raw;
-        const bool out = (ops & OP_OUT) != 0 || ss->done;
-        const int m = !out ? 0 : ss->on ? ss->n : (n_raw >= 0 && n_raw <= dev_max ? n_raw : 0);
-        const double* src = ss->on ? ss->P : raw;
+        const int n_raw = n_raw_s;
+        const bool out = (ops & OP_OUT) != 0 || h.done;
+        const int m = !out ? 0 : h.on ? h.n : (n_raw >= 0 && n_raw <= dev_max ? n_raw : 0);
+        const double* src = h.on ? P : raw;
         for (int k = tid; k < m * NQ; k += nt) hio->path[k] = src[k];
         if (tid == 0) {
+            unsigned long long cs = 0;
+            for (int i = 0; i < 64; ++i) cs += part[i];
 #pragma unroll
-            for (int w = 0; w < ST_WORDS; ++w) hio->status[w] = io->status[w];
+            for (int w = 0; w < ST_WORDS; ++w) hio->status[w] = st[w];
             hio->n_raw = n_raw;
             hio->n_out = m;
-            hio->counter = counter_sum(counter);
-            hio->simp_edges = ss->edges_total;
+            hio->counter = cs;
+            hio->simp_edges = h.edges_total;
             hio->out = out ? 1 : 0;
         }
         __threadfence_system();

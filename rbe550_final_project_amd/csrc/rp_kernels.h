@@ -464,8 +464,9 @@ __global__ __launch_bounds__(NNBLOCK) void k_ext_nn(const double* __restrict__ A
     // near_in: nearest nodes from the split search (k_nn_part + k_nn_reduce)
     const int32_t nn = near_in ? (active ? near_in[k] : 0) : nn_tiled(A, TA, qr, active, tile);
     if (!active) return;
-    double qn[NQ];
-    const double* near = A + (int64_t)nn * NQ;
+    double qn[NQ], near[NQ];
+#pragma unroll
+    for (int d = 0; d < NQ; ++d) near[d] = A[(int64_t)nn * NQ + d];
     steer(near, qr, range, qn);
     double* f = efrom + k * NQ;
     double* t = eto + k * NQ;
@@ -474,7 +475,8 @@ __global__ __launch_bounds__(NNBLOCK) void k_ext_nn(const double* __restrict__ A
         f[d] = a_start ? near[d] : qn[d];
         t[d] = a_start ? qn[d] : near[d];
     }
-    nd[k] = segment_count(f, t, res);
+    // (from the registers, not read back from the records: dist2 is symmetric)
+    nd[k] = segment_count(near, qn, res);
     valid[k] = 1;
     near_out[k] = nn;
 }
@@ -767,32 +769,40 @@ __global__ void k_ext_append(const int32_t* __restrict__ res, const int32_t* __r
 // threads keeps the global item order.
 constexpr int FUSE_THREADS = 1024, FUSE_MAX = FUSE_THREADS * 4;
 
-// exclusive scan of one int per thread over a FUSE_THREADS block; *total = sum
-__device__ __forceinline__ int block_scan_excl(int v, int* lds, int* total) {
+// block barrier ordering LDS only: unlike __syncthreads it does not wait for the
+// block's outstanding global loads and stores (use where no lane reads global data
+// another lane of the block wrote before it)
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// exclusive scan of one value per thread over a FUSE_THREADS block; *total = sum.
+// Wave scans, then every lane sums the wave totals below it (independent LDS reads,
+// not one lane's serial pass); LDS-only barriers.
+template <typename T>
+__device__ __forceinline__ T block_scan_excl(T v, T* lds, T* total) {
     constexpr int NW = FUSE_THREADS / 64;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    int x = v;
+    T x = v;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o, 64);
+        const T y = __shfl_up(x, o, 64);
         if (lane >= o) x += y;
     }
     if (lane == 63) lds[w] = x;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int run = 0;
-        for (int k = 0; k < NW; ++k) {
-            const int t = lds[k];
-            lds[k] = run;
-            run += t;
-        }
-        lds[NW] = run;
+    lds_barrier();
+    T pre = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        const T t = lds[k];
+        pre += k < w ? t : (T)0;
+        tot += t;
     }
-    __syncthreads();
-    const int ex = lds[w] + x - v;
-    *total = lds[NW];
-    __syncthreads();
-    return ex;
+    *total = tot;
+    lds_barrier();   // (lds reusable)
+    return pre + x - v;
 }
 
 template <int ITEMS>
@@ -870,7 +880,7 @@ __global__ __launch_bounds__(NNBLOCK) void k_conn_nn(const double* __restrict__ 
             f[d] = a_start ? nxt[d] : cur[d];
             t[d] = a_start ? cur[d] : nxt[d];
         }
-        nd[e] = segment_count(f, t, res);
+        nd[e] = segment_count(cur, nxt, res);
         valid[e] = 1;
 #pragma unroll
         for (int d = 0; d < NQ; ++d) cur[d] = nxt[d];
@@ -910,7 +920,9 @@ __global__ __launch_bounds__(NNBLOCK) void k_ext_conn_nn(const double* __restric
     sample_state(seed, g0 + (uint64_t)(active ? k : 0), bd.lo, bd.hi, qr);
     // near_in / y_in: nearest nodes from the split search (large trees)
     const int32_t nn = near_in ? (active ? near_in[k] : 0) : nn_tiled(A, TA, qr, active, tile);
-    const double* near = A + (int64_t)(nn >= 0 ? nn : 0) * NQ;
+    double near[NQ];
+#pragma unroll
+    for (int d = 0; d < NQ; ++d) near[d] = A[(int64_t)(nn >= 0 ? nn : 0) * NQ + d];
     steer(near, qr, range, x);
     const int32_t y = y_in ? (active ? y_in[k] : 0) : nn_tiled(Bt, TB, x, active, tile);
     if (!active) return;
@@ -924,7 +936,7 @@ __global__ __launch_bounds__(NNBLOCK) void k_ext_conn_nn(const double* __restric
             f[d] = a_start ? near[d] : x[d];
             t[d] = a_start ? x[d] : near[d];
         }
-        nd[e] = segment_count(f, t, res) | (a_start ? 0 : ND_FROM);
+        nd[e] = segment_count(near, x, res) | (a_start ? 0 : ND_FROM);   // (registers; dist2 symmetric)
         valid[e] = 1;
     }
     double cur[NQ], nxt[NQ];
@@ -946,7 +958,7 @@ __global__ __launch_bounds__(NNBLOCK) void k_ext_conn_nn(const double* __restric
             f[d] = a_start ? nxt[d] : cur[d];
             t[d] = a_start ? cur[d] : nxt[d];
         }
-        nd[e] = segment_count(f, t, res) | (a_start ? ND_FROM : 0);
+        nd[e] = segment_count(cur, nxt, res) | (a_start ? ND_FROM : 0);
         valid[e] = 1;
 #pragma unroll
         for (int d = 0; d < NQ; ++d) cur[d] = nxt[d];
@@ -1052,21 +1064,55 @@ __global__ void k_conn_append(const int32_t* __restrict__ rec, const int32_t* __
     if (b && lane == 0) atomicMin(first_reached, (int)(t + __builtin_ctzll(b)));
 }
 
+// what a fused accept kernel already holds in LDS of its iteration's appends: the
+// tail's join-node lookups and parent walks through new nodes then read LDS, not
+// a chain of dependent global loads
+struct TailLds {
+    const int32_t* apar; int64_t a0; int na;   // parents of tree A's new nodes [a0, a0 + na)
+    const int32_t* bpar; int64_t b0; int nb;   // parents of tree B's new nodes (the first nb)
+    const int32_t* cend; int nc;               // chain_end[t], t < nc
+    int first;                                 // ST_FIRST
+    double* P;                                 // LDS path (SPMAX states) for the simplifier's first step
+    // where the new nodes' states were copied from (records of the previous launch,
+    // visible without waiting for this block's stores): tree A's node a0 + t from
+    // ext_node + asrc[t] * NQ, tree B's node b0 + j from chain_node + bsrc[j] * NQ
+    const int32_t* asrc; const int32_t* bsrc;
+    const double* ext_node; const double* chain_node;
+    // state of node v of tree A (a) or B, `base` = that tree's states
+    __device__ __forceinline__ const double* state(bool a, int32_t v, const double* base) const {
+        if (a && v >= a0 && v < a0 + na) return ext_node + (int64_t)asrc[v - a0] * NQ;
+        if (!a && v >= b0 && v < b0 + nb) return chain_node + (int64_t)bsrc[v - b0] * NQ;
+        return base + (int64_t)v * NQ;
+    }
+};
+__device__ __forceinline__ int32_t parent_of(const int32_t* g, const int32_t* l, int64_t l0, int ln, int32_t v) {
+    if (v == 0) return -1;   // the roots (k_plan_init)
+    return (l && v >= l0 && v < l0 + ln) ? l[v - l0] : g[v];
+}
+
 // end of an iteration (single lane): nodes added to tree B; on success the join
 // nodes (OMPL steps back one node on the start side to avoid a duplicate state).
+// *sn = -2 when unsolved.
 __device__ __forceinline__ void finalize_one(int* status, int added, int64_t TA, int a_start,
-                                             const int32_t* Apar, const int32_t* Bpar, const int32_t* chain_end) {
+                                             const int32_t* Apar, const int32_t* Bpar, const int32_t* chain_end,
+                                             const TailLds* ov, int* sn, int* gn) {
     status[ST_ADDED] = added;
-    const int fr = status[ST_FIRST];
+    const int fr = ov ? ov->first : status[ST_FIRST];
+    *sn = -2;
     if (fr != 0x7fffffff) {
-        const int32_t end = chain_end[fr];
+        const int32_t end = (ov && fr < ov->nc) ? ov->cend[fr] : chain_end[fr];
+        int32_t s, g;
         if (a_start) {   // x in the start tree (tree A), chain end in the goal tree
-            status[ST_SNODE] = Apar[TA + fr];
-            status[ST_GNODE] = end;
+            s = ov ? parent_of(Apar, ov->apar, ov->a0, ov->na, (int32_t)(TA + fr)) : Apar[TA + fr];
+            g = end;
         } else {         // chain end in the start tree (tree B), x in the goal tree
-            status[ST_SNODE] = Bpar[end];
-            status[ST_GNODE] = (int32_t)(TA + fr);
+            s = ov ? parent_of(Bpar, ov->bpar, ov->b0, ov->nb, end) : Bpar[end];
+            g = (int32_t)(TA + fr);
         }
+        status[ST_SNODE] = s;
+        status[ST_GNODE] = g;
+        *sn = s;
+        *gn = g;
     }
 }
 
@@ -1116,11 +1162,20 @@ __device__ __forceinline__ double path_length(const double* P, int n) {
 
 __device__ __forceinline__ void emit_edge(int e, const double* a, const double* b, double res, double* efrom,
                                           double* eto, int* nd, uint8_t* valid) {
+    // endpoints into registers first: the stores may alias a / b for the compiler,
+    // which would otherwise wait out every load before the next
+    double av[NQ], bv[NQ];
+#pragma unroll
     for (int d = 0; d < NQ; ++d) {
-        efrom[(int64_t)e * NQ + d] = a[d];
-        eto[(int64_t)e * NQ + d] = b[d];
+        av[d] = a[d];
+        bv[d] = b[d];
     }
-    nd[e] = segment_count(a, b, res);
+#pragma unroll
+    for (int d = 0; d < NQ; ++d) {
+        efrom[(int64_t)e * NQ + d] = av[d];
+        eto[(int64_t)e * NQ + d] = bv[d];
+    }
+    nd[e] = segment_count(av, bv, res);
     valid[e] = 1;
 }
 
@@ -1131,8 +1186,9 @@ __device__ __forceinline__ void emit_edge(int e, const double* a, const double* 
 __device__ int simp_begin(int level, int dev_max, const double* __restrict__ raw, const PlanIO* io,
                           SimpState* ss, int n_known = -3, bool p_ready = false) {
     __shared__ int bn;
+    const bool known = n_known >= -1;
     if (threadIdx.x == 0) {
-        const int n = n_known >= -1 ? n_known : io->n_raw;
+        const int n = known ? n_known : io->n_raw;
         const bool on = level > 0 && n >= 0 && n <= dev_max;
         ss->on = on;
         ss->n = bn = on ? n : 0;
@@ -1141,30 +1197,38 @@ __device__ int simp_begin(int level, int dev_max, const double* __restrict__ raw
         ss->nedges = 0;
         ss->edges_total = 0;
     }
+    if (p_ready) {
+        lds_barrier();
+        return bn;
+    }
     __syncthreads();
     const int n = bn;
-    if (!p_ready)
-        for (int k = threadIdx.x; k < n * NQ; k += blockDim.x) ss->P[k] = raw[k];
+    for (int k = threadIdx.x; k < n * NQ; k += blockDim.x) ss->P[k] = raw[k];
     __syncthreads();
     return n;
 }
 
 // OP_PREP_REDUCE (block-cooperative): every shortcut (i, j >= i + 2) of P
 // n_known >= 0: ss->n as the caller holds it (right after simp_begin: done = n < 3)
+// Psrc: P as the caller holds it (LDS), else ss->P. n_known >= 0: right after
+// simp_begin (edges_total = 0), at the end of the caller's kernel (no barrier after)
 __device__ void simp_prep_reduce(double res, SimpState* ss, double* efrom, double* eto, int* nd, uint8_t* valid,
-                                 int n_known = -1) {
+                                 int n_known = -1, const double* Psrc = nullptr) {
+    const double* P = Psrc ? Psrc : ss->P;
     const int n = n_known >= 0 ? n_known : ss->n;
     const bool on = n_known >= 0 ? n >= 3 : !ss->done && n >= 3;
     if (on)
         for (int e = threadIdx.x; e < n * n; e += blockDim.x) {
             const int i = e / n, j = e - i * n;
-            if (j >= i + 2) emit_edge(pair_index(i, j, n), ss->P + i * NQ, ss->P + j * NQ, res, efrom, eto, nd, valid);
+            if (j >= i + 2) emit_edge(pair_index(i, j, n), P + i * NQ, P + j * NQ, res, efrom, eto, nd, valid);
         }
     if (threadIdx.x == 0) {
-        ss->nedges = on ? (n - 1) * (n - 2) / 2 : 0;
-        ss->edges_total += ss->nedges;
+        const int ne = on ? (n - 1) * (n - 2) / 2 : 0;
+        ss->nedges = ne;
+        if (n_known >= 0) ss->edges_total = ne;
+        else ss->edges_total += ne;
     }
-    __syncthreads();
+    if (n_known < 0) __syncthreads();
 }
 
 // where a solution path goes, and the first simplification step (OP_BEGIN, and
@@ -1193,37 +1257,51 @@ struct PathArgs {
 // copied by every lane, into pa.out and, when `also` (P of the simplification,
 // n <= also_max), there too. Returns n_raw (block-uniform).
 constexpr int PATH_LDS = 512;
+// ov / a_start: the caller's LDS view of this iteration's new nodes (tree A = the
+// start tree when a_start), also the path's LDS copy (ov->P) next to `also`.
 __device__ int build_path(const PathArgs& pa, int32_t s_node, int32_t g_node, PlanIO* io, double* also = nullptr,
-                          int also_max = -1) {
+                          int also_max = -1, const TailLds* ov = nullptr, int a_start = 1) {
     __shared__ int32_t sidx[PATH_LDS], gidx[PATH_LDS];
     __shared__ int bns, bng;
     const int tid = threadIdx.x;
     const int gl = blockDim.x >= 128 ? 64 : 0;   // the goal walk's lane
     if (tid == 0) {
+        const int32_t* l = ov ? (a_start ? ov->apar : ov->bpar) : nullptr;
+        const int64_t l0 = ov ? (a_start ? ov->a0 : ov->b0) : 0;
+        const int ln = ov ? (a_start ? ov->na : ov->nb) : 0;
         int ns = 0;
-        for (int32_t v = s_node; v >= 0; v = pa.Spar[v], ++ns)
+        for (int32_t v = s_node; v >= 0; v = parent_of(pa.Spar, l, l0, ln, v), ++ns)
             if (ns < PATH_LDS) sidx[ns] = v;
         bns = ns;
     }
     if (tid == gl) {
+        const int32_t* l = ov ? (a_start ? ov->bpar : ov->apar) : nullptr;
+        const int64_t l0 = ov ? (a_start ? ov->b0 : ov->a0) : 0;
+        const int ln = ov ? (a_start ? ov->nb : ov->na) : 0;
         int ng = 0;
-        for (int32_t v = g_node; v >= 0; v = pa.Gpar[v], ++ng)
+        for (int32_t v = g_node; v >= 0; v = parent_of(pa.Gpar, l, l0, ln, v), ++ng)
             if (ng < PATH_LDS) gidx[ng] = v;
         bng = ng;
     }
     __syncthreads();
+    RP_TSTAMP(0, 5);
     const int ns = bns, ng = bng, n = ns + ng;
     if (n > pa.cap) {
         if (tid == 0) io->n_raw = -1;
         return -1;
     }
     double* p2 = n <= also_max ? also : nullptr;
+    double* p3 = (p2 && ov) ? ov->P : nullptr;
     if (ns <= PATH_LDS && ng <= PATH_LDS) {
         for (int k = tid; k < n * NQ; k += blockDim.x) {
             const int i = k / NQ, d = k - i * NQ;
-            const double v = i < ns ? pa.S[(int64_t)sidx[ns - 1 - i] * NQ + d] : pa.G[(int64_t)gidx[i - ns] * NQ + d];
+            const double v = !ov ? (i < ns ? pa.S[(int64_t)sidx[ns - 1 - i] * NQ + d]
+                                           : pa.G[(int64_t)gidx[i - ns] * NQ + d])
+                                 : (i < ns ? ov->state(a_start, sidx[ns - 1 - i], pa.S)[d]
+                                           : ov->state(!a_start, gidx[i - ns], pa.G)[d]);
             pa.out[k] = v;
             if (p2) p2[k] = v;
+            if (p3) p3[k] = v;
         }
     } else if (tid == 0) {   // long paths: walk again
         int i = ns - 1;
@@ -1234,7 +1312,10 @@ __device__ int build_path(const PathArgs& pa, int32_t s_node, int32_t g_node, Pl
             for (int d = 0; d < NQ; ++d) pa.out[i * NQ + d] = pa.G[(int64_t)v * NQ + d];
         if (p2)
             for (int k = 0; k < n * NQ; ++k) p2[k] = pa.out[k];
+        if (p3)
+            for (int k = 0; k < n * NQ; ++k) p3[k] = pa.out[k];
     }
+    RP_TSTAMP(0, 6);
     if (tid == 0) io->n_raw = n;
     return n;
 }
@@ -1242,22 +1323,23 @@ __device__ int build_path(const PathArgs& pa, int32_t s_node, int32_t g_node, Pl
 // block tail of the last kernel of an iteration: join nodes and, on success, the
 // solution path. The status reaches the host through k_simp, which follows.
 __device__ void iteration_tail(int* status, int added, int64_t TA, int a_start, const int32_t* Apar,
-                               const int32_t* Bpar, const int32_t* chain_end, const PathArgs& pa, PlanIO* io) {
+                               const int32_t* Bpar, const int32_t* chain_end, const PathArgs& pa, PlanIO* io,
+                               const TailLds* ov = nullptr) {
     __shared__ int sn, gn;
-    if (threadIdx.x == 0) {
-        finalize_one(status, added, TA, a_start, Apar, Bpar, chain_end);
-        const bool ok = status[ST_FIRST] != 0x7fffffff;
-        sn = ok ? status[ST_SNODE] : -2;
-        gn = status[ST_GNODE];
-    }
+    if (threadIdx.x == 0) finalize_one(status, added, TA, a_start, Apar, Bpar, chain_end, ov, &sn, &gn);
     __syncthreads();
+    RP_TSTAMP(0, 4);
     const int nr = sn != -2 ? build_path(pa, sn, gn, io, pa.ss ? pa.ss->P : nullptr,
-                                         pa.level > 0 ? pa.dev_max : -1)
+                                         pa.level > 0 ? pa.dev_max : -1, ov, a_start)
                             : -3;   // no solution: simp_begin reads io->n_raw
     if (pa.ss) {   // (build_path's writes are ordered by simp_begin's barrier)
         const int n = simp_begin(pa.level, pa.dev_max, pa.out, io, pa.ss, nr, nr >= 0);
-        if (pa.prep_reduce) simp_prep_reduce(pa.res, pa.ss, pa.efrom, pa.eto, pa.nd, pa.valid, n);
+        RP_TSTAMP(0, 7);
+        if (pa.prep_reduce)
+            simp_prep_reduce(pa.res, pa.ss, pa.efrom, pa.eto, pa.nd, pa.valid, n,
+                             (ov && ov->P && nr >= 0) ? ov->P : nullptr);
     }
+    RP_TSTAMP(0, 8);
 }
 
 __global__ void k_finalize(int* status, const int32_t* __restrict__ inclL, int64_t TA, int a_start,
@@ -1307,6 +1389,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_conn_accept_small(
 // The nodes are copied from the edge records k_ext_conn_nn wrote (sample k's new
 // node is the checked endpoint of edge k * G, chain node s that of edge k * G + 1 +
 // s), not recomputed.
+constexpr int TAIL_LB = 4096;   // tree-B nodes an accept kernel keeps the parents of in LDS
 template <int ITEMS>
 __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
     const int* __restrict__ gfail, const int32_t* __restrict__ near, const int32_t* __restrict__ y,
@@ -1314,29 +1397,48 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
     const double* __restrict__ eto, double* A, int32_t* Apar, uint8_t* Acand, int64_t TA, double* Bt,
     int32_t* Bpar, uint8_t* Bcand, int64_t TB, int a_start, int32_t* chain_end, int* status,
     const uint8_t* valid, int64_t sg_edge, int sg_stride, PathArgs pa, PlanIO* io) {
-    __shared__ int lds[FUSE_THREADS / 64 + 1];
-    __shared__ int first;
-    const int64_t k0 = (int64_t)threadIdx.x * ITEMS;
-    int L[ITEMS];
-    int na = 0, nl = 0;
-#pragma unroll
-    for (int r = 0; r < ITEMS; ++r) {
-        const int64_t k = k0 + r;
-        const int g = k < B ? gfail[k] : 0;
-        const int mk = k < B ? (m[k] & CHAIN_LEN) : 0;
-        L[r] = g > 0 ? (g - 1 < mk ? g - 1 : mk) : -1;   // -1: extension rejected
-        na += L[r] >= 0;
-        nl += L[r] > 0 ? L[r] : 0;
-    }
-    int totalA, totalB;
-    const int exA = block_scan_excl(na, lds, &totalA);
-    const int exB = block_scan_excl(nl, lds, &totalB);
-    if (threadIdx.x == 0) first = 0x7fffffff;
-    __syncthreads();
+    __shared__ unsigned long long lds64[FUSE_THREADS / 64];
+    __shared__ int first, sgv;
+    __shared__ int32_t l_apar[FUSE_MAX], l_cend[FUSE_MAX], l_bpar[TAIL_LB], l_asrc[FUSE_MAX], l_bsrc[TAIL_LB];
+    __shared__ double l_P[SPMAX * NQ];
     // the checked endpoint of an edge is the new node: `to` on the start tree's
     // side (a_start: extension near -> new; chain next -> prev), else `from`
     const double* ext_node = a_start ? eto : efrom;
     const double* chain_node = a_start ? efrom : eto;
+    if (threadIdx.x == 64 && sg_edge >= 0) sgv = sg_flags(valid, sg_edge, sg_stride);   // (another wave)
+    RP_TSTAMP(0, 0);
+    // every per-sample input fetched at once (one round trip)
+    const int64_t k0 = (int64_t)threadIdx.x * ITEMS;
+    int L[ITEMS], M[ITEMS];
+    int32_t NR[ITEMS], Y[ITEMS];
+    double X[ITEMS][NQ];
+    int na = 0, nl = 0;
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+        const int64_t k = k0 + r;
+        const bool in = k < B;
+        const int64_t kc = in ? k : 0;
+        const int g = in ? gfail[kc] : 0;
+        M[r] = m[kc];
+        NR[r] = near[kc];
+        Y[r] = y[kc];
+        const double* xs = ext_node + kc * G * NQ;
+#pragma unroll
+        for (int d = 0; d < NQ; ++d) X[r][d] = xs[d];
+        const int mk = in ? (M[r] & CHAIN_LEN) : 0;
+        L[r] = g > 0 ? (g - 1 < mk ? g - 1 : mk) : -1;   // -1: extension rejected
+        na += L[r] >= 0;
+        nl += L[r] > 0 ? L[r] : 0;
+    }
+    RP_TSTAMP(0, 1);
+    // both scans in one: accepted extensions (high word), chain nodes (low word)
+    unsigned long long tot;
+    const unsigned long long ex = block_scan_excl(((unsigned long long)na << 32) | (unsigned)nl, lds64, &tot);
+    const int exA = (int)(ex >> 32), exB = (int)(ex & 0xffffffffu);
+    const int totalA = (int)(tot >> 32), totalB = (int)(tot & 0xffffffffu);
+    if (threadIdx.x == 0) first = 0x7fffffff;
+    lds_barrier();
+    RP_TSTAMP(0, 2);
     int t = exA;
     int64_t off = TB + exB;
 #pragma unroll
@@ -1344,32 +1446,52 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
         if (L[r] < 0) continue;
         const int64_t k = k0 + r, e0 = k * G;
         const int64_t pos = TA + t;
-        const double* xs = ext_node + e0 * NQ;
-        for (int d = 0; d < NQ; ++d) A[pos * NQ + d] = xs[d];
-        Apar[pos] = near[k];
-        int32_t par = y[k];
+        for (int d = 0; d < NQ; ++d) A[pos * NQ + d] = X[r][d];
+        Apar[pos] = NR[r];
+        l_apar[t] = NR[r];
+        l_asrc[t] = (int32_t)e0;
+        int32_t par = Y[r];
         for (int s = 0; s < L[r]; ++s) {
-            const double* cs = chain_node + (e0 + 1 + s) * NQ;
-            for (int d = 0; d < NQ; ++d) Bt[(off + s) * NQ + d] = cs[d];
+            const int64_t j = off + s - TB;
+            if (j < TAIL_LB) {   // state copied below, by the whole block
+                l_bpar[j] = par;
+                l_bsrc[j] = (int32_t)(e0 + 1 + s);
+            } else {
+                const double* cs = chain_node + (e0 + 1 + s) * NQ;
+                for (int d = 0; d < NQ; ++d) Bt[(off + s) * NQ + d] = cs[d];
+            }
             Bpar[off + s] = par;
             Bcand[off + s] = 0;
             par = (int32_t)(off + s);
         }
-        const int mk = m[k];
+        const int mk = M[r];
         const bool reached = L[r] == (mk & CHAIN_LEN) && (mk & CHAIN_REACHES);
         chain_end[t] = L[r] > 0 ? par : -1;
+        l_cend[t] = L[r] > 0 ? par : -1;
         Acand[pos] = (!reached && a_start) ? 1 : 0;
         if (reached) atomicMin(&first, t);
         off += L[r];
         ++t;
     }
-    __syncthreads();
+    // the tail reads this block's appends from LDS and their sources, unless tree B
+    // grew past the LDS window (then from global: a full barrier)
+    if (totalB > TAIL_LB) __syncthreads();
+    else lds_barrier();
+    // the chain nodes' states: one parallel copy (not a serial chain per sample)
+    const int nbw = totalB < TAIL_LB ? totalB : TAIL_LB;
+    for (int k = threadIdx.x; k < nbw * NQ; k += FUSE_THREADS) {
+        const int j = k / NQ, d = k - j * NQ;
+        Bt[(TB + j) * NQ + d] = chain_node[(int64_t)l_bsrc[j] * NQ + d];
+    }
     if (threadIdx.x == 0) {
         status[ST_NACC] = totalA;
         status[ST_FIRST] = first;
-        if (sg_edge >= 0) status[ST_SG] = sg_flags(valid, sg_edge, sg_stride);
+        if (sg_edge >= 0) status[ST_SG] = sgv;
     }
-    iteration_tail(status, totalB, TA, a_start, Apar, Bpar, chain_end, pa, io);
+    RP_TSTAMP(0, 3);
+    const TailLds ov{l_apar, TA, totalA, l_bpar, TB, totalB < TAIL_LB ? totalB : TAIL_LB, l_cend, totalA, first, l_P,
+                     l_asrc, l_bsrc, ext_node, chain_node};
+    iteration_tail(status, totalB, TA, a_start, Apar, Bpar, chain_end, pa, io, &ov);
 }
 
 // solution path for host-chosen join nodes (approximate solutions)
@@ -1557,12 +1679,14 @@ __global__ __launch_bounds__(256) void k_simp(int ops, int level, int dev_max, d
     __shared__ double P[SPMAX * NQ], X[SPMAX * NQ];   // X: subdivision / gather scratch
     __shared__ double T[(SPMAX / 2) * NQ];
     __shared__ double seg[SPMAX];
-    __shared__ uint8_t vl[(SPMAX - 1) * (SPMAX - 2) / 2];
+    __shared__ uint32_t vlw[((SPMAX - 1) * (SPMAX - 2) / 2 + 3) / 4];
+    uint8_t* vl = reinterpret_cast<uint8_t*>(vlw);
     __shared__ short keep[SPMAX];
     __shared__ int st[ST_WORDS], n_raw_s, mk;
     __shared__ unsigned long long part[64];
     const int tid = threadIdx.x, nt = blockDim.x;
     const bool pub = (ops & (OP_OUT | OP_STATUS)) != 0;
+    RP_TSTAMP(1, 0);
     // ---- fetch 1: head (wave 0), PlanIO words (wave 1), counter partials (wave 2)
     if (tid == 0) h = *static_cast<const SimpHead*>(ss);
     if (tid == 64) {
@@ -1576,7 +1700,17 @@ __global__ __launch_bounds__(256) void k_simp(int ops, int level, int dev_max, d
         for (int i = tid - 128; i < COUNTER_SLOTS; i += 64) v += counter[i];
         part[tid - 128] = v;
     }
+    // ... and, speculatively, the first SPEC_S states of P, SPEC_E edge flags and
+    // SPEC_S / 2 corner cuts (most paths fit: then no second round trip)
+    constexpr int SPEC_S = 64, SPEC_E = 2048;
+    const double* psrc = (ops & OP_BEGIN) ? raw : ss->P;
+    for (int k = tid; k < SPEC_S * NQ; k += nt) P[k] = psrc[k];
+    if (ops & (OP_APPLY_REDUCE | OP_APPLY_SMOOTH))
+        for (int w = tid; w < SPEC_E / 4; w += nt) vlw[w] = reinterpret_cast<const uint32_t*>(valid)[w];
+    if (ops & OP_APPLY_SMOOTH)
+        for (int k = tid; k < (SPEC_S / 2) * NQ; k += nt) T[k] = ss->T[k];
     __syncthreads();
+    RP_TSTAMP(1, 1);
     if (ops & OP_BEGIN) {   // the raw path -> P, state reset
         const int n = n_raw_s;
         const bool on = level > 0 && n >= 0 && n <= dev_max;
@@ -1591,18 +1725,21 @@ __global__ __launch_bounds__(256) void k_simp(int ops, int level, int dev_max, d
         }
         __syncthreads();
     }
-    // ---- fetch 2: P, and the pending stage's results
+    // ---- fetch 2: the rest of P and of the pending stage's results
     {
-        const double* src = (ops & OP_BEGIN) ? raw : ss->P;
-        for (int k = tid; k < h.n * NQ; k += nt) P[k] = src[k];
-        const bool red = (ops & OP_APPLY_REDUCE) && !h.done && h.nedges > 0;
-        const bool smo = (ops & OP_APPLY_SMOOTH) && !h.done && !h.stop && h.nedges > 0;
-        if (red || smo)
-            for (int e = tid; e < h.nedges; e += nt) vl[e] = valid[e];
-        if (smo)
-            for (int k = tid; k < h.ncand * NQ; k += nt) T[k] = ss->T[k];
+        const int np = h.n, ne = h.nedges, nc = h.ncand;
+        const bool red = (ops & OP_APPLY_REDUCE) && !h.done && ne > 0;
+        const bool smo = (ops & OP_APPLY_SMOOTH) && !h.done && !h.stop && ne > 0;
+        if (np > SPEC_S || ((red || smo) && ne > SPEC_E) || (smo && nc > SPEC_S / 2)) {
+            for (int k = SPEC_S * NQ + tid; k < np * NQ; k += nt) P[k] = psrc[k];
+            if (red || smo)
+                for (int e = SPEC_E + tid; e < ne; e += nt) vl[e] = valid[e];
+            if (smo)
+                for (int k = (SPEC_S / 2) * NQ + tid; k < nc * NQ; k += nt) T[k] = ss->T[k];
+            __syncthreads();
+        }
     }
-    __syncthreads();
+    RP_TSTAMP(1, 2);
     if (ops & OP_APPLY_REDUCE) {   // greedy farthest-valid walk (lane 0), then a gather
         if (!h.done && h.nedges > 0) {
             const int n = h.n;
@@ -1733,6 +1870,7 @@ __global__ __launch_bounds__(256) void k_simp(int ops, int level, int dev_max, d
         if (tid == 0) h.edges_total += h.nedges;
         __syncthreads();
     }
+    RP_TSTAMP(1, 3);
     // ---- write back (the next launches read the head, P and the edge records)
     if (tid == 0) *static_cast<SimpHead*>(ss) = h;
     if (ops & (OP_BEGIN | OP_APPLY_REDUCE | OP_APPLY_SMOOTH | OP_ROUND_END | OP_PREP_SMOOTH))
@@ -1759,6 +1897,7 @@ __global__ __launch_bounds__(256) void k_simp(int ops, int level, int dev_max, d
         __syncthreads();
         if (tid == 0) publish_seq(hio, seq);
     }
+    RP_TSTAMP(1, 4);
 }
 
 // approximate solution: argmin over candidate start-tree nodes of dist2(node, goal),

@@ -1989,6 +1989,11 @@ int rp_debug_stamps(unsigned long long* out, int64_t n) {
     if (n > (int64_t)STAMP_WAVES * STAMP_K) n = (int64_t)STAMP_WAVES * STAMP_K;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -1;
 }
+// ... and the plan kernels' block stamps (8 kernels x TSTAMP_K)
+int rp_debug_tstamps(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tstamps), sizeof(unsigned long long) * 8 * TSTAMP_K) == hipSuccess
+               ? 0 : -1;
+}
 #endif
 
 // Numerics self-test (test-only entry, not in the public header's contract list):

@@ -38,8 +38,21 @@ __device__ __forceinline__ void stamp(int k) {
     if (w < STAMP_WAVES && __lane_id() == __builtin_amdgcn_readfirstlane(__lane_id())) g_stamps[w * STAMP_K + k] = t;
 }
 #define RP_STAMP(k) stamp(k)
+// single-block kernels of the plan path: lane 0 of the block records
+// s_memrealtime (100 MHz) at point k of kernel slot `kid` (g_tstamps[kid][k])
+constexpr int TSTAMP_K = 16;
+__device__ unsigned long long g_tstamps[8 * TSTAMP_K];
+__device__ __forceinline__ void tstamp(int kid, int k) {
+    __builtin_amdgcn_sched_barrier(0);
+    unsigned long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (threadIdx.x == 0 && blockIdx.x == 0) g_tstamps[kid * TSTAMP_K + k] = t;
+}
+#define RP_TSTAMP(kid, k) tstamp(kid, k)
 #else
 #define RP_STAMP(k)
+#define RP_TSTAMP(kid, k)
 #endif
 
 // min / max / clamp as single instructions (v_min_f32, v_max_f32, v_med3_f32). The

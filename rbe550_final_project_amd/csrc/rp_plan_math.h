@@ -14,13 +14,20 @@ namespace rp {
 
 constexpr uint32_t SAMPLE_TAG = 0x52425035u;
 
+// (a 64-bit product, not __umulhi: the device-library call is not inlined into
+// kernels built with -mno-amdgpu-ieee, whose attributes differ; this is one
+// v_mul_hi_u32)
+__device__ __forceinline__ uint32_t mulhi32(uint32_t a, uint32_t b) {
+    return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
+}
+
 __device__ __forceinline__ void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
 #pragma unroll
     for (int r = 0; r < 10; ++r) {
         if (r > 0) { k0 += 0x9E3779B9u; k1 += 0xBB67AE85u; }
-        const uint32_t hi0 = __umulhi(0xD2511F53u, c[0]);
+        const uint32_t hi0 = mulhi32(0xD2511F53u, c[0]);
         const uint32_t lo0 = 0xD2511F53u * c[0];
-        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c[2]);
+        const uint32_t hi1 = mulhi32(0xCD9E8D57u, c[2]);
         const uint32_t lo1 = 0xCD9E8D57u * c[2];
         const uint32_t n0 = hi1 ^ c[1] ^ k0;
         const uint32_t n2 = hi0 ^ c[3] ^ k1;

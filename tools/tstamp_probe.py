@@ -1,0 +1,59 @@
+"""Phase durations inside the plan path's single-block kernels from a diagnostic
+build (-DRP_STAMPS): lane 0 of block 0 records s_memrealtime (100 MHz) at fixed
+points (rp_kernels.h RP_TSTAMP). Runs the goal3 RRT-forced queries.
+usage: RBE_LIB_PATH=build/variants/lib_stamps.so python tools/tstamp_probe.py [workload] [batch]"""
+import ctypes as C
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from rbe550_final_project_amd import _abi, model, scenes  # noqa: E402
+from rbe550_final_project_amd.native import Context  # noqa: E402
+
+K = 16
+KERNELS = {0: "k_iter_accept_small (+ tail)", 1: "k_simp (last call)", 2: "k_ext_conn_nn (block 0)"}
+
+
+def main():
+    name = sys.argv[1] if len(sys.argv) > 1 else "goal3_tallest_10box"
+    batch = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
+    wl = json.load(open(os.path.join(ROOT, "tests", "golden", "workloads", name + ".json")))
+    ctx = Context(0, model.robot_desc())
+    L = C.CDLL(os.path.abspath(os.environ["RBE_LIB_PATH"]))
+    L.rp_debug_tstamps.argtypes = [C.c_void_p]
+    buf = np.zeros(8 * K, dtype=np.uint64)
+    rows = []
+    for rep in range(3):
+        for i, q in enumerate(wl["queries"]):
+            sc = scenes.Scene.from_json(q["scene"])
+            ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+            ctx.set_attached(q["attached"])
+            p = _abi.make_params(seed=i, batch=batch, n_waypoints=150, timeout_s=10.0, tree_capacity=1 << 24)
+            buf[:] = 0
+            assert L.rp_debug_tstamps(buf.ctypes.data_as(C.c_void_p)) == 0
+            ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+            assert L.rp_debug_tstamps(buf.ctypes.data_as(C.c_void_p)) == 0
+            if rep:
+                rows.append(buf.copy().reshape(8, K).astype(np.int64))
+    r = np.stack(rows)
+    for kid, kname in KERNELS.items():
+        s = r[:, kid, :]
+        npts = int((s[0] > 0).sum())
+        if npts < 2:
+            continue
+        print(f"{kname}: {len(s)} plans, stamps 0..{npts - 1} (us, median)")
+        for k in range(1, npts):
+            ok = (s[:, k] > 0) & (s[:, k - 1] > 0)
+            d = (s[ok, k] - s[ok, k - 1]) / 100.0
+            if len(d):
+                print(f"   {k - 1}->{k}: {np.median(d):7.2f}  (p90 {np.percentile(d, 90):6.2f}, n {len(d)})")
+        ok = (s[:, npts - 1] > 0) & (s[:, 0] > 0)
+        print(f"   total {np.median((s[ok, npts - 1] - s[ok, 0]) / 100.0):7.2f}")
+
+
+if __name__ == "__main__":
+    main()

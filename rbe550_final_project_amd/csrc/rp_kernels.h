@@ -642,7 +642,9 @@ __global__ __launch_bounds__(64) void k_edges_ml(const double* __restrict__ from
     constexpr int SPW = 64 / GL;
     __shared__ CapsLds caps[SPW];
     __shared__ SceneLds scl;
+    if constexpr (GL == 16) RP_ESTAMP(0);
     scene_to_lds(sc, scl);
+    if constexpr (GL == 16) RP_ESTAMP(1);
     if (dcount) n_edges = min(n_edges, (int64_t)dcount[0] * per_item);
     if (dkmax) kmax = *dkmax;
     const int64_t total = n_edges * kmax;
@@ -669,6 +671,7 @@ __global__ __launch_bounds__(64) void k_edges_ml(const double* __restrict__ from
         const int slots = nde > 1 ? nde : 1;
         const bool run = in && nde >= 0 && slot < slots && ok && gf > gs;
         count_states(counter, __ballot(run && gl == 0));
+        if constexpr (GL == 16) RP_ESTAMP(2);
         if (!__any(run)) continue;
         double st[NQ];
         if (slot == 0 || !run) {
@@ -680,12 +683,15 @@ __global__ __launch_bounds__(64) void k_edges_ml(const double* __restrict__ from
         float qq[NQ];
 #pragma unroll
         for (int k = 0; k < NQ; ++k) qq[k] = (float)st[k];
+        if constexpr (GL == 16) RP_ESTAMP(3);
         const bool col = state_collides_ml<GL, BF>(qq, run, scl, caps);
+        if constexpr (GL == 16) RP_ESTAMP(4);
         if (run && col && gl == 0) {
             valid[e] = 0;
             if (gfail) atomicMin(&gfail[g], gs);
         }
     }
+    if constexpr (GL == 16) RP_ESTAMP(5);
 }
 
 // rp_plan prologue (one block): tree roots, float32 copies of start / goal, counters
@@ -694,40 +700,48 @@ __global__ __launch_bounds__(64) void k_edges_ml(const double* __restrict__ from
 // launch (each the only edge of its prefix group when stride > 1: the other slots
 // are empty and gfail = stride), so their validity comes with it.
 struct PlanRoots { double start[NQ]; double goal[NQ]; };
-__global__ void k_plan_init(PlanRoots r, double* S, int32_t* Spar, uint8_t* Scand, double* G, int32_t* Gpar,
-                            uint8_t* Gcand, float* q32, unsigned long long* counter, PlanIO* io, int64_t sg_edge,
-                            int sg_stride, double* efrom, double* eto, int* nd, uint8_t* valid, int* gfail) {
+struct PlanInit {
+    int on;   // (k_ext_conn_nn: run the prologue in block 0, trees hold only their roots)
+    PlanRoots r;
+    double* S; int32_t* Spar; uint8_t* Scand;
+    double* G; int32_t* Gpar; uint8_t* Gcand;
+    float* q32; unsigned long long* counter; PlanIO* io;
+    int64_t sg_edge; int sg_stride;
+    double* efrom; double* eto; int* nd; uint8_t* valid; int* gfail;
+};
+__device__ __forceinline__ void plan_init_block(const PlanInit& a) {
     const int t = threadIdx.x;
     if (t < NQ) {
-        S[t] = r.start[t];
-        G[t] = r.goal[t];
-        q32[t] = (float)r.start[t];
-        q32[NQ + t] = (float)r.goal[t];
-        if (sg_edge >= 0) {
-            const int64_t e1 = sg_edge + sg_stride;
-            efrom[sg_edge * NQ + t] = eto[sg_edge * NQ + t] = r.start[t];
-            efrom[e1 * NQ + t] = eto[e1 * NQ + t] = r.goal[t];
+        a.S[t] = a.r.start[t];
+        a.G[t] = a.r.goal[t];
+        a.q32[t] = (float)a.r.start[t];
+        a.q32[NQ + t] = (float)a.r.goal[t];
+        if (a.sg_edge >= 0) {
+            const int64_t e1 = a.sg_edge + a.sg_stride;
+            a.efrom[a.sg_edge * NQ + t] = a.eto[a.sg_edge * NQ + t] = a.r.start[t];
+            a.efrom[e1 * NQ + t] = a.eto[e1 * NQ + t] = a.r.goal[t];
         }
     }
-    if (sg_edge >= 0)
-        for (int k = 1 + t; k < sg_stride; k += blockDim.x) nd[sg_edge + k] = nd[sg_edge + sg_stride + k] = -1;
-    if (t < ST_WORDS) io->status[t] = 0;
-    for (int k = t; k < COUNTER_SLOTS; k += blockDim.x) counter[k] = 0;
+    if (a.sg_edge >= 0)
+        for (int k = 1 + t; k < a.sg_stride; k += blockDim.x) a.nd[a.sg_edge + k] = a.nd[a.sg_edge + a.sg_stride + k] = -1;
+    if (t < ST_WORDS) a.io->status[t] = 0;
+    for (int k = t; k < COUNTER_SLOTS; k += blockDim.x) a.counter[k] = 0;
     if (t == 0) {
-        Spar[0] = -1;
-        Gpar[0] = -1;
-        Scand[0] = 0;
-        Gcand[0] = 0;
-        io->n_raw = 0;
-        io->n_out = 0;
-        if (sg_edge >= 0) {
-            const int64_t e1 = sg_edge + sg_stride;
-            nd[sg_edge] = nd[e1] = 0;
-            valid[sg_edge] = valid[e1] = 1;
-            if (gfail) gfail[sg_edge / sg_stride] = gfail[e1 / sg_stride] = sg_stride;
+        a.Spar[0] = -1;
+        a.Gpar[0] = -1;
+        a.Scand[0] = 0;
+        a.Gcand[0] = 0;
+        a.io->n_raw = 0;
+        a.io->n_out = 0;
+        if (a.sg_edge >= 0) {
+            const int64_t e1 = a.sg_edge + a.sg_stride;
+            a.nd[a.sg_edge] = a.nd[e1] = 0;
+            a.valid[a.sg_edge] = a.valid[e1] = 1;
+            if (a.gfail) a.gfail[a.sg_edge / a.sg_stride] = a.gfail[e1 / a.sg_stride] = a.sg_stride;
         }
     }
 }
+__global__ void k_plan_init(PlanInit a) { plan_init_block(a); }
 
 __device__ __forceinline__ int sg_flags(const uint8_t* valid, int64_t sg_edge, int sg_stride) {
     return (valid[sg_edge] ? 1 : 0) | (valid[sg_edge + sg_stride] ? 0x100 : 0);
@@ -912,19 +926,22 @@ __global__ __launch_bounds__(NNBLOCK) void k_ext_conn_nn(const double* __restric
                                                          int32_t* __restrict__ near_out, int32_t* __restrict__ yout,
                                                          int32_t* __restrict__ mout,
                                                          const int32_t* __restrict__ near_in,
-                                                         const int32_t* __restrict__ y_in) {
+                                                         const int32_t* __restrict__ y_in, PlanInit ini) {
     __shared__ double tile[NNTILE * NQ];
+    // ini.on (a plan's first iteration): block 0 also runs the prologue, and both
+    // trees are their roots alone (start = tree A), read from the arguments
+    if (ini.on && blockIdx.x == 0) plan_init_block(ini);
     const int64_t k = (int64_t)blockIdx.x * NNBLOCK + threadIdx.x;
     const bool active = k < n;
     double qr[NQ], x[NQ];
     sample_state(seed, g0 + (uint64_t)(active ? k : 0), bd.lo, bd.hi, qr);
     // near_in / y_in: nearest nodes from the split search (large trees)
-    const int32_t nn = near_in ? (active ? near_in[k] : 0) : nn_tiled(A, TA, qr, active, tile);
+    const int32_t nn = ini.on ? 0 : near_in ? (active ? near_in[k] : 0) : nn_tiled(A, TA, qr, active, tile);
     double near[NQ];
 #pragma unroll
-    for (int d = 0; d < NQ; ++d) near[d] = A[(int64_t)(nn >= 0 ? nn : 0) * NQ + d];
+    for (int d = 0; d < NQ; ++d) near[d] = ini.on ? ini.r.start[d] : A[(int64_t)(nn >= 0 ? nn : 0) * NQ + d];
     steer(near, qr, range, x);
-    const int32_t y = y_in ? (active ? y_in[k] : 0) : nn_tiled(Bt, TB, x, active, tile);
+    const int32_t y = ini.on ? 0 : y_in ? (active ? y_in[k] : 0) : nn_tiled(Bt, TB, x, active, tile);
     if (!active) return;
     const int G = cmax + 1;
     int64_t e = k * G;
@@ -942,7 +959,7 @@ __global__ __launch_bounds__(NNBLOCK) void k_ext_conn_nn(const double* __restric
     double cur[NQ], nxt[NQ];
     const double* ys = Bt + (int64_t)y * NQ;
 #pragma unroll
-    for (int d = 0; d < NQ; ++d) cur[d] = ys[d];
+    for (int d = 0; d < NQ; ++d) cur[d] = ini.on ? ini.r.goal[d] : ys[d];
     int m = cmax, reached = 0;
     for (int s = 0; s < cmax; ++s) {
         ++e;

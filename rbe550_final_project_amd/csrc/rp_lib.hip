@@ -1012,16 +1012,31 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     }
     int64_t sg_edge = (!straight && !grouped && !oob) ? (spec0 ? p.batch_min * G : p.batch_min) : -1;
     const int sg_stride = spec0 ? G : 1;
-    {
-        PlanRoots roots;
-        for (int i = 0; i < NQ; ++i) { roots.start[i] = start[i]; roots.goal[i] = goal[i]; }
-        hipLaunchKernelGGL(k_plan_init, dim3(1), dim3(64), 0, c->stream, roots, c->tree[0].q.p, c->tree[0].par.p,
-                           c->tree[0].cand.p, c->tree[1].q.p, c->tree[1].par.p, c->tree[1].cand.p, c->q32.p,
-                           c->counter.p, io, sg_edge, sg_stride, c->efrom.p, c->eto.p, c->nd.p, c->valid.p,
-                           c->gfail.p);
+    // the prologue (k_plan_init): its own launch, or block 0 of the first
+    // speculative front when that is the plan's next GPU work (one launch fewer on
+    // the latency path); RBE_FUSE_INIT=0 keeps it separate (tests)
+    PlanInit ini{};
+    ini.on = 1;
+    for (int i = 0; i < NQ; ++i) { ini.r.start[i] = start[i]; ini.r.goal[i] = goal[i]; }
+    ini.S = c->tree[0].q.p; ini.Spar = c->tree[0].par.p; ini.Scand = c->tree[0].cand.p;
+    ini.G = c->tree[1].q.p; ini.Gpar = c->tree[1].par.p; ini.Gcand = c->tree[1].cand.p;
+    ini.q32 = c->q32.p; ini.counter = c->counter.p; ini.io = io;
+    ini.sg_edge = sg_edge; ini.sg_stride = sg_stride;
+    ini.efrom = c->efrom.p; ini.eto = c->eto.p; ini.nd = c->nd.p; ini.valid = c->valid.p; ini.gfail = c->gfail.p;
+    bool init_pending = true;
+    auto launch_init = [&]() {
+        if (!init_pending) return;
+        hipLaunchKernelGGL(k_plan_init, dim3(1), dim3(64), 0, c->stream, ini);
         HIP_TRY(hipGetLastError());
-        for (auto& t : c->tree) t.n = 1;
-    }
+        init_pending = false;
+    };
+    bool fuse_init = spec0 && !(sg_edge < 0 && !sg_known);
+    if (const char* e = std::getenv("RBE_NN_SPLIT"))   // (a forced split search reads the trees first)
+        if (*e && std::atoi(e) != 0) fuse_init = false;
+    if (const char* e = std::getenv("RBE_FUSE_INIT"))
+        if (*e) fuse_init = fuse_init && std::atoi(e) != 0;
+    if (!fuse_init) launch_init();
+    for (auto& t : c->tree) t.n = 1;
     auto check_endpoints_now = [&]() {
         launch_validity(c, c->q32.p, 2, (uint8_t*)(status + ST_SG), c->stream);
         read_status();
@@ -1123,6 +1138,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         spec_B = &Bt;
 
         const int64_t sg = (iter == 0) ? sg_edge : -1;   // start / goal ride along
+        if (!(speculate && B <= FUSE_MAX && !grouped)) launch_init();
         c->stats.samples += B;
         if (grouped) {
             // ---- rank group: the speculative front on my slice, ONE all-gather of
@@ -1136,7 +1152,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             hipLaunchKernelGGL(k_ext_conn_nn, dim3(blocks_for(per, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
                                Bt.q.p, TB, p.seed, gr0, per, bd, p.range,
                                p.resolution, cmax, a_start, c->efrom.p, c->eto.p, c->nd.p, c->valid.p, c->gfail.p,
-                               c->near_.p, c->yv.p, c->mv.p, nin, yin);
+                               c->near_.p, c->yv.p, c->mv.p, nin, yin, PlanInit{});
             HIP_TRY(hipGetLastError());
             prof_end(c, pn, 0, c->stream);
             c->prof.nn_pairs += (double)per * (double)(TA + TB);
@@ -1218,9 +1234,15 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             const int32_t *nin = nullptr, *yin = nullptr;
             spec_split(g0, B, nin, yin);
             const int pn = prof_begin(c, c->stream);
+            PlanInit ini_now{};
+            if (init_pending) {   // (iteration 0: trees of one root each, a_start)
+                ini_now = ini;
+                init_pending = false;
+            }
             hipLaunchKernelGGL(k_ext_conn_nn, dim3(blocks_for(B, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
                                Bt.q.p, TB, p.seed, g0, B, bd, p.range, p.resolution, cmax, a_start, c->efrom.p,
-                               c->eto.p, c->nd.p, c->valid.p, c->gfail.p, c->near_.p, c->yv.p, c->mv.p, nin, yin);
+                               c->eto.p, c->nd.p, c->valid.p, c->gfail.p, c->near_.p, c->yv.p, c->mv.p, nin, yin,
+                               ini_now);
             HIP_TRY(hipGetLastError());
             prof_end(c, pn, 0, c->stream);
             c->prof.nn_pairs += (double)B * (double)(TA + TB);
@@ -1366,6 +1388,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         }
 
     }
+    launch_init();   // (the loop ran no speculative iteration)
     if (!sg_known) {   // the loop ran no iteration
         if (const int code = check_endpoints_now()) return endpoint_fail(code);
     }
@@ -1990,6 +2013,10 @@ int rp_debug_stamps(unsigned long long* out, int64_t n) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(unsigned long long) * n) == hipSuccess ? 0 : -1;
 }
 // ... and the plan kernels' block stamps (8 kernels x TSTAMP_K)
+int rp_debug_estamps(unsigned long long* out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_estamps), sizeof(unsigned long long) * ESTAMP_BLOCKS * ESTAMP_K) ==
+                   hipSuccess ? 0 : -1;
+}
 int rp_debug_tstamps(unsigned long long* out) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tstamps), sizeof(unsigned long long) * 8 * TSTAMP_K) == hipSuccess
                ? 0 : -1;

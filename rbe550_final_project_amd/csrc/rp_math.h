@@ -50,9 +50,21 @@ __device__ __forceinline__ void tstamp(int kid, int k) {
     if (threadIdx.x == 0 && blockIdx.x == 0) g_tstamps[kid * TSTAMP_K + k] = t;
 }
 #define RP_TSTAMP(kid, k) tstamp(kid, k)
+// per-block stamps of a multi-block plan kernel (k_edges_ml: one wave per block)
+constexpr int ESTAMP_BLOCKS = 4096, ESTAMP_K = 8;
+__device__ unsigned long long g_estamps[ESTAMP_BLOCKS * ESTAMP_K];
+__device__ __forceinline__ void estamp(int k) {
+    __builtin_amdgcn_sched_barrier(0);
+    unsigned long long t;
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (threadIdx.x == 0 && blockIdx.x < ESTAMP_BLOCKS) g_estamps[blockIdx.x * ESTAMP_K + k] = t;
+}
+#define RP_ESTAMP(k) estamp(k)
 #else
 #define RP_STAMP(k)
 #define RP_TSTAMP(kid, k)
+#define RP_ESTAMP(k)
 #endif
 
 // min / max / clamp as single instructions (v_min_f32, v_max_f32, v_med3_f32). The

@@ -168,6 +168,25 @@ def test_plan_parity(gpu_ctx, oracle_lib, wl, qi, batch, seed, batch_min, specul
         (stats_ref["start_tree_size"], stats_ref["goal_tree_size"], stats_ref["iterations"])
 
 
+@pytest.mark.parametrize("wl,qi", PLAN_CASES[:4])
+@pytest.mark.parametrize("batch,seed", [(64, 11), (4096, 5)])
+def test_plan_parity_prologue_separate(gpu_ctx, oracle_lib, wl, qi, batch, seed, monkeypatch):
+    """RBE_FUSE_INIT=0: the plan prologue as its own launch (k_plan_init) instead of
+    block 0 of the first speculative front: the same trees."""
+    monkeypatch.setenv("RBE_FUSE_INIT", "0")
+    q = _wl(wl)["queries"][qi]
+    sc = scenes.Scene.from_json(q["scene"])
+    o = _both(gpu_ctx, oracle_lib, sc, q["attached"])
+    p = _abi.make_params(seed=seed, batch=batch, n_waypoints=150, timeout_s=60, straight_first=False)
+    ref, st_ref, stats_ref = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+    path, st = gpu_ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+    gst = gpu_ctx.stats()
+    assert st == st_ref == _abi.STATUS_EXACT
+    assert np.array_equal(path, ref)
+    assert (gst["start_tree_size"], gst["goal_tree_size"], gst["iterations"]) == \
+        (stats_ref["start_tree_size"], stats_ref["goal_tree_size"], stats_ref["iterations"])
+
+
 @pytest.mark.parametrize("wl,qi", PLAN_CASES)
 @pytest.mark.parametrize("batch,seed,batch_min", [(64, 11, 0), (16384, 8, 8192)])
 def test_plan_parity_packed_edges(gpu_ctx, oracle_lib, wl, qi, batch, seed, batch_min, monkeypatch):

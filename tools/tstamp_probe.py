@@ -25,20 +25,22 @@ def main():
     ctx = Context(0, model.robot_desc())
     L = C.CDLL(os.path.abspath(os.environ["RBE_LIB_PATH"]))
     L.rp_debug_tstamps.argtypes = [C.c_void_p]
+    L.rp_debug_estamps.argtypes = [C.c_void_p]
     buf = np.zeros(8 * K, dtype=np.uint64)
-    rows = []
+    ebuf = np.zeros(4096 * 8, dtype=np.uint64)
+    rows, erows = [], []
     for rep in range(3):
         for i, q in enumerate(wl["queries"]):
             sc = scenes.Scene.from_json(q["scene"])
             ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
             ctx.set_attached(q["attached"])
             p = _abi.make_params(seed=i, batch=batch, n_waypoints=150, timeout_s=10.0, tree_capacity=1 << 24)
-            buf[:] = 0
-            assert L.rp_debug_tstamps(buf.ctypes.data_as(C.c_void_p)) == 0
             ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
             assert L.rp_debug_tstamps(buf.ctypes.data_as(C.c_void_p)) == 0
+            assert L.rp_debug_estamps(ebuf.ctypes.data_as(C.c_void_p)) == 0
             if rep:
                 rows.append(buf.copy().reshape(8, K).astype(np.int64))
+                erows.append(ebuf.copy().reshape(4096, 8).astype(np.int64))
     r = np.stack(rows)
     for kid, kname in KERNELS.items():
         s = r[:, kid, :]
@@ -53,6 +55,27 @@ def main():
                 print(f"   {k - 1}->{k}: {np.median(d):7.2f}  (p90 {np.percentile(d, 90):6.2f}, n {len(d)})")
         ok = (s[:, npts - 1] > 0) & (s[:, 0] > 0)
         print(f"   total {np.median((s[ok, npts - 1] - s[ok, 0]) / 100.0):7.2f}")
+    # last k_edges_ml launch of each plan (stamps 0 entry, 1 scene in LDS, 2 edge
+    # words loaded, 3 state built, 4 collision done, 5 exit), blocks that ran a state
+    names = ["scene->LDS", "edge loads", "interp", "collides", "tail"]
+    acc = {k: [] for k in range(5)}
+    spans, lat = [], []
+    for e in erows:
+        act = (e[:, 4] > 0) & (e[:, 0] > 0) & (e[:, 3] >= e[:, 0]) & (e[:, 5] >= e[:, 4])
+        act &= (e[:, 5] - e[:, 0]) < 100000
+        if not act.any():
+            continue
+        a = e[act]
+        for k in range(5):
+            acc[k].append(np.median(a[:, k + 1] - a[:, k]) / 100.0)
+        allb = (e[:, 0] > 0) & (e[:, 5] >= e[:, 0]) & ((e[:, 5] - e[:, 0]) < 100000)
+        spans.append((e[allb, 5].max() - e[allb, 0].min()) / 100.0)
+        lat.append(np.median(a[:, 5] - a[:, 0]) / 100.0)
+    if spans:
+        print(f"k_edges_ml (last launch), blocks with a state: median of per-plan medians (us)")
+        for k in range(5):
+            print(f"   {names[k]:12s} {np.median(acc[k]):7.2f}")
+        print(f"   block latency {np.median(lat):7.2f}   launch span (first entry -> last exit) {np.median(spans):7.2f}")
 
 
 if __name__ == "__main__":

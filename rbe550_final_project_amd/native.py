@@ -171,18 +171,28 @@ class Context:
 
     # -- planning ------------------------------------------------------------
     def plan(self, start, goal, lo, hi, params, path_cap=4096):
-        start = np.ascontiguousarray(start, dtype=np.float64)
-        goal = np.ascontiguousarray(goal, dtype=np.float64)
-        lo = np.ascontiguousarray(lo, dtype=np.float64)
-        hi = np.ascontiguousarray(hi, dtype=np.float64)
-        out = getattr(self, "_plan_out", None)   # reused output buffer (no per-call allocation)
-        if out is None or len(out) < path_cap:
-            out = self._plan_out = np.empty((path_cap, _abi.NQ), dtype=np.float64)
-        n = C.c_int32(0)
-        status = C.c_int32(0)
-        self._check(load().rp_plan(self._h, _ptr(start), _ptr(goal), _ptr(lo), _ptr(hi), C.byref(params),
-                                   _ptr(out), path_cap, C.byref(n), C.byref(status)), "rp_plan")
-        return out[:n.value].copy(), status.value
+        # A plan of a few tens of microseconds: the call's own overhead matters, so the
+        # inputs go into one reused buffer whose address (and the output's) is taken
+        # once (ndarray.ctypes costs microseconds per use)
+        b = getattr(self, "_plan_bufs", None)
+        if b is None or len(b["out"]) < path_cap:
+            inp = np.empty(4 * _abi.NQ, dtype=np.float64)
+            out = np.empty((path_cap, _abi.NQ), dtype=np.float64)
+            n, status = C.c_int32(0), C.c_int32(0)
+            a = inp.ctypes.data
+            b = self._plan_bufs = {"inp": inp, "out": out, "n": n, "status": status, "fn": load().rp_plan,
+                                   "args": (a, a + 8 * _abi.NQ, a + 16 * _abi.NQ, a + 24 * _abi.NQ),
+                                   "out_addr": out.ctypes.data, "rn": C.byref(n), "rs": C.byref(status)}
+        inp, nq = b["inp"], _abi.NQ
+        inp[0:nq] = start
+        inp[nq:2 * nq] = goal
+        inp[2 * nq:3 * nq] = lo
+        inp[3 * nq:4 * nq] = hi
+        a0, a1, a2, a3 = b["args"]
+        rc = b["fn"](self._h, a0, a1, a2, a3, C.byref(params), b["out_addr"], path_cap, b["rn"], b["rs"])
+        if rc < 0:
+            self._check(rc, "rp_plan")
+        return b["out"][:b["n"].value].copy(), b["status"].value
 
     def ik(self, pos, quat, init, lo, hi, params=None):
         """Batched hand-link IK (rp_ik): pos (T, 3), quat (T, 4) as w, x, y, z, init

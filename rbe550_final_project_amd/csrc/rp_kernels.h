@@ -495,7 +495,10 @@ __global__ void k_ext_result_flag(const uint8_t* __restrict__ valid, const int32
 // to the other tree, [2] first REACHED target (INT_MAX: none), [3] start-side and
 // [4] goal-side join nodes of the solution, [5] start / goal validity flags (bytes
 // 0 and 1, written by the first validity launch of rp_plan).
-enum { ST_NACC = 0, ST_ADDED = 1, ST_FIRST = 2, ST_SNODE = 3, ST_GNODE = 4, ST_SG = 5, ST_STOP = 6, ST_WORDS = 8 };
+// ST_SL: the straight edge start -> goal rode along the plan's first edge launch and
+// is valid (1), else 0 (not checked, or colliding)
+enum { ST_NACC = 0, ST_ADDED = 1, ST_FIRST = 2, ST_SNODE = 3, ST_GNODE = 4, ST_SG = 5, ST_STOP = 6, ST_SL = 7,
+       ST_WORDS = 8 };
 
 // I/O record of one rp_plan call. The device copy holds the live status; a
 // pinned, host-coherent mirror receives what the host needs (status after every
@@ -576,13 +579,13 @@ __global__ __launch_bounds__(64) void k_validity_ml(const float* __restrict__ q,
     constexpr int SPW = 64 / GL;
     __shared__ CapsLds caps[SPW];
     __shared__ SceneLds scl;
-    scene_to_lds(sc, scl);
     const int64_t i = (int64_t)blockIdx.x * SPW + threadIdx.x / GL;
     const bool run = i < n;
     float qq[NQ];
     const float* src = q + (run ? i : 0) * NQ;
 #pragma unroll
     for (int k = 0; k < NQ; ++k) qq[k] = src[k];
+    scene_to_lds(sc, scl);   // (after the state loads are issued: both in one round trip)
     const bool col = state_collides_ml<GL, BF>(qq, run, scl, caps);
     if (run && (threadIdx.x & (GL - 1)) == 0) flags[i] = col ? 0 : 1;
 }
@@ -632,27 +635,40 @@ __global__ __launch_bounds__(64) void k_straight_ml(Endpoints ep, double res, co
     }
 }
 
+// The straight edge start -> goal riding along an edge launch (rp_plan's first
+// speculative front, RRT forced): `slots` extra items after the edge items, the
+// states the simplifier's shortcut (0, n - 1) would check (checkMotion mode 0: the
+// goal, then interp(start, goal, k / nd)); a collision clears *flag. It lets the
+// iteration that solves finish the simplification itself when that shortcut holds
+// (the greedy reduction then keeps [start, goal] whatever the other pairs are).
+struct StraightRide {
+    int slots;   // 0: none
+    int nd;
+    double a[NQ], b[NQ];
+    int* flag;
+};
+
 // k_edges with GL lanes per (edge, slot) item; grid-stride over the items
 template <int GL, bool BF>
 __global__ __launch_bounds__(64) void k_edges_ml(const double* __restrict__ from, const double* __restrict__ to,
                                                 const int* __restrict__ nd, int64_t n_edges, int kmax, int mode,
                                                 uint8_t* valid, int group, int* gfail, unsigned long long* counter,
                                                 const DevScene* __restrict__ sc, const int* __restrict__ dcount,
-                                                int per_item, const int* __restrict__ dkmax) {
+                                                int per_item, const int* __restrict__ dkmax, StraightRide sr) {
     constexpr int SPW = 64 / GL;
     __shared__ CapsLds caps[SPW];
     __shared__ SceneLds scl;
     if constexpr (GL == 16) RP_ESTAMP(0);
-    scene_to_lds(sc, scl);
-    if constexpr (GL == 16) RP_ESTAMP(1);
+    bool scene_pending = true;   // (loaded with the first edge words: one round trip, not two)
     if (dcount) n_edges = min(n_edges, (int64_t)dcount[0] * per_item);
     if (dkmax) kmax = *dkmax;
-    const int64_t total = n_edges * kmax;
+    const int64_t n_items = n_edges * kmax, total = n_items + sr.slots;
     const int gl = (int)(threadIdx.x & (GL - 1));
     for (int64_t base = (int64_t)blockIdx.x * SPW; base < total; base += (int64_t)gridDim.x * SPW) {
         const int64_t idx = base + threadIdx.x / GL;
-        const int64_t e = idx / kmax;
-        const int slot = (int)(idx - e * kmax);
+        const bool sl = idx >= n_items;   // a straight-edge item
+        const int64_t e = sl ? n_edges : idx / kmax;
+        const int slot = (int)(sl ? idx - n_items : idx - e * kmax);
         // the edge's words and endpoints loaded together (no dependent round trips)
         const bool in = e < n_edges;
         const int64_t ec = in ? e : 0;
@@ -668,8 +684,19 @@ __global__ __launch_bounds__(64) void k_edges_ml(const double* __restrict__ from
             emode = (nde & ND_FROM) ? 1 : 0;
             nde &= ~ND_FROM;
         }
+        if (sl) {
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) { a[k] = sr.a[k]; b[k] = sr.b[k]; }
+            nde = sr.nd;
+            emode = 0;
+        }
         const int slots = nde > 1 ? nde : 1;
-        const bool run = in && nde >= 0 && slot < slots && ok && gf > gs;
+        if (scene_pending) {
+            scene_to_lds(sc, scl);
+            scene_pending = false;
+            if constexpr (GL == 16) RP_ESTAMP(1);
+        }
+        const bool run = sl ? idx < total : in && nde >= 0 && slot < slots && ok && gf > gs;
         count_states(counter, __ballot(run && gl == 0));
         if constexpr (GL == 16) RP_ESTAMP(2);
         if (!__any(run)) continue;
@@ -687,8 +714,12 @@ __global__ __launch_bounds__(64) void k_edges_ml(const double* __restrict__ from
         const bool col = state_collides_ml<GL, BF>(qq, run, scl, caps);
         if constexpr (GL == 16) RP_ESTAMP(4);
         if (run && col && gl == 0) {
-            valid[e] = 0;
-            if (gfail) atomicMin(&gfail[g], gs);
+            if (sl) {
+                *sr.flag = 0;
+            } else {
+                valid[e] = 0;
+                if (gfail) atomicMin(&gfail[g], gs);
+            }
         }
     }
     if constexpr (GL == 16) RP_ESTAMP(5);
@@ -702,6 +733,7 @@ __global__ __launch_bounds__(64) void k_edges_ml(const double* __restrict__ from
 struct PlanRoots { double start[NQ]; double goal[NQ]; };
 struct PlanInit {
     int on;   // (k_ext_conn_nn: run the prologue in block 0, trees hold only their roots)
+    int sl;   // the straight edge rides along the first edge launch: ST_SL starts at 1
     PlanRoots r;
     double* S; int32_t* Spar; uint8_t* Scand;
     double* G; int32_t* Gpar; uint8_t* Gcand;
@@ -724,7 +756,7 @@ __device__ __forceinline__ void plan_init_block(const PlanInit& a) {
     }
     if (a.sg_edge >= 0)
         for (int k = 1 + t; k < a.sg_stride; k += blockDim.x) a.nd[a.sg_edge + k] = a.nd[a.sg_edge + a.sg_stride + k] = -1;
-    if (t < ST_WORDS) a.io->status[t] = 0;
+    if (t < ST_WORDS) a.io->status[t] = (t == ST_SL && a.sl) ? 1 : 0;
     for (int k = t; k < COUNTER_SLOTS; k += blockDim.x) a.counter[k] = 0;
     if (t == 0) {
         a.Spar[0] = -1;
@@ -1089,6 +1121,7 @@ struct TailLds {
     const int32_t* bpar; int64_t b0; int nb;   // parents of tree B's new nodes (the first nb)
     const int32_t* cend; int nc;               // chain_end[t], t < nc
     int first;                                 // ST_FIRST
+    int sl;                                    // ST_SL: the straight edge start -> goal is valid
     double* P;                                 // LDS path (SPMAX states) for the simplifier's first step
     // where the new nodes' states were copied from (records of the previous launch,
     // visible without waiting for this block's stores): tree A's node a0 + t from
@@ -1264,6 +1297,10 @@ struct PathArgs {
     double* eto;
     int* nd;
     uint8_t* valid;
+    // publication of a plan the iteration finishes itself (TailLds::sl)
+    PlanIO* hio;
+    const unsigned long long* counter;
+    int seq;
 };
 
 
@@ -1339,6 +1376,44 @@ __device__ int build_path(const PathArgs& pa, int32_t s_node, int32_t g_node, Pl
 
 // block tail of the last kernel of an iteration: join nodes and, on success, the
 // solution path. The status reaches the host through k_simp, which follows.
+// the simplification's end state after a straight shortcut, and the output record
+// (k_simp's publication with OP_OUT); P = the raw path (LDS), nr >= 3 states
+__device__ void tail_finish_straight(const PathArgs& pa, const PlanIO* io, int nr, const double* P) {
+    SimpState* ss = pa.ss;
+    PlanIO* hio = pa.hio;
+    const int t = threadIdx.x;
+    lds_barrier();   // (P: build_path's copy)
+    if (t < 2 * NQ) {
+        const double v = t < NQ ? P[t] : P[(nr - 1) * NQ + (t - NQ)];
+        ss->P[t] = v;
+        hio->path[t] = v;
+    }
+    if (t < 64) {   // states counted so far (the edge launches' counter words), wave 0
+        unsigned long long v = 0;
+        for (int i = t; i < COUNTER_SLOTS; i += 64) v += pa.counter[i];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        if (t == 0) {
+            ss->on = 1;
+            ss->n = 2;
+            ss->done = 1;
+            ss->stop = 0;
+            ss->nedges = 0;
+            ss->edges_total = 1;
+#pragma unroll
+            for (int w = 0; w < ST_WORDS; ++w) hio->status[w] = io->status[w];   // (this lane's own stores)
+            hio->n_raw = nr;
+            hio->n_out = 2;
+            hio->counter = v;
+            hio->simp_edges = 1;
+            hio->out = 1;
+        }
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (t == 0) publish_seq(hio, pa.seq);
+}
+
 __device__ void iteration_tail(int* status, int added, int64_t TA, int a_start, const int32_t* Apar,
                                const int32_t* Bpar, const int32_t* chain_end, const PathArgs& pa, PlanIO* io,
                                const TailLds* ov = nullptr) {
@@ -1349,6 +1424,13 @@ __device__ void iteration_tail(int* status, int added, int64_t TA, int a_start, 
     const int nr = sn != -2 ? build_path(pa, sn, gn, io, pa.ss ? pa.ss->P : nullptr,
                                          pa.level > 0 ? pa.dev_max : -1, ov, a_start)
                             : -3;   // no solution: simp_begin reads io->n_raw
+    if (pa.ss && ov && ov->sl && pa.prep_reduce && pa.hio && nr >= 3 && nr <= pa.dev_max) {
+        // the straight edge holds: the reduction keeps [start, goal] (its greedy walk
+        // takes the farthest valid shortcut from the start first), the program ends
+        // there (2 states); publish the output now
+        tail_finish_straight(pa, io, nr, ov->P);
+        return;
+    }
     if (pa.ss) {   // (build_path's writes are ordered by simp_begin's barrier)
         const int n = simp_begin(pa.level, pa.dev_max, pa.out, io, pa.ss, nr, nr >= 0);
         RP_TSTAMP(0, 7);
@@ -1415,14 +1497,17 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
     int32_t* Bpar, uint8_t* Bcand, int64_t TB, int a_start, int32_t* chain_end, int* status,
     const uint8_t* valid, int64_t sg_edge, int sg_stride, PathArgs pa, PlanIO* io) {
     __shared__ unsigned long long lds64[FUSE_THREADS / 64];
-    __shared__ int first, sgv;
+    __shared__ int first, sgv, slv;
     __shared__ int32_t l_apar[FUSE_MAX], l_cend[FUSE_MAX], l_bpar[TAIL_LB], l_asrc[FUSE_MAX], l_bsrc[TAIL_LB];
     __shared__ double l_P[SPMAX * NQ];
     // the checked endpoint of an edge is the new node: `to` on the start tree's
     // side (a_start: extension near -> new; chain next -> prev), else `from`
     const double* ext_node = a_start ? eto : efrom;
     const double* chain_node = a_start ? efrom : eto;
-    if (threadIdx.x == 64 && sg_edge >= 0) sgv = sg_flags(valid, sg_edge, sg_stride);   // (another wave)
+    if (threadIdx.x == 64) {   // (another wave)
+        if (sg_edge >= 0) sgv = sg_flags(valid, sg_edge, sg_stride);
+        slv = io->status[ST_SL];
+    }
     RP_TSTAMP(0, 0);
     // every per-sample input fetched at once (one round trip)
     const int64_t k0 = (int64_t)threadIdx.x * ITEMS;
@@ -1506,8 +1591,8 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
         if (sg_edge >= 0) status[ST_SG] = sgv;
     }
     RP_TSTAMP(0, 3);
-    const TailLds ov{l_apar, TA, totalA, l_bpar, TB, totalB < TAIL_LB ? totalB : TAIL_LB, l_cend, totalA, first, l_P,
-                     l_asrc, l_bsrc, ext_node, chain_node};
+    const TailLds ov{l_apar, TA, totalA, l_bpar, TB, totalB < TAIL_LB ? totalB : TAIL_LB, l_cend, totalA, first, slv,
+                     l_P, l_asrc, l_bsrc, ext_node, chain_node};
     iteration_tail(status, totalB, TA, a_start, Apar, Bpar, chain_end, pa, io, &ov);
 }
 

@@ -324,31 +324,37 @@ int ml_lanes(int64_t states, bool edges) {
 template <int GL>
 void launch_edges_ml(rp_ctx* c, const double* from, const double* to, const int* nd, int64_t n, int kmax, int mode,
                      uint8_t* valid, int group, int* gfail, hipStream_t s, const int* dcount, int per_item,
-                     unsigned max_blocks, const int* dkmax) {
+                     unsigned max_blocks, const int* dkmax, const StraightRide& sr) {
     constexpr int SPW = 64 / GL;
-    unsigned nb = blocks_for(n * (int64_t)kmax, SPW);
+    unsigned nb = blocks_for(n * (int64_t)kmax + sr.slots, SPW);
     nb = std::min<unsigned>(nb, max_blocks ? std::max(max_blocks, 4096u) : 16384u);
     if (base_fixed(c->scene))
         hipLaunchKernelGGL((k_edges_ml<GL, true>), dim3(nb), dim3(64), 0, s, from, to, nd, n, kmax, mode, valid, group,
-                           gfail, c->counter.p, c->d_scene, dcount, per_item, dkmax);
+                           gfail, c->counter.p, c->d_scene, dcount, per_item, dkmax, sr);
     else
         hipLaunchKernelGGL((k_edges_ml<GL, false>), dim3(nb), dim3(64), 0, s, from, to, nd, n, kmax, mode, valid,
-                           group, gfail, c->counter.p, c->d_scene, dcount, per_item, dkmax);
+                           group, gfail, c->counter.p, c->d_scene, dcount, per_item, dkmax, sr);
 }
 
+// sr: the straight edge riding along (rp_plan's first front; lane-group kernels only)
 void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd, int64_t n, int kmax,
                   int mode, uint8_t* valid, int group, int* gfail, hipStream_t s, const int* dcount = nullptr,
-                  int per_item = 1, unsigned max_blocks = 0, const int* dkmax = nullptr, int64_t expect = 0) {
+                  int per_item = 1, unsigned max_blocks = 0, const int* dkmax = nullptr, int64_t expect = 0,
+                  const StraightRide* sr = nullptr) {
     if (n <= 0) return;
     const int64_t threads = n * (int64_t)kmax;   // (dkmax: kmax is only the grid's size hint)
+    StraightRide none{};
+    const StraightRide& ride = sr ? *sr : none;
     // expect: the states a gated launch (dcount) usually has, when far below its bound
-    if (const int gl = ml_lanes(expect > 0 ? expect : dkmax ? n * 32 : threads, true); gl > 1) {
+    int gl = ml_lanes(expect > 0 ? expect : dkmax ? n * 32 : threads + ride.slots, true);
+    if (ride.slots > 0 && gl == 1) gl = 8;   // (the ride-along exists in the lane-group kernels)
+    if (gl > 1) {
         const int ps = prof_begin(c, s);
         switch (gl) {
-            case 8: launch_edges_ml<8>(c, from, to, nd, n, kmax, mode, valid, group, gfail, s, dcount, per_item, max_blocks, dkmax); break;
-            case 16: launch_edges_ml<16>(c, from, to, nd, n, kmax, mode, valid, group, gfail, s, dcount, per_item, max_blocks, dkmax); break;
-            case 32: launch_edges_ml<32>(c, from, to, nd, n, kmax, mode, valid, group, gfail, s, dcount, per_item, max_blocks, dkmax); break;
-            default: launch_edges_ml<64>(c, from, to, nd, n, kmax, mode, valid, group, gfail, s, dcount, per_item, max_blocks, dkmax); break;
+            case 8: launch_edges_ml<8>(c, from, to, nd, n, kmax, mode, valid, group, gfail, s, dcount, per_item, max_blocks, dkmax, ride); break;
+            case 16: launch_edges_ml<16>(c, from, to, nd, n, kmax, mode, valid, group, gfail, s, dcount, per_item, max_blocks, dkmax, ride); break;
+            case 32: launch_edges_ml<32>(c, from, to, nd, n, kmax, mode, valid, group, gfail, s, dcount, per_item, max_blocks, dkmax, ride); break;
+            default: launch_edges_ml<64>(c, from, to, nd, n, kmax, mode, valid, group, gfail, s, dcount, per_item, max_blocks, dkmax, ride); break;
         }
         HIP_TRY(hipGetLastError());
         prof_end(c, ps, 1, s);
@@ -1023,6 +1029,28 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     ini.q32 = c->q32.p; ini.counter = c->counter.p; ini.io = io;
     ini.sg_edge = sg_edge; ini.sg_stride = sg_stride;
     ini.efrom = c->efrom.p; ini.eto = c->eto.p; ini.nd = c->nd.p; ini.valid = c->valid.p; ini.gfail = c->gfail.p;
+    // RRT forced (no straight-first launch) with simplification on: the straight edge
+    // start -> goal rides along the first speculative edge launch (StraightRide), so
+    // an iteration that solves while it holds finishes the plan in its own last
+    // kernel (rp_kernels.h tail_finish_straight) instead of running the shortcut
+    // stage's launches; RBE_STRAIGHT_RIDE=0 turns it off (tests)
+    StraightRide ride{};
+    if (!straight && !oob && level >= 1 && spec0) {
+        bool on = true;
+        if (const char* e = std::getenv("RBE_STRAIGHT_RIDE"))
+            if (*e) on = std::atoi(e) != 0;
+        const int nd_s = (int)std::ceil(std::sqrt(h_dist2(start, goal)) / p.resolution);
+        const int slots = nd_s > 1 ? nd_s : 1;
+        // (the first front's edge launch: (batch_min + 2) * G edges x kmax slots)
+        const int64_t items = (p.batch_min + 2) * (int64_t)G * kmax;
+        if (on && slots <= 8192 && ml_lanes(items + slots, true) > 1) {
+            ride.slots = slots;
+            ride.nd = nd_s;
+            for (int i = 0; i < NQ; ++i) { ride.a[i] = start[i]; ride.b[i] = goal[i]; }
+            ride.flag = status + ST_SL;
+        }
+    }
+    ini.sl = ride.slots > 0;
     bool init_pending = true;
     auto launch_init = [&]() {
         if (!init_pending) return;
@@ -1094,6 +1122,9 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     pa.eto = c->eto.p;
     pa.nd = c->nd.p;
     pa.valid = c->valid.p;
+    pa.hio = h;
+    pa.counter = c->counter.p;
+    pa.seq = 0;
 
     Bounds bd;
     for (int i = 0; i < NQ; ++i) { bd.lo[i] = lo[i]; bd.hi[i] = hi[i]; }
@@ -1247,7 +1278,9 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             prof_end(c, pn, 0, c->stream);
             c->prof.nn_pairs += (double)B * (double)(TA + TB);
             launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, (B + (sg >= 0 ? 2 : 0)) * G, kmax, 2, c->valid.p, G,
-                         c->gfail.p, c->stream);
+                         c->gfail.p, c->stream, nullptr, 1, 0, nullptr, 0,
+                         (iter == 0 && ride.slots > 0) ? &ride : nullptr);
+            pa.seq = seq;   // (an iteration that finishes the plan publishes it)
 #define RP_ITER_SMALL(IT)                                                                                           \
     hipLaunchKernelGGL(k_iter_accept_small<IT>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, (const int*)c->gfail.p,   \
                        (const int32_t*)c->near_.p, (const int32_t*)c->yv.p, (const int32_t*)c->mv.p, B, G,          \

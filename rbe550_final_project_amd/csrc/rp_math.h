@@ -51,7 +51,7 @@ __device__ __forceinline__ void tstamp(int kid, int k) {
 }
 #define RP_TSTAMP(kid, k) tstamp(kid, k)
 // per-block stamps of a multi-block plan kernel (k_edges_ml: one wave per block)
-constexpr int ESTAMP_BLOCKS = 4096, ESTAMP_K = 8;
+constexpr int ESTAMP_BLOCKS = 4096, ESTAMP_K = 16;
 __device__ unsigned long long g_estamps[ESTAMP_BLOCKS * ESTAMP_K];
 __device__ __forceinline__ void estamp(int k) {
     __builtin_amdgcn_sched_barrier(0);
@@ -884,10 +884,13 @@ __device__ __forceinline__ bool state_collides_ml(const float q[NQ], bool run, c
         jt.s[i] = __shfl(sj, base + i, 64);
         jt.c[i] = __shfl(cj, base + i, 64);
     }
+    if constexpr (GL == 16) RP_ESTAMP(8);
     __syncthreads();   // the block's SceneLds (scene_to_lds, issued before the caller's state setup)
+    if constexpr (GL == 16) RP_ESTAMP(9);
     Capsules k;
     NoVisitPlane pv{sc.plane_z};
     bool hit = run && fk_walk_j<NoVisitPlane, BF>(q, jt, sc.base, k, pv);
+    if constexpr (GL == 16) RP_ESTAMP(10);
     if (!__any(run && !hit)) return hit;   // every state decided by the plane (or idle)
     if (gl == 0) {
 #pragma unroll
@@ -898,6 +901,7 @@ __device__ __forceinline__ bool state_collides_ml(const float q[NQ], bool run, c
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    if constexpr (GL == 16) RP_ESTAMP(11);
     const int nb = sc.nb;
     const int units = NPAIR + NCAP * nb;
     const bool active = run && !hit;   // uniform within the group
@@ -933,6 +937,7 @@ __device__ __forceinline__ bool state_collides_ml(const float q[NQ], bool run, c
         hit = hit || ((m >> base) & GMASK) != 0;
         if (!__any(active && !hit)) break;   // every group decided
     }
+    if constexpr (GL == 16) RP_ESTAMP(12);
     __builtin_amdgcn_wave_barrier();   // the LDS capsules are reused by the next state
     return hit;
 }

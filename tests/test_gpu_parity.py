@@ -168,12 +168,16 @@ def test_plan_parity(gpu_ctx, oracle_lib, wl, qi, batch, seed, batch_min, specul
         (stats_ref["start_tree_size"], stats_ref["goal_tree_size"], stats_ref["iterations"])
 
 
-@pytest.mark.parametrize("wl,qi", PLAN_CASES[:4])
+@pytest.mark.parametrize("wl,qi", PLAN_CASES[:5])
 @pytest.mark.parametrize("batch,seed", [(64, 11), (4096, 5)])
-def test_plan_parity_prologue_separate(gpu_ctx, oracle_lib, wl, qi, batch, seed, monkeypatch):
-    """RBE_FUSE_INIT=0: the plan prologue as its own launch (k_plan_init) instead of
-    block 0 of the first speculative front: the same trees."""
-    monkeypatch.setenv("RBE_FUSE_INIT", "0")
+@pytest.mark.parametrize("knob", ["RBE_FUSE_INIT", "RBE_STRAIGHT_RIDE"])
+def test_plan_parity_latency_paths_off(gpu_ctx, oracle_lib, wl, qi, batch, seed, knob, monkeypatch):
+    """The plan-latency shortcuts turned off, one at a time: RBE_FUSE_INIT=0 runs the
+    prologue as its own launch (k_plan_init) instead of block 0 of the first
+    speculative front; RBE_STRAIGHT_RIDE=0 leaves the straight edge out of the first
+    edge launch, so a solving iteration runs the shortcut stage's launches instead of
+    finishing the plan itself. Same trees, same paths (the default runs them on)."""
+    monkeypatch.setenv(knob, "0")
     q = _wl(wl)["queries"][qi]
     sc = scenes.Scene.from_json(q["scene"])
     o = _both(gpu_ctx, oracle_lib, sc, q["attached"])
@@ -326,6 +330,26 @@ def test_hand_built_collision_cases(gpu_ctx, oracle_lib):
         assert o.check_states(qq)[0] == expect
         assert gpu_ctx.check_states(qq)[0] == expect
         assert sorted(gpu_ctx.contacts(np.asarray(q, dtype=np.float64))) == sorted(o.contacts(q))
+
+
+@pytest.mark.parametrize("wl", ["goal1_scattered_6box", "goal3_tallest_10box", "goal4_pentagon_10box", "clutter64",
+                                "single_pick_place_5box"])
+def test_plan_parity_rrt_forced_every_query(gpu_ctx, oracle_lib, wl):
+    """RRT-Connect forced on every query of the workload (the C1 / C3 RRT-forced
+    bench legs): queries whose straight edge holds finish inside the solving
+    iteration (the ride-along), the others run the shortcut / smoothing launches;
+    every path, status, tree and iteration count equals the oracle's."""
+    for qi, q in enumerate(_wl(wl)["queries"]):
+        sc = scenes.Scene.from_json(q["scene"])
+        o = _both(gpu_ctx, oracle_lib, sc, q["attached"])
+        p = _abi.make_params(seed=qi, batch=4096, n_waypoints=150, timeout_s=60, straight_first=False)
+        ref, st_ref, stats_ref = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+        path, st = gpu_ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+        g = gpu_ctx.stats()
+        assert st == st_ref == _abi.STATUS_EXACT, (wl, qi)
+        assert np.array_equal(path, ref), (wl, qi)
+        assert (g["start_tree_size"], g["goal_tree_size"], g["iterations"]) == \
+            (stats_ref["start_tree_size"], stats_ref["goal_tree_size"], stats_ref["iterations"]), (wl, qi)
 
 
 @pytest.mark.parametrize("wl", ["goal1_scattered_6box", "goal3_tallest_10box", "goal4_pentagon_10box", "clutter64",

@@ -27,7 +27,7 @@ def main():
     L.rp_debug_tstamps.argtypes = [C.c_void_p]
     L.rp_debug_estamps.argtypes = [C.c_void_p]
     buf = np.zeros(8 * K, dtype=np.uint64)
-    ebuf = np.zeros(4096 * 8, dtype=np.uint64)
+    ebuf = np.zeros(4096 * 16, dtype=np.uint64)
     rows, erows = [], []
     for rep in range(3):
         for i, q in enumerate(wl["queries"]):
@@ -40,7 +40,7 @@ def main():
             assert L.rp_debug_estamps(ebuf.ctypes.data_as(C.c_void_p)) == 0
             if rep:
                 rows.append(buf.copy().reshape(8, K).astype(np.int64))
-                erows.append(ebuf.copy().reshape(4096, 8).astype(np.int64))
+                erows.append(ebuf.copy().reshape(4096, 16).astype(np.int64))
     r = np.stack(rows)
     for kid, kname in KERNELS.items():
         s = r[:, kid, :]
@@ -76,6 +76,18 @@ def main():
         for k in range(5):
             print(f"   {names[k]:12s} {np.median(acc[k]):7.2f}")
         print(f"   block latency {np.median(lat):7.2f}   launch span (first entry -> last exit) {np.median(spans):7.2f}")
+        # inside the collision check: 3 -> 8 sincos + exchange, 8 -> 9 scene wait,
+        # 9 -> 10 FK walk, 10 -> 11 capsules to LDS, 11 -> 12 test loop
+        sub = {"sincos+shfl": (3, 8), "scene wait": (8, 9), "fk walk": (9, 10), "caps->LDS": (10, 11),
+               "tests": (11, 12)}
+        for nm, (i, j) in sub.items():
+            vals = []
+            for e in erows:
+                ok = (e[:, i] > 0) & (e[:, j] >= e[:, i]) & ((e[:, j] - e[:, i]) < 100000) & (e[:, 4] > 0)
+                if ok.any():
+                    vals.append(np.median(e[ok, j] - e[ok, i]) / 100.0)
+            if vals:
+                print(f"      {nm:12s} {np.median(vals):7.2f}")
 
 
 if __name__ == "__main__":

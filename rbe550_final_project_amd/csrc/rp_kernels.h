@@ -1122,6 +1122,8 @@ struct TailLds {
     const int32_t* cend; int nc;               // chain_end[t], t < nc
     int first;                                 // ST_FIRST
     int sl;                                    // ST_SL: the straight edge start -> goal is valid
+    const int* st0;                            // the status words at kernel start (LDS)
+    const unsigned long long* cpart;           // 64 partial sums of the state counters (LDS)
     double* P;                                 // LDS path (SPMAX states) for the simplifier's first step
     // where the new nodes' states were copied from (records of the previous launch,
     // visible without waiting for this block's stores): tree A's node a0 + t from
@@ -1378,7 +1380,10 @@ __device__ int build_path(const PathArgs& pa, int32_t s_node, int32_t g_node, Pl
 // solution path. The status reaches the host through k_simp, which follows.
 // the simplification's end state after a straight shortcut, and the output record
 // (k_simp's publication with OP_OUT); P = the raw path (LDS), nr >= 3 states
-__device__ void tail_finish_straight(const PathArgs& pa, const PlanIO* io, int nr, const double* P) {
+// st: this iteration's status words; cpart: 64 partial sums of the state counters
+// (both fetched by the caller at its start: the edge launches before it are done)
+__device__ void tail_finish_straight(const PathArgs& pa, const int* st, const unsigned long long* cpart, int nr,
+                                     const double* P) {
     SimpState* ss = pa.ss;
     PlanIO* hio = pa.hio;
     const int t = threadIdx.x;
@@ -1388,26 +1393,21 @@ __device__ void tail_finish_straight(const PathArgs& pa, const PlanIO* io, int n
         ss->P[t] = v;
         hio->path[t] = v;
     }
-    if (t < 64) {   // states counted so far (the edge launches' counter words), wave 0
+    if (t < ST_WORDS) hio->status[t] = st[t];
+    if (t == 64) {
         unsigned long long v = 0;
-        for (int i = t; i < COUNTER_SLOTS; i += 64) v += pa.counter[i];
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        if (t == 0) {
-            ss->on = 1;
-            ss->n = 2;
-            ss->done = 1;
-            ss->stop = 0;
-            ss->nedges = 0;
-            ss->edges_total = 1;
-#pragma unroll
-            for (int w = 0; w < ST_WORDS; ++w) hio->status[w] = io->status[w];   // (this lane's own stores)
-            hio->n_raw = nr;
-            hio->n_out = 2;
-            hio->counter = v;
-            hio->simp_edges = 1;
-            hio->out = 1;
-        }
+        for (int i = 0; i < 64; ++i) v += cpart[i];
+        ss->on = 1;
+        ss->n = 2;
+        ss->done = 1;
+        ss->stop = 0;
+        ss->nedges = 0;
+        ss->edges_total = 1;
+        hio->n_raw = nr;
+        hio->n_out = 2;
+        hio->counter = v;
+        hio->simp_edges = 1;
+        hio->out = 1;
     }
     __threadfence_system();
     __syncthreads();
@@ -1428,7 +1428,13 @@ __device__ void iteration_tail(int* status, int added, int64_t TA, int a_start, 
         // the straight edge holds: the reduction keeps [start, goal] (its greedy walk
         // takes the farthest valid shortcut from the start first), the program ends
         // there (2 states); publish the output now
-        tail_finish_straight(pa, io, nr, ov->P);
+        __shared__ int stw[ST_WORDS];
+        if (threadIdx.x < ST_WORDS) {   // this iteration's words over the ones at kernel start
+            const int w = threadIdx.x;
+            stw[w] = w == ST_NACC ? ov->na : w == ST_ADDED ? added : w == ST_FIRST ? ov->first
+                   : w == ST_SNODE ? sn : w == ST_GNODE ? gn : ov->st0[w];
+        }
+        tail_finish_straight(pa, stw, ov->cpart, nr, ov->P);
         return;
     }
     if (pa.ss) {   // (build_path's writes are ordered by simp_begin's barrier)
@@ -1497,7 +1503,8 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
     int32_t* Bpar, uint8_t* Bcand, int64_t TB, int a_start, int32_t* chain_end, int* status,
     const uint8_t* valid, int64_t sg_edge, int sg_stride, PathArgs pa, PlanIO* io) {
     __shared__ unsigned long long lds64[FUSE_THREADS / 64];
-    __shared__ int first, sgv, slv;
+    __shared__ int first, sgv, slv, st0[ST_WORDS];
+    __shared__ unsigned long long cpart[64];
     __shared__ int32_t l_apar[FUSE_MAX], l_cend[FUSE_MAX], l_bpar[TAIL_LB], l_asrc[FUSE_MAX], l_bsrc[TAIL_LB];
     __shared__ double l_P[SPMAX * NQ];
     // the checked endpoint of an edge is the new node: `to` on the start tree's
@@ -1507,6 +1514,13 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
     if (threadIdx.x == 64) {   // (another wave)
         if (sg_edge >= 0) sgv = sg_flags(valid, sg_edge, sg_stride);
         slv = io->status[ST_SL];
+#pragma unroll
+        for (int w = 0; w < ST_WORDS; ++w) st0[w] = io->status[w];
+    }
+    if (threadIdx.x >= 128 && threadIdx.x < 192) {   // state counters, for a plan this kernel may finish
+        unsigned long long v = 0;
+        for (int i = threadIdx.x - 128; i < COUNTER_SLOTS; i += 64) v += pa.counter[i];
+        cpart[threadIdx.x - 128] = v;
     }
     RP_TSTAMP(0, 0);
     // every per-sample input fetched at once (one round trip)
@@ -1590,9 +1604,10 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
         status[ST_FIRST] = first;
         if (sg_edge >= 0) status[ST_SG] = sgv;
     }
+    if (threadIdx.x == 64 && sg_edge >= 0) st0[ST_SG] = sgv;   // (st0 read by the tail after its barriers)
     RP_TSTAMP(0, 3);
     const TailLds ov{l_apar, TA, totalA, l_bpar, TB, totalB < TAIL_LB ? totalB : TAIL_LB, l_cend, totalA, first, slv,
-                     l_P, l_asrc, l_bsrc, ext_node, chain_node};
+                     st0, cpart, l_P, l_asrc, l_bsrc, ext_node, chain_node};
     iteration_tail(status, totalB, TA, a_start, Apar, Bpar, chain_end, pa, io, &ov);
 }
 

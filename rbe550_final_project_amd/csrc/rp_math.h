@@ -308,7 +308,7 @@ __device__ __forceinline__ float excess_dot(V3 a, V3 d, V3 h, float t, float* f2
 // quadratic in t with C^1 joins; its derivative g is piecewise linear and
 // nondecreasing with breakpoints where a coordinate crosses +-h. Locate the root of
 // g between the sorted breakpoints and interpolate linearly inside that piece.
-__device__ __attribute__((noinline)) float segment_box_dist2(V3 a, V3 b, V3 h) {
+__device__ __forceinline__ float segment_box_dist2_body(V3 a, V3 b, V3 h) {
     const V3 d = {b.x - a.x, b.y - a.y, b.z - a.z};
     float T[6];
     {
@@ -350,7 +350,7 @@ __device__ __attribute__((noinline)) float segment_box_dist2(V3 a, V3 b, V3 h) {
 }
 
 // Closest distance^2 between segments a1-b1 and a2-b2.
-__device__ __attribute__((noinline)) float segment_segment_dist2(V3 a1, V3 b1, V3 a2, V3 b2) {
+__device__ __forceinline__ float segment_segment_dist2_body(V3 a1, V3 b1, V3 a2, V3 b2) {
     const V3 d1 = {b1.x - a1.x, b1.y - a1.y, b1.z - a1.z};
     const V3 d2 = {b2.x - a2.x, b2.y - a2.y, b2.z - a2.z};
     const V3 w = {a1.x - a2.x, a1.y - a2.y, a1.z - a2.z};
@@ -380,8 +380,19 @@ __device__ __attribute__((noinline)) float segment_segment_dist2(V3 a1, V3 b1, V
     return dot3(dd, dd);
 }
 
+// The throughput kernels call the narrow phases as functions (one copy each instead
+// of one per call site: 35 pair sites in k_validity); the lane-group kernels, with
+// a couple of sites, inline them (a call there costs more than the code size saves).
+__device__ __attribute__((noinline)) float segment_box_dist2(V3 a, V3 b, V3 h) {
+    return segment_box_dist2_body(a, b, h);
+}
+__device__ __attribute__((noinline)) float segment_segment_dist2(V3 a1, V3 b1, V3 a2, V3 b2) {
+    return segment_segment_dist2_body(a1, b1, a2, b2);
+}
+
 // narrow phase of capsule (a, b, r) against box record bx (world -> box frame:
 // rotation by -yaw about z)
+template <bool INL = false>
 __device__ __forceinline__ bool capsule_box_narrow(V3 a, V3 b, float r, const float* __restrict__ bx) {
     const float cs = bx[6], sn = bx[7];
     V3 pa, pb;
@@ -394,7 +405,7 @@ __device__ __forceinline__ bool capsule_box_narrow(V3 a, V3 b, float r, const fl
         pb.x = fma_(cs, dx, sn * dy); pb.y = fma_(cs, dy, -(sn * dx)); pb.z = dz;
     }
     const V3 h = {bx[3], bx[4], bx[5]};
-    return segment_box_dist2(pa, pb, h) <= r * r;
+    return (INL ? segment_box_dist2_body(pa, pb, h) : segment_box_dist2(pa, pb, h)) <= r * r;
 }
 
 // Capsule C vs the plane and every box of the scene (skipping exempt pairs). The
@@ -918,7 +929,7 @@ __device__ __forceinline__ bool state_collides_ml(const float q[NQ], bool run, c
                 const float ri = sc.rad[i], rj = sc.rad[j];
                 if (!aabb_disjoint2(capsule_aabb(a1, b1, ri), capsule_aabb(a2, b2, rj))) {
                     const float rr = ri + rj;
-                    h = segment_segment_dist2(a1, b1, a2, b2) <= rr * rr;
+                    h = segment_segment_dist2_body(a1, b1, a2, b2) <= rr * rr;
                 }
             } else {
                 const int w = u - NPAIR;
@@ -928,7 +939,7 @@ __device__ __forceinline__ bool state_collides_ml(const float q[NQ], bool run, c
                     const float* pc = cs.v[c];
                     const V3 a = {pc[0], pc[1], pc[2]}, b = {pc[3], pc[4], pc[5]};
                     const float r = sc.rad[c];
-                    if (!aabb_disjoint(capsule_aabb(a, b, r), bx + 8, bx + 11)) h = capsule_box_narrow(a, b, r, bx);
+                    if (!aabb_disjoint(capsule_aabb(a, b, r), bx + 8, bx + 11)) h = capsule_box_narrow<true>(a, b, r, bx);
                 }
             }
         }

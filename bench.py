@@ -404,6 +404,9 @@ def main():
                 plan[key] = plan_record(tq, sq, stq, batch, dev, distributed, extra)
             except Exception as ex:
                 plan[key] = {"error": repr(ex)[:300]}
+        if group is not None:   # every rank done with the group's segment / communicator
+            dist.barrier()
+            group.leave()
 
     # ---- nearest-node and edge-launch rooflines on large trees (this rank, no group)
     rooflines_plan = None

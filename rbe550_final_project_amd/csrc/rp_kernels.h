@@ -1679,7 +1679,7 @@ template <int ITEMS>
 __global__ __launch_bounds__(FUSE_THREADS) void k_group_accept_small(
     GroupRecs gr, int64_t B, uint64_t seed, uint64_t g0, Bounds bd, double range, int cmax, double* A,
     int32_t* Apar, uint8_t* Acand, int64_t TA, double* Bt, int32_t* Bpar, uint8_t* Bcand, int64_t TB, int a_start,
-    int32_t* chain_end, int* status, PathArgs pa, PlanIO* io) {
+    int32_t* chain_end, int* status, PathArgs pa, PlanIO* io, const uint8_t* valid, int64_t sg_edge, int sg_stride) {
     __shared__ int lds[FUSE_THREADS / 64 + 1];
     __shared__ int first;
     const bool stop = gr.stop();
@@ -1719,6 +1719,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_group_accept_small(
         status[ST_NACC] = totalA;
         status[ST_FIRST] = first;
         status[ST_STOP] = stop ? 1 : 0;
+        if (sg_edge >= 0) status[ST_SG] = sg_flags(valid, sg_edge, sg_stride);   // (this rank's own check)
     }
     iteration_tail(status, totalB, TA, a_start, Apar, Bpar, chain_end, pa, io);
 }
@@ -1761,9 +1762,13 @@ __global__ void k_group_append(GroupRecs gr, const unsigned long long* __restric
 
 __global__ void k_group_finalize(const unsigned long long* __restrict__ incl, int64_t B, int* status, int64_t TA,
                                  int a_start, const int32_t* __restrict__ Apar, const int32_t* __restrict__ Bpar,
-                                 const int32_t* __restrict__ chain_end, PathArgs pa, PlanIO* io) {
+                                 const int32_t* __restrict__ chain_end, PathArgs pa, PlanIO* io,
+                                 const uint8_t* valid, int64_t sg_edge, int sg_stride) {
     const unsigned long long v = (B > 0 && !status[ST_STOP]) ? incl[B - 1] : 0ull;
-    if (threadIdx.x == 0) status[ST_NACC] = (int)(v >> GCOUNT_SHIFT);
+    if (threadIdx.x == 0) {
+        status[ST_NACC] = (int)(v >> GCOUNT_SHIFT);
+        if (sg_edge >= 0) status[ST_SG] = sg_flags(valid, sg_edge, sg_stride);
+    }
     iteration_tail(status, (int)(v & ((1ull << GCOUNT_SHIFT) - 1)), TA, a_start, Apar, Bpar, chain_end, pa, io);
 }
 

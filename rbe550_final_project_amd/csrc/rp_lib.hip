@@ -1016,8 +1016,13 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             return RP_OK;
         }
     }
-    int64_t sg_edge = (!straight && !grouped && !oob) ? (spec0 ? p.batch_min * G : p.batch_min) : -1;
-    const int sg_stride = spec0 ? G : 1;
+    // (a rank group rides them along its first front too, after its slice's groups,
+    // unless that launch is work-compacted)
+    const bool grouped_sg = grouped && !packed((p.batch_min / world) * G);
+    int64_t sg_edge = (!straight && !oob && (!grouped || grouped_sg))
+                          ? (spec0 ? p.batch_min * G : grouped ? (p.batch_min / world) * G : p.batch_min)
+                          : -1;
+    const int sg_stride = (spec0 || grouped) ? G : 1;
     // the prologue (k_plan_init): its own launch, or block 0 of the first
     // speculative front when that is the plan's next GPU work (one launch fewer on
     // the latency path); RBE_FUSE_INIT=0 keeps it separate (tests)
@@ -1058,7 +1063,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         HIP_TRY(hipGetLastError());
         init_pending = false;
     };
-    bool fuse_init = spec0 && !(sg_edge < 0 && !sg_known);
+    bool fuse_init = (spec0 || grouped) && !(sg_edge < 0 && !sg_known);
     if (const char* e = std::getenv("RBE_NN_SPLIT"))   // (a forced split search reads the trees first)
         if (*e && std::atoi(e) != 0) fuse_init = false;
     if (const char* e = std::getenv("RBE_FUSE_INIT"))
@@ -1169,7 +1174,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         spec_B = &Bt;
 
         const int64_t sg = (iter == 0) ? sg_edge : -1;   // start / goal ride along
-        if (!(speculate && B <= FUSE_MAX && !grouped)) launch_init();
+        if (!(grouped || (speculate && B <= FUSE_MAX))) launch_init();
         c->stats.samples += B;
         if (grouped) {
             // ---- rank group: the speculative front on my slice, ONE all-gather of
@@ -1180,10 +1185,15 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             const int32_t *nin = nullptr, *yin = nullptr;
             spec_split(gr0, per, nin, yin);
             const int pn = prof_begin(c, c->stream);
+            PlanInit ini_g{};
+            if (init_pending) {   // (iteration 0: trees of one root each, a_start)
+                ini_g = ini;
+                init_pending = false;
+            }
             hipLaunchKernelGGL(k_ext_conn_nn, dim3(blocks_for(per, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
                                Bt.q.p, TB, p.seed, gr0, per, bd, p.range,
                                p.resolution, cmax, a_start, c->efrom.p, c->eto.p, c->nd.p, c->valid.p, c->gfail.p,
-                               c->near_.p, c->yv.p, c->mv.p, nin, yin, PlanInit{});
+                               c->near_.p, c->yv.p, c->mv.p, nin, yin, ini_g);
             HIP_TRY(hipGetLastError());
             prof_end(c, pn, 0, c->stream);
             c->prof.nn_pairs += (double)per * (double)(TA + TB);
@@ -1191,8 +1201,8 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                 launch_edges_packed(c, c->efrom.p, c->eto.p, c->nd.p, per * G, kmax, 2, c->valid.p, G, c->gfail.p,
                                     c->stream, nullptr, 1);
             else
-                launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, per * G, kmax, 2, c->valid.p, G, c->gfail.p,
-                             c->stream);
+                launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, (per + (sg >= 0 ? 2 : 0)) * G, kmax, 2, c->valid.p, G,
+                             c->gfail.p, c->stream);
             // without a transport (world 1) the records go straight to the gathered buffer
             int32_t* recs = c->g_recv.p;   // every rank's records, rank-major
             int32_t* own = c->transport == TR_NONE ? c->g_recv.p : c->g_send.p;
@@ -1219,7 +1229,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
 #define RP_GROUP_SMALL(IT)                                                                                          \
     hipLaunchKernelGGL(k_group_accept_small<IT>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, gr, B, p.seed, g0, bd,  \
                        p.range, cmax, A.q.p, A.par.p, A.cand.p, TA, Bt.q.p, Bt.par.p, Bt.cand.p, TB, a_start,      \
-                       c->chain_end.p, status, pa, io)
+                       c->chain_end.p, status, pa, io, (const uint8_t*)c->valid.p, sg, sg_stride)
                 if (B <= FUSE_THREADS) RP_GROUP_SMALL(1);
                 else RP_GROUP_SMALL(4);
 #undef RP_GROUP_SMALL
@@ -1234,7 +1244,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                 hipLaunchKernelGGL(k_group_finalize, dim3(1), dim3(256), 0, c->stream,
                                    (const unsigned long long*)c->g_incl.p, B, status, TA, a_start,
                                    (const int32_t*)A.par.p, (const int32_t*)Bt.par.p, (const int32_t*)c->chain_end.p,
-                                   pa, io);
+                                   pa, io, (const uint8_t*)c->valid.p, sg, sg_stride);
             }
             HIP_TRY(hipGetLastError());
             run_program(0, tail_steps, seq, true);
@@ -1244,6 +1254,10 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                 if (hipEventElapsedTime(&ms, c->gx0, c->gx1) == hipSuccess) c->stats.exchange_ms += ms;
             }
             const int* st = h->status;
+            if (!sg_known) {   // (the same flags on every rank: they all leave here)
+                if (const int code = endpoint_status(st[ST_SG])) return endpoint_fail(code);
+                sg_known = true;
+            }
             if (st[ST_STOP]) break;   // some rank timed out: all leave at this iteration
             A.n = TA + st[ST_NACC];
             Bt.n = TB + st[ST_ADDED];

@@ -293,8 +293,9 @@ const char* rp_last_error(rp_ctx* ctx);
  * launches without opening another hardware queue. */
 int rp_get_stream(rp_ctx* ctx, void** stream_out);
 
-/* Kernel-level timing of the last rp_check_states_device call: average duration of
- * the validity kernel measured with HIP events on the context's stream (ms). */
+/* Kernel-level timing of the last rp_check_states_device call made with profiling
+ * on (rp_set_profiling): the validity kernel's duration measured with HIP events on
+ * the launch's stream (ms). RP_ERR_ARG if no such call was made. */
 int rp_last_kernel_ms(rp_ctx* ctx, double* ms);
 
 /* Numerics self-test (used by the parity tests): device sqrt(|x|), 0.13037 / x,

@@ -136,6 +136,7 @@ struct rp_ctx {
     PlanIO* h_io = nullptr;              // its pinned host mirror
     // kernel profile (rp_set_profiling): event pairs around NN and edge launches
     bool profiling = false;
+    bool timed = false;                  // a rp_check_states_device call recorded ev0 / ev1
     bool in_plan = false;
     rp_profile prof{};
     std::vector<hipEvent_t> pev;         // pool: pev[2i], pev[2i+1] = launch i
@@ -1784,9 +1785,14 @@ int rp_check_states_device(rp_ctx* c, const float* q, int64_t n, uint8_t* flags,
     if (n == 0) return RP_OK;
     RP_GUARD_BEGIN
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
-    HIP_TRY(hipEventRecord(c->ev0, s));
+    // the timing events only when profiling is on: two more API calls per launch make
+    // back-to-back small launches host-bound
+    if (c->profiling) HIP_TRY(hipEventRecord(c->ev0, s));
     launch_validity(c, q, n, flags, s);
-    HIP_TRY(hipEventRecord(c->ev1, s));
+    if (c->profiling) {
+        HIP_TRY(hipEventRecord(c->ev1, s));
+        c->timed = true;
+    }
     c->stats.states_checked = n;
     return RP_OK;
     RP_GUARD_END(c)
@@ -1794,6 +1800,10 @@ int rp_check_states_device(rp_ctx* c, const float* q, int64_t n, uint8_t* flags,
 
 int rp_last_kernel_ms(rp_ctx* c, double* ms) {
     if (!c || !ms) return RP_ERR_ARG;
+    if (!c->timed) {
+        c->err = "no timed rp_check_states_device call (rp_set_profiling on first)";
+        return RP_ERR_ARG;
+    }
     RP_GUARD_BEGIN
     HIP_TRY(hipEventSynchronize(c->ev1));
     float v = 0.0f;

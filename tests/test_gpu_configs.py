@@ -107,3 +107,26 @@ def test_kernel_profile_of_a_plan(gpu_ctx):
     assert pr["nn_launches"] >= META["C5_well_s4"]["iterations"] and pr["edge_launches"] > 0
     assert pr["nn_ms"] > 0 and pr["edge_ms"] > 0 and pr["nn_pairs"] > 1e9
     assert pr["edge_states"] == s["states_checked"]
+
+
+def test_validity_kernel_timing_needs_profiling():
+    """rp_last_kernel_ms: HIP events around rp_check_states_device only with
+    profiling on (they cost two API calls per launch); an error before any timed
+    call, a positive kernel time after one."""
+    import torch
+    ctx = Context(device=0, robot=model.robot_desc())
+    try:
+        sc = scenes.goal3_tallest()
+        ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+        dev = torch.device("cuda", 0)
+        q = torch.rand((4096, 9), device=dev, dtype=torch.float32)
+        f = torch.empty(4096, dtype=torch.uint8, device=dev)
+        ctx.check_states_device(q.data_ptr(), 4096, f.data_ptr())
+        with pytest.raises(native.NativeError):
+            ctx.last_kernel_ms()
+        ctx.set_profiling(True)
+        ctx.check_states_device(q.data_ptr(), 4096, f.data_ptr())
+        assert ctx.last_kernel_ms() > 0.0
+        ctx.set_profiling(False)
+    finally:
+        ctx.close()

@@ -112,21 +112,28 @@ def test_kernel_profile_of_a_plan(gpu_ctx):
 def test_validity_kernel_timing_needs_profiling():
     """rp_last_kernel_ms: HIP events around rp_check_states_device only with
     profiling on (they cost two API calls per launch); an error before any timed
-    call, a positive kernel time after one."""
-    import torch
+    call, a positive kernel time after one. (Device buffers through the HIP runtime
+    the library itself loaded, not torch's.)"""
+    import ctypes as C
+    hip = C.CDLL("libamdhip64.so.7")
     ctx = Context(device=0, robot=model.robot_desc())
+    n = 4096
+    q = (np.random.default_rng(1).random((n, 9)) * (model.Q_HI - model.Q_LO) + model.Q_LO).astype(np.float32)
+    dq, df = C.c_void_p(), C.c_void_p()
+    assert hip.hipMalloc(C.byref(dq), C.c_size_t(q.nbytes)) == 0
+    assert hip.hipMalloc(C.byref(df), C.c_size_t(n)) == 0
     try:
+        assert hip.hipMemcpy(dq, q.ctypes.data_as(C.c_void_p), C.c_size_t(q.nbytes), 1) == 0
         sc = scenes.goal3_tallest()
         ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
-        dev = torch.device("cuda", 0)
-        q = torch.rand((4096, 9), device=dev, dtype=torch.float32)
-        f = torch.empty(4096, dtype=torch.uint8, device=dev)
-        ctx.check_states_device(q.data_ptr(), 4096, f.data_ptr())
+        ctx.check_states_device(dq.value, n, df.value)
         with pytest.raises(native.NativeError):
             ctx.last_kernel_ms()
         ctx.set_profiling(True)
-        ctx.check_states_device(q.data_ptr(), 4096, f.data_ptr())
+        ctx.check_states_device(dq.value, n, df.value)
         assert ctx.last_kernel_ms() > 0.0
         ctx.set_profiling(False)
     finally:
         ctx.close()
+        hip.hipFree(dq)
+        hip.hipFree(df)

@@ -1,3 +1,3 @@
-for w in goal3_tallest_10box goal1_scattered_6box goal4_pentagon_10box; do
-SWEEP_STRAIGHT=0 timeout -k 10 120 python -u tools/plan_sweep.py $w 4096 16 32 64 128 256 512 > gpurun_out/sw_$w.log 2>&1; echo "== $w"; cat gpurun_out/sw_$w.log
-done
+export TMPDIR=/tmp
+timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tl_rrt -o t -- python tools/plan_trace.py goal3_tallest_10box 4096 > gpurun_out/tl_rrt.log 2>&1 || exit 1
+python tools/timeline.py gpurun_out/tl_rrt/t_kernel_trace.csv 40 > gpurun_out/tl_rrt.txt

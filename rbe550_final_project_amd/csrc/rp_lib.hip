@@ -341,7 +341,7 @@ void launch_edges_ml(rp_ctx* c, const double* from, const double* to, const int*
 void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd, int64_t n, int kmax,
                   int mode, uint8_t* valid, int group, int* gfail, hipStream_t s, const int* dcount = nullptr,
                   int per_item = 1, unsigned max_blocks = 0, const int* dkmax = nullptr, int64_t expect = 0,
-                  const StraightRide* sr = nullptr) {
+                  const StraightRide* sr = nullptr, bool front = false) {
     if (n <= 0) return;
     const int64_t threads = n * (int64_t)kmax;   // (dkmax: kmax is only the grid's size hint)
     StraightRide none{};
@@ -349,6 +349,13 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
     // expect: the states a gated launch (dcount) usually has, when far below its bound
     int gl = ml_lanes(expect > 0 ? expect : dkmax ? n * 32 : threads + ride.slots, true);
     if (ride.slots > 0 && gl == 1) gl = 8;   // (the ride-along exists in the lane-group kernels)
+    if (front) {   // RBE_ML_LANES_FRONT: the speculative fronts' launches only (A/B)
+        static const int f = [] {
+            const char* e = std::getenv("RBE_ML_LANES_FRONT");
+            return (e && *e) ? std::atoi(e) : 0;
+        }();
+        if (f == 8 || f == 16 || f == 32 || f == 64) gl = f;
+    }
     if (gl > 1) {
         const int ps = prof_begin(c, s);
         switch (gl) {
@@ -1294,7 +1301,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             c->prof.nn_pairs += (double)B * (double)(TA + TB);
             launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, (B + (sg >= 0 ? 2 : 0)) * G, kmax, 2, c->valid.p, G,
                          c->gfail.p, c->stream, nullptr, 1, 0, nullptr, 0,
-                         (iter == 0 && ride.slots > 0) ? &ride : nullptr);
+                         (iter == 0 && ride.slots > 0) ? &ride : nullptr, true);
             pa.seq = seq;   // (an iteration that finishes the plan publishes it)
 #define RP_ITER_SMALL(IT)                                                                                           \
     hipLaunchKernelGGL(k_iter_accept_small<IT>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, (const int*)c->gfail.p,   \

@@ -348,7 +348,10 @@ def main():
             from rbe550_final_project_amd.distributed import Group
             group = Group(ctx, transport="shm" if args.backend == "gloo" else "rccl")
         try:
-            run_plans(ctx, {"queries": wl["queries"][:2]}, args.plan_batch, 100, group)   # warm-up
+            # warm-up: one untimed pass over the whole C3 workload in both modes (a
+            # 2-query warm-up left the first timed workload at 2x its median on one box)
+            run_plans(ctx, wl, args.plan_batch, 100, group)
+            run_plans(ctx, wl, args.plan_batch, 100, group, straight_first=False)
             times, pstates, st = run_plans(ctx, wl, args.plan_batch, 0, group)
             plan = plan_record(times, pstates, st, args.plan_batch, dev, distributed,
                                {"mode": "product default: straight edge first, then RRT-Connect"})

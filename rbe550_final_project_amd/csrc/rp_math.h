@@ -284,6 +284,12 @@ __device__ __forceinline__ Aabb capsule_aabb(V3 a, V3 b, float r) {
     o.lo.z = fminr(a.z, b.z) - r; o.hi.z = fmaxr(a.z, b.z) + r;
     return o;
 }
+// separation of capsule AABB u from box [lo, hi]: > 0 iff disjoint (max of the six
+// interval differences; see aabb_disjoint)
+__device__ __forceinline__ float aabb_sep(const Aabb& u, const float* lo, const float* hi) {
+    const float a = fmaxr(fmaxr(u.lo.x - hi[0], lo[0] - u.hi.x), fmaxr(u.lo.y - hi[1], lo[1] - u.hi.y));
+    return fmaxr(a, fmaxr(u.lo.z - hi[2], lo[2] - u.hi.z));
+}
 #ifndef RP_AABB_CMP
 // The six interval tests as one max of differences: for finite (or infinite, never
 // NaN) operands with subnormals kept, x - y > 0 <=> x > y (x != y => x - y != 0), so
@@ -652,14 +658,32 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
 #pragma unroll
     for (int cl = 0; cl < NCL; ++cl) {
         const float* cr = s.cl.c[cl];
+#ifndef RP_ENV_CMP
+        // cluster test, box test and exempt bit folded into one separation value:
+        // candidate iff max(cluster sep, box sep, exempt ? inf : -inf) <= 0 (one lane
+        // mask per box instead of three combined by scalar ops: A/B +1.9 % goal3 4M,
+        // +1.6 % at 64k; -DRP_ENV_CMP builds the mask form)
+        const float csep = aabb_sep(u, cr, cr + 4);
+        if (!__any(csep <= 0.0f)) continue;
+#else
         const bool near_cl = !aabb_disjoint(u, cr, cr + 4);
         if (!__any(near_cl)) continue;
+#endif
         const int j0 = __float_as_int(cr[3]), nj = __float_as_int(cr[7]);
         for (int j = j0; j < j0 + nj; ++j) {
             // the whole 64-B record in one scalar load; branch-free candidate test
             struct Rec { float v[16]; };
             const Rec rec = *reinterpret_cast<const Rec*>(sc->box[j]);
             const float* bx = rec.v;
+#ifndef RP_ENV_CMP
+            const float ex = ((__float_as_uint(bx[14]) >> C) & 1u) ? __builtin_inff() : -__builtin_inff();
+            const bool cand = fmaxr(fmaxr(csep, ex), aabb_sep(u, bx + 8, bx + 11)) <= 0.0f;
+            const unsigned long long m = __ballot(cand);
+            if (!m) continue;
+            room_sb(s, __popcll(m));
+            if (cand) enqueue_sb<C>(k, bx, r, s, m);
+            s.nsb += __popcll(m);
+#else
             const bool exempt = (__float_as_uint(bx[14]) >> C) & 1u;
             const bool apart = aabb_disjoint(u, bx + 8, bx + 11);   // both evaluated: no branch
             const bool cand = near_cl && !exempt && !apart;
@@ -668,6 +692,7 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
             room_sb(s, __popcll(m));
             if (cand) enqueue_sb<C>(k, bx, r, s, m);
             s.nsb += __popcll(m);
+#endif
         }
     }
     return false;

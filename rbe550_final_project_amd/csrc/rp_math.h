@@ -840,9 +840,18 @@ __device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene
     v.s.nsb = 0;
     v.s.lane = (int)__lane_id();
     {
+#ifndef RP_LIM_CMP
+        // q_j in [lo_j, hi_j] for all j <=> max_j max(lo_j - q_j, q_j - hi_j) <= 0 (the
+        // aabb_disjoint argument; one lane mask instead of 18 ANDed: +1.9 % goal3 A/B)
+        float ex = -__builtin_inff();
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) ex = fmaxr(ex, fmaxr(Q_LO_F[j] - q[j], q[j] - Q_HI_F[j]));
+        const bool in = ex <= 0.0f;
+#else
         bool in = true;
 #pragma unroll
         for (int j = 0; j < NQ; ++j) in = in && q[j] >= Q_LO_F[j] && q[j] <= Q_HI_F[j];
+#endif
         v.s.in_limits = !__any(!in);
     }
     v.s.plane_z = sc->plane_z;

@@ -574,7 +574,13 @@ __device__ __forceinline__ void pop_ss(S& s) {
         const Aabb v = capsule_aabb(a2, b2, rj);
         if (!aabb_disjoint2(u, v)) {
             const float rr = ri + rj;
+#ifndef RP_HIT_STORE
+            // an LDS OR (ds_or_b32) from every popping lane instead of a store under a
+            // per-lane branch: no exec-mask save / restore (+2.9 % goal3 A/B)
+            atomicOr(&s.Q->hit[tag & 63], (int)(segment_segment_dist2(a1, b1, a2, b2) <= rr * rr));
+#else
             if (segment_segment_dist2(a1, b1, a2, b2) <= rr * rr) s.Q->hit[tag & 63] = 1;
+#endif
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -589,7 +595,11 @@ __device__ __forceinline__ void pop_sb(S& s) {
     if (r < take) {
         const float* it = s.Q->sb[s.nsb - 1 - r];
         const V3 pa = {it[0], it[1], it[2]}, pb = {it[3], it[4], it[5]}, h = {it[6], it[7], it[8]};
+#ifndef RP_HIT_STORE
+        atomicOr(&s.Q->hit[__float_as_int(it[10])], (int)(segment_box_dist2(pa, pb, h) <= it[9]));
+#else
         if (segment_box_dist2(pa, pb, h) <= it[9]) s.Q->hit[__float_as_int(it[10])] = 1;
+#endif
     }
     __builtin_amdgcn_wave_barrier();
     s.nsb -= take;

@@ -122,7 +122,12 @@ typedef struct rp_plan_params {
                                start -> goal first and return it when valid (the path the
                                shortcut stage would reduce any solution to); < 0 = always
                                run RRT-Connect; ignored when simplify == 0               */
-    int32_t reserved;       /* 0                                                            */
+    int32_t chunk;          /* execution only, never the result: an iteration runs as ordered
+                               sub-batches of chunk, 4 chunk, 16 chunk, ... samples and ends
+                               after the sub-batch holding the first REACHED sample (the
+                               trees keep the appends up to that sample, DESIGN.md §4 step
+                               5, whatever the sub-batching). 0 = default 4096; < 0 = the
+                               whole iteration as one batch                               */
 } rp_plan_params;
 
 /* rp_ik parameters (defaults follow Genesis inverse_kinematics). Zero / negative
@@ -277,6 +282,13 @@ int rp_group_init(rp_ctx* ctx, int32_t rank, int32_t world, rp_allgather_fn fn, 
 int rp_group_init_shm(rp_ctx* ctx, int32_t rank, int32_t world, void* base, int64_t bytes);
 int rp_group_rccl_unique_id(uint8_t id_out[RP_RCCL_ID_BYTES]);
 int rp_group_init_rccl(rp_ctx* ctx, int32_t rank, int32_t world, const uint8_t id[RP_RCCL_ID_BYTES]);
+
+/* What the context's rank group is, as its transport sees it: for RCCL the
+ * communicator's own ncclCommUserRank / ncclCommCount (so a measurement at N GPUs can
+ * show that RCCL saw N ranks); otherwise the rank / world given at initialisation.
+ * transport: RP_TRANSPORT_*; a context outside any group reports rank 0 of 1, NONE. */
+enum { RP_TRANSPORT_NONE = 0, RP_TRANSPORT_HOST = 1, RP_TRANSPORT_RCCL = 2, RP_TRANSPORT_SHM = 3 };
+int rp_group_info(rp_ctx* ctx, int32_t* rank_out, int32_t* world_out, int32_t* transport_out);
 
 int rp_get_stats(rp_ctx* ctx, rp_stats* out);
 

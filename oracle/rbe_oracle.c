@@ -913,7 +913,12 @@ int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], co
         } else {
             memcpy(trec, tmine, sizeof(int32_t) * 2 * pt);
         }
-        /* append connect chains in target order; first REACHED wins */
+        /* append connect chains in target order; the first REACHED target wins and
+         * ends the iteration: the trees keep the appends of the samples up to and
+         * including the winning one, none after it (rp_lib.hip plan_impl runs an
+         * iteration as ordered sub-batches and stops after the one that solves; the
+         * path only depends on the iteration's snapshot and the winning sample, so
+         * this truncation is what makes the result independent of the sub-batching) */
         for (int64_t t = 0; t < nacc; ++t) {
             const int32_t y = trec[2 * t];
             const int L = trec[2 * t + 1];
@@ -923,7 +928,7 @@ int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], co
             int32_t par = y;
             for (int c = 0; c < L; ++c) par = (int32_t)tree_add(Bt, chain[c], par);
             const int reached = (L == m) && reach;
-            if (reached && !solved) {
+            if (reached) {
                 solved = 1;
                 if (a_start) {       /* x in start tree, chain end in goal tree */
                     s_node = A->parent[tnode[t]];
@@ -932,8 +937,10 @@ int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], co
                     s_node = Bt->parent[par];
                     g_node = (int32_t)tnode[t];
                 }
+                A->n = tnode[t] + 1;   /* drop the later samples' extension nodes */
+                break;
             }
-            if (!reached && a_start) A->cand[tnode[t]] = 1;
+            if (a_start) A->cand[tnode[t]] = 1;
         }
         gbase += (uint64_t)B;
         B = 2 * B < BMAX ? 2 * B : BMAX;

@@ -17,6 +17,7 @@ OK = 0
 ERR_ARG, ERR_DEVICE, ERR_STATE, ERR_CAPACITY, ERR_EXCHANGE = -1, -2, -3, -4, -5
 
 STATUS_NONE, STATUS_EXACT, STATUS_APPROXIMATE, STATUS_TIMEOUT, STATUS_INVALID_START, STATUS_INVALID_GOAL = range(6)
+TRANSPORT_NAMES = {0: "none", 1: "host", 2: "rccl", 3: "shm"}   # RP_TRANSPORT_*
 STATUS_NAMES = {0: "NONE", 1: "EXACT", 2: "APPROXIMATE", 3: "TIMEOUT", 4: "INVALID_START", 5: "INVALID_GOAL"}
 
 
@@ -37,7 +38,7 @@ class PlanParams(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("batch", C.c_int64), ("batch_min", C.c_int64), ("range", C.c_double),
                 ("resolution", C.c_double), ("timeout_s", C.c_double), ("max_iters", C.c_int64),
                 ("n_waypoints", C.c_int32), ("simplify", C.c_int32), ("tree_capacity", C.c_int64),
-                ("straight_first", C.c_int32), ("reserved", C.c_int32)]
+                ("straight_first", C.c_int32), ("chunk", C.c_int32)]
 
 
 class IkParams(C.Structure):
@@ -90,7 +91,7 @@ def make_boxes(boxes):
 
 
 def make_params(seed=0, batch=4096, range_=0.0, resolution=0.0, timeout_s=5.0, max_iters=0, batch_min=0,
-                n_waypoints=100, simplify=True, tree_capacity=0, straight_first=True):
+                n_waypoints=100, simplify=True, tree_capacity=0, straight_first=True, chunk=0):
     p = PlanParams()
     p.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     p.batch = int(batch)
@@ -103,4 +104,5 @@ def make_params(seed=0, batch=4096, range_=0.0, resolution=0.0, timeout_s=5.0, m
     p.simplify = 1 if simplify else 0
     p.tree_capacity = int(tree_capacity)
     p.straight_first = 0 if straight_first else -1   # 0 = default (on with simplification)
+    p.chunk = int(chunk)   # first sub-batch of an iteration (execution only; 0 = 4096, < 0 = none)
     return p

@@ -497,8 +497,9 @@ __global__ void k_ext_result_flag(const uint8_t* __restrict__ valid, const int32
 // 0 and 1, written by the first validity launch of rp_plan).
 // ST_SL: the straight edge start -> goal rode along the plan's first edge launch and
 // is valid (1), else 0 (not checked, or colliding)
+// ST_FIRSTI: the sample index of the first REACHED target (large group accepts)
 enum { ST_NACC = 0, ST_ADDED = 1, ST_FIRST = 2, ST_SNODE = 3, ST_GNODE = 4, ST_SG = 5, ST_STOP = 6, ST_SL = 7,
-       ST_WORDS = 8 };
+       ST_FIRSTI = 8, ST_WORDS = 9 };
 
 // I/O record of one rp_plan call. The device copy holds the live status; a
 // pinned, host-coherent mirror receives what the host needs (status after every
@@ -1450,8 +1451,13 @@ __device__ void iteration_tail(int* status, int added, int64_t TA, int a_start, 
 __global__ void k_finalize(int* status, const int32_t* __restrict__ inclL, int64_t TA, int a_start,
                            const int32_t* __restrict__ Apar, const int32_t* __restrict__ Bpar,
                            const int32_t* __restrict__ chain_end, PathArgs pa, PlanIO* io) {
-    const int nacc = status[ST_NACC];
-    iteration_tail(status, nacc > 0 ? inclL[nacc - 1] : 0, TA, a_start, Apar, Bpar, chain_end, pa, io);
+    // the first REACHED target ends the iteration: the trees keep the appends up to it
+    const int nacc = status[ST_NACC], fr = status[ST_FIRST];
+    const bool solved = fr != 0x7fffffff;
+    __syncthreads();   // (every lane has read the words before lane 0 rewrites ST_NACC)
+    if (solved && threadIdx.x == 0) status[ST_NACC] = fr + 1;
+    iteration_tail(status, solved ? inclL[fr] : nacc > 0 ? inclL[nacc - 1] : 0, TA, a_start, Apar, Bpar, chain_end,
+                   pa, io);
 }
 
 // single-block connect record + scan + append + iteration tail (targets <= FUSE_MAX)
@@ -1461,9 +1467,9 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_conn_accept_small(
     const double* A, int64_t TA0, double* Bt, int32_t* Bpar, uint8_t* Bcand, int64_t TB, double range, int cmax,
     int a_start, uint8_t* Acand, const int32_t* Apar, int32_t* chain_end, PathArgs pa, PlanIO* io) {
     __shared__ int lds[FUSE_THREADS / 64 + 1];
-    __shared__ int first;
+    __shared__ unsigned long long firstpk;   // first REACHED: (target << 32) | tree-B nodes up to it
     const int nacc = status[ST_NACC];
-    if (threadIdx.x == 0) first = 0x7fffffff;
+    if (threadIdx.x == 0) firstpk = ~0ull;
     const int64_t t0 = (int64_t)threadIdx.x * ITEMS;
     int L[ITEMS];
     int cnt = 0;
@@ -1474,18 +1480,25 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_conn_accept_small(
         cnt += L[r] > 0 ? L[r] : 0;
     }
     int total;
-    int64_t off = TB + block_scan_excl(cnt, lds, &total);   // (its barriers also order `first`)
+    int64_t off = TB + block_scan_excl(cnt, lds, &total);   // (its barriers also order `firstpk`)
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
         if (L[r] < 0) continue;
         const int64_t t = t0 + r;
-        if (conn_append_one(t, y[t], L[r], off, A, TA0, Bt, Bpar, Bcand, range, cmax, a_start, Acand, chain_end))
-            atomicMin(&first, (int)t);
+        const bool reached =
+            conn_append_one(t, y[t], L[r], off, A, TA0, Bt, Bpar, Bcand, range, cmax, a_start, Acand, chain_end);
         off += L[r];
+        if (reached) atomicMin(&firstpk, ((unsigned long long)t << 32) | (unsigned)(off - TB));
     }
     __syncthreads();
-    if (threadIdx.x == 0) status[ST_FIRST] = first;
-    iteration_tail(status, total, TA0, a_start, Apar, Bpar, chain_end, pa, io);
+    // the first REACHED target ends the iteration: the trees keep the appends up to it
+    const bool solved = firstpk != ~0ull;
+    if (threadIdx.x == 0) {
+        status[ST_FIRST] = solved ? (int)(firstpk >> 32) : 0x7fffffff;
+        if (solved) status[ST_NACC] = (int)(firstpk >> 32) + 1;
+    }
+    iteration_tail(status, solved ? (int)(firstpk & 0xffffffffu) : total, TA0, a_start, Apar, Bpar, chain_end, pa,
+                   io);
 }
 
 // single-block accept of a speculative iteration (k_ext_conn_nn): extension
@@ -1503,7 +1516,8 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
     int32_t* Bpar, uint8_t* Bcand, int64_t TB, int a_start, int32_t* chain_end, int* status,
     const uint8_t* valid, int64_t sg_edge, int sg_stride, PathArgs pa, PlanIO* io) {
     __shared__ unsigned long long lds64[FUSE_THREADS / 64];
-    __shared__ int first, sgv, slv, st0[ST_WORDS];
+    __shared__ int sgv, slv, st0[ST_WORDS];
+    __shared__ unsigned long long firstpk;   // first REACHED: (target << 32) | tree-B nodes up to it
     __shared__ unsigned long long cpart[64];
     __shared__ int32_t l_apar[FUSE_MAX], l_cend[FUSE_MAX], l_bpar[TAIL_LB], l_asrc[FUSE_MAX], l_bsrc[TAIL_LB];
     __shared__ double l_P[SPMAX * NQ];
@@ -1551,8 +1565,8 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
     unsigned long long tot;
     const unsigned long long ex = block_scan_excl(((unsigned long long)na << 32) | (unsigned)nl, lds64, &tot);
     const int exA = (int)(ex >> 32), exB = (int)(ex & 0xffffffffu);
-    const int totalA = (int)(tot >> 32), totalB = (int)(tot & 0xffffffffu);
-    if (threadIdx.x == 0) first = 0x7fffffff;
+    const int totalB = (int)(tot & 0xffffffffu);
+    if (threadIdx.x == 0) firstpk = ~0ull;
     lds_barrier();
     RP_TSTAMP(0, 2);
     int t = exA;
@@ -1585,30 +1599,35 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
         chain_end[t] = L[r] > 0 ? par : -1;
         l_cend[t] = L[r] > 0 ? par : -1;
         Acand[pos] = (!reached && a_start) ? 1 : 0;
-        if (reached) atomicMin(&first, t);
         off += L[r];
+        if (reached) atomicMin(&firstpk, ((unsigned long long)t << 32) | (unsigned)(off - TB));
         ++t;
     }
     // the tail reads this block's appends from LDS and their sources, unless tree B
     // grew past the LDS window (then from global: a full barrier)
     if (totalB > TAIL_LB) __syncthreads();
     else lds_barrier();
+    // the first REACHED target ends the iteration: the trees keep the appends up to
+    // it; nodes written past the new sizes are dead
+    const int first = firstpk == ~0ull ? 0x7fffffff : (int)(firstpk >> 32);
+    const int nA = firstpk == ~0ull ? (int)(tot >> 32) : first + 1;
+    const int nB = firstpk == ~0ull ? totalB : (int)(firstpk & 0xffffffffu);
     // the chain nodes' states: one parallel copy (not a serial chain per sample)
-    const int nbw = totalB < TAIL_LB ? totalB : TAIL_LB;
+    const int nbw = nB < TAIL_LB ? nB : TAIL_LB;
     for (int k = threadIdx.x; k < nbw * NQ; k += FUSE_THREADS) {
         const int j = k / NQ, d = k - j * NQ;
         Bt[(TB + j) * NQ + d] = chain_node[(int64_t)l_bsrc[j] * NQ + d];
     }
     if (threadIdx.x == 0) {
-        status[ST_NACC] = totalA;
+        status[ST_NACC] = nA;
         status[ST_FIRST] = first;
         if (sg_edge >= 0) status[ST_SG] = sgv;
     }
     if (threadIdx.x == 64 && sg_edge >= 0) st0[ST_SG] = sgv;   // (st0 read by the tail after its barriers)
     RP_TSTAMP(0, 3);
-    const TailLds ov{l_apar, TA, totalA, l_bpar, TB, totalB < TAIL_LB ? totalB : TAIL_LB, l_cend, totalA, first, slv,
+    const TailLds ov{l_apar, TA, nA, l_bpar, TB, nbw, l_cend, nA, first, slv,
                      st0, cpart, l_P, l_asrc, l_bsrc, ext_node, chain_node};
-    iteration_tail(status, totalB, TA, a_start, Apar, Bpar, chain_end, pa, io, &ov);
+    iteration_tail(status, nB, TA, a_start, Apar, Bpar, chain_end, pa, io, &ov);
 }
 
 // solution path for host-chosen join nodes (approximate solutions)
@@ -1681,7 +1700,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_group_accept_small(
     int32_t* Apar, uint8_t* Acand, int64_t TA, double* Bt, int32_t* Bpar, uint8_t* Bcand, int64_t TB, int a_start,
     int32_t* chain_end, int* status, PathArgs pa, PlanIO* io, const uint8_t* valid, int64_t sg_edge, int sg_stride) {
     __shared__ int lds[FUSE_THREADS / 64 + 1];
-    __shared__ int first;
+    __shared__ unsigned long long firstpk;   // first REACHED: (target << 32) | tree-B nodes up to it
     const bool stop = gr.stop();
     const int64_t k0 = (int64_t)threadIdx.x * ITEMS;
     int L[ITEMS];
@@ -1700,7 +1719,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_group_accept_small(
     int totalA, totalB;
     const int exA = block_scan_excl(na, lds, &totalA);
     const int exB = block_scan_excl(nl, lds, &totalB);
-    if (threadIdx.x == 0) first = 0x7fffffff;
+    if (threadIdx.x == 0) firstpk = ~0ull;
     __syncthreads();
     int t = exA;
     int64_t off = TB + exB;
@@ -1708,20 +1727,23 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_group_accept_small(
     for (int r = 0; r < ITEMS; ++r) {
         if (L[r] < 0) continue;
         const int64_t i = k0 + r;
-        if (group_append_one(i, gr.rec(i), t, off, seed, g0, bd, range, cmax, A, Apar, Acand, TA, Bt, Bpar, Bcand,
-                             a_start, chain_end))
-            atomicMin(&first, t);
+        const bool reached = group_append_one(i, gr.rec(i), t, off, seed, g0, bd, range, cmax, A, Apar, Acand, TA,
+                                              Bt, Bpar, Bcand, a_start, chain_end);
         off += L[r];
+        if (reached) atomicMin(&firstpk, ((unsigned long long)t << 32) | (unsigned)(off - TB));
         ++t;
     }
     __syncthreads();
+    // the first REACHED target ends the iteration: the trees keep the appends up to it
+    const bool solved = firstpk != ~0ull;
     if (threadIdx.x == 0) {
-        status[ST_NACC] = totalA;
-        status[ST_FIRST] = first;
+        status[ST_NACC] = solved ? (int)(firstpk >> 32) + 1 : totalA;
+        status[ST_FIRST] = solved ? (int)(firstpk >> 32) : 0x7fffffff;
         status[ST_STOP] = stop ? 1 : 0;
         if (sg_edge >= 0) status[ST_SG] = sg_flags(valid, sg_edge, sg_stride);   // (this rank's own check)
     }
-    iteration_tail(status, totalB, TA, a_start, Apar, Bpar, chain_end, pa, io);
+    iteration_tail(status, solved ? (int)(firstpk & 0xffffffffu) : totalB, TA, a_start, Apar, Bpar, chain_end, pa,
+                   io);
 }
 
 // large batches: per-sample counts (accepted << 40 | chain nodes), an inclusive
@@ -1732,6 +1754,7 @@ __global__ void k_group_counts(GroupRecs gr, int64_t B, unsigned long long* __re
     const bool stop = gr.stop();
     if (i == 0) {
         status[ST_FIRST] = 0x7fffffff;
+        status[ST_FIRSTI] = 0x7fffffff;
         status[ST_STOP] = stop ? 1 : 0;
     }
     if (i >= B) return;
@@ -1756,15 +1779,21 @@ __global__ void k_group_append(GroupRecs gr, const unsigned long long* __restric
     const int64_t t = (int64_t)(v >> GCOUNT_SHIFT) - 1;
     const int64_t off = TB + (int64_t)(v & ((1ull << GCOUNT_SHIFT) - 1)) - L;
     if (group_append_one(i, rc, t, off, seed, g0, bd, range, cmax, A, Apar, Acand, TA, Bt, Bpar, Bcand, a_start,
-                         chain_end))
-        atomicMin(&status[ST_FIRST], (int)t);   // a reached chain solves: rare, one atomic each
+                         chain_end)) {   // a reached chain solves: rare, two atomics each
+        atomicMin(&status[ST_FIRST], (int)t);
+        atomicMin(&status[ST_FIRSTI], (int)i);   // (t and i rise together: the same sample)
+    }
 }
 
 __global__ void k_group_finalize(const unsigned long long* __restrict__ incl, int64_t B, int* status, int64_t TA,
                                  int a_start, const int32_t* __restrict__ Apar, const int32_t* __restrict__ Bpar,
                                  const int32_t* __restrict__ chain_end, PathArgs pa, PlanIO* io,
                                  const uint8_t* valid, int64_t sg_edge, int sg_stride) {
-    const unsigned long long v = (B > 0 && !status[ST_STOP]) ? incl[B - 1] : 0ull;
+    // the first REACHED sample ends the iteration: the trees keep the appends up to
+    // and including it (its inclusive counts)
+    const int fi = status[ST_FIRSTI];
+    const unsigned long long v = (B > 0 && !status[ST_STOP]) ? incl[fi != 0x7fffffff ? fi : B - 1] : 0ull;
+    __syncthreads();   // (every lane has read the words before lane 0 rewrites ST_NACC)
     if (threadIdx.x == 0) {
         status[ST_NACC] = (int)(v >> GCOUNT_SHIFT);
         if (sg_edge >= 0) status[ST_SG] = sg_flags(valid, sg_edge, sg_stride);

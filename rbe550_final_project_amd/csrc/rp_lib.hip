@@ -167,6 +167,10 @@ struct rp_ctx {
     char* shm_dev = nullptr;
     int64_t shm_bytes = 0;
     int64_t shm_k = 0;                   // exchanges done (lockstep on every rank)
+    // a grouped plan that failed on this rank (an error inside the iteration loop)
+    // leaves the group out of step: every later grouped rp_plan fails with
+    // RP_ERR_EXCHANGE until the group is initialised again (no silent divergence)
+    bool group_broken = false;
     DevBuf<DI2> nn_part;                 // split nearest-node search: (distance, index) per range
 
     void free_staging() {
@@ -185,6 +189,7 @@ struct rp_ctx {
         rank = 0;
         world = 1;
         transport = 0;
+        group_broken = false;
         g_fn = nullptr;
         g_user = nullptr;
     }
@@ -866,7 +871,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     }
     const int64_t ne = std::max<int64_t>({PMAX + 2, ((BMAX + world - 1) / world) * cmax, (int64_t)SPMAX * SPMAX / 2,
                                           (std::min<int64_t>(BMAX, FUSE_MAX) + 2) * (cmax + 1),
-                                          grouped ? PMAX * (cmax + 1) : 0});
+                                          grouped ? (PMAX + 2) * (cmax + 1) : 0});
     c->efrom.ensure(ne * NQ);
     c->eto.ensure(ne * NQ);
     c->nd.ensure(ne);
@@ -934,7 +939,20 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     auto packed = [&](int64_t n_edges) {
         return packed_mode >= 0 ? packed_mode == 1 : n_edges * (int64_t)kmax >= ((int64_t)1 << 20);
     };
-    const bool spec0 = speculate && p.batch_min <= FUSE_MAX;
+    // sub-batches (rp_plan_params.chunk): an iteration runs as ordered sub-batches of
+    // chunk0, chunk0 * chunk_growth, ... samples and ends after the one holding the
+    // first REACHED sample; the trees do not depend on it (the oracle appends up to
+    // that sample whatever the split). RBE_PLAN_CHUNK / RBE_CHUNK_GROWTH override it
+    // (tests, A/B).
+    int64_t chunk0 = p.chunk > 0 ? p.chunk : p.chunk < 0 ? INT64_MAX : 4096;
+    if (const char* e = std::getenv("RBE_PLAN_CHUNK"))
+        if (*e) chunk0 = std::atoll(e) > 0 ? std::atoll(e) : INT64_MAX;
+    if (chunk0 != INT64_MAX) chunk0 = ((chunk0 + world - 1) / world) * world;
+    int64_t chunk_growth = 4;
+    if (const char* e = std::getenv("RBE_CHUNK_GROWTH"))
+        if (*e) chunk_growth = std::max<int64_t>(1, std::atoll(e));
+    const int64_t C00 = std::min<int64_t>(p.batch_min, chunk0);   // the plan's first sub-batch
+    const bool spec0 = speculate && C00 <= FUSE_MAX;
     const int level = p.simplify < 0 ? 0 : p.simplify > 2 ? 1 : p.simplify;
     // straight-first (rp_plan_params.straight_first): with simplification on, a valid
     // straight edge start -> goal is the path the shortcut stage (REDUCE's greedy
@@ -1026,9 +1044,9 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     }
     // (a rank group rides them along its first front too, after its slice's groups,
     // unless that launch is work-compacted)
-    const bool grouped_sg = grouped && !packed((p.batch_min / world) * G);
+    const bool grouped_sg = grouped && !packed((C00 / world) * G);
     int64_t sg_edge = (!straight && !oob && (!grouped || grouped_sg))
-                          ? (spec0 ? p.batch_min * G : grouped ? (p.batch_min / world) * G : p.batch_min)
+                          ? (spec0 ? C00 * G : grouped ? (C00 / world) * G : C00)
                           : -1;
     const int sg_stride = (spec0 || grouped) ? G : 1;
     // the prologue (k_plan_init): its own launch, or block 0 of the first
@@ -1054,8 +1072,8 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             if (*e) on = std::atoi(e) != 0;
         const int nd_s = (int)std::ceil(std::sqrt(h_dist2(start, goal)) / p.resolution);
         const int slots = nd_s > 1 ? nd_s : 1;
-        // (the first front's edge launch: (batch_min + 2) * G edges x kmax slots)
-        const int64_t items = (p.batch_min + 2) * (int64_t)G * kmax;
+        // (the first front's edge launch: (C00 + 2) * G edges x kmax slots)
+        const int64_t items = (C00 + 2) * (int64_t)G * kmax;
         if (on && slots <= 8192 && ml_lanes(items + slots, true) > 1) {
             ride.slots = slots;
             ride.nd = nd_s;
@@ -1143,9 +1161,11 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     for (int i = 0; i < NQ; ++i) { bd.lo[i] = lo[i]; bd.hi[i] = hi[i]; }
     // speculative fronts on large trees: nearest nodes by the split search (both
     // searches; the second's queries are the steered new nodes, so it needs the
-    // first's result: a large second search forces the first)
+    // first's result: a large second search forces the first). Searches run over the
+    // iteration's snapshot (snap_*), not over the nodes earlier sub-batches appended.
     Tree* spec_A = nullptr;
     Tree* spec_B = nullptr;
+    int64_t snap_A = 0, snap_B = 0;
     auto spec_split = [&](uint64_t gs0, int64_t n, const int32_t*& nin, const int32_t*& yin) {
         NnQuery q1{};
         q1.kind = NNQ_SAMPLE;
@@ -1154,14 +1174,14 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         q1.i0 = 0;
         q1.bd = bd;
         q1.range = p.range;
-        const bool big_b = (double)n * (double)spec_B->n >= (double)(1 << 24);
-        if (!nn_split(c, q1, n, spec_A->q.p, spec_A->n, c->near_.p, big_b)) return;
+        const bool big_b = (double)n * (double)snap_B >= (double)(1 << 24);
+        if (!nn_split(c, q1, n, spec_A->q.p, snap_A, c->near_.p, big_b)) return;
         nin = c->near_.p;
         NnQuery q2 = q1;
         q2.kind = NNQ_STEER;
         q2.A = spec_A->q.p;
         q2.near = c->near_.p;
-        if (nn_split(c, q2, n, spec_B->q.p, spec_B->n, c->yv.p)) yin = c->yv.p;
+        if (nn_split(c, q2, n, spec_B->q.p, snap_B, c->yv.p)) yin = c->yv.p;
     };
     int solved = 0;
     int32_t s_node = -1, g_node = -1;
@@ -1169,258 +1189,269 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     int64_t iter = 0, B = p.batch_min;
     uint64_t gbase = 0;
     for (; iter < p.max_iters; ++iter, gbase += (uint64_t)B, B = std::min(BMAX, 2 * B)) {
-        const int64_t per = B / world;
         const int tflag = (now_s() - t_solve) >= p.timeout_s;
         if (!grouped && tflag) break;   // (a group votes through its exchange)
         const int a_start = (iter % 2) == 0;
         Tree& A = c->tree[a_start ? 0 : 1];
         Tree& Bt = c->tree[a_start ? 1 : 0];
         if (A.n + B > cap || Bt.n + B * cmax > cap) break;
+        // the iteration's snapshot: every nearest-node search of its samples runs over
+        // these nodes; appends go to the trees' current ends
         const int64_t TA = A.n, TB = Bt.n;
-        const uint64_t g0 = gbase;
         spec_A = &A;
         spec_B = &Bt;
-
-        const int64_t sg = (iter == 0) ? sg_edge : -1;   // start / goal ride along
-        if (!(grouped || (speculate && B <= FUSE_MAX))) launch_init();
-        c->stats.samples += B;
-        if (grouped) {
-            // ---- rank group: the speculative front on my slice, ONE all-gather of
-            // sample records, every rank appends the same nodes, one host round trip
-            const int seq = ++c->seq;
-            const int64_t slot = (int64_t)GREC * per + 1;
-            const uint64_t gr0 = g0 + (uint64_t)rank * (uint64_t)per;
-            const int32_t *nin = nullptr, *yin = nullptr;
-            spec_split(gr0, per, nin, yin);
-            const int pn = prof_begin(c, c->stream);
-            PlanInit ini_g{};
-            if (init_pending) {   // (iteration 0: trees of one root each, a_start)
-                ini_g = ini;
-                init_pending = false;
-            }
-            hipLaunchKernelGGL(k_ext_conn_nn, dim3(blocks_for(per, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
-                               Bt.q.p, TB, p.seed, gr0, per, bd, p.range,
-                               p.resolution, cmax, a_start, c->efrom.p, c->eto.p, c->nd.p, c->valid.p, c->gfail.p,
-                               c->near_.p, c->yv.p, c->mv.p, nin, yin, ini_g);
-            HIP_TRY(hipGetLastError());
-            prof_end(c, pn, 0, c->stream);
-            c->prof.nn_pairs += (double)per * (double)(TA + TB);
-            if (packed(per * G))
-                launch_edges_packed(c, c->efrom.p, c->eto.p, c->nd.p, per * G, kmax, 2, c->valid.p, G, c->gfail.p,
-                                    c->stream, nullptr, 1);
-            else
-                launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, (per + (sg >= 0 ? 2 : 0)) * G, kmax, 2, c->valid.p, G,
-                             c->gfail.p, c->stream);
-            // without a transport (world 1) the records go straight to the gathered buffer
-            int32_t* recs = c->g_recv.p;   // every rank's records, rank-major
-            int32_t* own = c->transport == TR_NONE ? c->g_recv.p : c->g_send.p;
-            int64_t shm_k = 0;
-            if (c->transport == TR_SHM) {   // pack in place into the shared segment
-                shm_k = ++c->shm_k;
-                recs = shm_records(c, shm_k, slot);
-                own = recs + (int64_t)rank * slot;
-            }
-            hipLaunchKernelGGL(k_group_pack, dim3(blocks_for(per, 256)), dim3(256), 0, c->stream,
-                               (const int*)c->gfail.p, (const int32_t*)c->near_.p, (const int32_t*)c->yv.p,
-                               (const int32_t*)c->mv.p, per, tflag, own);
-            HIP_TRY(hipGetLastError());
-            if (c->transport == TR_SHM) {
-                HIP_TRY(hipStreamSynchronize(c->stream));   // my records are in the segment
-                const double te = now_s();
-                shm_barrier(c, shm_k);
-                c->stats.exchange_ms += 1e3 * (now_s() - te);
-            } else if (c->transport != TR_NONE) {
-                group_exchange(c, slot);
-            }
-            GroupRecs gr{recs, per, world};
-            if (B <= FUSE_MAX) {
+        snap_A = TA;
+        snap_B = TB;
+        bool stop = false;
+        // ordered sub-batches of the iteration's samples: chunk0, x chunk_growth, ...;
+        // the iteration ends after the sub-batch holding the first REACHED sample
+        int64_t C = std::min(B, chunk0);
+        for (int64_t done = 0; done < B && !solved && !stop; done += C, C = std::min(B - done, C * chunk_growth)) {
+            C = std::min(C, B - done);
+            const uint64_t g0 = gbase + (uint64_t)done;
+            const int64_t An = A.n, Bn = Bt.n;   // append positions of this sub-batch
+            const bool first_launch = iter == 0 && done == 0;
+            const int64_t sg = first_launch ? sg_edge : -1;   // start / goal ride along
+            const int64_t per = C / world;
+            if (!(grouped || (speculate && C <= FUSE_MAX))) launch_init();
+            c->stats.samples += C;
+            if (grouped) {
+                // ---- rank group: the speculative front on my slice, ONE all-gather of
+                // sample records, every rank appends the same nodes, one host round trip
+                const int seq = ++c->seq;
+                const int64_t slot = (int64_t)GREC * per + 1;
+                const uint64_t gr0 = g0 + (uint64_t)rank * (uint64_t)per;
+                const int32_t *nin = nullptr, *yin = nullptr;
+                spec_split(gr0, per, nin, yin);
+                const int pn = prof_begin(c, c->stream);
+                PlanInit ini_g{};
+                if (init_pending) {   // (iteration 0: trees of one root each, a_start)
+                    ini_g = ini;
+                    init_pending = false;
+                }
+                hipLaunchKernelGGL(k_ext_conn_nn, dim3(blocks_for(per, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p,
+                                   TA, Bt.q.p, TB, p.seed, gr0, per, bd, p.range, p.resolution, cmax, a_start,
+                                   c->efrom.p, c->eto.p, c->nd.p, c->valid.p, c->gfail.p, c->near_.p, c->yv.p, c->mv.p,
+                                   nin, yin, ini_g);
+                HIP_TRY(hipGetLastError());
+                prof_end(c, pn, 0, c->stream);
+                c->prof.nn_pairs += (double)per * (double)(TA + TB);
+                if (packed(per * G))
+                    launch_edges_packed(c, c->efrom.p, c->eto.p, c->nd.p, per * G, kmax, 2, c->valid.p, G,
+                                        c->gfail.p, c->stream, nullptr, 1);
+                else
+                    launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, (per + (sg >= 0 ? 2 : 0)) * G, kmax, 2,
+                                 c->valid.p, G, c->gfail.p, c->stream);
+                // without a transport (world 1) the records go straight to the gathered buffer
+                int32_t* recs = c->g_recv.p;   // every rank's records, rank-major
+                int32_t* own = c->transport == TR_NONE ? c->g_recv.p : c->g_send.p;
+                int64_t shm_k = 0;
+                if (c->transport == TR_SHM) {   // pack in place into the shared segment
+                    shm_k = ++c->shm_k;
+                    recs = shm_records(c, shm_k, slot);
+                    own = recs + (int64_t)rank * slot;
+                }
+                // the timeout vote rides on an iteration's first exchange (the oracle's rule)
+                hipLaunchKernelGGL(k_group_pack, dim3(blocks_for(per, 256)), dim3(256), 0, c->stream,
+                                   (const int*)c->gfail.p, (const int32_t*)c->near_.p, (const int32_t*)c->yv.p,
+                                   (const int32_t*)c->mv.p, per, done == 0 ? tflag : 0, own);
+                HIP_TRY(hipGetLastError());
+                if (c->transport == TR_SHM) {
+                    HIP_TRY(hipStreamSynchronize(c->stream));   // my records are in the segment
+                    const double te = now_s();
+                    shm_barrier(c, shm_k);
+                    c->stats.exchange_ms += 1e3 * (now_s() - te);
+                } else if (c->transport != TR_NONE) {
+                    group_exchange(c, slot);
+                }
+                GroupRecs gr{recs, per, world};
+                if (C <= FUSE_MAX) {
 #define RP_GROUP_SMALL(IT)                                                                                          \
-    hipLaunchKernelGGL(k_group_accept_small<IT>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, gr, B, p.seed, g0, bd,  \
-                       p.range, cmax, A.q.p, A.par.p, A.cand.p, TA, Bt.q.p, Bt.par.p, Bt.cand.p, TB, a_start,      \
+    hipLaunchKernelGGL(k_group_accept_small<IT>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, gr, C, p.seed, g0, bd,  \
+                       p.range, cmax, A.q.p, A.par.p, A.cand.p, An, Bt.q.p, Bt.par.p, Bt.cand.p, Bn, a_start,      \
                        c->chain_end.p, status, pa, io, (const uint8_t*)c->valid.p, sg, sg_stride)
-                if (B <= FUSE_THREADS) RP_GROUP_SMALL(1);
-                else RP_GROUP_SMALL(4);
+                    if (C <= FUSE_THREADS) RP_GROUP_SMALL(1);
+                    else RP_GROUP_SMALL(4);
 #undef RP_GROUP_SMALL
-            } else {
-                hipLaunchKernelGGL(k_group_counts, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, gr, B,
-                                   c->g_cnt.p, status);
-                scan_incl_u64(c, c->g_cnt.p, c->g_incl.p, B);
-                hipLaunchKernelGGL(k_group_append, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, gr,
-                                   (const unsigned long long*)c->g_incl.p, B, p.seed, g0, bd, p.range, cmax, A.q.p,
-                                   A.par.p, A.cand.p, TA, Bt.q.p, Bt.par.p, Bt.cand.p, TB, a_start, c->chain_end.p,
-                                   status);
-                hipLaunchKernelGGL(k_group_finalize, dim3(1), dim3(256), 0, c->stream,
-                                   (const unsigned long long*)c->g_incl.p, B, status, TA, a_start,
-                                   (const int32_t*)A.par.p, (const int32_t*)Bt.par.p, (const int32_t*)c->chain_end.p,
-                                   pa, io, (const uint8_t*)c->valid.p, sg, sg_stride);
+                } else {
+                    hipLaunchKernelGGL(k_group_counts, dim3(blocks_for(C, 256)), dim3(256), 0, c->stream, gr, C,
+                                       c->g_cnt.p, status);
+                    scan_incl_u64(c, c->g_cnt.p, c->g_incl.p, C);
+                    hipLaunchKernelGGL(k_group_append, dim3(blocks_for(C, 256)), dim3(256), 0, c->stream, gr,
+                                       (const unsigned long long*)c->g_incl.p, C, p.seed, g0, bd, p.range, cmax,
+                                       A.q.p, A.par.p, A.cand.p, An, Bt.q.p, Bt.par.p, Bt.cand.p, Bn, a_start,
+                                       c->chain_end.p, status);
+                    hipLaunchKernelGGL(k_group_finalize, dim3(1), dim3(256), 0, c->stream,
+                                       (const unsigned long long*)c->g_incl.p, C, status, An, a_start,
+                                       (const int32_t*)A.par.p, (const int32_t*)Bt.par.p,
+                                       (const int32_t*)c->chain_end.p, pa, io, (const uint8_t*)c->valid.p, sg,
+                                       sg_stride);
+                }
+                HIP_TRY(hipGetLastError());
+                run_program(0, tail_steps, seq, true);
+                wait_seq(c, seq);
+                if (c->transport == TR_RCCL) {
+                    float ms = 0.0f;
+                    if (hipEventElapsedTime(&ms, c->gx0, c->gx1) == hipSuccess) c->stats.exchange_ms += ms;
+                }
+                const int* st = h->status;
+                if (!sg_known) {   // (the same flags on every rank: they all leave here)
+                    if (const int code = endpoint_status(st[ST_SG])) return endpoint_fail(code);
+                    sg_known = true;
+                }
+                if (st[ST_STOP]) {   // some rank timed out: all leave at this iteration
+                    stop = true;
+                    break;
+                }
+                A.n = An + st[ST_NACC];
+                Bt.n = Bn + st[ST_ADDED];
+                c->stats.edges_checked += per * G;
+                if (st[ST_FIRST] != INT_MAX) {
+                    solved = 1;
+                    s_node = st[ST_SNODE];
+                    g_node = st[ST_GNODE];
+                }
+                continue;
             }
-            HIP_TRY(hipGetLastError());
-            run_program(0, tail_steps, seq, true);
-            wait_seq(c, seq);
-            if (c->transport == TR_RCCL) {
-                float ms = 0.0f;
-                if (hipEventElapsedTime(&ms, c->gx0, c->gx1) == hipSuccess) c->stats.exchange_ms += ms;
-            }
-            const int* st = h->status;
-            if (!sg_known) {   // (the same flags on every rank: they all leave here)
-                if (const int code = endpoint_status(st[ST_SG])) return endpoint_fail(code);
-                sg_known = true;
-            }
-            if (st[ST_STOP]) break;   // some rank timed out: all leave at this iteration
-            A.n = TA + st[ST_NACC];
-            Bt.n = TB + st[ST_ADDED];
-            c->stats.edges_checked += per * G;
-            if (st[ST_FIRST] != INT_MAX) {
-                solved = 1;
-                s_node = st[ST_SNODE];
-                g_node = st[ST_GNODE];
-                ++iter;
-                break;
-            }
-            continue;
-        }
-        if (speculate && B <= FUSE_MAX) {
-            // ---- single rank, speculative: one NN kernel (both trees), one edge
-            // launch, one accept kernel, the first simplification steps (no-ops
-            // until a path exists), one host round trip
-            const int seq = ++c->seq;
-            const int32_t *nin = nullptr, *yin = nullptr;
-            spec_split(g0, B, nin, yin);
-            const int pn = prof_begin(c, c->stream);
-            PlanInit ini_now{};
-            if (init_pending) {   // (iteration 0: trees of one root each, a_start)
-                ini_now = ini;
-                init_pending = false;
-            }
-            hipLaunchKernelGGL(k_ext_conn_nn, dim3(blocks_for(B, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
-                               Bt.q.p, TB, p.seed, g0, B, bd, p.range, p.resolution, cmax, a_start, c->efrom.p,
-                               c->eto.p, c->nd.p, c->valid.p, c->gfail.p, c->near_.p, c->yv.p, c->mv.p, nin, yin,
-                               ini_now);
-            HIP_TRY(hipGetLastError());
-            prof_end(c, pn, 0, c->stream);
-            c->prof.nn_pairs += (double)B * (double)(TA + TB);
-            launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, (B + (sg >= 0 ? 2 : 0)) * G, kmax, 2, c->valid.p, G,
-                         c->gfail.p, c->stream, nullptr, 1, 0, nullptr, 0,
-                         (iter == 0 && ride.slots > 0) ? &ride : nullptr, true);
-            pa.seq = seq;   // (an iteration that finishes the plan publishes it)
+            if (speculate && C <= FUSE_MAX) {
+                // ---- single rank, speculative: one NN kernel (both trees), one edge
+                // launch, one accept kernel, the first simplification steps (no-ops
+                // until a path exists), one host round trip
+                const int seq = ++c->seq;
+                const int32_t *nin = nullptr, *yin = nullptr;
+                spec_split(g0, C, nin, yin);
+                const int pn = prof_begin(c, c->stream);
+                PlanInit ini_now{};
+                if (init_pending) {   // (iteration 0: trees of one root each, a_start)
+                    ini_now = ini;
+                    init_pending = false;
+                }
+                hipLaunchKernelGGL(k_ext_conn_nn, dim3(blocks_for(C, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p,
+                                   TA, Bt.q.p, TB, p.seed, g0, C, bd, p.range, p.resolution, cmax, a_start,
+                                   c->efrom.p, c->eto.p, c->nd.p, c->valid.p, c->gfail.p, c->near_.p, c->yv.p, c->mv.p,
+                                   nin, yin, ini_now);
+                HIP_TRY(hipGetLastError());
+                prof_end(c, pn, 0, c->stream);
+                c->prof.nn_pairs += (double)C * (double)(TA + TB);
+                launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, (C + (sg >= 0 ? 2 : 0)) * G, kmax, 2, c->valid.p, G,
+                             c->gfail.p, c->stream, nullptr, 1, 0, nullptr, 0,
+                             (first_launch && ride.slots > 0) ? &ride : nullptr, true);
+                pa.seq = seq;   // (an iteration that finishes the plan publishes it)
 #define RP_ITER_SMALL(IT)                                                                                           \
     hipLaunchKernelGGL(k_iter_accept_small<IT>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, (const int*)c->gfail.p,   \
-                       (const int32_t*)c->near_.p, (const int32_t*)c->yv.p, (const int32_t*)c->mv.p, B, G,          \
-                       (const double*)c->efrom.p, (const double*)c->eto.p, A.q.p, A.par.p, A.cand.p, TA, Bt.q.p,    \
-                       Bt.par.p, Bt.cand.p, TB, a_start, c->chain_end.p, status, (const uint8_t*)c->valid.p, sg,    \
+                       (const int32_t*)c->near_.p, (const int32_t*)c->yv.p, (const int32_t*)c->mv.p, C, G,          \
+                       (const double*)c->efrom.p, (const double*)c->eto.p, A.q.p, A.par.p, A.cand.p, An, Bt.q.p,    \
+                       Bt.par.p, Bt.cand.p, Bn, a_start, c->chain_end.p, status, (const uint8_t*)c->valid.p, sg,    \
                        sg_stride, pa, io)
-            if (B <= FUSE_THREADS) RP_ITER_SMALL(1);
-            else RP_ITER_SMALL(4);
+                if (C <= FUSE_THREADS) RP_ITER_SMALL(1);
+                else RP_ITER_SMALL(4);
 #undef RP_ITER_SMALL
+                HIP_TRY(hipGetLastError());
+                run_program(0, tail_steps, seq, true);
+                wait_seq(c, seq);
+                if (!sg_known) {
+                    if (const int code = endpoint_status(h->status[ST_SG])) return endpoint_fail(code);
+                    sg_known = true;
+                }
+                const int* st = h->status;
+                A.n = An + st[ST_NACC];
+                Bt.n = Bn + st[ST_ADDED];
+                c->stats.edges_checked += C * G;
+                if (st[ST_FIRST] != INT_MAX) {
+                    solved = 1;
+                    s_node = st[ST_SNODE];
+                    g_node = st[ST_GNODE];
+                }
+                continue;
+            }
+
+            // ---- single rank, two-phase (large sub-batches, or RBE_PLAN_SPECULATE=0)
+            debug_wait(c, "iteration start");
+            NnQuery qe{};
+            qe.kind = NNQ_SAMPLE;
+            qe.seed = p.seed;
+            qe.g0 = g0;
+            qe.i0 = 0;
+            qe.bd = bd;
+            const bool esplit = nn_split(c, qe, C, A.q.p, TA, c->near_.p);
+            const int pn1 = prof_begin(c, c->stream);
+            hipLaunchKernelGGL(k_ext_nn, dim3(blocks_for(C, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
+                               p.seed, g0, (int64_t)0, C, bd, p.range, p.resolution, a_start, c->efrom.p, c->eto.p,
+                               c->nd.p, c->valid.p, c->near_.p, esplit ? (const int32_t*)c->near_.p : nullptr);
             HIP_TRY(hipGetLastError());
-            run_program(0, tail_steps, seq, true);
-            wait_seq(c, seq);
-            if (!sg_known) {
-                if (const int code = endpoint_status(h->status[ST_SG])) return endpoint_fail(code);
-                sg_known = true;
-            }
-            const int* st = h->status;
-            A.n = TA + st[ST_NACC];
-            Bt.n = TB + st[ST_ADDED];
-            c->stats.edges_checked += B * G;
-            if (st[ST_FIRST] != INT_MAX) {
-                solved = 1;
-                s_node = st[ST_SNODE];
-                g_node = st[ST_GNODE];
-                ++iter;
-                break;
-            }
-            continue;
-        }
+            prof_end(c, pn1, 0, c->stream);
+            c->prof.nn_pairs += (double)C * (double)TA;
+            debug_wait(c, "k_ext_nn");
+            launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, C + (sg >= 0 ? 2 : 0), kmax, a_start ? 0 : 1, c->valid.p,
+                         1, nullptr, c->stream);
+            debug_wait(c, "ext edges");
+            c->stats.edges_checked += C;
 
-        // ---- single rank, two-phase (large batches, or RBE_PLAN_SPECULATE=0)
-        debug_wait(c, "iteration start");
-        NnQuery qe{};
-        qe.kind = NNQ_SAMPLE;
-        qe.seed = p.seed;
-        qe.g0 = g0;
-        qe.i0 = (int64_t)rank * per;
-        qe.bd = bd;
-        const bool esplit = nn_split(c, qe, per, A.q.p, TA, c->near_.p);
-        const int pn1 = prof_begin(c, c->stream);
-        hipLaunchKernelGGL(k_ext_nn, dim3(blocks_for(per, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA, p.seed,
-                           g0, (int64_t)rank * per, per, bd, p.range, p.resolution, a_start, c->efrom.p, c->eto.p,
-                           c->nd.p, c->valid.p, c->near_.p, esplit ? (const int32_t*)c->near_.p : nullptr);
-        HIP_TRY(hipGetLastError());
-        prof_end(c, pn1, 0, c->stream);
-        c->prof.nn_pairs += (double)per * (double)TA;
-        debug_wait(c, "k_ext_nn");
-        launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, per + (sg >= 0 ? 2 : 0), kmax, a_start ? 0 : 1, c->valid.p,
-                     1, nullptr, c->stream);
-        debug_wait(c, "ext edges");
-        c->stats.edges_checked += per;
-
-        {
-            // device-side counts, one host round trip per iteration; batches
+            // device-side counts, one host round trip per sub-batch; sub-batches
             // <= FUSE_MAX use the single-block accept kernels
-            const bool fused = B <= FUSE_MAX;
+            const bool fused = C <= FUSE_MAX;
             const int seq = ++c->seq;
             if (fused) {
-                if (B <= FUSE_THREADS)
+                if (C <= FUSE_THREADS)
                     hipLaunchKernelGGL(k_ext_accept_small<1>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, c->valid.p,
-                                       c->near_.p, B, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA, status,
+                                       c->near_.p, C, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, An, status,
                                        sg, sg_stride);
                 else
                     hipLaunchKernelGGL(k_ext_accept_small<4>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, c->valid.p,
-                                       c->near_.p, B, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA, status,
+                                       c->near_.p, C, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, An, status,
                                        sg, sg_stride);
             } else {
-                hipLaunchKernelGGL(k_ext_result_flag, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream,
-                                   c->valid.p, c->near_.p, B, c->res.p, c->acc.p);
-                scan_incl(c, c->acc.p, c->incl.p, B);
-                hipLaunchKernelGGL(k_ext_append, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->res.p,
-                                   c->incl.p, B, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, TA, status,
+                hipLaunchKernelGGL(k_ext_result_flag, dim3(blocks_for(C, 256)), dim3(256), 0, c->stream,
+                                   c->valid.p, c->near_.p, C, c->res.p, c->acc.p);
+                scan_incl(c, c->acc.p, c->incl.p, C);
+                hipLaunchKernelGGL(k_ext_append, dim3(blocks_for(C, 256)), dim3(256), 0, c->stream, c->res.p,
+                                   c->incl.p, C, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, An, status,
                                    (const uint8_t*)c->valid.p, sg, sg_stride);
             }
             debug_wait(c, "ext accept");
             NnQuery qc{};
             qc.kind = NNQ_ROWS;
             qc.A = A.q.p;
-            qc.TA0 = TA;
+            qc.TA0 = An;
             qc.t0 = 0;
             qc.status = status;   // accepted extensions (ST_NACC), on the device
-            const bool csplit = nn_split(c, qc, B, Bt.q.p, TB, c->yv.p);
+            const bool csplit = nn_split(c, qc, C, Bt.q.p, TB, c->yv.p);
             const int pn2 = prof_begin(c, c->stream);
-            hipLaunchKernelGGL(k_conn_nn, dim3(blocks_for(B, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
-                               (int64_t)0, B, Bt.q.p, TB, p.range, p.resolution, cmax, a_start, c->efrom.p,
+            hipLaunchKernelGGL(k_conn_nn, dim3(blocks_for(C, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, An,
+                               (int64_t)0, C, Bt.q.p, TB, p.range, p.resolution, cmax, a_start, c->efrom.p,
                                c->eto.p, c->nd.p, c->valid.p, c->gfail.p, c->yv.p, c->mv.p, (const int*)status,
                                csplit ? (const int32_t*)c->yv.p : nullptr);
             HIP_TRY(hipGetLastError());
             prof_end(c, pn2, 0, c->stream);
             debug_wait(c, "k_conn_nn");
-            if (packed(B * cmax))
-                launch_edges_packed(c, c->efrom.p, c->eto.p, c->nd.p, B * cmax, kmax, a_start ? 1 : 0, c->valid.p,
+            if (packed(C * cmax))
+                launch_edges_packed(c, c->efrom.p, c->eto.p, c->nd.p, C * cmax, kmax, a_start ? 1 : 0, c->valid.p,
                                     cmax, c->gfail.p, c->stream, status, cmax);
             else
-                launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, B * cmax, kmax, a_start ? 1 : 0, c->valid.p, cmax,
+                launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, C * cmax, kmax, a_start ? 1 : 0, c->valid.p, cmax,
                              c->gfail.p, c->stream, status, cmax);
             debug_wait(c, "conn edges");
             if (fused) {
 #define RP_CONN_SMALL(IT)                                                                                        \
     hipLaunchKernelGGL(k_conn_accept_small<IT>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, c->yv.p, c->mv.p,      \
-                       c->gfail.p, status, A.q.p, TA, Bt.q.p, Bt.par.p, Bt.cand.p, TB, p.range, cmax, a_start,   \
+                       c->gfail.p, status, A.q.p, An, Bt.q.p, Bt.par.p, Bt.cand.p, Bn, p.range, cmax, a_start,   \
                        A.cand.p, A.par.p, c->chain_end.p, pa, io)
-                if (B <= FUSE_THREADS) RP_CONN_SMALL(1);
+                if (C <= FUSE_THREADS) RP_CONN_SMALL(1);
                 else RP_CONN_SMALL(4);
 #undef RP_CONN_SMALL
             } else {
-                hipLaunchKernelGGL(k_conn_record_len, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->yv.p,
-                                   c->mv.p, c->gfail.p, (const int*)status, B, c->rec.p, c->Lv.p);
-                scan_incl(c, c->Lv.p, c->incl.p, B);
-                hipLaunchKernelGGL(k_conn_append, dim3(blocks_for(B, 256)), dim3(256), 0, c->stream, c->rec.p,
-                                   c->incl.p, B, A.q.p, TA, Bt.q.p, Bt.par.p, Bt.cand.p, TB, p.range, cmax,
+                hipLaunchKernelGGL(k_conn_record_len, dim3(blocks_for(C, 256)), dim3(256), 0, c->stream, c->yv.p,
+                                   c->mv.p, c->gfail.p, (const int*)status, C, c->rec.p, c->Lv.p);
+                scan_incl(c, c->Lv.p, c->incl.p, C);
+                hipLaunchKernelGGL(k_conn_append, dim3(blocks_for(C, 256)), dim3(256), 0, c->stream, c->rec.p,
+                                   c->incl.p, C, A.q.p, An, Bt.q.p, Bt.par.p, Bt.cand.p, Bn, p.range, cmax,
                                    a_start, A.cand.p, status + ST_FIRST, c->chain_end.p, (const int*)status,
                                    (const double*)(a_start ? c->efrom.p : c->eto.p), (const int32_t*)c->mv.p);
-                hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, c->stream, status, c->incl.p, TA, a_start,
+                hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, c->stream, status, c->incl.p, An, a_start,
                                    A.par.p, Bt.par.p, c->chain_end.p, pa, io);
             }
-            // the first simplification steps run every iteration (empty unless this
-            // one solved), so a solving iteration needs no extra host round trip
+            // the first simplification steps run every sub-batch (empty unless this one
+            // solved), so a solving sub-batch needs no extra host round trip
             run_program(0, tail_steps, seq, true);
             wait_seq(c, seq);
             if (!sg_known) {
@@ -1428,20 +1459,21 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                 sg_known = true;
             }
             const int* st = h->status;
-            A.n = TA + st[ST_NACC];
-            Bt.n = TB + st[ST_ADDED];
+            A.n = An + st[ST_NACC];
+            Bt.n = Bn + st[ST_ADDED];
             c->stats.edges_checked += (int64_t)st[ST_NACC] * cmax;
             c->prof.nn_pairs += (double)st[ST_NACC] * (double)TB;   // k_conn_nn: accepted targets x tree B
             if (st[ST_FIRST] != INT_MAX) {
                 solved = 1;
                 s_node = st[ST_SNODE];
                 g_node = st[ST_GNODE];
-                ++iter;
-                break;
             }
-            continue;
         }
-
+        if (stop) break;
+        if (solved) {
+            ++iter;
+            break;
+        }
     }
     launch_init();   // (the loop ran no speculative iteration)
     if (!sg_known) {   // the loop ran no iteration
@@ -1881,6 +1913,10 @@ int rp_plan(rp_ctx* c, const double start[RP_NQ], const double goal[RP_NQ], cons
         return RP_ERR_ARG;
     RP_GUARD_BEGIN
     HIP_TRY(hipSetDevice(c->device));
+    if (c->transport != TR_NONE && c->group_broken) {
+        c->err = "rank group broken by an earlier failed plan on this rank; initialise the group again";
+        return RP_ERR_EXCHANGE;
+    }
     c->prof = rp_profile{};
     c->pused = 0;
     c->in_plan = true;
@@ -1890,6 +1926,7 @@ int rp_plan(rp_ctx* c, const double start[RP_NQ], const double goal[RP_NQ], cons
     } catch (...) {
         c->in_plan = false;
         c->pused = 0;
+        if (c->transport != TR_NONE) c->group_broken = true;
         throw;
     }
     c->in_plan = false;
@@ -1986,6 +2023,25 @@ int rp_group_init_rccl(rp_ctx* c, int32_t rank, int32_t world, const uint8_t id[
     c->rank = rank;
     c->world = world;
     c->transport = TR_RCCL;
+    return RP_OK;
+    RP_GUARD_END(c)
+}
+
+int rp_group_info(rp_ctx* c, int32_t* rank, int32_t* world, int32_t* transport) {
+    if (!c || !rank || !world || !transport) return RP_ERR_ARG;
+    RP_GUARD_BEGIN
+    static_assert(TR_NONE == RP_TRANSPORT_NONE && TR_HOST == RP_TRANSPORT_HOST && TR_RCCL == RP_TRANSPORT_RCCL &&
+                      TR_SHM == RP_TRANSPORT_SHM, "transport codes");
+    *transport = c->transport;
+    *rank = c->rank;
+    *world = c->world;
+    if (c->transport == TR_RCCL && c->comm) {   // the communicator's own view
+        int n = 0, r = 0;
+        NCCL_TRY(ncclCommCount(c->comm, &n));
+        NCCL_TRY(ncclCommUserRank(c->comm, &r));
+        *world = n;
+        *rank = r;
+    }
     return RP_OK;
     RP_GUARD_END(c)
 }

@@ -21,7 +21,7 @@ EXPORTS = ("rp_version", "rp_default_robot", "rp_create", "rp_destroy", "rp_set_
            "rp_check_states", "rp_check_states_device", "rp_check_edges", "rp_check_edges_device",
            "rp_state_contacts", "rp_plan", "rp_group_init", "rp_group_init_shm", "rp_group_rccl_unique_id", "rp_group_init_rccl",
            "rp_get_stats", "rp_last_error", "rp_last_kernel_ms", "rp_selftest_f64", "rp_ik", "rp_set_profiling",
-           "rp_get_profile", "rp_get_stream")
+           "rp_get_profile", "rp_get_stream", "rp_group_info")
 
 # rp_allgather_fn(user, send, recv, bytes_per_rank): library-owned pinned host buffers
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64)
@@ -62,6 +62,7 @@ def load():
     L.rp_group_init_shm.argtypes = [vp, i32, i32, vp, i64]
     L.rp_group_init_rccl.argtypes = [vp, i32, i32, vp]
     L.rp_get_stats.argtypes = [vp, C.POINTER(_abi.Stats)]
+    L.rp_group_info.argtypes = [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]
     L.rp_set_profiling.argtypes = [vp, i32]
     L.rp_get_stream.argtypes = [vp, C.POINTER(vp)]
     L.rp_get_profile.argtypes = [vp, C.POINTER(_abi.Profile)]
@@ -264,6 +265,13 @@ class Context:
         """Shared-memory transport over a host segment mapped by every rank of the node."""
         self._check(load().rp_group_init_shm(self._h, int(rank), int(world), C.c_void_p(address), int(nbytes)),
                     "rp_group_init_shm")
+
+    def group_info(self):
+        """The rank group as its transport sees it (rp_group_info): for RCCL the
+        communicator's ncclCommUserRank / ncclCommCount."""
+        r, w, t = C.c_int32(), C.c_int32(), C.c_int32()
+        self._check(load().rp_group_info(self._h, C.byref(r), C.byref(w), C.byref(t)), "rp_group_info")
+        return {"rank": r.value, "world": w.value, "transport": _abi.TRANSPORT_NAMES.get(t.value, str(t.value))}
 
     def group_leave(self):
         """Back to single-rank planning."""

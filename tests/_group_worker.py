@@ -34,7 +34,7 @@ def main():
         if logf:
             logf.write(line + "\n")
             logf.flush()
-    faulthandler.dump_traceback_later(150, exit=True)
+    faulthandler.dump_traceback_later(int(os.environ.get("RBE_WORKER_TIMEOUT", "150")), exit=True)
     log("start")
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -63,19 +63,59 @@ def main():
             res[f"{tag}/{c['name']}/path"] = path
             res[f"{tag}/{c['name']}/info"] = np.array([st, s["iterations"], s["start_tree_size"], s["goal_tree_size"]])
 
+    def broken_group(res):
+        """a rank whose grouped plan fails must not go on with the group
+        out of step. Rank 1 skips one plan; rank 0's plan gives up at the exchange
+        (wait watchdog) and every later grouped plan on rank 0 fails at once until
+        the group is initialised again; then both ranks plan together again."""
+        nonlocal grp
+        from rbe550_final_project_amd.native import NativeError
+        c = cases[0]
+        q = json.load(open(os.path.join(ROOT, "tests", "golden", "workloads", c["workload"] + ".json")))
+        q = q["queries"][c["query"]]
+        sc = scenes.Scene.from_json(q["scene"])
+        ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+        ctx.set_attached(q["attached"])
+        p = _abi.make_params(seed=c["seed"], batch=c["batch"], n_waypoints=150, timeout_s=3600.0,
+                             straight_first=False)
+        dist.barrier()
+        if rank == 0:
+            os.environ["RBE_WAIT_WATCHDOG_S"] = "2"
+            errs = []
+            for _ in range(2):
+                try:
+                    ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+                    errs.append("")
+                except NativeError as e:
+                    errs.append(str(e))
+            os.environ["RBE_WAIT_WATCHDOG_S"] = "30"
+            log(f"break: {errs}")
+            res["break/first_failed"] = np.array([int(bool(errs[0]))])
+            res["break/second_broken"] = np.array([int("broken" in errs[1])])
+        dist.barrier()
+        grp.leave()
+        grp = Group(ctx, transport=transport)
+        path, st = ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+        res["break/path_after_reinit"] = path
+        log(f"break: plan after re-init status {st}")
+
     order = os.environ.get("RBE_WORKER_ORDER", "group_first")
     if order == "single_first" and rank == 0:
         grp.leave()
         run("single")
         grp = Group(ctx, transport=transport)
     dist.barrier()
+    grp_info = ctx.group_info()
     run("group")
     calls = grp.calls if transport == "host" else len(cases)
+    if os.environ.get("RBE_WORKER_BREAK") and world > 1:
+        broken_group(res)
     dist.barrier()
     if rank == 0 and order != "single_first":
         grp.leave()
         run("single")
     res["calls"] = np.array([calls])
+    res["info"] = np.array([grp_info["rank"], grp_info["world"]])
     np.savez(f"{out}.{rank}.npz", **res)
     if os.environ.get("RBE_WORKER_KEEP"):
         log("final barrier (context kept)")

@@ -41,29 +41,82 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("transport", ["shm", "host"])
-def test_two_process_group_plans_equal_world1_and_oracle(tmp_path, oracle_lib, transport):
+# the BASELINE shard shapes: C4 = 4 ranks x 65,536 samples per
+# iteration, C5 = 8 ranks x 16,384 (the covered well, up to the 2^20-sample budget)
+CASES_W4 = [
+    {"name": "C4_q0", "workload": "goal4_pentagon_10box", "query": 0, "seed": 0, "batch": 262144,
+     "batch_min": 262144},
+    {"name": "C4_q5", "workload": "goal4_pentagon_10box", "query": 5, "seed": 5, "batch": 262144,
+     "batch_min": 262144},
+]
+CASES_W8 = [
+    {"name": "C5_well_s4", "workload": "clutter64_well", "query": 0, "seed": 4, "batch": 131072,
+     "batch_min": 131072, "max_iters": 8},
+    {"name": "C5_well_s2", "workload": "clutter64_well", "query": 0, "seed": 2, "batch": 131072,
+     "batch_min": 131072, "max_iters": 8},
+]
+
+
+def _run_group(tmp_path, world, transport, cases, extra_env=None, timeout=160):
     out = str(tmp_path / "res")
     port = str(_free_port())
-    env = dict(os.environ, RBE_WAIT_WATCHDOG_S="30", RBE_WORKER_TRANSPORT=transport)
-    procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "_group_worker.py"), str(r), "2", port, out,
-                               json.dumps(CASES)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+    env = dict(os.environ, RBE_WAIT_WATCHDOG_S="30", RBE_WORKER_TRANSPORT=transport,
+               RBE_WORKER_TIMEOUT=str(timeout - 10), **(extra_env or {}))
+    procs = [subprocess.Popen([sys.executable, "-u", os.path.join(HERE, "_group_worker.py"), str(r), str(world), port,
+                               out, json.dumps(cases)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
                               env=env)
-             for r in range(2)]
+             for r in range(world)]
     logs = []
     for pr in procs:
         try:
-            logs.append(pr.communicate(timeout=160)[0])
+            logs.append(pr.communicate(timeout=timeout)[0])
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()
             raise
     for pr, log in zip(procs, logs):
         assert pr.returncode == 0, log[-3000:]
-    r0, r1 = (np.load(f"{out}.{r}.npz") for r in range(2))
+    res = [np.load(f"{out}.{r}.npz") for r in range(world)]
+    for r, x in enumerate(res):
+        assert list(x["info"]) == [r, world]   # rp_group_info: the transport's own view
+    return res
+
+
+def _check_golden(res, cases):
+    """every rank's group plan == rank 0's world-1 plan == the golden oracle plan"""
+    fix = np.load(os.path.join(GOLD, "plans_configured.npz"))
+    meta = json.loads(str(fix["meta"]))
+    r0 = res[0]
+    for c in cases:
+        n = c["name"]
+        for r in res:
+            assert np.array_equal(r[f"group/{n}/path"], r0[f"single/{n}/path"]), n
+            assert np.array_equal(r[f"group/{n}/info"], r0[f"single/{n}/info"]), n
+        m = meta[n]
+        assert list(r0[f"group/{n}/info"]) == [m["status"], m["iterations"], m["start_tree"], m["goal_tree"]], n
+        assert np.array_equal(r0[f"group/{n}/path"], fix[n]), n
+
+
+@pytest.mark.parametrize("world,cases", [(4, CASES_W4), (8, CASES_W8)])
+def test_baseline_shard_shapes_as_processes(tmp_path, world, cases):
+    """C4 at world 4 and C5 at world 8, each rank a fresh process on the one GPU
+    (shared-memory transport): the plans equal the world-1 plan and the golden
+    oracle plans (status, iterations, both tree sizes, 150 waypoints)."""
+    res = _run_group(tmp_path, world, "shm", cases, timeout=300)
+    _check_golden(res, cases)
+
+
+@pytest.mark.parametrize("transport", ["shm", "host"])
+def test_two_process_group_plans_equal_world1_and_oracle(tmp_path, oracle_lib, transport):
+    res = _run_group(tmp_path, 2, transport, CASES, {"RBE_WORKER_BREAK": "1" if transport == "shm" else ""})
+    r0, r1 = res
     fix = np.load(os.path.join(GOLD, "plans_configured.npz"))
     meta = json.loads(str(fix["meta"]))
     assert int(r0["calls"][0]) >= len(CASES) and int(r1["calls"][0]) == int(r0["calls"][0])
+    if transport == "shm":   # a rank-local failure leaves the group broken, not diverged
+        assert int(r0["break/first_failed"][0]) == 1 and int(r0["break/second_broken"][0]) == 1
+        for r in (r0, r1):
+            assert np.array_equal(r["break/path_after_reinit"], r0[f"group/{CASES[0]['name']}/path"])
     for c in CASES:
         n = c["name"]
         for r in (r0, r1):

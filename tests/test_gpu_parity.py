@@ -168,6 +168,36 @@ def test_plan_parity(gpu_ctx, oracle_lib, wl, qi, batch, seed, batch_min, specul
         (stats_ref["start_tree_size"], stats_ref["goal_tree_size"], stats_ref["iterations"])
 
 
+@pytest.mark.parametrize("wl,qi", PLAN_CASES)
+@pytest.mark.parametrize("chunk,growth,speculate", [("-1", "", "1"), ("64", "", "1"), ("1000", "2", "1"),
+                                                    ("4096", "", "0"), ("256", "3", "0"), ("", "", "1")])
+def test_plan_parity_sub_batches(gpu_ctx, oracle_lib, wl, qi, chunk, growth, speculate, monkeypatch):
+    """Iterations of 16,384 samples (batch_min = batch) run as ordered sub-batches
+    (rp_plan_params.chunk: first sub-batch, x growth after) that end after the one
+    holding the first REACHED sample; "-1" = the whole iteration in one launch
+    sequence. The oracle appends up to the winning sample whatever the split: the
+    trees and paths are the same for every sub-batching."""
+    monkeypatch.setenv("RBE_PLAN_SPECULATE", speculate)
+    if chunk:
+        monkeypatch.setenv("RBE_PLAN_CHUNK", chunk)
+    if growth:
+        monkeypatch.setenv("RBE_CHUNK_GROWTH", growth)
+    q = _wl(wl)["queries"][qi]
+    sc = scenes.Scene.from_json(q["scene"])
+    o = _both(gpu_ctx, oracle_lib, sc, q["attached"])
+    p = _abi.make_params(seed=qi + 7, batch=16384, batch_min=16384, n_waypoints=150, timeout_s=60,
+                         straight_first=False)
+    ref, st_ref, stats_ref = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+    path, st = gpu_ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+    gst = gpu_ctx.stats()
+    assert st == st_ref == _abi.STATUS_EXACT
+    assert np.array_equal(path, ref)
+    assert (gst["start_tree_size"], gst["goal_tree_size"], gst["iterations"]) == \
+        (stats_ref["start_tree_size"], stats_ref["goal_tree_size"], stats_ref["iterations"])
+    # samples processed: whole sub-batches up to the solving one, never past the schedule
+    assert 0 < gst["samples"] <= stats_ref["samples"]
+
+
 @pytest.mark.parametrize("wl,qi", PLAN_CASES[:5])
 @pytest.mark.parametrize("batch,seed", [(64, 11), (4096, 5)])
 @pytest.mark.parametrize("knob", ["RBE_FUSE_INIT", "RBE_STRAIGHT_RIDE"])

@@ -16,12 +16,13 @@ sc = scenes.Scene.from_json(q["scene"])
 ctx = Context(0)
 ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
 ctx.set_attached(q["attached"])
-grouped = len(sys.argv) > 1 and sys.argv[1] == "grouped"
+grouped = "grouped" in sys.argv[1:]
 if grouped:
     os.environ["RBE_PLAN_GROUPED"] = "1"
-for prof in (False, True):
+pmc = "pmc" in sys.argv[1:]   # counter passes: two plans, profiling off
+for prof in ((False,) if pmc else (False, True)):
     ctx.set_profiling(prof)
-    for seed in (2, 3, 4, 0):
+    for seed in ((2, 4) if pmc else (2, 3, 4, 0)):
         p = _abi.make_params(seed=seed, batch=131072, batch_min=131072, n_waypoints=150, timeout_s=60.0,
                              straight_first=False, tree_capacity=1 << 23, max_iters=8)
         path, st = ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)

@@ -507,11 +507,122 @@ int64_t ro_check_edges(const ro_scene* s, const double* qa, const double* qb, in
 /* trees                                                                     */
 /* ------------------------------------------------------------------------- */
 
+/* Exact nearest-node index for the sequential (batch 1) CPU baseline: an
+ * insert-only bucket kd-tree over a tree's nodes. OMPL's RRTConnect searches a
+ * GNAT [EXT-OMPL, planning.py:156], not a linear scan, so the CPU planner the GPU
+ * is timed against gets a sublinear exact search too. The answer is the linear
+ * scan's bit for bit: the same dist2, the lexicographic (distance, index) minimum
+ * (= the strict-< scan's lowest index among ties), and a subtree is skipped only
+ * if fl(fl(split - x)^2) > best, a lower bound of every dist2 in it (rounding is
+ * monotone, the sum's terms are non-negative), so no tie is ever pruned. */
+#define KD_LEAF 16
+typedef struct {
+    int dim;          /* < 0: leaf */
+    double split;     /* internal: left = coordinate < split, right = >= split */
+    int32_t child[2];
+    int32_t* idx;     /* leaf: node indices */
+    int32_t cnt, cap;
+} kd_node;
+typedef struct {
+    kd_node* nodes;
+    int32_t n, cap;
+} kd_tree;
+
+static int32_t kd_new_leaf(kd_tree* k) {
+    if (k->n == k->cap) {
+        k->cap = k->cap ? 2 * k->cap : 256;
+        k->nodes = (kd_node*)realloc(k->nodes, sizeof(kd_node) * k->cap);
+    }
+    kd_node* nd = &k->nodes[k->n];
+    nd->dim = -1;
+    nd->split = 0.0;
+    nd->child[0] = nd->child[1] = -1;
+    nd->cap = KD_LEAF;
+    nd->cnt = 0;
+    nd->idx = (int32_t*)malloc(sizeof(int32_t) * KD_LEAF);
+    return k->n++;
+}
+static void kd_free(kd_tree* k) {
+    for (int32_t i = 0; i < k->n; ++i) free(k->nodes[i].idx);
+    free(k->nodes);
+    k->nodes = NULL;
+    k->n = k->cap = 0;
+}
+static int cmp_double(const void* a, const void* b) {
+    const double x = *(const double*)a, y = *(const double*)b;
+    return x < y ? -1 : x > y;
+}
+/* add node `id` (state q, pts = the tree's states) */
+static void kd_insert(kd_tree* k, const double* pts, int32_t id) {
+    if (k->n == 0) kd_new_leaf(k);
+    const double* q = pts + NQ * (int64_t)id;
+    int32_t v = 0;
+    while (k->nodes[v].dim >= 0) v = k->nodes[v].child[q[k->nodes[v].dim] >= k->nodes[v].split];
+    kd_node* L = &k->nodes[v];
+    if (L->cnt == L->cap) {
+        /* split at the median of the widest dimension; identical points stay in a
+         * growing leaf */
+        int dim = -1;
+        double spread = 0.0;
+        for (int d = 0; d < NQ; ++d) {
+            double lo = INFINITY, hi = -INFINITY;
+            for (int i = 0; i < L->cnt; ++i) {
+                const double c = pts[NQ * (int64_t)L->idx[i] + d];
+                lo = c < lo ? c : lo;
+                hi = c > hi ? c : hi;
+            }
+            if (hi - lo > spread) { spread = hi - lo; dim = d; }
+        }
+        double cs[KD_LEAF];
+        if (dim >= 0 && L->cnt == KD_LEAF) {
+            for (int i = 0; i < L->cnt; ++i) cs[i] = pts[NQ * (int64_t)L->idx[i] + dim];
+            qsort(cs, L->cnt, sizeof(double), cmp_double);
+            double split = cs[L->cnt / 2];
+            if (!(split > cs[0])) split = cs[L->cnt - 1];   /* both sides non-empty */
+            const int32_t a = kd_new_leaf(k), b = kd_new_leaf(k);
+            L = &k->nodes[v];   /* (realloc) */
+            for (int i = 0; i < L->cnt; ++i) {
+                const int32_t j = L->idx[i];
+                kd_node* C = &k->nodes[pts[NQ * (int64_t)j + dim] >= split ? b : a];
+                C->idx[C->cnt++] = j;
+            }
+            free(L->idx);
+            L->idx = NULL;
+            L->cnt = L->cap = 0;
+            L->dim = dim;
+            L->split = split;
+            L->child[0] = a;
+            L->child[1] = b;
+            kd_insert(k, pts, id);
+            return;
+        }
+        L->cap *= 2;
+        L->idx = (int32_t*)realloc(L->idx, sizeof(int32_t) * L->cap);
+    }
+    L->idx[L->cnt++] = id;
+}
+static void kd_search(const kd_tree* k, int32_t v, const double* pts, const double* x, double* best, int32_t* bi) {
+    const kd_node* nd = &k->nodes[v];
+    if (nd->dim < 0) {
+        for (int i = 0; i < nd->cnt; ++i) {
+            const int32_t j = nd->idx[i];
+            const double d = dist2(pts + NQ * (int64_t)j, x);
+            if (d < *best || (d == *best && j < *bi)) { *best = d; *bi = j; }
+        }
+        return;
+    }
+    const int side = x[nd->dim] >= nd->split;
+    kd_search(k, nd->child[side], pts, x, best, bi);
+    const double g = side ? x[nd->dim] - nd->split : nd->split - x[nd->dim];
+    if (g * g <= *best) kd_search(k, nd->child[!side], pts, x, best, bi);
+}
+
 typedef struct {
     double* q;
     int32_t* parent;
     uint8_t* cand;   /* start tree: extension node whose connect did not reach */
     int64_t n, cap;
+    kd_tree* kd;     /* sequential baseline: exact index over all n nodes (else NULL) */
 } tree_t;
 
 static int tree_init(tree_t* t, int64_t cap) {
@@ -520,23 +631,34 @@ static int tree_init(tree_t* t, int64_t cap) {
     t->cand = (uint8_t*)calloc(cap, 1);
     t->n = 0;
     t->cap = cap;
+    t->kd = NULL;
     return t->q && t->parent && t->cand;
 }
 static void tree_free(tree_t* t) {
     free(t->q);
     free(t->parent);
     free(t->cand);
+    if (t->kd) {
+        kd_free(t->kd);
+        free(t->kd);
+    }
 }
 static int64_t tree_add(tree_t* t, const double* q, int32_t parent) {
     memcpy(t->q + NQ * t->n, q, sizeof(double) * NQ);
     t->parent[t->n] = parent;
     t->cand[t->n] = 0;
+    if (t->kd) kd_insert(t->kd, t->q, (int32_t)t->n);
     return t->n++;
 }
-/* nearest node among the first n (ties -> lowest index) */
+/* nearest node among the first n (ties -> lowest index); the kd index (which holds
+ * exactly the tree's nodes) when the tree has one and n is all of them */
 static int32_t nearest(const tree_t* t, int64_t n, const double* x) {
     double best = INFINITY;
     int32_t idx = -1;
+    if (t->kd && n == t->n && t->kd->n > 0) {
+        kd_search(t->kd, 0, t->q, x, &best, &idx);
+        return idx;
+    }
     for (int64_t j = 0; j < n; ++j) {
         double d = dist2(t->q + NQ * j, x);
         if (d < best) { best = d; idx = (int32_t)j; }
@@ -805,6 +927,15 @@ int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], co
 
     tree_t T[2];
     if (!tree_init(&T[0], p.tree_capacity) || !tree_init(&T[1], p.tree_capacity)) return RP_ERR_CAPACITY;
+    /* the sequential loop (one sample per iteration, one rank): exact kd-tree
+     * nearest-node searches (RBE_ORACLE_KD=0: the linear scan, same answers) */
+    {
+        const char* e = getenv("RBE_ORACLE_KD");
+        if (p.batch == 1 && world == 1 && !(e && *e == '0')) {
+            T[0].kd = (kd_tree*)calloc(1, sizeof(kd_tree));
+            T[1].kd = (kd_tree*)calloc(1, sizeof(kd_tree));
+        }
+    }
     tree_add(&T[0], start, -1);
     tree_add(&T[1], goal, -1);
 

@@ -211,3 +211,28 @@ def test_straight_first_off_without_simplification(oracle_lib):
     p = _abi.make_params(seed=3, batch=64, n_waypoints=0, timeout_s=30, simplify=False)
     _, st, stats = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
     assert st == _abi.STATUS_EXACT and stats["iterations"] >= 1
+
+
+@pytest.mark.parametrize("wl,qi,max_iters", [("clutter64_well", 0, 20000), ("goal4_pentagon_10box", 8, 0),
+                                             ("clutter64", 0, 0)])
+def test_sequential_kd_nearest_equals_linear_scan(oracle_lib, wl, qi, max_iters, monkeypatch):
+    """The sequential (batch 1) CPU baseline searches nearest nodes with an exact
+    kd-tree (OMPL uses a GNAT, not a linear scan): same trees and paths as the
+    linear scan (RBE_ORACLE_KD=0), including 10^3-node trees of the covered well."""
+    q = json.load(open(os.path.join(GOLD, "workloads", wl + ".json")))["queries"][qi]
+    sc = scenes.Scene.from_json(q["scene"])
+    o = oracle_lib.OracleScene()
+    o.set_scene(sc.boxes, sc.plane_z, sc.base)
+    o.set_attached(q["attached"])
+    out = {}
+    for kd in ("1", "0"):
+        monkeypatch.setenv("RBE_ORACLE_KD", kd)
+        p = _abi.make_params(seed=5, batch=1, range_=0.3 if wl == "goal4_pentagon_10box" else 0.0, n_waypoints=150,
+                             timeout_s=600.0, straight_first=False, max_iters=max_iters)
+        out[kd] = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+    (pa, sa, ta), (pb, sb, tb) = out["1"], out["0"]
+    assert sa == sb and np.array_equal(pa, pb)
+    for k in ("iterations", "start_tree_size", "goal_tree_size", "states_checked"):
+        assert ta[k] == tb[k], k
+    if max_iters:
+        assert ta["start_tree_size"] > 1000

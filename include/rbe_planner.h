@@ -315,6 +315,14 @@ int rp_last_kernel_ms(rp_ctx* ctx, double* ms);
  * steering and segment counts rely on these being IEEE correctly rounded. */
 int rp_selftest_f64(rp_ctx* ctx, const double* x, int64_t n, double* out);
 
+/* Nearest-node self-test (used by the parity tests): out[i] = the index of the tree
+ * state nearest to query i (n x 9 and T x 9 float64, host memory; lowest index among
+ * equal squared distances, the oracle's strict-< scan), by the planner's large-tree
+ * search with the filter constants of bounds [lo, hi]. mode 0: packed-f32 filter;
+ * 1 / 4 / 8: matrix-core filter with 1 / 4 / 8 row blocks of 16 queries per wave. */
+int rp_selftest_nn(rp_ctx* ctx, const double* q, int64_t n, const double* tree, int64_t T,
+                   const double lo[RP_NQ], const double hi[RP_NQ], int32_t mode, int32_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -21,6 +21,7 @@
 #include "../../include/rbe_planner.h"
 #include "rp_ik.h"
 #include "rp_kernels.h"
+#include "rp_nn.h"
 
 using namespace rp;
 
@@ -172,6 +173,10 @@ struct rp_ctx {
     // RP_ERR_EXCHANGE until the group is initialised again (no silent divergence)
     bool group_broken = false;
     DevBuf<DI2> nn_part;                 // split nearest-node search: (distance, index) per range
+    DevBuf<double> nn_qx;                // its queries as f64 states (matrix-core search)
+    NnMfma nnm{};                        // the matrix-core filter's constants for this plan's bounds
+    bool nnm_ok = false;
+    int nn_S = 0;                        // tree ranges of the last matrix-core launch
 
     void free_staging() {
         if (h_send) (void)hipHostFree(h_send);
@@ -203,7 +208,7 @@ struct rp_ctx {
         rec.release(); Lv.release(); chain_end.release(); gfail.release();
         eslot.release(); eincl.release(); echunk.release();
         cub_tmp.release(); path.release(); io.release(); simp.release(); partial.release();
-        g_send.release(); g_recv.release(); g_cnt.release(); g_incl.release(); nn_part.release();
+        g_send.release(); g_recv.release(); g_cnt.release(); g_incl.release(); nn_part.release(); nn_qx.release();
         leave_group();
         for (hipEvent_t e : pev) (void)hipEventDestroy(e);
         if (gx0) (void)hipEventDestroy(gx0);
@@ -755,6 +760,51 @@ bool out_of_bounds(const double* q, const double* lo, const double* hi) {
 // Nearest nodes of n queries over a large tree by the split search (rp_kernels.h
 // k_nn_part + k_nn_reduce) into out[0..n); false (nothing launched) when n x T is
 // small enough for the fused kernels' own search. RBE_NN_SPLIT=0/1 forces it.
+// The matrix-core filter's constants for bounds [lo, hi] (rp_nn.h):
+// coordinates x' = x - c with |x'| <= R0, scaled by S (S R0 <= 16384, inside the f16
+// range with the hi / lo split's residuals mostly normal), the half-norm and
+// threshold slots scaled by 2^-G, 2^-H into the f16 range. The margin e0 + e1 best
+// covers, with a factor of ~2, the f16 hi / lo representation error of the
+// coordinates, norms and threshold (<= 2^-22 relative each, dropped x_lo y_lo terms)
+// and a worst-case f32 accumulation of the 32 products (gamma_33 sum |a_k b_k|):
+// 1.8e-5 R0^2 + 2.3e-6 thr in total.
+bool nn_mfma_params(const double* lo, const double* hi, NnMfma* P) {
+    double r2 = 0.0;
+    for (int i = 0; i < NQ; ++i) {
+        P->c[i] = 0.5 * (lo[i] + hi[i]);
+        const double h = 0.5 * (hi[i] - lo[i]);
+        r2 += h * h;
+    }
+    const double R0 = std::sqrt(r2) * (1.0 + 1e-9) + 1e-12;
+    if (!(R0 > 1e-6 && R0 < 1e6)) return false;
+    P->S = std::ldexp(1.0, (int)std::floor(std::log2(16384.0 / R0)));
+    const double s2r2 = P->S * P->S * R0 * R0;
+    const int H = (int)std::ceil(std::log2(2.2 * s2r2 / 65504.0));
+    const int G = (int)std::ceil(std::log2(0.55 * s2r2 / 65504.0));
+    if (H > 15 || G > 15) return false;
+    P->H2 = std::ldexp(1.0, H);
+    P->G2 = std::ldexp(1.0, G);
+    P->e0 = 8e-5 * R0 * R0 + 1e-12;
+    P->e1 = 2e-5;
+    P->thr0 = 4.04 * R0 * R0 + P->e0;   // >= every |x - y|^2 of in-bounds states
+    return true;
+}
+
+template <int RB>
+void launch_nn_mfma(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, const double* tree, int64_t T) {
+    const int64_t per_block = (int64_t)NNM_WAVES * 16 * RB;
+    const int64_t qblocks = (n + per_block - 1) / per_block;
+    const int64_t stages = (T + NNM_STAGE - 1) / NNM_STAGE;
+    const int64_t want = std::max<int64_t>(1, (1024 + qblocks - 1) / qblocks);   // >= 1024 blocks
+    const int64_t S0 = std::min<int64_t>(want, stages);
+    const int64_t chunk = ((stages + S0 - 1) / S0) * NNM_STAGE;
+    const int S = (int)((T + chunk - 1) / chunk);
+    c->nn_part.ensure((size_t)S * n);
+    hipLaunchKernelGGL((k_nn_mfma<RB>), dim3((unsigned)qblocks, (unsigned)S), dim3(64 * NNM_WAVES), 0, c->stream, qx,
+                       n, Q.status, Q.t0, tree, T, chunk, c->nnm, c->nn_part.p);
+    c->nn_S = S;
+}
+
 bool nn_split(rp_ctx* c, const NnQuery& Q, int64_t n, const double* tree, int64_t T, int32_t* out,
               bool force = false) {
     if (n <= 0 || T <= 0) return false;
@@ -762,6 +812,29 @@ bool nn_split(rp_ctx* c, const NnQuery& Q, int64_t n, const double* tree, int64_
     if (const char* e = std::getenv("RBE_NN_SPLIT"))
         if (*e) mode = std::atoi(e) != 0;
     if (mode == 0 || (mode < 0 && !force && (double)n * (double)T < (double)(1 << 24))) return false;
+    // the matrix-core search (rp_nn.h) unless RBE_NN_MFMA=0 (the packed-f32 k_nn_part)
+    int mfma_rb = 4;   // (read per search: large-tree searches take milliseconds)
+    if (const char* e = std::getenv("RBE_NN_MFMA"))
+        if (*e) mfma_rb = std::atoi(e);
+    if (mfma_rb > 0 && c->nnm_ok) {
+        const double* qx;
+        if (Q.kind == NNQ_ROWS) {
+            qx = Q.A + (Q.TA0 + Q.t0) * NQ;
+        } else {
+            c->nn_qx.ensure((size_t)n * NQ);
+            hipLaunchKernelGGL(k_nn_queries, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, Q, n, c->nn_qx.p);
+            qx = c->nn_qx.p;
+        }
+        const int ps = prof_begin(c, c->stream);
+        if (mfma_rb >= 8) launch_nn_mfma<8>(c, qx, n, Q, tree, T);
+        else if (mfma_rb >= 2) launch_nn_mfma<4>(c, qx, n, Q, tree, T);
+        else launch_nn_mfma<1>(c, qx, n, Q, tree, T);
+        hipLaunchKernelGGL(k_nn_reduce, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream,
+                           (const DI2*)c->nn_part.p, n, c->nn_S, Q.status, Q.t0, out);
+        HIP_TRY(hipGetLastError());
+        prof_end(c, ps, 0, c->stream);
+        return true;
+    }
     const int64_t per_block = (int64_t)NNBLOCK * NN_QPT;
     const int64_t qblocks = (n + per_block - 1) / per_block;
     const int64_t tiles = (T + NNTILE - 1) / NNTILE;
@@ -1159,6 +1232,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
 
     Bounds bd;
     for (int i = 0; i < NQ; ++i) { bd.lo[i] = lo[i]; bd.hi[i] = hi[i]; }
+    c->nnm_ok = nn_mfma_params(lo, hi, &c->nnm);
     // speculative fronts on large trees: nearest nodes by the split search (both
     // searches; the second's queries are the steered new nodes, so it needs the
     // first's result: a large second search forces the first). Searches run over the
@@ -2159,6 +2233,55 @@ int rp_selftest_f64(rp_ctx* c, const double* x, int64_t n, double* out) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     dx.release();
     dy.release();
+    return RP_OK;
+    RP_GUARD_END(c)
+}
+
+// Nearest-node self-test (used by the parity tests): for each of n query states the
+// nearest of T tree states (lowest index among equal distances) by the large-tree
+// search of rp_plan, with the planner's filter constants for bounds [lo, hi];
+// mode 0: the packed-f32 filter (k_nn_part), mode 1/4/8: the matrix-core filter
+// (k_nn_mfma, 1/4/8 row blocks per wave).
+int rp_selftest_nn(rp_ctx* c, const double* q, int64_t n, const double* tree, int64_t T, const double lo[RP_NQ],
+                   const double hi[RP_NQ], int32_t mode, int32_t* out) {
+    if (!c || n <= 0 || T <= 0 || !q || !tree || !lo || !hi || !out) return RP_ERR_ARG;
+    if (T >= ((int64_t)1 << 31)) return RP_ERR_ARG;
+    RP_GUARD_BEGIN
+    HIP_TRY(hipSetDevice(c->device));
+    DevBuf<double> dq, dt;
+    DevBuf<int32_t> dout;
+    dq.ensure((size_t)n * NQ);
+    dt.ensure((size_t)T * NQ);
+    dout.ensure(n);
+    HIP_TRY(hipMemcpyAsync(dq.p, q, sizeof(double) * NQ * n, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(dt.p, tree, sizeof(double) * NQ * T, hipMemcpyHostToDevice, c->stream));
+    NnQuery Q{};
+    Q.kind = NNQ_ROWS;
+    Q.A = dq.p;
+    c->nnm_ok = nn_mfma_params(lo, hi, &c->nnm);
+    if (mode == 0) {
+        c->nn_part.ensure((size_t)n * ((T + NNTILE - 1) / NNTILE));
+        hipLaunchKernelGGL(k_nn_part, dim3((unsigned)((n + NNBLOCK * NN_QPT - 1) / (NNBLOCK * NN_QPT)), 1),
+                           dim3(NNBLOCK), 0, c->stream, Q, n, (const double*)dt.p, T, T, c->nn_part.p);
+        hipLaunchKernelGGL(k_nn_reduce, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream,
+                           (const DI2*)c->nn_part.p, n, 1, (const int*)nullptr, (int64_t)0, dout.p);
+    } else {
+        if (!c->nnm_ok) {
+            c->err = "bounds out of the matrix-core filter's range";
+            return RP_ERR_ARG;
+        }
+        if (mode >= 8) launch_nn_mfma<8>(c, dq.p, n, Q, dt.p, T);
+        else if (mode >= 2) launch_nn_mfma<4>(c, dq.p, n, Q, dt.p, T);
+        else launch_nn_mfma<1>(c, dq.p, n, Q, dt.p, T);
+        hipLaunchKernelGGL(k_nn_reduce, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream,
+                           (const DI2*)c->nn_part.p, n, c->nn_S, (const int*)nullptr, (int64_t)0, dout.p);
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(out, dout.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    dq.release();
+    dt.release();
+    dout.release();
     return RP_OK;
     RP_GUARD_END(c)
 }

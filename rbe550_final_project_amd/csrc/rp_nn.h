@@ -1,0 +1,261 @@
+// rp_nn.h — nearest tree node for many queries on the matrix cores (gfx950 MFMA).
+//
+// RRTConnect's nearest-neighbour query (OMPL NearestNeighbors, code/planning.py:156,
+// 190) over trees of 10^5 nodes is n x T squared distances, a distance matrix:
+// |x - y|^2 = |x|^2 + |y|^2 - 2 x.y is a GEMM of the queries against the nodes plus
+// rank-1 terms. Here v_mfma_f32_16x16x32_f16 computes, for a tile of 16 queries x 16
+// nodes, the whole FILTER VALUE
+//
+//     Q = S^2 x~.y~  -  S^2 |y'|^2 / 2  +  S^2 (thr - |x'|^2) / 2      (x' = x - c)
+//
+// in ONE instruction: the K = 32 slots hold the 9 coordinates as f16 hi / lo parts
+// (x_hi y_hi + x_lo y_hi + x_hi y_lo: 27 slots), the node's half norm as a hi / lo
+// pair against -2^G, and the query's threshold term as a hi / lo pair against 2^H.
+// Q >= 0 <=> (approximately) |x - y|^2 <= thr. The approximation error is bounded
+// (DESIGN.md §5.2): every node whose exact f64 distance is <= the query's exact
+// best so far has Q >= 0 when thr = best + e0 + e1 best, so the filter never drops a
+// node that could be the answer. A node that passes gets the oracle's exact f64
+// dist2 (same operands, same order) and the lexicographic (distance, index) update,
+// so the result is bit for bit the linear strict-< scan's: the nearest node, lowest
+// index among equal distances. Large trees only (rp_lib.hip nn_split): the ranges of
+// the tree go to grid.y, k_nn_reduce merges them as for k_nn_part.
+#pragma once
+#include "rp_plan_math.h"
+
+namespace rp {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// per-plan constants of the filter (host: nn_mfma_params in rp_lib.hip)
+struct NnMfma {
+    double c[NQ];   // centre of the bounds (coordinates x' = x - c, |x'| <= R0)
+    double S;       // coordinate scale, a power of two (S R0 <= 16384: f16 range)
+    double G2;      // 2^G: the node half-norm slots (A: -2^G, B: g / 2^G, hi / lo)
+    double H2;      // 2^H: the threshold slots (A: h / 2^H, hi / lo; B: 2^H)
+    double e0, e1;  // thr = best + e0 + e1 * best
+    double thr0;    // threshold while a query has no exact best (every node passes)
+};
+
+constexpr int NNM_WAVES = 4;    // waves per block, each with its own queries
+constexpr int NNM_STAGE = 64;   // nodes per LDS stage: 4 column tiles of 16, 16 per wave to build
+constexpr int NNM_IMG = 40;     // f16 per node image row: 32 slots + 8 pad (80 B rows spread LDS banks)
+
+__device__ __forceinline__ void split16(double v, _Float16& hi, _Float16& lo) {
+    hi = (_Float16)v;
+    lo = (_Float16)(v - (double)hi);   // (v - hi is exact in f64)
+}
+
+// LDS ordering between the lanes of one wave (stores, then other lanes' loads)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// threshold slots (f16 hi / lo of h / 2^H) of a query with exact best b
+__device__ __forceinline__ void thr_slots(const NnMfma& P, double b, double na, _Float16& hh, _Float16& hl) {
+    const double thr = b < 1e300 ? b + (P.e0 + P.e1 * b) : P.thr0;
+    split16((P.S * P.S) * (thr - na) * 0.5 / P.H2, hh, hl);
+}
+
+// A fragment of a query (row), k chunk `ch` (lane >> 4) of 8 slots
+__device__ __forceinline__ h8 a_frag(const NnMfma& P, const double* x, bool live, int ch, double* na_out,
+                                     _Float16* hh_out, _Float16* hl_out) {
+    _Float16 xh[NQ], xl[NQ];
+    double na = 0.0;
+#pragma unroll
+    for (int d = 0; d < NQ; ++d) {
+        const double xd = x[d] - P.c[d];
+        na += xd * xd;
+        split16(P.S * xd, xh[d], xl[d]);
+    }
+    _Float16 hh, hl;
+    thr_slots(P, __builtin_inf(), na, hh, hl);
+    const _Float16 z = (_Float16)0.0f, mg = (_Float16)(-P.G2);
+    h8 a;
+    if (!live) {   // no query: Q = -65504 * 2^H < 0 for every node
+        a = h8{z, z, z, z, z, z, z, z};
+        if (ch == 3) a[5] = (_Float16)(-65504.0f);
+    } else if (ch == 0) {
+        a = h8{xh[0], xh[1], xh[2], xh[3], xh[4], xh[5], xh[6], xh[7]};
+    } else if (ch == 1) {
+        a = h8{xh[8], xl[0], xl[1], xl[2], xl[3], xl[4], xl[5], xl[6]};
+    } else if (ch == 2) {
+        a = h8{xl[7], xl[8], xh[0], xh[1], xh[2], xh[3], xh[4], xh[5]};
+    } else {
+        a = h8{xh[6], xh[7], xh[8], mg, mg, hh, hl, z};
+    }
+    *na_out = na;
+    *hh_out = hh;
+    *hl_out = hl;
+    return a;
+}
+
+// B image chunk of a node: its 8 slots of k chunk `ch`
+__device__ __forceinline__ h8 b_frag(const NnMfma& P, const double* y, int ch) {
+    _Float16 yh[NQ], yl[NQ];
+    double nb = 0.0;
+#pragma unroll
+    for (int d = 0; d < NQ; ++d) {
+        const double yd = y[d] - P.c[d];
+        nb += yd * yd;
+        split16(P.S * yd, yh[d], yl[d]);
+    }
+    _Float16 gh, gl;
+    split16((P.S * P.S) * nb * 0.5 / P.G2, gh, gl);
+    const _Float16 z = (_Float16)0.0f, h2 = (_Float16)P.H2;
+    if (ch == 0) return h8{yh[0], yh[1], yh[2], yh[3], yh[4], yh[5], yh[6], yh[7]};
+    if (ch == 1) return h8{yh[8], yh[0], yh[1], yh[2], yh[3], yh[4], yh[5], yh[6]};
+    if (ch == 2) return h8{yh[7], yh[8], yl[0], yl[1], yl[2], yl[3], yl[4], yl[5]};
+    return h8{yl[6], yl[7], yl[8], gh, gl, h2, h2, z};
+}
+
+// Nearest node of each query over tree range [y * chunk, (y + 1) * chunk) ->
+// part[y * n + q] (exact distance, index; index -1: no node). Queries: qx (n x 9
+// f64); status (NNQ_ROWS): n = min(n, status[0] - t0). RB row blocks of 16 queries
+// per wave.
+template <int RB>
+__global__ __launch_bounds__(64 * NNM_WAVES) void k_nn_mfma(const double* __restrict__ qx, int64_t n,
+                                                          const int* status, int64_t t0,
+                                                          const double* __restrict__ tree, int64_t T, int64_t chunk,
+                                                          NnMfma P, DI2* __restrict__ part) {
+    constexpr int QW = 16 * RB;   // queries per wave
+    __shared__ double s_q[NNM_WAVES][QW][NQ];               // query states (exact path)
+    __shared__ unsigned long long s_best[NNM_WAVES][QW];    // exact best distance (f64 bits; >= 0)
+    __shared__ int s_bi[NNM_WAVES][QW];                     // its node (lowest index among equal)
+    __shared__ int s_ti[NNM_WAVES][QW];                     // a round's lowest node at the new best
+    __shared__ double s_node[NNM_STAGE][NQ];                // the stage's node states (exact path)
+    __shared__ alignas(16) _Float16 s_img[NNM_STAGE][NNM_IMG];   // their B operand images
+    if (status) n = min(n, (int64_t)status[0] - t0);
+    const int64_t qb0 = (int64_t)blockIdx.x * NNM_WAVES * QW;
+    if (qb0 >= n) return;   // whole block idle (uniform)
+    const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63), ch = lane >> 4;
+    const int64_t t_lo = (int64_t)blockIdx.y * chunk, t_hi = min(T, t_lo + chunk);
+    const int64_t qw0 = qb0 + (int64_t)w * QW;
+
+    for (int i = lane; i < QW * NQ; i += 64) {
+        const int r = i / NQ, d = i - r * NQ;
+        const int64_t q = qw0 + r;
+        s_q[w][r][d] = q < n ? qx[q * NQ + d] : 0.0;
+    }
+    for (int r = lane; r < QW; r += 64) {
+        s_best[w][r] = 0x7FF0000000000000ull;   // +inf
+        s_bi[w][r] = -1;
+    }
+    wave_lds_sync();
+    // A fragments (row lane & 15 of each row block; k chunk ch); the threshold slots
+    // (chunk 3, elements 5 / 6) follow each row's exact best
+    h8 a[RB];
+    double na[RB], curb[RB];
+#pragma unroll
+    for (int rb = 0; rb < RB; ++rb) {
+        const int r = rb * 16 + (lane & 15);
+        _Float16 hh, hl;
+        a[rb] = a_frag(P, &s_q[w][r][0], qw0 + r < n, ch, &na[rb], &hh, &hl);
+        curb[rb] = __builtin_inf();
+    }
+    const int jn = w * 16 + (lane & 15);   // the node of the stage this lane builds
+    double nx[NQ];
+    {
+        const int64_t j = t_lo + jn;
+#pragma unroll
+        for (int d = 0; d < NQ; ++d) nx[d] = j < t_hi ? tree[j * NQ + d] : 0.0;
+    }
+    const f4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int64_t base = t_lo; base < t_hi; base += NNM_STAGE) {
+        const int cnt = (int)min((int64_t)NNM_STAGE, t_hi - base);
+        __syncthreads();   // the previous stage is consumed
+        *reinterpret_cast<h8*>(&s_img[jn][ch * 8]) = b_frag(P, nx, ch);
+        if (ch == 0)
+#pragma unroll
+            for (int d = 0; d < NQ; ++d) s_node[jn][d] = nx[d];
+        {   // next stage's node, in flight during this stage's MFMAs
+            const int64_t j = base + NNM_STAGE + jn;
+#pragma unroll
+            for (int d = 0; d < NQ; ++d) nx[d] = j < t_hi ? tree[j * NQ + d] : 0.0;
+        }
+        __syncthreads();
+#pragma unroll 1
+        for (int ct = 0; ct < NNM_STAGE / 16; ++ct) {
+            if (ct * 16 >= cnt) break;   // (uniform)
+            const int col = ct * 16 + (lane & 15);
+            const h8 b = *reinterpret_cast<const h8*>(&s_img[col][ch * 8]);
+            f4 acc[RB];
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rb], b, zero, 0, 0, 0);
+            // this lane's column: acc[rb][e] = row rb * 16 + 4 ch + e
+            float m = -1.0f;
+            if (col < cnt) {
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb) m = fmaxf(m, fmaxf(fmaxf(acc[rb][0], acc[rb][1]), fmaxf(acc[rb][2], acc[rb][3])));
+            }
+            if (!__any(m >= 0.0f)) continue;
+            // ---- exact path: the passing (row, node) pairs, in rounds of one per lane
+            unsigned pm = 0;
+            if (col < cnt) {
+#pragma unroll
+                for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) pm |= (acc[rb][e] >= 0.0f ? 1u : 0u) << (rb * 4 + e);
+            }
+            const int node = (int)(base + col);
+            while (__any(pm != 0)) {
+                const bool has = pm != 0;
+                const int e = has ? __builtin_ctz(pm) : 0;
+                pm &= pm - 1;
+                const int row = (e >> 2) * 16 + ch * 4 + (e & 3);
+                unsigned long long prev = 0, db = 0;
+                if (has) {
+                    prev = s_best[w][row];
+                    s_ti[w][row] = 0x7fffffff;
+                    db = (unsigned long long)__double_as_longlong(dist2(&s_node[col][0], &s_q[w][row][0]));
+                }
+                wave_lds_sync();
+                if (has) atomicMin(&s_best[w][row], db);
+                wave_lds_sync();
+                const unsigned long long cur = has ? s_best[w][row] : 0ull;
+                if (has && db == cur) atomicMin(&s_ti[w][row], node);
+                wave_lds_sync();
+                if (has && db == cur && s_ti[w][row] == node) {   // the row's lowest node at its new best
+                    if (cur < prev) s_bi[w][row] = node;
+                    else if (node < s_bi[w][row]) s_bi[w][row] = node;
+                }
+                wave_lds_sync();
+            }
+            // rows whose best improved: new threshold slots (chunk-3 lanes)
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb) {
+                const int r = rb * 16 + (lane & 15);
+                const double bnow = __longlong_as_double((long long)s_best[w][r]);
+                if (ch == 3 && bnow != curb[rb]) {
+                    curb[rb] = bnow;
+                    _Float16 hh, hl;
+                    thr_slots(P, bnow, na[rb], hh, hl);
+                    a[rb][5] = hh;
+                    a[rb][6] = hl;
+                }
+            }
+        }
+    }
+    wave_lds_sync();
+    for (int r = lane; r < QW; r += 64) {
+        const int64_t q = qw0 + r;
+        if (q < n)
+            part[(int64_t)blockIdx.y * n + q] =
+                DI2{__longlong_as_double((long long)s_best[w][r]), s_bi[w][r], 0};
+    }
+}
+
+// the queries of a split search as f64 states (NNQ_SAMPLE / NNQ_STEER: Philox samples,
+// steered; nn_query of rp_kernels.h)
+__global__ void k_nn_queries(NnQuery Q, int64_t n, double* __restrict__ qx) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    double x[NQ];
+    nn_query(Q, k, x);
+#pragma unroll
+    for (int d = 0; d < NQ; ++d) qx[k * NQ + d] = x[d];
+}
+
+}  // namespace rp

@@ -21,7 +21,7 @@ EXPORTS = ("rp_version", "rp_default_robot", "rp_create", "rp_destroy", "rp_set_
            "rp_check_states", "rp_check_states_device", "rp_check_edges", "rp_check_edges_device",
            "rp_state_contacts", "rp_plan", "rp_group_init", "rp_group_init_shm", "rp_group_rccl_unique_id", "rp_group_init_rccl",
            "rp_get_stats", "rp_last_error", "rp_last_kernel_ms", "rp_selftest_f64", "rp_ik", "rp_set_profiling",
-           "rp_get_profile", "rp_get_stream", "rp_group_info")
+           "rp_get_profile", "rp_get_stream", "rp_group_info", "rp_selftest_nn")
 
 # rp_allgather_fn(user, send, recv, bytes_per_rank): library-owned pinned host buffers
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64)
@@ -70,6 +70,7 @@ def load():
     L.rp_last_error.restype = C.c_char_p
     L.rp_last_kernel_ms.argtypes = [vp, C.POINTER(f64)]
     L.rp_selftest_f64.argtypes = [vp, vp, i64, vp]
+    L.rp_selftest_nn.argtypes = [vp, vp, i64, vp, i64, vp, vp, i32, vp]
     L.rp_ik.argtypes = [vp, i32, vp, vp, vp, vp, vp, C.POINTER(_abi.IkParams), vp, vp]
     _lib = L
     return L
@@ -168,6 +169,17 @@ class Context:
         x = np.ascontiguousarray(x, dtype=np.float64)
         out = np.zeros((len(x), 4), dtype=np.float64)
         self._check(load().rp_selftest_f64(self._h, _ptr(x), len(x), _ptr(out)), "rp_selftest_f64")
+        return out
+
+    def selftest_nn(self, q, tree, lo, hi, mode):
+        """rp_selftest_nn: nearest tree state of each query (lowest index on ties)."""
+        q = np.ascontiguousarray(q, dtype=np.float64).reshape(-1, _abi.NQ)
+        tree = np.ascontiguousarray(tree, dtype=np.float64).reshape(-1, _abi.NQ)
+        lo = np.ascontiguousarray(lo, dtype=np.float64)
+        hi = np.ascontiguousarray(hi, dtype=np.float64)
+        out = np.zeros(len(q), dtype=np.int32)
+        self._check(load().rp_selftest_nn(self._h, _ptr(q), len(q), _ptr(tree), len(tree), _ptr(lo), _ptr(hi),
+                                          int(mode), _ptr(out)), "rp_selftest_nn")
         return out
 
     # -- planning ------------------------------------------------------------

@@ -103,12 +103,24 @@ def test_rccl_transport_world1(name):
 
 @pytest.mark.parametrize("name,split", [("C2_q0_s1", "1"), ("C4_q5", "1"), ("C5_well_s4", "0"), ("C5_well_s2", "1")])
 @pytest.mark.parametrize("grouped", ["0", "1"])
-def test_nearest_node_split_forced(gpu_ctx, name, split, grouped, monkeypatch):
-    """The split nearest-node search (k_nn_part + k_nn_reduce: queries x tree ranges,
-    lexicographic (distance, index) minimum) forced on / off, through the two-phase
-    and the group iteration: same plans as the oracle."""
+@pytest.mark.parametrize("mfma", ["4", "0"])
+def test_nearest_node_split_forced(gpu_ctx, name, split, grouped, mfma, monkeypatch):
+    """The split nearest-node search (queries x tree ranges, lexicographic (distance,
+    index) minimum over the ranges) forced on / off, with the matrix-core filter
+    (k_nn_mfma, the default) and the packed-f32 one (k_nn_part, RBE_NN_MFMA=0),
+    through the two-phase and the group iteration: same plans as the oracle."""
     monkeypatch.setenv("RBE_NN_SPLIT", split)
     monkeypatch.setenv("RBE_PLAN_GROUPED", grouped)
+    monkeypatch.setenv("RBE_NN_MFMA", mfma)
+    _check(gpu_ctx, name)
+
+
+@pytest.mark.parametrize("name", ["C5_well_s0", "C5_well_s3"])
+@pytest.mark.parametrize("mfma", ["1", "8"])
+def test_nearest_node_mfma_row_blocks(gpu_ctx, name, mfma, monkeypatch):
+    """The matrix-core search with 1 and 8 row blocks of 16 queries per wave on the
+    largest trees (3.3 x 10^5 nodes, 7-8 iterations): same plans."""
+    monkeypatch.setenv("RBE_NN_MFMA", mfma)
     _check(gpu_ctx, name)
 
 

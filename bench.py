@@ -37,6 +37,8 @@ HBM_PEAK_GBPS = ROOF["peaks"]["hbm_gbps"]
 BYTES_PER_STATE = ROOF["state_check"]["bytes"]     # 9 x fp32 in, 1 B flag out
 BYTES_PER_EDGE = ROOF["edge_check"]["bytes"]
 NN_FLOP_PER_PAIR = ROOF["nearest_node"]["flop"]
+NN_MFMA_FLOP_PER_PAIR = ROOF["nearest_node"]["mfma_flop"]
+F16_MFMA_PEAK_TFLOPS = ROOF["peaks"]["f16_mfma_dense_tflops"]
 C2_BATCH = 65536             # BASELINE C2: 64k-sample batch
 C4_BATCH = 262144            # BASELINE C4: 256k-sample iterations
 C5_BATCH = 131072            # BASELINE C5: 131,072-sample iterations (2^20 budget)
@@ -230,14 +232,22 @@ def well_profile(ctx, seeds=(2, 3, 4, 0)):
                 tot[k] += pr[k]
     finally:
         ctx.set_profiling(False)
-    nn_tf = tot["nn_pairs"] * NN_FLOP_PER_PAIR / (tot["nn_ms"] * 1e-3) / 1e12
+    pairs_per_s = tot["nn_pairs"] / (tot["nn_ms"] * 1e-3)
+    nn_mfma_tf = pairs_per_s * NN_MFMA_FLOP_PER_PAIR / 1e12   # the matrix cores' executed work
+    nn_alg_tf = pairs_per_s * NN_FLOP_PER_PAIR / 1e12        # the squared distance's algorithmic FLOP
     fps = flops_per_state(len(sc.boxes))
     ed_tf = tot["edge_states"] * fps / (tot["edge_ms"] * 1e-3) / 1e12
-    sample = f"C5 covered-well plans, seeds {list(seeds)}, 131,072-sample iterations (trees up to 3.3e5 nodes)"
-    return ({"bound": "fp64", "achieved": round(nn_tf, 3), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-             "frac": round(nn_tf / FP64_PEAK_TFLOPS, 4), "kernel": "k_ext_nn/k_conn_nn/k_ext_conn_nn",
+    sample = (f"C5 covered-well plans, seeds {list(seeds)}, 131,072-sample iterations (trees up to 3.3e5 nodes); "
+              "every nearest-node launch of the plans (large trees: k_nn_mfma; small: the fused LDS-tile kernels)")
+    return ({"bound": "mfma", "achieved": round(nn_mfma_tf, 3), "peak": F16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+             "frac": round(nn_mfma_tf / F16_MFMA_PEAK_TFLOPS, 4),
+             "kernel": "k_nn_mfma (+ k_ext_conn_nn / k_ext_nn / k_conn_nn on small trees)",
              "launches": tot["nn_launches"], "kernel_ms": round(tot["nn_ms"], 3), "pairs": tot["nn_pairs"],
-             "flop_per_pair": NN_FLOP_PER_PAIR, "sample": sample},
+             "pairs_per_sec": round(pairs_per_s, 1), "mfma_flop_per_pair": NN_MFMA_FLOP_PER_PAIR,
+             "algorithmic": {"flop_per_pair": NN_FLOP_PER_PAIR, "achieved": round(nn_alg_tf, 3),
+                             "fp32_vector_peak": VALU_PEAK_TFLOPS,
+                             "frac_of_fp32_vector_peak": round(nn_alg_tf / VALU_PEAK_TFLOPS, 4)},
+             "sample": sample},
             {"bound": "valu", "achieved": round(ed_tf, 3), "peak": VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
              "frac": round(ed_tf / VALU_PEAK_TFLOPS, 4), "kernel": "k_edges/k_edges_packed",
              "launches": tot["edge_launches"], "kernel_ms": round(tot["edge_ms"], 3),
@@ -339,6 +349,7 @@ def main():
     # (131,072-sample iterations); every iteration is sharded over the ranks when
     # N > 1 (RCCL all-gather per phase)
     plan = None
+    rank_group = None
     if not args.no_plan:
         # the rank group is built outside the per-workload error handling: at N > 1 a
         # plan number without the group would be a single-rank number, so a failure
@@ -347,6 +358,12 @@ def main():
         if distributed:
             from rbe550_final_project_amd.distributed import Group
             group = Group(ctx, transport="shm" if args.backend == "gloo" else "rccl")
+            # what the transport itself reports on every rank (RCCL: ncclCommUserRank /
+            # ncclCommCount of the library's communicator)
+            views = [None] * world
+            dist.all_gather_object(views, ctx.group_info())
+            rank_group = {"transport": views[0]["transport"], "ranks": views,
+                          "consistent": all(v["world"] == world and v["rank"] == r for r, v in enumerate(views))}
         try:
             # warm-up: one untimed pass over the whole C3 workload in both modes (a
             # 2-query warm-up left the first timed workload at 2x its median on one box)
@@ -384,7 +401,7 @@ def main():
         # configured-batch workloads: C4 (262,144-sample iterations) and C5
         # (131,072-sample iterations: clutter64, and the covered well, whose trees
         # grow to 10^5 - 3 x 10^5 nodes over up to 8 iterations = the 2^20 budget);
-        # "_sched": the product's batch schedule (256 samples first, doubling to the
+        # "_sched": the product's batch schedule (64 samples first, doubling to the
         # configured batch) on the same queries
         well = load_workload("clutter64_well")
         wellx = {"queries": well["queries"] * 4}
@@ -446,7 +463,14 @@ def main():
             cpu = {"value": round(rate, 1), "unit": "states/s", "cores": threads, "kind": "port",
                    "sample": f"{sample} uniform states, goal3 10-box scene, OpenMP CPU oracle ({dt:.1f} s)",
                    "per_core": round(rate1, 1), "per_core_sample": f"{1 << 22} states on 1 thread ({dt1:.1f} s)",
-                   "host": hi}
+                   "host": hi,
+                   # the whole host, extrapolated: this job's CPU share is OMP_NUM_THREADS
+                   # threads (the pool's rule for one GPU), so the affinity count is not
+                   # run; measured per-thread rate at `threads` x the affinity count
+                   "full_host_extrapolated": {
+                       "value": round(rate / threads * (hi["affinity"] or threads), 1), "threads": hi["affinity"],
+                       "basis": f"{threads}-thread rate / {threads} x {hi['affinity']} threads (linear scaling, "
+                                "an upper bound: SMT threads share cores)"}}
             # plan wall-time of the reference's CPU planner class (sequential
             # RRT-Connect, batch 1, one core, 10 s budget per query)
             plans = {}
@@ -462,7 +486,8 @@ def main():
                 w = {"queries": w["queries"] * reps}
                 t, stc = cpu_plan_baseline(w, 0, straight_first=sf)
                 plans[key] = cpu_plan_record(t, stc, f"{wname}: {'straight edge first, then ' if sf else ''}"
-                                                     "sequential RRT-Connect (batch 1), CPU oracle, 1 core, "
+                                                     "sequential RRT-Connect (batch 1, OMPL's loop) with an exact "
+                                                     "kd-tree nearest-node index (OMPL: GNAT), CPU oracle, 1 core, "
                                                      "10 s budget per query")
             cpu["plans"] = plans
             # legacy keys (round 1 records)
@@ -480,6 +505,7 @@ def main():
                "config": {"workload": "C3 goal3_tallest 10-block scene: validity batch per GPU + 21-query plan",
                           "states_per_gpu": n, "global_batch": n * world, "parallelism": f"dp{world}",
                           "valid_fraction": round(valid_frac, 4)},
+               "rank_group": rank_group,
                "plan_wall": plan, "per_config": per_config, "roofline": roofline,
                "rooflines_plan": rooflines_plan, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)

@@ -698,7 +698,9 @@ __global__ __launch_bounds__(64) void k_edges_ml(const double* __restrict__ from
             if constexpr (GL == 16) RP_ESTAMP(1);
         }
         const bool run = sl ? idx < total : in && nde >= 0 && slot < slots && ok && gf > gs;
-        count_states(counter, __ballot(run && gl == 0));
+        // (the straight-edge items are not counted: states_checked stays the solve
+        // loop's count whether the ride is on or off and whatever the lane count)
+        count_states(counter, __ballot(run && gl == 0 && !sl));
         if constexpr (GL == 16) RP_ESTAMP(2);
         if (!__any(run)) continue;
         double st[NQ];

@@ -152,7 +152,9 @@ __device__ __forceinline__ V3 xform(const Frame& f, float a0, float a1, float a2
     return w;
 }
 
-struct Capsules { V3 a[NCAP]; V3 b[NCAP]; };
+// a, b: segment endpoints (world); m = a + b (twice the centre: the self-pair
+// sphere prefilter's operand, made once per capsule instead of once per pair)
+struct Capsules { V3 a[NCAP]; V3 b[NCAP]; V3 m[NCAP]; };
 
 // fma(a2, c2, fma(a1, c1, fma(a0, c0, p))) with compile-time a: a zero term is
 // skipped (fma(0, x, p) == p for finite x, up to the sign of a zero result, which
@@ -171,6 +173,7 @@ template <int C>
 __device__ __forceinline__ void place(Capsules& k, const Frame& f) {
     k.a[C] = xform_c<C, 0>(f);
     k.b[C] = xform_c<C, 3>(f);
+    k.m[C] = {k.a[C].x + k.b[C].x, k.a[C].y + k.b[C].y, k.a[C].z + k.b[C].z};   // (dead unless a sphere uses it)
 }
 // Franka Panda forward kinematics (MJCF bodies of
 // panda.xml that Genesis loads at code/scenes.py:85) -> world capsule endpoints.
@@ -548,6 +551,7 @@ struct QueueState {
     WaveQ* Q;
     int nss, nsb;     // wave-uniform item counts
     bool in_limits;   // every state of the wave inside the joint limits (skip never pairs)
+    unsigned hand_near;   // bit I: the sphere test of pair (capsule I, hand) passed (this lane)
     int lane;
     float plane_z;
     ClusterRegs<NCL> cl;
@@ -738,8 +742,14 @@ template <int P>
 __device__ __forceinline__ bool pair_sphere(const Capsules& k) {
     constexpr int I = PAIRS[P][0], J = PAIRS[P][1];
     constexpr float RS = sphere_radius<I>() + sphere_radius<J>();
+#ifndef RP_SPHERE_PAIRSUM
+    // the centres' sums made once per capsule (place): -6 VALU per pair, 25 pairs per
+    // state; the same values (the same two adds), so the same bools
+    const V3 d = {k.m[I].x - k.m[J].x, k.m[I].y - k.m[J].y, k.m[I].z - k.m[J].z};
+#else
     const V3 d = {(k.a[I].x + k.b[I].x) - (k.a[J].x + k.b[J].x), (k.a[I].y + k.b[I].y) - (k.a[J].y + k.b[J].y),
                   (k.a[I].z + k.b[I].z) - (k.a[J].z + k.b[J].z)};
+#endif
     // |centre_I - centre_J| <= RS  <=>  |2 centre_I - 2 centre_J|^2 <= (2 RS)^2
     return dot3(d, d) <= (2.0f * RS) * (2.0f * RS);
 }
@@ -789,8 +799,32 @@ __device__ __forceinline__ void pairs_each(const Capsules& k, S& s) {
         // which lowers the register peak); waves with a state outside the joint
         // limits test them afterwards (never_pairs_outside_limits)
         if constexpr (!pair_never(L.p[T])) {
-            const bool cand = pair_sphere<L.p[T]>(k);
-            pair_enqueue<L.p[T]>(k, s, cand, __ballot(cand));
+            constexpr int P = L.p[T], I = PAIRS[P][0];
+#ifdef RP_HAND_CONTAIN
+            // Inside the joint limits the finger capsules lie inside the hand capsule's
+            // bounding sphere (finger tips <= 0.0882 m from the hand capsule's centre at
+            // finger travel <= 0.04; the sphere is 0.0901 m: 1.9 mm to spare, far above
+            // rounding), so a capsule whose sphere misses the hand's misses the
+            // fingers: their pairs are candidates only after (I, hand) passed, and a
+            // wave where no lane's (I, hand) passed skips the finger tests. Exact
+            // reject: same flags.
+            if constexpr (J == C_HAND) {
+                const bool cand = pair_sphere<P>(k);
+                s.hand_near |= (cand ? 1u : 0u) << I;
+                pair_enqueue<P>(k, s, cand, __ballot(cand));
+            } else if constexpr (J == C_LFINGER || J == C_RFINGER) {
+                const bool near = ((s.hand_near >> I) & 1u) != 0u;
+                if (!s.in_limits || __any(near)) {
+                    const bool cand = (near || !s.in_limits) && pair_sphere<P>(k);
+                    pair_enqueue<P>(k, s, cand, __ballot(cand));
+                }
+            } else
+#endif
+            {
+                const bool cand = pair_sphere<P>(k);
+                pair_enqueue<P>(k, s, cand, __ballot(cand));
+            }
+            (void)I;
         }
         pairs_each<J, T + 1, S>(k, s);
     }
@@ -872,6 +906,7 @@ __device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene
         v.s.in_limits = !__any(!in);
     }
     v.s.plane_z = sc->plane_z;
+    v.s.hand_near = 0u;
     v.s.cl.load(sc);
     Q.hit[v.s.lane] = 0;
     __builtin_amdgcn_wave_barrier();

@@ -15,7 +15,8 @@ Transports (inside librbe_mi355x.so):
   shm   ranks of one node: a POSIX shared-memory segment (made by rank 0, its
         name broadcast with torch.distributed) that every rank maps; the kernels
         write and read the records in it in place and the ranks meet at a spin
-        barrier in it — no copies, no collective call. The default with gloo.
+        barrier in it — no copies, no collective call. The default with gloo
+        when every rank is on one host ("host" otherwise).
   host  the records pass through pinned host buffers and a torch.distributed
         all-gather on CPU tensors (backend "gloo").
 """
@@ -34,7 +35,13 @@ class Group:
         self.rank = dist.get_rank()
         self.world = dist.get_world_size()
         if transport is None:
-            transport = "rccl" if dist.get_backend() == "nccl" else "shm"
+            if dist.get_backend() == "nccl":
+                transport = "rccl"
+            else:   # the shared-memory segment exists only on rank 0's host
+                import socket
+                hosts = [None] * self.world
+                dist.all_gather_object(hosts, socket.gethostname())
+                transport = "shm" if len(set(hosts)) == 1 else "host"
         if transport not in ("rccl", "host", "shm"):
             raise ValueError(f"unknown transport {transport!r}")
         self.transport = transport

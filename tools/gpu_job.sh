@@ -22,15 +22,15 @@ for s in "$@"; do
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) step bench 600 python bench.py ;;
     benchq) step bench 300 python bench.py --steps 20 --no-cpu ;;
-    ab) step ab 600 python tools/variant_bench.py build/variants/*.so && step ab_clutter 600 python tools/variant_bench.py --scene clutter64 build/variants/*.so && step ab_small 600 python tools/variant_bench.py --states 65536 --iters 50 build/variants/*.so ;;
+    ab) step ab 600 python tools/variant_bench.py abvariants/*.so && step ab_clutter 600 python tools/variant_bench.py --scene clutter64 abvariants/*.so && step ab_small 600 python tools/variant_bench.py --states 65536 --iters 50 abvariants/*.so ;;
     ptrace) step ptrace 600 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d gpurun_out/ptrace -o pt -- python tools/plan_trace.py && step plantime 300 python tools/plan_trace.py ;;
     gridab) step gridab 600 python tools/grid_ab.py ;;
     ptrace4) step ptrace4 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ptrace4 -o pt -- python tools/plan_trace.py goal4_pentagon_10box 262144 full && python tools/trace_summary.py gpurun_out/ptrace4/pt_kernel_trace.csv > gpurun_out/ptrace4_summary.txt && step ptrace5 600 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ptrace5 -o pt -- python tools/plan_trace.py clutter64 131072 full && python tools/trace_summary.py gpurun_out/ptrace5/pt_kernel_trace.csv > gpurun_out/ptrace5_summary.txt ;;
     rates) step rates 600 python tools/scene_rates.py ;;
-    stamps) step stamps 300 python tools/stamp_probe.py build/variants/lib_stamps.so ;;
+    stamps) step stamps 300 python tools/stamp_probe.py abvariants/lib_stamps.so ;;
     sweep) step sweep 600 python tools/plan_sweep.py goal3_tallest_10box 4096 32 64 128 256 512 && step sweep4 600 python tools/plan_sweep.py goal4_pentagon_10box 4096 32 64 128 256 512 ;;
-    planab) for v in build/variants/*.so; do step planab_$(basename $v .so) 300 python tools/plan_bench.py $v goal4_pentagon_10box 262144 full; done ;;
-    planab3) for v in build/variants/*.so; do step planab3_$(basename $v .so) 300 python tools/plan_bench.py $v goal3_tallest_10box 4096; done ;;
+    planab) for v in abvariants/*.so; do step planab_$(basename $v .so) 300 python tools/plan_bench.py $v goal4_pentagon_10box 262144 full; done ;;
+    planab3) for v in abvariants/*.so; do step planab3_$(basename $v .so) 300 python tools/plan_bench.py $v goal3_tallest_10box 4096; done ;;
     bench2) step bench2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --no-cpu --backend gloo ;;
     lat) step lat 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/lat -o lt -- python tools/latency_probe.py && python tools/latency_probe.py --summarize gpurun_out/lat/lt_kernel_trace.csv > gpurun_out/lat_summary.txt ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o kt -- python bench.py --steps 20 --no-cpu --no-plan --no-configs ;;
@@ -39,6 +39,7 @@ for s in "$@"; do
     c5prof) step c5prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c5prof -o kt -- python tools/c5_profile.py ;;
     nnpmc) step nnpmc_a 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH --output-format csv -d gpurun_out/nnpmc_a -o a -- python tools/c5_profile.py pmc && step nnpmc_b 300 rocprofv3 --pmc SQ_WAVES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/nnpmc_b -o b -- python tools/c5_profile.py pmc && python tools/pmc_summary.py gpurun_out/nnpmc_a gpurun_out/nnpmc_b --kernel k_nn_part --json gpurun_out/nn_pmc.json > gpurun_out/nn_pmc.txt ;;
     c5stats) step c5stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c5stats -o kt -- python tools/c5_profile.py ;;
+    nntest) step pytest_nn 600 python -u -m pytest tests/test_gpu_nn.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     chunks) step chunks 600 python tools/chunk_sweep.py -1 256 1024 4096 ;;
     ptests) step pytest_plan 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
     procs) step pytest_procs 900 python -u -m pytest tests/test_gpu_group_procs.py -m gpu -x -v --timeout 400 --timeout-method thread ;;

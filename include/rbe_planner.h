@@ -123,11 +123,12 @@ typedef struct rp_plan_params {
                                shortcut stage would reduce any solution to); < 0 = always
                                run RRT-Connect; ignored when simplify == 0               */
     int32_t chunk;          /* execution only, never the result: an iteration runs as ordered
-                               sub-batches of chunk, 4 chunk, 16 chunk, ... samples and ends
-                               after the sub-batch holding the first REACHED sample (the
-                               trees keep the appends up to that sample, DESIGN.md §4 step
-                               5, whatever the sub-batching). 0 = default 4096; < 0 = the
-                               whole iteration as one batch                               */
+                               sub-batches — chunk samples, then each next one 4x the last
+                               but at least a quarter of what is left — and ends after the
+                               sub-batch holding the first REACHED sample (the trees keep
+                               the appends up to that sample, DESIGN.md §4 step 5, whatever
+                               the sub-batching). 0 = default 256; < 0 = the whole
+                               iteration as one batch                                     */
 } rp_plan_params;
 
 /* rp_ik parameters (defaults follow Genesis inverse_kinematics). Zero / negative

@@ -95,8 +95,10 @@ struct Tree {
     DevBuf<double> q;
     DevBuf<int32_t> par;
     DevBuf<uint8_t> cand;
+    DevBuf<h8> img;        // matrix-core search: B operand image of each node (rp_nn.h), 4 x 16 B
     int64_t n = 0;
-    void release() { q.release(); par.release(); cand.release(); }
+    int64_t n_img = 0;     // nodes [0, n_img) have their image for this plan's bounds
+    void release() { q.release(); par.release(); cand.release(); img.release(); }
 };
 
 struct rp_ctx {
@@ -791,22 +793,36 @@ bool nn_mfma_params(const double* lo, const double* hi, NnMfma* P) {
 }
 
 template <int RB>
-void launch_nn_mfma(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, const double* tree, int64_t T) {
+void launch_nn_mfma(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, const double* tree, const h8* img,
+                    int64_t T) {
     const int64_t per_block = (int64_t)NNM_WAVES * 16 * RB;
     const int64_t qblocks = (n + per_block - 1) / per_block;
     const int64_t stages = (T + NNM_STAGE - 1) / NNM_STAGE;
     const int64_t want = std::max<int64_t>(1, (1024 + qblocks - 1) / qblocks);   // >= 1024 blocks
-    const int64_t S0 = std::min<int64_t>(want, stages);
+    // ranges of >= 32 stages (2,048 nodes): a range's first stages hold most of its
+    // threshold updates (exact-path rounds), which a longer range amortises
+    const int64_t S0 = std::max<int64_t>(1, std::min<int64_t>(want, stages / 32));
     const int64_t chunk = ((stages + S0 - 1) / S0) * NNM_STAGE;
     const int S = (int)((T + chunk - 1) / chunk);
     c->nn_part.ensure((size_t)S * n);
-    hipLaunchKernelGGL((k_nn_mfma<RB>), dim3((unsigned)qblocks, (unsigned)S), dim3(64 * NNM_WAVES), 0, c->stream, qx,
-                       n, Q.status, Q.t0, tree, T, chunk, c->nnm, c->nn_part.p);
+    hipLaunchKernelGGL((k_nn_mfma<RB>), dim3((unsigned)(qblocks * S)), dim3(64 * NNM_WAVES), 0, c->stream, qx, n,
+                       Q.status, Q.t0, tree, img, T, chunk, qblocks, c->nnm, c->nn_part.p);
     c->nn_S = S;
 }
 
-bool nn_split(rp_ctx* c, const NnQuery& Q, int64_t n, const double* tree, int64_t T, int32_t* out,
-              bool force = false) {
+// images of tree nodes [t.n_img, T) for the matrix-core search (once per node and plan)
+const h8* tree_images(rp_ctx* c, Tree& t, int64_t T) {
+    if (t.n_img < T) {
+        t.img.ensure((size_t)t.q.n / NQ * 4);
+        hipLaunchKernelGGL(k_nn_image, dim3(blocks_for((T - t.n_img) * 4, 256)), dim3(256), 0, c->stream,
+                           (const double*)t.q.p, t.n_img, T, c->nnm, t.img.p);
+        t.n_img = T;
+    }
+    return t.img.p;
+}
+
+bool nn_split(rp_ctx* c, const NnQuery& Q, int64_t n, Tree& tr, int64_t T, int32_t* out, bool force = false) {
+    const double* tree = tr.q.p;
     if (n <= 0 || T <= 0) return false;
     int mode = -1;
     if (const char* e = std::getenv("RBE_NN_SPLIT"))
@@ -825,10 +841,11 @@ bool nn_split(rp_ctx* c, const NnQuery& Q, int64_t n, const double* tree, int64_
             hipLaunchKernelGGL(k_nn_queries, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, Q, n, c->nn_qx.p);
             qx = c->nn_qx.p;
         }
+        const h8* img = tree_images(c, tr, T);
         const int ps = prof_begin(c, c->stream);
-        if (mfma_rb >= 8) launch_nn_mfma<8>(c, qx, n, Q, tree, T);
-        else if (mfma_rb >= 2) launch_nn_mfma<4>(c, qx, n, Q, tree, T);
-        else launch_nn_mfma<1>(c, qx, n, Q, tree, T);
+        if (mfma_rb >= 8) launch_nn_mfma<8>(c, qx, n, Q, tree, img, T);
+        else if (mfma_rb >= 2) launch_nn_mfma<4>(c, qx, n, Q, tree, img, T);
+        else launch_nn_mfma<1>(c, qx, n, Q, tree, img, T);
         hipLaunchKernelGGL(k_nn_reduce, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream,
                            (const DI2*)c->nn_part.p, n, c->nn_S, Q.status, Q.t0, out);
         HIP_TRY(hipGetLastError());
@@ -941,6 +958,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         t.par.ensure(cap);
         t.cand.ensure(cap);
         t.n = 0;
+        t.n_img = 0;
     }
     const int64_t ne = std::max<int64_t>({PMAX + 2, ((BMAX + world - 1) / world) * cmax, (int64_t)SPMAX * SPMAX / 2,
                                           (std::min<int64_t>(BMAX, FUSE_MAX) + 2) * (cmax + 1),
@@ -1017,7 +1035,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     // first REACHED sample; the trees do not depend on it (the oracle appends up to
     // that sample whatever the split). RBE_PLAN_CHUNK / RBE_CHUNK_GROWTH override it
     // (tests, A/B).
-    int64_t chunk0 = p.chunk > 0 ? p.chunk : p.chunk < 0 ? INT64_MAX : 4096;
+    int64_t chunk0 = p.chunk > 0 ? p.chunk : p.chunk < 0 ? INT64_MAX : 256;
     if (const char* e = std::getenv("RBE_PLAN_CHUNK"))
         if (*e) chunk0 = std::atoll(e) > 0 ? std::atoll(e) : INT64_MAX;
     if (chunk0 != INT64_MAX) chunk0 = ((chunk0 + world - 1) / world) * world;
@@ -1249,13 +1267,13 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         q1.bd = bd;
         q1.range = p.range;
         const bool big_b = (double)n * (double)snap_B >= (double)(1 << 24);
-        if (!nn_split(c, q1, n, spec_A->q.p, snap_A, c->near_.p, big_b)) return;
+        if (!nn_split(c, q1, n, *spec_A, snap_A, c->near_.p, big_b)) return;
         nin = c->near_.p;
         NnQuery q2 = q1;
         q2.kind = NNQ_STEER;
         q2.A = spec_A->q.p;
         q2.near = c->near_.p;
-        if (nn_split(c, q2, n, spec_B->q.p, snap_B, c->yv.p)) yin = c->yv.p;
+        if (nn_split(c, q2, n, *spec_B, snap_B, c->yv.p)) yin = c->yv.p;
     };
     int solved = 0;
     int32_t s_node = -1, g_node = -1;
@@ -1280,7 +1298,14 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         // ordered sub-batches of the iteration's samples: chunk0, x chunk_growth, ...;
         // the iteration ends after the sub-batch holding the first REACHED sample
         int64_t C = std::min(B, chunk0);
-        for (int64_t done = 0; done < B && !solved && !stop; done += C, C = std::min(B - done, C * chunk_growth)) {
+        // next sub-batch: x chunk_growth, but at least a quarter of what is left, so an
+        // iteration that does not solve runs at most ~4 sub-batches (each one a round
+        // trip and nearest-node launches over the whole snapshot)
+        auto next_chunk = [&](int64_t cur, int64_t left) {
+            const int64_t quarter = ((left / 4 + world - 1) / world) * world;
+            return std::min(left, std::max(cur * chunk_growth, quarter));
+        };
+        for (int64_t done = 0; done < B && !solved && !stop; done += C, C = next_chunk(C, B - done)) {
             C = std::min(C, B - done);
             const uint64_t g0 = gbase + (uint64_t)done;
             const int64_t An = A.n, Bn = Bt.n;   // append positions of this sub-batch
@@ -1447,7 +1472,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             qe.g0 = g0;
             qe.i0 = 0;
             qe.bd = bd;
-            const bool esplit = nn_split(c, qe, C, A.q.p, TA, c->near_.p);
+            const bool esplit = nn_split(c, qe, C, A, TA, c->near_.p);
             const int pn1 = prof_begin(c, c->stream);
             hipLaunchKernelGGL(k_ext_nn, dim3(blocks_for(C, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
                                p.seed, g0, (int64_t)0, C, bd, p.range, p.resolution, a_start, c->efrom.p, c->eto.p,
@@ -1489,7 +1514,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             qc.TA0 = An;
             qc.t0 = 0;
             qc.status = status;   // accepted extensions (ST_NACC), on the device
-            const bool csplit = nn_split(c, qc, C, Bt.q.p, TB, c->yv.p);
+            const bool csplit = nn_split(c, qc, C, Bt, TB, c->yv.p);
             const int pn2 = prof_begin(c, c->stream);
             hipLaunchKernelGGL(k_conn_nn, dim3(blocks_for(C, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, An,
                                (int64_t)0, C, Bt.q.p, TB, p.range, p.resolution, cmax, a_start, c->efrom.p,
@@ -2200,6 +2225,15 @@ int rp_ik(rp_ctx* c, int32_t n_targets, const double* pos, const double* quat, c
     RP_GUARD_END(c)
 }
 
+#ifdef RP_NN_COUNT
+// diagnostic builds: the matrix-core search's counters (rp_nn.h g_nncount), then reset
+int rp_debug_nncount(unsigned long long* out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_nncount), sizeof(unsigned long long) * 4) != hipSuccess) return -1;
+    const unsigned long long z[4] = {0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_nncount), z, sizeof z) == hipSuccess ? 0 : -1;
+}
+#endif
+
 #ifdef RP_STAMPS
 // diagnostic builds: copy the k_validity wave stamps (STAMP_WAVES x STAMP_K) out
 int rp_debug_stamps(unsigned long long* out, int64_t n) {
@@ -2270,9 +2304,15 @@ int rp_selftest_nn(rp_ctx* c, const double* q, int64_t n, const double* tree, in
             c->err = "bounds out of the matrix-core filter's range";
             return RP_ERR_ARG;
         }
-        if (mode >= 8) launch_nn_mfma<8>(c, dq.p, n, Q, dt.p, T);
-        else if (mode >= 2) launch_nn_mfma<4>(c, dq.p, n, Q, dt.p, T);
-        else launch_nn_mfma<1>(c, dq.p, n, Q, dt.p, T);
+        DevBuf<h8> dimg;
+        dimg.ensure((size_t)T * 4);
+        hipLaunchKernelGGL(k_nn_image, dim3(blocks_for(T * 4, 256)), dim3(256), 0, c->stream, (const double*)dt.p,
+                           (int64_t)0, T, c->nnm, dimg.p);
+        if (mode >= 8) launch_nn_mfma<8>(c, dq.p, n, Q, dt.p, dimg.p, T);
+        else if (mode >= 2) launch_nn_mfma<4>(c, dq.p, n, Q, dt.p, dimg.p, T);
+        else launch_nn_mfma<1>(c, dq.p, n, Q, dt.p, dimg.p, T);
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        dimg.release();
         hipLaunchKernelGGL(k_nn_reduce, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream,
                            (const DI2*)c->nn_part.p, n, c->nn_S, (const int*)nullptr, (int64_t)0, dout.p);
     }

@@ -40,10 +40,17 @@ struct NnMfma {
 constexpr int NNM_WAVES = 4;    // waves per block, each with its own queries
 constexpr int NNM_STAGE = 64;   // nodes per LDS stage: 4 column tiles of 16, 16 per wave to build
 constexpr int NNM_IMG = 40;     // f16 per node image row: 32 slots + 8 pad (80 B rows spread LDS banks)
+constexpr int NNM_SEEDS = 8;    // nodes per range evaluated exactly before the scan (threshold seeds)
 
+// v = hi + lo to ~2^-22 |v|: through f32 (hardware conversions; an f64 -> f16
+// conversion has no instruction and compiles to a ~60-instruction correctly rounded
+// sequence): |v - vf| <= 2^-24 |v|, vf - hi is exact in f32, |vf - hi - lo| <= 2^-11
+// |vf - hi| <= 2^-22 |vf| (or half an f16 subnormal step) — the representation error
+// the filter's margin is sized for (rp_lib.hip nn_mfma_params)
 __device__ __forceinline__ void split16(double v, _Float16& hi, _Float16& lo) {
-    hi = (_Float16)v;
-    lo = (_Float16)(v - (double)hi);   // (v - hi is exact in f64)
+    const float vf = (float)v;
+    hi = (_Float16)vf;
+    lo = (_Float16)(vf - (float)hi);
 }
 
 // LDS ordering between the lanes of one wave (stores, then other lanes' loads)
@@ -111,15 +118,51 @@ __device__ __forceinline__ h8 b_frag(const NnMfma& P, const double* y, int ch) {
     return h8{yl[6], yl[7], yl[8], gh, gl, h2, h2, z};
 }
 
+// B operand images of tree nodes [t0, t1): img[node][32] f16 (64 B), made once per
+// node and plan (the searches read them; rp_lib.hip keeps a per-tree count)
+__global__ void k_nn_image(const double* __restrict__ tree, int64_t t0, int64_t t1, NnMfma P, h8* __restrict__ img) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t node = t0 + (i >> 2);
+    const int ch = (int)(i & 3);
+    if (node >= t1) return;
+    double y[NQ];
+#pragma unroll
+    for (int d = 0; d < NQ; ++d) y[d] = tree[node * NQ + d];
+    img[node * 4 + ch] = b_frag(P, y, ch);
+}
+
 // Nearest node of each query over tree range [y * chunk, (y + 1) * chunk) ->
 // part[y * n + q] (exact distance, index; index -1: no node). Queries: qx (n x 9
 // f64); status (NNQ_ROWS): n = min(n, status[0] - t0). RB row blocks of 16 queries
 // per wave.
+// Grid: 1-D, qblocks x (tree ranges) blocks. Blocks are remapped so that each group
+// of blocks sharing an XCD (blockIdx % 8 labels them, cdna_hip_programming.md T1,
+// the bijective form) takes a contiguous run of (range, query block) pairs: the
+// blocks of one tree range sit on one XCD and its L2 holds that range (the tree's
+// 72 B/node are re-read by every query block).
+__device__ __forceinline__ void nn_block_coords(int64_t qblocks, int64_t* qb, int64_t* y) {
+    const int64_t nwg = (int64_t)gridDim.x, lid = (int64_t)blockIdx.x;
+    const int64_t q = nwg / 8, r = nwg % 8, xcd = lid % 8;
+    const int64_t wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + lid / 8;
+    *y = wgid / qblocks;
+    *qb = wgid - *y * qblocks;
+}
+
+#ifdef RP_NN_COUNT
+// diagnostic builds: [0] column tiles scanned (per wave), [1] tiles that took the
+// exact path, [2] exact-path rounds, [3] passing (row, node) elements
+__device__ unsigned long long g_nncount[4];
+#define RP_NNC(i, v) do { if (lane == 0) atomicAdd(&g_nncount[i], (unsigned long long)(v)); } while (0)
+#else
+#define RP_NNC(i, v) do { } while (0)
+#endif
+
 template <int RB>
 __global__ __launch_bounds__(64 * NNM_WAVES) void k_nn_mfma(const double* __restrict__ qx, int64_t n,
                                                           const int* status, int64_t t0,
-                                                          const double* __restrict__ tree, int64_t T, int64_t chunk,
-                                                          NnMfma P, DI2* __restrict__ part) {
+                                                          const double* __restrict__ tree, const h8* __restrict__ img,
+                                                          int64_t T, int64_t chunk, int64_t qblocks, NnMfma P,
+                                                          DI2* __restrict__ part) {
     constexpr int QW = 16 * RB;   // queries per wave
     __shared__ double s_q[NNM_WAVES][QW][NQ];               // query states (exact path)
     __shared__ unsigned long long s_best[NNM_WAVES][QW];    // exact best distance (f64 bits; >= 0)
@@ -128,10 +171,12 @@ __global__ __launch_bounds__(64 * NNM_WAVES) void k_nn_mfma(const double* __rest
     __shared__ double s_node[NNM_STAGE][NQ];                // the stage's node states (exact path)
     __shared__ alignas(16) _Float16 s_img[NNM_STAGE][NNM_IMG];   // their B operand images
     if (status) n = min(n, (int64_t)status[0] - t0);
-    const int64_t qb0 = (int64_t)blockIdx.x * NNM_WAVES * QW;
+    int64_t qb, yr;
+    nn_block_coords(qblocks, &qb, &yr);
+    const int64_t qb0 = qb * NNM_WAVES * QW;
     if (qb0 >= n) return;   // whole block idle (uniform)
     const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63), ch = lane >> 4;
-    const int64_t t_lo = (int64_t)blockIdx.y * chunk, t_hi = min(T, t_lo + chunk);
+    const int64_t t_lo = yr * chunk, t_hi = min(T, t_lo + chunk);
     const int64_t qw0 = qb0 + (int64_t)w * QW;
 
     for (int i = lane; i < QW * NQ; i += 64) {
@@ -139,9 +184,31 @@ __global__ __launch_bounds__(64 * NNM_WAVES) void k_nn_mfma(const double* __rest
         const int64_t q = qw0 + r;
         s_q[w][r][d] = q < n ? qx[q * NQ + d] : 0.0;
     }
+    wave_lds_sync();
+    // seed every query's exact best with NNM_SEEDS nodes spread over the range (the
+    // exact f64 distance, lexicographic (distance, index) minimum): the filter then
+    // starts from a typical distance instead of letting every node of the first stage
+    // through to the exact path. Order does not matter: the result is the range's
+    // lexicographic minimum whatever order its nodes are evaluated in.
     for (int r = lane; r < QW; r += 64) {
-        s_best[w][r] = 0x7FF0000000000000ull;   // +inf
-        s_bi[w][r] = -1;
+        unsigned long long bb = 0x7FF0000000000000ull;   // +inf
+        int bi = -1;
+        if (qw0 + r < n) {
+            const int64_t R = t_hi - t_lo;
+#pragma unroll 1
+            for (int k = 0; k < NNM_SEEDS; ++k) {
+                const int64_t j = t_lo + (R * k) / NNM_SEEDS;
+                if (k > 0 && j == t_lo + (R * (k - 1)) / NNM_SEEDS) continue;
+                const unsigned long long db =
+                    (unsigned long long)__double_as_longlong(dist2(tree + j * NQ, &s_q[w][r][0]));
+                if (db < bb || (db == bb && (int)j < bi)) {
+                    bb = db;
+                    bi = (int)j;
+                }
+            }
+        }
+        s_best[w][r] = bb;
+        s_bi[w][r] = bi;
     }
     wave_lds_sync();
     // A fragments (row lane & 15 of each row block; k chunk ch); the threshold slots
@@ -154,27 +221,45 @@ __global__ __launch_bounds__(64 * NNM_WAVES) void k_nn_mfma(const double* __rest
         _Float16 hh, hl;
         a[rb] = a_frag(P, &s_q[w][r][0], qw0 + r < n, ch, &na[rb], &hh, &hl);
         curb[rb] = __builtin_inf();
+        const double b0 = __longlong_as_double((long long)s_best[w][r]);
+        if (ch == 3 && qw0 + r < n && b0 < 1e300) {   // the seeded threshold
+            curb[rb] = b0;
+            thr_slots(P, b0, na[rb], hh, hl);
+            a[rb][5] = hh;
+            a[rb][6] = hl;
+        }
     }
-    const int jn = w * 16 + (lane & 15);   // the node of the stage this lane builds
-    double nx[NQ];
-    {
-        const int64_t j = t_lo + jn;
+    // staging: lane (w, l) copies image chunk ch of node w * 16 + (l & 15) and three
+    // of the stage's 576 f64 node words; the next stage's are loaded during this
+    // stage's MFMAs
+    const int jn = w * 16 + (lane & 15);
+    const int tid = (int)threadIdx.x;
+    constexpr int NW = NNM_STAGE * NQ;   // f64 words of a stage
+    h8 nimg;
+    double nw[3];
+    auto fetch = [&](int64_t b) {
+        const int64_t j = b + jn;
+        const h8 z = {};
+        nimg = j < t_hi ? img[j * 4 + ch] : z;
+        const int64_t lim = (min(t_hi, b + NNM_STAGE) - b) * NQ;
 #pragma unroll
-        for (int d = 0; d < NQ; ++d) nx[d] = j < t_hi ? tree[j * NQ + d] : 0.0;
-    }
+        for (int k = 0; k < 3; ++k) {
+            const int o = tid + 256 * k;
+            nw[k] = (o < NW && o < lim) ? tree[b * NQ + o] : 0.0;
+        }
+    };
+    fetch(t_lo);
     const f4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
     for (int64_t base = t_lo; base < t_hi; base += NNM_STAGE) {
         const int cnt = (int)min((int64_t)NNM_STAGE, t_hi - base);
         __syncthreads();   // the previous stage is consumed
-        *reinterpret_cast<h8*>(&s_img[jn][ch * 8]) = b_frag(P, nx, ch);
-        if (ch == 0)
+        *reinterpret_cast<h8*>(&s_img[jn][ch * 8]) = nimg;
 #pragma unroll
-            for (int d = 0; d < NQ; ++d) s_node[jn][d] = nx[d];
-        {   // next stage's node, in flight during this stage's MFMAs
-            const int64_t j = base + NNM_STAGE + jn;
-#pragma unroll
-            for (int d = 0; d < NQ; ++d) nx[d] = j < t_hi ? tree[j * NQ + d] : 0.0;
+        for (int k = 0; k < 3; ++k) {
+            const int o = tid + 256 * k;
+            if (o < NW) (&s_node[0][0])[o] = nw[k];
         }
+        if (base + NNM_STAGE < t_hi) fetch(base + NNM_STAGE);
         __syncthreads();
 #pragma unroll 1
         for (int ct = 0; ct < NNM_STAGE / 16; ++ct) {
@@ -190,7 +275,9 @@ __global__ __launch_bounds__(64 * NNM_WAVES) void k_nn_mfma(const double* __rest
 #pragma unroll
                 for (int rb = 0; rb < RB; ++rb) m = fmaxf(m, fmaxf(fmaxf(acc[rb][0], acc[rb][1]), fmaxf(acc[rb][2], acc[rb][3])));
             }
+            RP_NNC(0, 1);
             if (!__any(m >= 0.0f)) continue;
+            RP_NNC(1, 1);
             // ---- exact path: the passing (row, node) pairs, in rounds of one per lane
             unsigned pm = 0;
             if (col < cnt) {
@@ -200,7 +287,15 @@ __global__ __launch_bounds__(64 * NNM_WAVES) void k_nn_mfma(const double* __rest
                     for (int e = 0; e < 4; ++e) pm |= (acc[rb][e] >= 0.0f ? 1u : 0u) << (rb * 4 + e);
             }
             const int node = (int)(base + col);
+#ifdef RP_NN_COUNT
+            {
+                unsigned tot = __popc(pm);
+                for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+                RP_NNC(3, tot);
+            }
+#endif
             while (__any(pm != 0)) {
+                RP_NNC(2, 1);
                 const bool has = pm != 0;
                 const int e = has ? __builtin_ctz(pm) : 0;
                 pm &= pm - 1;
@@ -242,7 +337,7 @@ __global__ __launch_bounds__(64 * NNM_WAVES) void k_nn_mfma(const double* __rest
     for (int r = lane; r < QW; r += 64) {
         const int64_t q = qw0 + r;
         if (q < n)
-            part[(int64_t)blockIdx.y * n + q] =
+            part[yr * n + q] =
                 DI2{__longlong_as_double((long long)s_best[w][r]), s_bi[w][r], 0};
     }
 }

@@ -135,7 +135,7 @@ def test_kernel_profile_of_a_plan(gpu_ctx):
     finally:
         gpu_ctx.set_profiling(False)
     assert pr["nn_launches"] >= META["C5_well_s4"]["iterations"] and pr["edge_launches"] > 0
-    assert pr["nn_ms"] > 0 and pr["edge_ms"] > 0 and pr["nn_pairs"] > 1e9
+    assert pr["nn_ms"] > 0 and pr["edge_ms"] > 0 and pr["nn_pairs"] > 1e8
     assert pr["edge_states"] == s["states_checked"]
 
 

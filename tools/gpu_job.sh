@@ -40,7 +40,10 @@ for s in "$@"; do
     nnpmc) step nnpmc_a 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH --output-format csv -d gpurun_out/nnpmc_a -o a -- python tools/c5_profile.py pmc && step nnpmc_b 300 rocprofv3 --pmc SQ_WAVES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/nnpmc_b -o b -- python tools/c5_profile.py pmc && python tools/pmc_summary.py gpurun_out/nnpmc_a gpurun_out/nnpmc_b --kernel k_nn_part --json gpurun_out/nn_pmc.json > gpurun_out/nn_pmc.txt ;;
     c5stats) step c5stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c5stats -o kt -- python tools/c5_profile.py ;;
     nntest) step pytest_nn 600 python -u -m pytest tests/test_gpu_nn.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
-    chunks) step chunks 600 python tools/chunk_sweep.py -1 256 1024 4096 ;;
+    wellab) step wellab 600 python tools/well_ab.py ;;
+    wellprof) step wellprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/wellprof -o kt -- python tools/well_ab.py mfma=RBE_NN_MFMA:4,RBE_PLAN_CHUNK:-1 part=RBE_NN_MFMA:0,RBE_PLAN_CHUNK:-1 ;;
+    nncount) step nncount 300 python tools/nn_count.py abvariants/lib_nncount.so 4 8 ;;
+    chunks) step chunks 600 python tools/chunk_sweep.py -1 64 256 1024 ;;
     ptests) step pytest_plan 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
     procs) step pytest_procs 900 python -u -m pytest tests/test_gpu_group_procs.py -m gpu -x -v --timeout 400 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;

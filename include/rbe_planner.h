@@ -127,8 +127,9 @@ typedef struct rp_plan_params {
                                but at least a quarter of what is left — and ends after the
                                sub-batch holding the first REACHED sample (the trees keep
                                the appends up to that sample, DESIGN.md §4 step 5, whatever
-                               the sub-batching). 0 = default 256; < 0 = the whole
-                               iteration as one batch                                     */
+                               the sub-batching); on trees of >= 4,096 nodes the first
+                               sub-batch is at least a quarter of the iteration. 0 =
+                               default 64; < 0 = the whole iteration as one batch        */
 } rp_plan_params;
 
 /* rp_ik parameters (defaults follow Genesis inverse_kinematics). Zero / negative

@@ -104,5 +104,5 @@ def make_params(seed=0, batch=4096, range_=0.0, resolution=0.0, timeout_s=5.0, m
     p.simplify = 1 if simplify else 0
     p.tree_capacity = int(tree_capacity)
     p.straight_first = 0 if straight_first else -1   # 0 = default (on with simplification)
-    p.chunk = int(chunk)   # first sub-batch of an iteration (execution only; 0 = 256, < 0 = none)
+    p.chunk = int(chunk)   # first sub-batch of an iteration (execution only; 0 = 64, < 0 = none)
     return p

@@ -792,10 +792,11 @@ bool nn_mfma_params(const double* lo, const double* hi, NnMfma* P) {
     return true;
 }
 
-template <int RB>
-void launch_nn_mfma(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, const double* tree, const h8* img,
-                    int64_t T) {
-    const int64_t per_block = (int64_t)NNM_WAVES * 16 * RB;
+template <int RB, int W>
+void launch_nn_mfma_w(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, const double* tree, const h8* img,
+                      int64_t T) {
+    constexpr int64_t NNM_STAGE = 64;   // (range sizing: 64-node units)
+    const int64_t per_block = (int64_t)W * 16 * RB;
     const int64_t qblocks = (n + per_block - 1) / per_block;
     const int64_t stages = (T + NNM_STAGE - 1) / NNM_STAGE;
     const int64_t want = std::max<int64_t>(1, (1024 + qblocks - 1) / qblocks);   // >= 1024 blocks
@@ -805,9 +806,28 @@ void launch_nn_mfma(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, co
     const int64_t chunk = ((stages + S0 - 1) / S0) * NNM_STAGE;
     const int S = (int)((T + chunk - 1) / chunk);
     c->nn_part.ensure((size_t)S * n);
-    hipLaunchKernelGGL((k_nn_mfma<RB>), dim3((unsigned)(qblocks * S)), dim3(64 * NNM_WAVES), 0, c->stream, qx, n,
+    hipLaunchKernelGGL((k_nn_mfma<RB, W>), dim3((unsigned)(qblocks * S)), dim3(64 * W), 0, c->stream, qx, n,
                        Q.status, Q.t0, tree, img, T, chunk, qblocks, c->nnm, c->nn_part.p);
     c->nn_S = S;
+}
+// waves per block: RBE_NN_WAVES (1, 2, 4)
+template <int RB>
+void launch_nn_mfma(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, const double* tree, const h8* img,
+                    int64_t T) {
+    int w = 4;
+    if (const char* e = std::getenv("RBE_NN_WAVES"))
+        if (*e) w = std::atoi(e);
+    if (w == 1) launch_nn_mfma_w<RB, 1>(c, qx, n, Q, tree, img, T);
+    else if (w == 2) launch_nn_mfma_w<RB, 2>(c, qx, n, Q, tree, img, T);
+    else launch_nn_mfma_w<RB, 4>(c, qx, n, Q, tree, img, T);
+}
+
+// whether n queries against T nodes take the split search: it pays ~4 launches; the
+// fused kernels give each block 256 queries against the whole tree, so a few queries
+// against a large tree would leave the chip idle
+bool nn_big(int64_t n, int64_t T) {
+    const double pairs = (double)n * (double)T;
+    return pairs >= (double)(1 << 24) || (T >= 8192 && pairs >= (double)(1 << 20));
 }
 
 // images of tree nodes [t.n_img, T) for the matrix-core search (once per node and plan)
@@ -827,7 +847,7 @@ bool nn_split(rp_ctx* c, const NnQuery& Q, int64_t n, Tree& tr, int64_t T, int32
     int mode = -1;
     if (const char* e = std::getenv("RBE_NN_SPLIT"))
         if (*e) mode = std::atoi(e) != 0;
-    if (mode == 0 || (mode < 0 && !force && (double)n * (double)T < (double)(1 << 24))) return false;
+    if (mode == 0 || (mode < 0 && !force && !nn_big(n, T))) return false;
     // the matrix-core search (rp_nn.h) unless RBE_NN_MFMA=0 (the packed-f32 k_nn_part)
     int mfma_rb = 4;   // (read per search: large-tree searches take milliseconds)
     if (const char* e = std::getenv("RBE_NN_MFMA"))
@@ -844,7 +864,8 @@ bool nn_split(rp_ctx* c, const NnQuery& Q, int64_t n, Tree& tr, int64_t T, int32
         const h8* img = tree_images(c, tr, T);
         const int ps = prof_begin(c, c->stream);
         if (mfma_rb >= 8) launch_nn_mfma<8>(c, qx, n, Q, tree, img, T);
-        else if (mfma_rb >= 2) launch_nn_mfma<4>(c, qx, n, Q, tree, img, T);
+        else if (mfma_rb >= 4) launch_nn_mfma<4>(c, qx, n, Q, tree, img, T);
+        else if (mfma_rb >= 2) launch_nn_mfma<2>(c, qx, n, Q, tree, img, T);
         else launch_nn_mfma<1>(c, qx, n, Q, tree, img, T);
         hipLaunchKernelGGL(k_nn_reduce, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream,
                            (const DI2*)c->nn_part.p, n, c->nn_S, Q.status, Q.t0, out);
@@ -1035,11 +1056,14 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     // first REACHED sample; the trees do not depend on it (the oracle appends up to
     // that sample whatever the split). RBE_PLAN_CHUNK / RBE_CHUNK_GROWTH override it
     // (tests, A/B).
-    int64_t chunk0 = p.chunk > 0 ? p.chunk : p.chunk < 0 ? INT64_MAX : 256;
+    int64_t chunk0 = p.chunk > 0 ? p.chunk : p.chunk < 0 ? INT64_MAX : 64;
     if (const char* e = std::getenv("RBE_PLAN_CHUNK"))
         if (*e) chunk0 = std::atoll(e) > 0 ? std::atoll(e) : INT64_MAX;
     if (chunk0 != INT64_MAX) chunk0 = ((chunk0 + world - 1) / world) * world;
     int64_t chunk_growth = 4;
+    int64_t chunk_tree = 4096;
+    if (const char* e = std::getenv("RBE_CHUNK_TREE"))
+        if (*e) chunk_tree = std::max<int64_t>(1, std::atoll(e));
     if (const char* e = std::getenv("RBE_CHUNK_GROWTH"))
         if (*e) chunk_growth = std::max<int64_t>(1, std::atoll(e));
     const int64_t C00 = std::min<int64_t>(p.batch_min, chunk0);   // the plan's first sub-batch
@@ -1266,7 +1290,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         q1.i0 = 0;
         q1.bd = bd;
         q1.range = p.range;
-        const bool big_b = (double)n * (double)snap_B >= (double)(1 << 24);
+        const bool big_b = nn_big(n, snap_B);
         if (!nn_split(c, q1, n, *spec_A, snap_A, c->near_.p, big_b)) return;
         nin = c->near_.p;
         NnQuery q2 = q1;
@@ -1297,7 +1321,11 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         bool stop = false;
         // ordered sub-batches of the iteration's samples: chunk0, x chunk_growth, ...;
         // the iteration ends after the sub-batch holding the first REACHED sample
+        // on large trees every sub-batch pays nearest-node searches over the whole
+        // snapshot (their setup and threshold warm-up), so the first sub-batch is at
+        // least a quarter of the iteration there (RBE_CHUNK_TREE: the node count)
         int64_t C = std::min(B, chunk0);
+        if (TA + TB >= chunk_tree) C = std::min(B, std::max(C, ((B / 4 + world - 1) / world) * world));
         // next sub-batch: x chunk_growth, but at least a quarter of what is left, so an
         // iteration that does not solve runs at most ~4 sub-batches (each one a round
         // trip and nearest-node launches over the whole snapshot)
@@ -2309,7 +2337,8 @@ int rp_selftest_nn(rp_ctx* c, const double* q, int64_t n, const double* tree, in
         hipLaunchKernelGGL(k_nn_image, dim3(blocks_for(T * 4, 256)), dim3(256), 0, c->stream, (const double*)dt.p,
                            (int64_t)0, T, c->nnm, dimg.p);
         if (mode >= 8) launch_nn_mfma<8>(c, dq.p, n, Q, dt.p, dimg.p, T);
-        else if (mode >= 2) launch_nn_mfma<4>(c, dq.p, n, Q, dt.p, dimg.p, T);
+        else if (mode >= 4) launch_nn_mfma<4>(c, dq.p, n, Q, dt.p, dimg.p, T);
+        else if (mode >= 2) launch_nn_mfma<2>(c, dq.p, n, Q, dt.p, dimg.p, T);
         else launch_nn_mfma<1>(c, dq.p, n, Q, dt.p, dimg.p, T);
         HIP_TRY(hipStreamSynchronize(c->stream));
         dimg.release();

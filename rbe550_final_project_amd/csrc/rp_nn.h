@@ -37,8 +37,8 @@ struct NnMfma {
     double thr0;    // threshold while a query has no exact best (every node passes)
 };
 
-constexpr int NNM_WAVES = 4;    // waves per block, each with its own queries
-constexpr int NNM_STAGE = 64;   // nodes per LDS stage: 4 column tiles of 16, 16 per wave to build
+// waves per block (template W): each with its own queries; a stage is W column tiles
+// of 16 nodes (16 W nodes), each wave building the image rows of one tile
 constexpr int NNM_IMG = 40;     // f16 per node image row: 32 slots + 8 pad (80 B rows spread LDS banks)
 constexpr int NNM_SEEDS = 8;    // nodes per range evaluated exactly before the scan (threshold seeds)
 
@@ -157,23 +157,24 @@ __device__ unsigned long long g_nncount[4];
 #define RP_NNC(i, v) do { } while (0)
 #endif
 
-template <int RB>
-__global__ __launch_bounds__(64 * NNM_WAVES) void k_nn_mfma(const double* __restrict__ qx, int64_t n,
+template <int RB, int W>
+__global__ __launch_bounds__(64 * W) void k_nn_mfma(const double* __restrict__ qx, int64_t n,
                                                           const int* status, int64_t t0,
                                                           const double* __restrict__ tree, const h8* __restrict__ img,
                                                           int64_t T, int64_t chunk, int64_t qblocks, NnMfma P,
                                                           DI2* __restrict__ part) {
     constexpr int QW = 16 * RB;   // queries per wave
-    __shared__ double s_q[NNM_WAVES][QW][NQ];               // query states (exact path)
-    __shared__ unsigned long long s_best[NNM_WAVES][QW];    // exact best distance (f64 bits; >= 0)
-    __shared__ int s_bi[NNM_WAVES][QW];                     // its node (lowest index among equal)
-    __shared__ int s_ti[NNM_WAVES][QW];                     // a round's lowest node at the new best
+    constexpr int NNM_STAGE = 16 * W;   // nodes per stage
+    __shared__ double s_q[W][QW][NQ];                       // query states (exact path)
+    __shared__ unsigned long long s_best[W][QW];            // exact best distance (f64 bits; >= 0)
+    __shared__ int s_bi[W][QW];                             // its node (lowest index among equal)
+    __shared__ int s_ti[W][QW];                             // a round's lowest node at the new best
     __shared__ double s_node[NNM_STAGE][NQ];                // the stage's node states (exact path)
     __shared__ alignas(16) _Float16 s_img[NNM_STAGE][NNM_IMG];   // their B operand images
     if (status) n = min(n, (int64_t)status[0] - t0);
     int64_t qb, yr;
     nn_block_coords(qblocks, &qb, &yr);
-    const int64_t qb0 = qb * NNM_WAVES * QW;
+    const int64_t qb0 = qb * W * QW;
     if (qb0 >= n) return;   // whole block idle (uniform)
     const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63), ch = lane >> 4;
     const int64_t t_lo = yr * chunk, t_hi = min(T, t_lo + chunk);
@@ -244,7 +245,7 @@ __global__ __launch_bounds__(64 * NNM_WAVES) void k_nn_mfma(const double* __rest
         const int64_t lim = (min(t_hi, b + NNM_STAGE) - b) * NQ;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            const int o = tid + 256 * k;
+            const int o = tid + 64 * W * k;
             nw[k] = (o < NW && o < lim) ? tree[b * NQ + o] : 0.0;
         }
     };
@@ -256,13 +257,13 @@ __global__ __launch_bounds__(64 * NNM_WAVES) void k_nn_mfma(const double* __rest
         *reinterpret_cast<h8*>(&s_img[jn][ch * 8]) = nimg;
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
-            const int o = tid + 256 * k;
+            const int o = tid + 64 * W * k;
             if (o < NW) (&s_node[0][0])[o] = nw[k];
         }
         if (base + NNM_STAGE < t_hi) fetch(base + NNM_STAGE);
         __syncthreads();
 #pragma unroll 1
-        for (int ct = 0; ct < NNM_STAGE / 16; ++ct) {
+        for (int ct = 0; ct < W; ++ct) {
             if (ct * 16 >= cnt) break;   // (uniform)
             const int col = ct * 16 + (lane & 15);
             const h8 b = *reinterpret_cast<const h8*>(&s_img[col][ch * 8]);

@@ -37,13 +37,13 @@ for s in "$@"; do
     pmc) step pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH --output-format csv -d gpurun_out/pmc_sq -o sq -- python bench.py --steps 3 --warmup 1 --no-cpu --no-plan --no-configs && step pmc_sq2 600 rocprofv3 --pmc SQ_WAVES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_sq2 -o sq2 -- python bench.py --steps 3 --warmup 1 --no-cpu --no-plan --no-configs && step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o f -- python bench.py --steps 3 --warmup 1 --no-cpu --no-plan --no-configs && step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o w -- python bench.py --steps 3 --warmup 1 --no-cpu --no-plan --no-configs ;;
     pmcsum) python tools/pmc_summary.py gpurun_out/pmc_sq gpurun_out/pmc_sq2 --json gpurun_out/validity_pmc_sq.json > gpurun_out/validity_pmc_sq.txt && python tools/make_pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write 4194304 gpurun_out/pmc_validity.json > /dev/null && echo pmcsum ok ;;
     c5prof) step c5prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c5prof -o kt -- python tools/c5_profile.py ;;
-    nnpmc) step nnpmc_a 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH --output-format csv -d gpurun_out/nnpmc_a -o a -- python tools/c5_profile.py pmc && step nnpmc_b 300 rocprofv3 --pmc SQ_WAVES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/nnpmc_b -o b -- python tools/c5_profile.py pmc && python tools/pmc_summary.py gpurun_out/nnpmc_a gpurun_out/nnpmc_b --kernel k_nn_part --json gpurun_out/nn_pmc.json > gpurun_out/nn_pmc.txt ;;
+    nnpmc) step nnpmc_a 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH --output-format csv -d gpurun_out/nnpmc_a -o a -- python tools/c5_profile.py pmc && step nnpmc_b 300 rocprofv3 --pmc SQ_WAVES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/nnpmc_b -o b -- python tools/c5_profile.py pmc && python tools/pmc_summary.py gpurun_out/nnpmc_a gpurun_out/nnpmc_b --kernel k_nn_mfma --json gpurun_out/nn_pmc.json > gpurun_out/nn_pmc.txt ;;
     c5stats) step c5stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c5stats -o kt -- python tools/c5_profile.py ;;
     nntest) step pytest_nn 600 python -u -m pytest tests/test_gpu_nn.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     wellab) step wellab 600 python tools/well_ab.py ;;
     wellprof) step wellprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/wellprof -o kt -- python tools/well_ab.py mfma=RBE_NN_MFMA:4,RBE_PLAN_CHUNK:-1 part=RBE_NN_MFMA:0,RBE_PLAN_CHUNK:-1 ;;
     nncount) step nncount 300 python tools/nn_count.py abvariants/lib_nncount.so 4 8 ;;
-    chunks) step chunks 600 python tools/chunk_sweep.py -1 64 256 1024 ;;
+    chunks) step chunks 600 python tools/chunk_sweep.py -1 16 64 256 ;;
     ptests) step pytest_plan 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
     procs) step pytest_procs 900 python -u -m pytest tests/test_gpu_group_procs.py -m gpu -x -v --timeout 400 --timeout-method thread ;;
     *) echo "unknown step $s"; exit 2 ;;

@@ -17,9 +17,10 @@ from rbe550_final_project_amd.native import Context  # noqa: E402
 CONFIGS = {
     "part_whole": {"RBE_NN_MFMA": "0", "RBE_PLAN_CHUNK": "-1"},
     "mfma4_whole": {"RBE_NN_MFMA": "4", "RBE_PLAN_CHUNK": "-1"},
-    "mfma8_whole": {"RBE_NN_MFMA": "8", "RBE_PLAN_CHUNK": "-1"},
-    "mfma1_whole": {"RBE_NN_MFMA": "1", "RBE_PLAN_CHUNK": "-1"},
-    "mfma4_c4096": {"RBE_NN_MFMA": "4", "RBE_PLAN_CHUNK": "4096"},
+    "default": {},
+    "c64_tree1e9": {"RBE_PLAN_CHUNK": "64", "RBE_CHUNK_TREE": "1000000000"},
+    "c1024": {"RBE_PLAN_CHUNK": "1024"},
+    "tree65536": {"RBE_CHUNK_TREE": "65536"},
 }
 
 
@@ -36,7 +37,7 @@ def main():
     ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
     ctx.set_attached(q["attached"])
     ctx.set_profiling(True)
-    keys = ("RBE_NN_MFMA", "RBE_PLAN_CHUNK")
+    keys = ("RBE_NN_MFMA", "RBE_PLAN_CHUNK", "RBE_CHUNK_TREE", "RBE_NN_WAVES")
     for rep in range(2):   # rep 0: warm-up
         for name, env in cfgs.items():
             for k in keys:

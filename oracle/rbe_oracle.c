@@ -623,6 +623,7 @@ typedef struct {
     uint8_t* cand;   /* start tree: extension node whose connect did not reach */
     int64_t n, cap;
     kd_tree* kd;     /* sequential baseline: exact index over all n nodes (else NULL) */
+    int kd_want;     /* build the index once the tree outgrows a linear scan */
 } tree_t;
 
 static int tree_init(tree_t* t, int64_t cap) {
@@ -632,6 +633,7 @@ static int tree_init(tree_t* t, int64_t cap) {
     t->n = 0;
     t->cap = cap;
     t->kd = NULL;
+    t->kd_want = 0;
     return t->q && t->parent && t->cand;
 }
 static void tree_free(tree_t* t) {
@@ -651,10 +653,17 @@ static int64_t tree_add(tree_t* t, const double* q, int32_t parent) {
     return t->n++;
 }
 /* nearest node among the first n (ties -> lowest index); the kd index (which holds
- * exactly the tree's nodes) when the tree has one and n is all of them */
-static int32_t nearest(const tree_t* t, int64_t n, const double* x) {
+ * exactly the tree's nodes) when the tree has one and n is all of them. The index is
+ * built when a tree that wants one passes KD_MIN nodes (a linear scan is faster
+ * below), then kept up to date by tree_add. */
+#define KD_MIN 256
+static int32_t nearest(tree_t* t, int64_t n, const double* x) {
     double best = INFINITY;
     int32_t idx = -1;
+    if (t->kd_want && !t->kd && t->n > KD_MIN) {
+        t->kd = (kd_tree*)calloc(1, sizeof(kd_tree));
+        for (int64_t j = 0; j < t->n; ++j) kd_insert(t->kd, t->q, (int32_t)j);
+    }
     if (t->kd && n == t->n && t->kd->n > 0) {
         kd_search(t->kd, 0, t->q, x, &best, &idx);
         return idx;
@@ -931,10 +940,7 @@ int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], co
      * nearest-node searches (RBE_ORACLE_KD=0: the linear scan, same answers) */
     {
         const char* e = getenv("RBE_ORACLE_KD");
-        if (p.batch == 1 && world == 1 && !(e && *e == '0')) {
-            T[0].kd = (kd_tree*)calloc(1, sizeof(kd_tree));
-            T[1].kd = (kd_tree*)calloc(1, sizeof(kd_tree));
-        }
+        if (p.batch == 1 && world == 1 && !(e && *e == '0')) T[0].kd_want = T[1].kd_want = 1;
     }
     tree_add(&T[0], start, -1);
     tree_add(&T[1], goal, -1);

@@ -802,7 +802,9 @@ void launch_nn_mfma_w(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, 
     const int64_t want = std::max<int64_t>(1, (1024 + qblocks - 1) / qblocks);   // >= 1024 blocks
     // ranges of >= 32 stages (2,048 nodes): a range's first stages hold most of its
     // threshold updates (exact-path rounds), which a longer range amortises
-    const int64_t S0 = std::max<int64_t>(1, std::min<int64_t>(want, stages / 32));
+    int64_t S0 = std::max<int64_t>(1, std::min<int64_t>(want, stages / 32));
+    if (const char* e = std::getenv("RBE_NN_RANGES"))   // (A/B: cap on the tree ranges)
+        if (*e) S0 = std::max<int64_t>(1, std::min<int64_t>(S0, std::atoll(e)));
     const int64_t chunk = ((stages + S0 - 1) / S0) * NNM_STAGE;
     const int S = (int)((T + chunk - 1) / chunk);
     c->nn_part.ensure((size_t)S * n);

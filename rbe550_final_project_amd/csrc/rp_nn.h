@@ -37,9 +37,7 @@ struct NnMfma {
     double thr0;    // threshold while a query has no exact best (every node passes)
 };
 
-// waves per block (template W): each with its own queries; a stage is W column tiles
-// of 16 nodes (16 W nodes), each wave building the image rows of one tile
-constexpr int NNM_IMG = 40;     // f16 per node image row: 32 slots + 8 pad (80 B rows spread LDS banks)
+// waves per block (template W): each with its own queries and tree stream
 constexpr int NNM_SEEDS = 8;    // nodes per range evaluated exactly before the scan (threshold seeds)
 
 // v = hi + lo to ~2^-22 |v|: through f32 (hardware conversions; an f64 -> f16
@@ -164,13 +162,10 @@ __global__ __launch_bounds__(64 * W) void k_nn_mfma(const double* __restrict__ q
                                                           int64_t T, int64_t chunk, int64_t qblocks, NnMfma P,
                                                           DI2* __restrict__ part) {
     constexpr int QW = 16 * RB;   // queries per wave
-    constexpr int NNM_STAGE = 16 * W;   // nodes per stage
     __shared__ double s_q[W][QW][NQ];                       // query states (exact path)
     __shared__ unsigned long long s_best[W][QW];            // exact best distance (f64 bits; >= 0)
     __shared__ int s_bi[W][QW];                             // its node (lowest index among equal)
     __shared__ int s_ti[W][QW];                             // a round's lowest node at the new best
-    __shared__ double s_node[NNM_STAGE][NQ];                // the stage's node states (exact path)
-    __shared__ alignas(16) _Float16 s_img[NNM_STAGE][NNM_IMG];   // their B operand images
     if (status) n = min(n, (int64_t)status[0] - t0);
     int64_t qb, yr;
     nn_block_coords(qblocks, &qb, &yr);
@@ -230,49 +225,42 @@ __global__ __launch_bounds__(64 * W) void k_nn_mfma(const double* __restrict__ q
             a[rb][6] = hl;
         }
     }
-    // staging: lane (w, l) copies image chunk ch of node w * 16 + (l & 15) and three
-    // of the stage's 576 f64 node words; the next stage's are loaded during this
-    // stage's MFMAs
-    const int jn = w * 16 + (lane & 15);
-    const int tid = (int)threadIdx.x;
-    constexpr int NW = NNM_STAGE * NQ;   // f64 words of a stage
-    h8 nimg;
-    double nw[3];
-    auto fetch = [&](int64_t b) {
-        const int64_t j = b + jn;
-        const h8 z = {};
-        nimg = j < t_hi ? img[j * 4 + ch] : z;
-        const int64_t lim = (min(t_hi, b + NNM_STAGE) - b) * NQ;
+    // Each wave streams its range's node images itself, B fragments straight from
+    // global memory (L2: the XCD-grouped blocks of a range read the same lines)
+    // prefetched PF column tiles ahead; there is no block barrier, so a wave in its
+    // exact path holds up no other wave.
+    // (Measured and not kept: the f64 states of the tile staged in LDS for the exact
+    // path, and 4-wave LDS staging of the images behind block barriers: the same
+    // rate, more registers.)
+    constexpr int PF = 4;
+    const int64_t ntiles = (t_hi - t_lo + 15) / 16;
+    const int col = lane & 15;   // this lane's column of every tile
+    const h8 hz = {};
+    h8 bq[PF];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int o = tid + 64 * W * k;
-            nw[k] = (o < NW && o < lim) ? tree[b * NQ + o] : 0.0;
-        }
-    };
-    fetch(t_lo);
+    for (int u = 0; u < PF; ++u) {
+        const int64_t j = t_lo + (int64_t)u * 16 + col;
+        bq[u] = j < t_hi ? img[j * 4 + ch] : hz;
+    }
     const f4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
-    for (int64_t base = t_lo; base < t_hi; base += NNM_STAGE) {
-        const int cnt = (int)min((int64_t)NNM_STAGE, t_hi - base);
-        __syncthreads();   // the previous stage is consumed
-        *reinterpret_cast<h8*>(&s_img[jn][ch * 8]) = nimg;
+    for (int64_t tb = 0; tb < ntiles; tb += PF) {
 #pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int o = tid + 64 * W * k;
-            if (o < NW) (&s_node[0][0])[o] = nw[k];
-        }
-        if (base + NNM_STAGE < t_hi) fetch(base + NNM_STAGE);
-        __syncthreads();
-#pragma unroll 1
-        for (int ct = 0; ct < W; ++ct) {
-            if (ct * 16 >= cnt) break;   // (uniform)
-            const int col = ct * 16 + (lane & 15);
-            const h8 b = *reinterpret_cast<const h8*>(&s_img[col][ch * 8]);
+        for (int u = 0; u < PF; ++u) {
+            const int64_t tile = tb + u;
+            if (tile >= ntiles) break;   // (uniform)
+            const h8 b = bq[u];
+            {
+                const int64_t j = t_lo + (tile + PF) * 16 + col;
+                bq[u] = j < t_hi ? img[j * 4 + ch] : hz;
+            }
+            const int64_t base = t_lo + tile * 16;
+            const bool live = base + col < t_hi;
             f4 acc[RB];
 #pragma unroll
             for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rb], b, zero, 0, 0, 0);
             // this lane's column: acc[rb][e] = row rb * 16 + 4 ch + e
             float m = -1.0f;
-            if (col < cnt) {
+            if (live) {
 #pragma unroll
                 for (int rb = 0; rb < RB; ++rb) m = fmaxf(m, fmaxf(fmaxf(acc[rb][0], acc[rb][1]), fmaxf(acc[rb][2], acc[rb][3])));
             }
@@ -281,7 +269,7 @@ __global__ __launch_bounds__(64 * W) void k_nn_mfma(const double* __restrict__ q
             RP_NNC(1, 1);
             // ---- exact path: the passing (row, node) pairs, in rounds of one per lane
             unsigned pm = 0;
-            if (col < cnt) {
+            if (live) {
 #pragma unroll
                 for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
@@ -305,7 +293,7 @@ __global__ __launch_bounds__(64 * W) void k_nn_mfma(const double* __restrict__ q
                 if (has) {
                     prev = s_best[w][row];
                     s_ti[w][row] = 0x7fffffff;
-                    db = (unsigned long long)__double_as_longlong(dist2(&s_node[col][0], &s_q[w][row][0]));
+                    db = (unsigned long long)__double_as_longlong(dist2(tree + (int64_t)node * NQ, &s_q[w][row][0]));
                 }
                 wave_lds_sync();
                 if (has) atomicMin(&s_best[w][row], db);

@@ -15,12 +15,12 @@ from rbe550_final_project_amd import _abi, model, scenes  # noqa: E402
 from rbe550_final_project_amd.native import Context  # noqa: E402
 
 CONFIGS = {
-    "part_whole": {"RBE_NN_MFMA": "0", "RBE_PLAN_CHUNK": "-1"},
-    "mfma4_whole": {"RBE_NN_MFMA": "4", "RBE_PLAN_CHUNK": "-1"},
+    "mfma4_w4_whole": {"RBE_NN_MFMA": "4", "RBE_PLAN_CHUNK": "-1"},
+    "mfma4_w4_r1": {"RBE_NN_MFMA": "4", "RBE_PLAN_CHUNK": "-1", "RBE_NN_RANGES": "1"},
+    "mfma4_w1_r1": {"RBE_NN_MFMA": "4", "RBE_NN_WAVES": "1", "RBE_PLAN_CHUNK": "-1", "RBE_NN_RANGES": "1"},
+    "mfma8_w4_r1": {"RBE_NN_MFMA": "8", "RBE_PLAN_CHUNK": "-1", "RBE_NN_RANGES": "1"},
+    "mfma2_w4_r1": {"RBE_NN_MFMA": "2", "RBE_PLAN_CHUNK": "-1", "RBE_NN_RANGES": "1"},
     "default": {},
-    "c64_tree1e9": {"RBE_PLAN_CHUNK": "64", "RBE_CHUNK_TREE": "1000000000"},
-    "c1024": {"RBE_PLAN_CHUNK": "1024"},
-    "tree65536": {"RBE_CHUNK_TREE": "65536"},
 }
 
 
@@ -37,7 +37,7 @@ def main():
     ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
     ctx.set_attached(q["attached"])
     ctx.set_profiling(True)
-    keys = ("RBE_NN_MFMA", "RBE_PLAN_CHUNK", "RBE_CHUNK_TREE", "RBE_NN_WAVES")
+    keys = ("RBE_NN_MFMA", "RBE_PLAN_CHUNK", "RBE_CHUNK_TREE", "RBE_NN_WAVES", "RBE_NN_RANGES")
     for rep in range(2):   # rep 0: warm-up
         for name, env in cfgs.items():
             for k in keys:

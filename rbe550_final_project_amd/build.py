@@ -9,7 +9,8 @@ import sys
 _HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(_HERE, "csrc", "rp_lib.hip")
 OUT = os.path.join(_HERE, "librbe_mi355x.so")
-HEADERS = [os.path.join(_HERE, "csrc", f) for f in ("rp_kernels.h", "rp_math.h", "rp_plan_math.h", "rp_model.h")]
+# every header the library includes (a stale .so would otherwise ship to the GPU box)
+HEADERS = sorted(os.path.join(_HERE, "csrc", f) for f in os.listdir(os.path.join(_HERE, "csrc")) if f.endswith(".h"))
 HEADERS.append(os.path.join(os.path.dirname(_HERE), "include", "rbe_planner.h"))
 
 # -ffp-contract=off: no FMA contraction on host or device — the numerics contract

@@ -15,11 +15,12 @@ from rbe550_final_project_amd import _abi, model, scenes  # noqa: E402
 from rbe550_final_project_amd.native import Context  # noqa: E402
 
 CONFIGS = {
+    "part_whole": {"RBE_NN_MFMA": "0", "RBE_PLAN_CHUNK": "-1"},
     "mfma4_w4_whole": {"RBE_NN_MFMA": "4", "RBE_PLAN_CHUNK": "-1"},
+    "mfma4_w1_whole": {"RBE_NN_MFMA": "4", "RBE_NN_WAVES": "1", "RBE_PLAN_CHUNK": "-1"},
+    "mfma8_w4_whole": {"RBE_NN_MFMA": "8", "RBE_PLAN_CHUNK": "-1"},
     "mfma4_w4_r1": {"RBE_NN_MFMA": "4", "RBE_PLAN_CHUNK": "-1", "RBE_NN_RANGES": "1"},
-    "mfma4_w1_r1": {"RBE_NN_MFMA": "4", "RBE_NN_WAVES": "1", "RBE_PLAN_CHUNK": "-1", "RBE_NN_RANGES": "1"},
-    "mfma8_w4_r1": {"RBE_NN_MFMA": "8", "RBE_PLAN_CHUNK": "-1", "RBE_NN_RANGES": "1"},
-    "mfma2_w4_r1": {"RBE_NN_MFMA": "2", "RBE_PLAN_CHUNK": "-1", "RBE_NN_RANGES": "1"},
+    "mfma4_w4_r8": {"RBE_NN_MFMA": "4", "RBE_PLAN_CHUNK": "-1", "RBE_NN_RANGES": "8"},
     "default": {},
 }
 

@@ -46,6 +46,7 @@ for s in "$@"; do
     chunks) step chunks 600 python tools/chunk_sweep.py -1 16 64 256 ;;
     ptests) step pytest_plan 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
     procs) step pytest_procs 900 python -u -m pytest tests/test_gpu_group_procs.py -m gpu -x -v --timeout 400 --timeout-method thread ;;
+    small) step small 300 python tools/small_launch.py && step smallprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/smallprof -o kt -- python tools/small_launch.py "" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

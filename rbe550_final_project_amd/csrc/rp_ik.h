@@ -150,7 +150,7 @@ struct IkArgs {
 // stop below 1% of both tolerances). out: q (9), errors (2), converged flag.
 __global__ __launch_bounds__(64) void k_ik(IkArgs a, double* __restrict__ q_out, double* __restrict__ err_out,
                                            uint8_t* __restrict__ conv, float* __restrict__ q32) {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t g = (int64_t)rp_bid() * rp_bdim() + rp_tid();
     if (g >= (int64_t)a.n_targets * a.n_seeds) return;
     const int t = (int)(g / a.n_seeds), k = (int)(g - (int64_t)t * a.n_seeds);
     double q[NQ];
@@ -242,7 +242,7 @@ __global__ __launch_bounds__(64) void k_ik(IkArgs a, double* __restrict__ q_out,
 __global__ void k_ik_select(IkArgs a, const double* __restrict__ q, const double* __restrict__ err,
                             const uint8_t* __restrict__ conv, const uint8_t* __restrict__ valid,
                             double* __restrict__ q_best, int32_t* __restrict__ status) {
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    const int t = rp_bid() * rp_bdim() + rp_tid();
     if (t >= a.n_targets) return;
     const double* qi = a.init + (int64_t)t * NQ;
     int best_k = 0, best_c = 3;

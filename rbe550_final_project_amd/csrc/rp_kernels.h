@@ -16,8 +16,8 @@ namespace rp {
 
 constexpr int VBLOCK = 64;      // validity / edge block size: one wave (its LDS = its queue)
 // waves per SIMD requested from the register allocator. k_validity on cluster
-// scenes: 5 (96 VGPRs, 3 spilled in a cold path; needs the 8160-B queue of
-// QCAP 76 — 20 one-wave workgroups per CU): +4.5 % goal3 over 4 waves. Grid scenes
+// scenes: 5 (96 VGPRs; the queue's LDS lets 20 one-wave workgroups share a CU,
+// rp_math.h QCAP): +4.5 % goal3 over 4 waves. Grid scenes
 // keep 4 (their broad phase spills at 96). The edge kernels: 4 (was uncapped at
 // 136 VGPRs = 3 waves): C4 262k-sample plans -12 %; 5 spills.
 #ifndef RP_VALIDITY_WAVES
@@ -39,13 +39,19 @@ constexpr int NNTILE = 256;     // tree nodes per LDS tile (256 x 72 B = 18 KiB)
 // One lane per state; one wave per workgroup, whose LDS holds the wave's
 // narrow-phase queue (rp_math.h WaveQ). The scene record is read with wave-uniform
 // scalar loads (measured faster than staging it in LDS: 10.74 vs 10.52 G states/s).
+#ifndef RP_VWPB
+#define RP_VWPB 1
+#endif
+constexpr int VWPB = RP_VWPB;            // waves per k_validity workgroup (one queue each)
+constexpr int VTHREADS = 64 * VWPB;
 template <int NCL, bool BF = false>
-__global__ __launch_bounds__(VBLOCK, NCL == NCL_GRID ? RP_VALIDITY_WAVES_GRID : RP_VALIDITY_WAVES) void k_validity(const float* __restrict__ q, int64_t n,
+__global__ __launch_bounds__(VTHREADS, NCL == NCL_GRID ? RP_VALIDITY_WAVES_GRID : RP_VALIDITY_WAVES) void k_validity(const float* __restrict__ q, int64_t n,
                                                                        uint8_t* __restrict__ flags,
                                                                        const DevScene* __restrict__ sc) {
-    __shared__ WaveQ wq;
+    __shared__ WaveQ wqs[VWPB];
+    WaveQ& wq = wqs[VWPB == 1 ? 0 : rp_tid() / 64];
     RP_STAMP(0);
-    const int64_t i = (int64_t)blockIdx.x * VBLOCK + threadIdx.x;
+    const int64_t i = (int64_t)rp_bid() * VTHREADS + rp_tid();
     if (i >= n) return;
     float qq[NQ];
 #pragma unroll
@@ -74,8 +80,8 @@ constexpr int ND_FROM = 1 << 30;   // nd flag (mode 2): the edge's checked endpo
 // for a 90k-wave edge launch); readers sum the words
 constexpr int COUNTER_SLOTS = 256;
 __device__ __forceinline__ void count_states(unsigned long long* counter, unsigned long long ballot) {
-    if (counter && (threadIdx.x & 63) == 0 && ballot)
-        atomicAdd(counter + (blockIdx.x & (COUNTER_SLOTS - 1)), (unsigned long long)__popcll(ballot));
+    if (counter && (rp_tid() & 63) == 0 && ballot)
+        atomicAdd(counter + (rp_bid() & (COUNTER_SLOTS - 1)), (unsigned long long)__popcll(ballot));
 }
 __device__ __forceinline__ unsigned long long counter_sum(const unsigned long long* counter) {
     unsigned long long s = 0;
@@ -99,8 +105,8 @@ __global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_edges(const double* _
     if (dcount) n_edges = min(n_edges, (int64_t)dcount[0] * per_item);
     if (dkmax) kmax = *dkmax;
     const int64_t total = n_edges * kmax;
-    for (int64_t base = (int64_t)blockIdx.x * VBLOCK; base < total; base += (int64_t)gridDim.x * VBLOCK) {
-        const int64_t idx = base + threadIdx.x;
+    for (int64_t base = (int64_t)rp_bid() * VBLOCK; base < total; base += (int64_t)rp_gdim() * VBLOCK) {
+        const int64_t idx = base + rp_tid();
         const int64_t e = idx / kmax;
         const int slot = (int)(idx - e * kmax);
         bool run = false;
@@ -153,7 +159,7 @@ __global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_edges(const double* _
 // slots[e] = checks of edge e (0 for an empty edge or one past the device count)
 __global__ void k_edge_slots(const int* __restrict__ nd, int64_t n_edges, const int* __restrict__ dcount,
                              int per_item, int32_t* __restrict__ slots) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t e = (int64_t)rp_bid() * rp_bdim() + rp_tid();
     if (e >= n_edges) return;
     const int64_t n = dcount ? min(n_edges, (int64_t)dcount[0] * per_item) : n_edges;
     int v = 0;
@@ -170,7 +176,7 @@ __global__ void k_edge_slots(const int* __restrict__ nd, int64_t n_edges, const 
 // chunk_first[c] = the edge holding item 64 c (incl = inclusive scan of the slot
 // counts: item t belongs to the edge e with incl[e-1] <= t < incl[e])
 __global__ void k_chunk_first(const int32_t* __restrict__ incl, int64_t n_edges, int32_t* __restrict__ chunk_first) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t e = (int64_t)rp_bid() * rp_bdim() + rp_tid();
     if (e >= n_edges) return;
     const int64_t lo = e > 0 ? incl[e - 1] : 0, hi = incl[e];
     for (int64_t c = (lo + VBLOCK - 1) / VBLOCK; c * VBLOCK < hi; ++c) chunk_first[c] = (int32_t)e;
@@ -190,8 +196,8 @@ __global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_edges_packed(
     __shared__ int32_t e_of[VBLOCK];
     if (n_edges <= 0) return;
     const int64_t total = incl[n_edges - 1];
-    const int lane = threadIdx.x;
-    for (int64_t base = (int64_t)blockIdx.x * VBLOCK; base < total; base += (int64_t)gridDim.x * VBLOCK) {
+    const int lane = rp_tid();
+    for (int64_t base = (int64_t)rp_bid() * VBLOCK; base < total; base += (int64_t)rp_gdim() * VBLOCK) {
         const int64_t bend = min(base + VBLOCK, total);
         for (int64_t e0 = chunk_first[base / VBLOCK];; e0 += VBLOCK) {
             const int64_t ej = e0 + lane;
@@ -253,7 +259,7 @@ __global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_edges_packed(
 // nd for arbitrary edges (API / simplification) and the max over edges
 __global__ void k_edge_prep(const double* __restrict__ from, const double* __restrict__ to, int64_t n,
                             double res, int* nd, uint8_t* valid, int* kmax) {
-    const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t e = (int64_t)rp_bid() * rp_bdim() + rp_tid();
     int v = 0;
     if (e < n) {
         const int c = segment_count(from + e * NQ, to + e * NQ, res);
@@ -262,7 +268,7 @@ __global__ void k_edge_prep(const double* __restrict__ from, const double* __res
         v = c > 1 ? c : 1;
     }
     for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));   // wave max: one atomic per wave
-    if ((threadIdx.x & 63) == 0 && v > 0) atomicMax(kmax, v);
+    if ((rp_tid() & 63) == 0 && v > 0) atomicMax(kmax, v);
 }
 
 // ---------------------------------------------------------------------------
@@ -278,7 +284,7 @@ __device__ __forceinline__ int32_t nn_tiled(const double* __restrict__ tree, int
         const int cnt = (int)((T - base) < NNTILE ? (T - base) : NNTILE);
         __syncthreads();
         const double* src = tree + base * NQ;
-        for (int k = threadIdx.x; k < cnt * NQ; k += blockDim.x) tile[k] = src[k];
+        for (int k = rp_tid(); k < cnt * NQ; k += rp_bdim()) tile[k] = src[k];
         __syncthreads();
         if (active) {
             for (int j = 0; j < cnt; ++j) {
@@ -360,16 +366,16 @@ __global__ __launch_bounds__(NNBLOCK) void k_nn_part(NnQuery Q, int64_t n, const
     __shared__ double tile[NNTILE * NQ];
     __shared__ float tile32[NNTILE * NQ];
     if (Q.status) n = min(n, (int64_t)Q.status[0] - Q.t0);   // ST_NACC
-    const int64_t q0 = (int64_t)blockIdx.x * NNBLOCK * NN_QPT;
+    const int64_t q0 = (int64_t)rp_bid() * NNBLOCK * NN_QPT;
     if (q0 >= n) return;   // whole block idle (uniform)
-    const int64_t t_lo = (int64_t)blockIdx.y * chunk, t_hi = min(T, t_lo + chunk);
+    const int64_t t_lo = (int64_t)rp_bid_y() * chunk, t_hi = min(T, t_lo + chunk);
     double x[NN_QPT][NQ], best[NN_QPT];
     nnf2 x2[NN_QPT / 2][NQ];
     float thr[NN_QPT];
     int32_t bi[NN_QPT];
 #pragma unroll
     for (int r = 0; r < NN_QPT; ++r) {
-        const int64_t k = q0 + threadIdx.x + (int64_t)r * NNBLOCK;
+        const int64_t k = q0 + rp_tid() + (int64_t)r * NNBLOCK;
         nn_query(Q, k < n ? k : 0, x[r]);
         best[r] = __builtin_inf();
         thr[r] = __builtin_inff();
@@ -383,7 +389,7 @@ __global__ __launch_bounds__(NNBLOCK) void k_nn_part(NnQuery Q, int64_t n, const
         const int cnt = (int)((t_hi - base) < NNTILE ? (t_hi - base) : NNTILE);
         __syncthreads();
         const double* src = tree + base * NQ;
-        for (int k = threadIdx.x; k < cnt * NQ; k += NNBLOCK) {
+        for (int k = rp_tid(); k < cnt * NQ; k += NNBLOCK) {
             const double v = src[k];
             tile[k] = v;
             tile32[k] = (float)v;
@@ -427,15 +433,15 @@ __global__ __launch_bounds__(NNBLOCK) void k_nn_part(NnQuery Q, int64_t n, const
     }
 #pragma unroll
     for (int r = 0; r < NN_QPT; ++r) {
-        const int64_t k = q0 + threadIdx.x + (int64_t)r * NNBLOCK;
-        if (k < n) part[(int64_t)blockIdx.y * n + k] = DI2{best[r], bi[r], 0};
+        const int64_t k = q0 + rp_tid() + (int64_t)r * NNBLOCK;
+        if (k < n) part[(int64_t)rp_bid_y() * n + k] = DI2{best[r], bi[r], 0};
     }
 }
 
 // lexicographic (distance, index) minimum over the S tree ranges -> out[k]
 __global__ void k_nn_reduce(const DI2* __restrict__ part, int64_t n, int S, const int* status, int64_t t0,
                             int32_t* __restrict__ out) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t k = (int64_t)rp_bid() * rp_bdim() + rp_tid();
     if (status) n = min(n, (int64_t)status[0] - t0);
     if (k >= n) return;
     double bd = __builtin_inf();
@@ -457,7 +463,7 @@ __global__ __launch_bounds__(NNBLOCK) void k_ext_nn(const double* __restrict__ A
                                                     int32_t* __restrict__ near_out,
                                                     const int32_t* __restrict__ near_in) {
     __shared__ double tile[NNTILE * NQ];
-    const int64_t k = (int64_t)blockIdx.x * NNBLOCK + threadIdx.x;
+    const int64_t k = (int64_t)rp_bid() * NNBLOCK + rp_tid();
     const bool active = k < n;
     double qr[NQ];
     sample_state(seed, g0 + (uint64_t)(i0 + (active ? k : 0)), bd.lo, bd.hi, qr);
@@ -484,7 +490,7 @@ __global__ __launch_bounds__(NNBLOCK) void k_ext_nn(const double* __restrict__ A
 // world == 1: res[k] and its accept flag in one pass
 __global__ void k_ext_result_flag(const uint8_t* __restrict__ valid, const int32_t* __restrict__ near, int64_t n,
                                   int32_t* __restrict__ res, int32_t* __restrict__ acc) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t k = (int64_t)rp_bid() * rp_bdim() + rp_tid();
     if (k >= n) return;
     const int32_t v = valid[k] ? near[k] : -1;
     res[k] = v;
@@ -537,7 +543,7 @@ __global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_straight(Endpoints ep
     __shared__ int last;
     const int nd = segment_count(ep.start, ep.goal, res);
     const int64_t lanes = nd >= 1 ? (int64_t)nd + 1 : 2;
-    const int64_t idx = (int64_t)blockIdx.x * VBLOCK + threadIdx.x;
+    const int64_t idx = (int64_t)rp_bid() * VBLOCK + rp_tid();
     unsigned bad = 0;
     if (idx < lanes) {
         double st[NQ];
@@ -554,14 +560,14 @@ __global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_straight(Endpoints ep
     }
     // wave OR, then one atomic per block (a block is one wave)
     const unsigned long long b1 = __ballot(bad & 1u), b2 = __ballot(bad & 2u), b4 = __ballot(bad & 4u);
-    if (threadIdx.x == 0) {
+    if (rp_tid() == 0) {
         const unsigned wbad = (b1 ? 1u : 0u) | (b2 ? 2u : 0u) | (b4 ? 4u : 0u);
         if (wbad) atomicOr(&sync[0], wbad);
         __threadfence();
-        last = atomicAdd(&sync[1], 1u) == gridDim.x - 1;
+        last = atomicAdd(&sync[1], 1u) == rp_gdim() - 1;
     }
     __syncthreads();
-    if (last && threadIdx.x == 0) {
+    if (last && rp_tid() == 0) {
         __threadfence();
         const unsigned f = atomicOr(&sync[0], 0u);
         hio->status[ST_SG] = ((f & 1u) ? 0 : 1) | ((f & 2u) ? 0 : 0x100) | ((f & 6u) ? 0 : 0x10000);
@@ -580,7 +586,7 @@ __global__ __launch_bounds__(64) void k_validity_ml(const float* __restrict__ q,
     constexpr int SPW = 64 / GL;
     __shared__ CapsLds caps[SPW];
     __shared__ SceneLds scl;
-    const int64_t i = (int64_t)blockIdx.x * SPW + threadIdx.x / GL;
+    const int64_t i = (int64_t)rp_bid() * SPW + rp_tid() / GL;
     const bool run = i < n;
     float qq[NQ];
     const float* src = q + (run ? i : 0) * NQ;
@@ -588,7 +594,7 @@ __global__ __launch_bounds__(64) void k_validity_ml(const float* __restrict__ q,
     for (int k = 0; k < NQ; ++k) qq[k] = src[k];
     scene_to_lds(sc, scl);   // (after the state loads are issued: both in one round trip)
     const bool col = state_collides_ml<GL, BF>(qq, run, scl, caps);
-    if (run && (threadIdx.x & (GL - 1)) == 0) flags[i] = col ? 0 : 1;
+    if (run && (rp_tid() & (GL - 1)) == 0) flags[i] = col ? 0 : 1;
 }
 
 // ---- low-latency variants (rp_math.h state_collides_ml): GL lanes per state, for
@@ -603,7 +609,7 @@ __global__ __launch_bounds__(64) void k_straight_ml(Endpoints ep, double res, co
     scene_to_lds(sc, scl);
     const int nd = segment_count(ep.start, ep.goal, res);
     const int64_t states = nd >= 1 ? (int64_t)nd + 1 : 2;
-    const int64_t idx = (int64_t)blockIdx.x * SPW + threadIdx.x / GL;
+    const int64_t idx = (int64_t)rp_bid() * SPW + rp_tid() / GL;
     const bool run = idx < states;
     double st[NQ];
     if (idx < 2 || !run) {
@@ -618,14 +624,14 @@ __global__ __launch_bounds__(64) void k_straight_ml(Endpoints ep, double res, co
     const bool col = state_collides_ml<GL, BF>(qq, run, scl, caps);
     const unsigned bad = (run && col) ? (idx == 0 ? 1u : idx == 1 ? 2u : 4u) : 0u;
     const unsigned long long b1 = __ballot(bad & 1u), b2 = __ballot(bad & 2u), b4 = __ballot(bad & 4u);
-    if (threadIdx.x == 0) {
+    if (rp_tid() == 0) {
         const unsigned wbad = (b1 ? 1u : 0u) | (b2 ? 2u : 0u) | (b4 ? 4u : 0u);
         if (wbad) atomicOr(&sync[0], wbad);
         __threadfence();
-        last = atomicAdd(&sync[1], 1u) == gridDim.x - 1;
+        last = atomicAdd(&sync[1], 1u) == rp_gdim() - 1;
     }
     __syncthreads();
-    if (last && threadIdx.x == 0) {
+    if (last && rp_tid() == 0) {
         __threadfence();
         const unsigned f = atomicOr(&sync[0], 0u);
         hio->status[ST_SG] = ((f & 1u) ? 0 : 1) | ((f & 2u) ? 0 : 0x100) | ((f & 6u) ? 0 : 0x10000);
@@ -664,9 +670,9 @@ __global__ __launch_bounds__(64) void k_edges_ml(const double* __restrict__ from
     if (dcount) n_edges = min(n_edges, (int64_t)dcount[0] * per_item);
     if (dkmax) kmax = *dkmax;
     const int64_t n_items = n_edges * kmax, total = n_items + sr.slots;
-    const int gl = (int)(threadIdx.x & (GL - 1));
-    for (int64_t base = (int64_t)blockIdx.x * SPW; base < total; base += (int64_t)gridDim.x * SPW) {
-        const int64_t idx = base + threadIdx.x / GL;
+    const int gl = (int)(rp_tid() & (GL - 1));
+    for (int64_t base = (int64_t)rp_bid() * SPW; base < total; base += (int64_t)rp_gdim() * SPW) {
+        const int64_t idx = base + rp_tid() / GL;
         const bool sl = idx >= n_items;   // a straight-edge item
         const int64_t e = sl ? n_edges : idx / kmax;
         const int slot = (int)(sl ? idx - n_items : idx - e * kmax);
@@ -745,7 +751,7 @@ struct PlanInit {
     double* efrom; double* eto; int* nd; uint8_t* valid; int* gfail;
 };
 __device__ __forceinline__ void plan_init_block(const PlanInit& a) {
-    const int t = threadIdx.x;
+    const int t = rp_tid();
     if (t < NQ) {
         a.S[t] = a.r.start[t];
         a.G[t] = a.r.goal[t];
@@ -758,9 +764,9 @@ __device__ __forceinline__ void plan_init_block(const PlanInit& a) {
         }
     }
     if (a.sg_edge >= 0)
-        for (int k = 1 + t; k < a.sg_stride; k += blockDim.x) a.nd[a.sg_edge + k] = a.nd[a.sg_edge + a.sg_stride + k] = -1;
+        for (int k = 1 + t; k < a.sg_stride; k += rp_bdim()) a.nd[a.sg_edge + k] = a.nd[a.sg_edge + a.sg_stride + k] = -1;
     if (t < ST_WORDS) a.io->status[t] = (t == ST_SL && a.sl) ? 1 : 0;
-    for (int k = t; k < COUNTER_SLOTS; k += blockDim.x) a.counter[k] = 0;
+    for (int k = t; k < COUNTER_SLOTS; k += rp_bdim()) a.counter[k] = 0;
     if (t == 0) {
         a.Spar[0] = -1;
         a.Gpar[0] = -1;
@@ -801,7 +807,7 @@ __global__ void k_ext_append(const int32_t* __restrict__ res, const int32_t* __r
                              uint64_t seed, uint64_t g0, Bounds bd, double range, double* A, int32_t* Apar,
                              uint8_t* Acand, int64_t TA, int* status, const uint8_t* valid, int64_t sg_edge,
                              int sg_stride) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i = (int64_t)rp_bid() * rp_bdim() + rp_tid();
     if (i >= B) return;
     if (status && i == B - 1) {
         status[ST_NACC] = incl[B - 1];
@@ -833,7 +839,7 @@ __device__ __forceinline__ void lds_barrier() {
 template <typename T>
 __device__ __forceinline__ T block_scan_excl(T v, T* lds, T* total) {
     constexpr int NW = FUSE_THREADS / 64;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = rp_tid() & 63, w = rp_tid() >> 6;
     T x = v;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -862,7 +868,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_ext_accept_small(const uint8_t
                                                                    uint8_t* Acand, int64_t TA, int* status,
                                                                    int64_t sg_edge, int sg_stride) {
     __shared__ int lds[FUSE_THREADS / 64 + 1];
-    const int64_t i0 = (int64_t)threadIdx.x * ITEMS;
+    const int64_t i0 = (int64_t)rp_tid() * ITEMS;
     int32_t nn[ITEMS];
     int cnt = 0;
 #pragma unroll
@@ -876,7 +882,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_ext_accept_small(const uint8_t
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r)
         if (nn[r] >= 0) ext_append_one(i0 + r, nn[r], pos++, seed, g0, bd, range, A, Apar, Acand);
-    if (threadIdx.x == 0) {
+    if (rp_tid() == 0) {
         status[ST_NACC] = total;
         status[ST_FIRST] = 0x7fffffff;
         if (sg_edge >= 0) status[ST_SG] = sg_flags(valid, sg_edge, sg_stride);
@@ -901,8 +907,8 @@ __global__ __launch_bounds__(NNBLOCK) void k_conn_nn(const double* __restrict__ 
                                                      const int32_t* __restrict__ y_in) {
     __shared__ double tile[NNTILE * NQ];
     if (status) n = min(n, (int64_t)status[ST_NACC] - t0);
-    if ((int64_t)blockIdx.x * NNBLOCK >= n) return;   // whole block idle (uniform)
-    const int64_t k = (int64_t)blockIdx.x * NNBLOCK + threadIdx.x;
+    if ((int64_t)rp_bid() * NNBLOCK >= n) return;   // whole block idle (uniform)
+    const int64_t k = (int64_t)rp_bid() * NNBLOCK + rp_tid();
     const bool active = k < n;
     double x[NQ];
     const double* xs = A + (TA0 + t0 + (active ? k : 0)) * NQ;
@@ -965,8 +971,8 @@ __global__ __launch_bounds__(NNBLOCK) void k_ext_conn_nn(const double* __restric
     __shared__ double tile[NNTILE * NQ];
     // ini.on (a plan's first iteration): block 0 also runs the prologue, and both
     // trees are their roots alone (start = tree A), read from the arguments
-    if (ini.on && blockIdx.x == 0) plan_init_block(ini);
-    const int64_t k = (int64_t)blockIdx.x * NNBLOCK + threadIdx.x;
+    if (ini.on && rp_bid() == 0) plan_init_block(ini);
+    const int64_t k = (int64_t)rp_bid() * NNBLOCK + rp_tid();
     const bool active = k < n;
     double qr[NQ], x[NQ];
     sample_state(seed, g0 + (uint64_t)(active ? k : 0), bd.lo, bd.hi, qr);
@@ -1029,7 +1035,7 @@ __global__ __launch_bounds__(NNBLOCK) void k_ext_conn_nn(const double* __restric
 __global__ void k_conn_record_len(const int32_t* __restrict__ y, const int32_t* __restrict__ m,
                                   const int* __restrict__ gfail, const int* __restrict__ status, int64_t B,
                                   int32_t* __restrict__ rec, int32_t* __restrict__ L) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t k = (int64_t)rp_bid() * rp_bdim() + rp_tid();
     if (k >= B) return;
     if (k < status[ST_NACC]) {
         const int mk = m[k] & CHAIN_LEN;
@@ -1085,7 +1091,7 @@ __global__ void k_conn_append(const int32_t* __restrict__ rec, const int32_t* __
                               int64_t TB, double range, int cmax, int a_start, uint8_t* Acand,
                               int* first_reached, int32_t* chain_end, const int* __restrict__ status,
                               const double* __restrict__ chain_nodes, const int32_t* __restrict__ m) {
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t t = (int64_t)rp_bid() * rp_bdim() + rp_tid();
     if (status) n = min(n, (int64_t)status[ST_NACC]);
     bool reached = false;
     if (t < n) {
@@ -1112,7 +1118,7 @@ __global__ void k_conn_append(const int32_t* __restrict__ rec, const int32_t* __
     // first REACHED target: one atomic per wave (its lowest reached lane), not per
     // lane — every lane's atomic on the one word queued in a single L2 channel
     const unsigned long long b = __ballot(reached);
-    const int lane = (int)(threadIdx.x & 63);
+    const int lane = (int)(rp_tid() & 63);
     if (b && lane == 0) atomicMin(first_reached, (int)(t + __builtin_ctzll(b)));
 }
 
@@ -1242,7 +1248,7 @@ __device__ int simp_begin(int level, int dev_max, const double* __restrict__ raw
                           SimpState* ss, int n_known = -3, bool p_ready = false) {
     __shared__ int bn;
     const bool known = n_known >= -1;
-    if (threadIdx.x == 0) {
+    if (rp_tid() == 0) {
         const int n = known ? n_known : io->n_raw;
         const bool on = level > 0 && n >= 0 && n <= dev_max;
         ss->on = on;
@@ -1258,7 +1264,7 @@ __device__ int simp_begin(int level, int dev_max, const double* __restrict__ raw
     }
     __syncthreads();
     const int n = bn;
-    for (int k = threadIdx.x; k < n * NQ; k += blockDim.x) ss->P[k] = raw[k];
+    for (int k = rp_tid(); k < n * NQ; k += rp_bdim()) ss->P[k] = raw[k];
     __syncthreads();
     return n;
 }
@@ -1273,11 +1279,11 @@ __device__ void simp_prep_reduce(double res, SimpState* ss, double* efrom, doubl
     const int n = n_known >= 0 ? n_known : ss->n;
     const bool on = n_known >= 0 ? n >= 3 : !ss->done && n >= 3;
     if (on)
-        for (int e = threadIdx.x; e < n * n; e += blockDim.x) {
+        for (int e = rp_tid(); e < n * n; e += rp_bdim()) {
             const int i = e / n, j = e - i * n;
             if (j >= i + 2) emit_edge(pair_index(i, j, n), P + i * NQ, P + j * NQ, res, efrom, eto, nd, valid);
         }
-    if (threadIdx.x == 0) {
+    if (rp_tid() == 0) {
         const int ne = on ? (n - 1) * (n - 2) / 2 : 0;
         ss->nedges = ne;
         if (n_known >= 0) ss->edges_total = ne;
@@ -1322,8 +1328,8 @@ __device__ int build_path(const PathArgs& pa, int32_t s_node, int32_t g_node, Pl
                           int also_max = -1, const TailLds* ov = nullptr, int a_start = 1) {
     __shared__ int32_t sidx[PATH_LDS], gidx[PATH_LDS];
     __shared__ int bns, bng;
-    const int tid = threadIdx.x;
-    const int gl = blockDim.x >= 128 ? 64 : 0;   // the goal walk's lane
+    const int tid = rp_tid();
+    const int gl = rp_bdim() >= 128 ? 64 : 0;   // the goal walk's lane
     if (tid == 0) {
         const int32_t* l = ov ? (a_start ? ov->apar : ov->bpar) : nullptr;
         const int64_t l0 = ov ? (a_start ? ov->a0 : ov->b0) : 0;
@@ -1352,7 +1358,7 @@ __device__ int build_path(const PathArgs& pa, int32_t s_node, int32_t g_node, Pl
     double* p2 = n <= also_max ? also : nullptr;
     double* p3 = (p2 && ov) ? ov->P : nullptr;
     if (ns <= PATH_LDS && ng <= PATH_LDS) {
-        for (int k = tid; k < n * NQ; k += blockDim.x) {
+        for (int k = tid; k < n * NQ; k += rp_bdim()) {
             const int i = k / NQ, d = k - i * NQ;
             const double v = !ov ? (i < ns ? pa.S[(int64_t)sidx[ns - 1 - i] * NQ + d]
                                            : pa.G[(int64_t)gidx[i - ns] * NQ + d])
@@ -1389,7 +1395,7 @@ __device__ void tail_finish_straight(const PathArgs& pa, const int* st, const un
                                      const double* P) {
     SimpState* ss = pa.ss;
     PlanIO* hio = pa.hio;
-    const int t = threadIdx.x;
+    const int t = rp_tid();
     lds_barrier();   // (P: build_path's copy)
     if (t < 2 * NQ) {
         const double v = t < NQ ? P[t] : P[(nr - 1) * NQ + (t - NQ)];
@@ -1421,7 +1427,7 @@ __device__ void iteration_tail(int* status, int added, int64_t TA, int a_start, 
                                const int32_t* Bpar, const int32_t* chain_end, const PathArgs& pa, PlanIO* io,
                                const TailLds* ov = nullptr) {
     __shared__ int sn, gn;
-    if (threadIdx.x == 0) finalize_one(status, added, TA, a_start, Apar, Bpar, chain_end, ov, &sn, &gn);
+    if (rp_tid() == 0) finalize_one(status, added, TA, a_start, Apar, Bpar, chain_end, ov, &sn, &gn);
     __syncthreads();
     RP_TSTAMP(0, 4);
     const int nr = sn != -2 ? build_path(pa, sn, gn, io, pa.ss ? pa.ss->P : nullptr,
@@ -1432,8 +1438,8 @@ __device__ void iteration_tail(int* status, int added, int64_t TA, int a_start, 
         // takes the farthest valid shortcut from the start first), the program ends
         // there (2 states); publish the output now
         __shared__ int stw[ST_WORDS];
-        if (threadIdx.x < ST_WORDS) {   // this iteration's words over the ones at kernel start
-            const int w = threadIdx.x;
+        if (rp_tid() < ST_WORDS) {   // this iteration's words over the ones at kernel start
+            const int w = rp_tid();
             stw[w] = w == ST_NACC ? ov->na : w == ST_ADDED ? added : w == ST_FIRST ? ov->first
                    : w == ST_SNODE ? sn : w == ST_GNODE ? gn : ov->st0[w];
         }
@@ -1457,7 +1463,7 @@ __global__ void k_finalize(int* status, const int32_t* __restrict__ inclL, int64
     const int nacc = status[ST_NACC], fr = status[ST_FIRST];
     const bool solved = fr != 0x7fffffff;
     __syncthreads();   // (every lane has read the words before lane 0 rewrites ST_NACC)
-    if (solved && threadIdx.x == 0) status[ST_NACC] = fr + 1;
+    if (solved && rp_tid() == 0) status[ST_NACC] = fr + 1;
     iteration_tail(status, solved ? inclL[fr] : nacc > 0 ? inclL[nacc - 1] : 0, TA, a_start, Apar, Bpar, chain_end,
                    pa, io);
 }
@@ -1471,8 +1477,8 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_conn_accept_small(
     __shared__ int lds[FUSE_THREADS / 64 + 1];
     __shared__ unsigned long long firstpk;   // first REACHED: (target << 32) | tree-B nodes up to it
     const int nacc = status[ST_NACC];
-    if (threadIdx.x == 0) firstpk = ~0ull;
-    const int64_t t0 = (int64_t)threadIdx.x * ITEMS;
+    if (rp_tid() == 0) firstpk = ~0ull;
+    const int64_t t0 = (int64_t)rp_tid() * ITEMS;
     int L[ITEMS];
     int cnt = 0;
 #pragma unroll
@@ -1495,7 +1501,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_conn_accept_small(
     __syncthreads();
     // the first REACHED target ends the iteration: the trees keep the appends up to it
     const bool solved = firstpk != ~0ull;
-    if (threadIdx.x == 0) {
+    if (rp_tid() == 0) {
         status[ST_FIRST] = solved ? (int)(firstpk >> 32) : 0x7fffffff;
         if (solved) status[ST_NACC] = (int)(firstpk >> 32) + 1;
     }
@@ -1527,20 +1533,20 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
     // side (a_start: extension near -> new; chain next -> prev), else `from`
     const double* ext_node = a_start ? eto : efrom;
     const double* chain_node = a_start ? efrom : eto;
-    if (threadIdx.x == 64) {   // (another wave)
+    if (rp_tid() == 64) {   // (another wave)
         if (sg_edge >= 0) sgv = sg_flags(valid, sg_edge, sg_stride);
         slv = io->status[ST_SL];
 #pragma unroll
         for (int w = 0; w < ST_WORDS; ++w) st0[w] = io->status[w];
     }
-    if (threadIdx.x >= 128 && threadIdx.x < 192) {   // state counters, for a plan this kernel may finish
+    if (rp_tid() >= 128 && rp_tid() < 192) {   // state counters, for a plan this kernel may finish
         unsigned long long v = 0;
-        for (int i = threadIdx.x - 128; i < COUNTER_SLOTS; i += 64) v += pa.counter[i];
-        cpart[threadIdx.x - 128] = v;
+        for (int i = rp_tid() - 128; i < COUNTER_SLOTS; i += 64) v += pa.counter[i];
+        cpart[rp_tid() - 128] = v;
     }
     RP_TSTAMP(0, 0);
     // every per-sample input fetched at once (one round trip)
-    const int64_t k0 = (int64_t)threadIdx.x * ITEMS;
+    const int64_t k0 = (int64_t)rp_tid() * ITEMS;
     int L[ITEMS], M[ITEMS];
     int32_t NR[ITEMS], Y[ITEMS];
     double X[ITEMS][NQ];
@@ -1568,7 +1574,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
     const unsigned long long ex = block_scan_excl(((unsigned long long)na << 32) | (unsigned)nl, lds64, &tot);
     const int exA = (int)(ex >> 32), exB = (int)(ex & 0xffffffffu);
     const int totalB = (int)(tot & 0xffffffffu);
-    if (threadIdx.x == 0) firstpk = ~0ull;
+    if (rp_tid() == 0) firstpk = ~0ull;
     lds_barrier();
     RP_TSTAMP(0, 2);
     int t = exA;
@@ -1616,16 +1622,16 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
     const int nB = firstpk == ~0ull ? totalB : (int)(firstpk & 0xffffffffu);
     // the chain nodes' states: one parallel copy (not a serial chain per sample)
     const int nbw = nB < TAIL_LB ? nB : TAIL_LB;
-    for (int k = threadIdx.x; k < nbw * NQ; k += FUSE_THREADS) {
+    for (int k = rp_tid(); k < nbw * NQ; k += FUSE_THREADS) {
         const int j = k / NQ, d = k - j * NQ;
         Bt[(TB + j) * NQ + d] = chain_node[(int64_t)l_bsrc[j] * NQ + d];
     }
-    if (threadIdx.x == 0) {
+    if (rp_tid() == 0) {
         status[ST_NACC] = nA;
         status[ST_FIRST] = first;
         if (sg_edge >= 0) status[ST_SG] = sgv;
     }
-    if (threadIdx.x == 64 && sg_edge >= 0) st0[ST_SG] = sgv;   // (st0 read by the tail after its barriers)
+    if (rp_tid() == 64 && sg_edge >= 0) st0[ST_SG] = sgv;   // (st0 read by the tail after its barriers)
     RP_TSTAMP(0, 3);
     const TailLds ov{l_apar, TA, nA, l_bpar, TB, nbw, l_cend, nA, first, slv,
                      st0, cpart, l_P, l_asrc, l_bsrc, ext_node, chain_node};
@@ -1656,7 +1662,7 @@ constexpr int GREC = 3;
 __global__ void k_group_pack(const int* __restrict__ gfail, const int32_t* __restrict__ near,
                              const int32_t* __restrict__ y, const int32_t* __restrict__ m, int64_t per, int tflag,
                              int32_t* __restrict__ rec) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t k = (int64_t)rp_bid() * rp_bdim() + rp_tid();
     if (k == 0) rec[GREC * per] = tflag;
     if (k >= per) return;
     const int g = gfail[k];
@@ -1704,7 +1710,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_group_accept_small(
     __shared__ int lds[FUSE_THREADS / 64 + 1];
     __shared__ unsigned long long firstpk;   // first REACHED: (target << 32) | tree-B nodes up to it
     const bool stop = gr.stop();
-    const int64_t k0 = (int64_t)threadIdx.x * ITEMS;
+    const int64_t k0 = (int64_t)rp_tid() * ITEMS;
     int L[ITEMS];
     int na = 0, nl = 0;
 #pragma unroll
@@ -1721,7 +1727,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_group_accept_small(
     int totalA, totalB;
     const int exA = block_scan_excl(na, lds, &totalA);
     const int exB = block_scan_excl(nl, lds, &totalB);
-    if (threadIdx.x == 0) firstpk = ~0ull;
+    if (rp_tid() == 0) firstpk = ~0ull;
     __syncthreads();
     int t = exA;
     int64_t off = TB + exB;
@@ -1738,7 +1744,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_group_accept_small(
     __syncthreads();
     // the first REACHED target ends the iteration: the trees keep the appends up to it
     const bool solved = firstpk != ~0ull;
-    if (threadIdx.x == 0) {
+    if (rp_tid() == 0) {
         status[ST_NACC] = solved ? (int)(firstpk >> 32) + 1 : totalA;
         status[ST_FIRST] = solved ? (int)(firstpk >> 32) : 0x7fffffff;
         status[ST_STOP] = stop ? 1 : 0;
@@ -1752,7 +1758,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_group_accept_small(
 // scan (hipCUB, u64), the appends, then a one-block finalize
 constexpr int GCOUNT_SHIFT = 40;
 __global__ void k_group_counts(GroupRecs gr, int64_t B, unsigned long long* __restrict__ cnt, int* status) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i = (int64_t)rp_bid() * rp_bdim() + rp_tid();
     const bool stop = gr.stop();
     if (i == 0) {
         status[ST_FIRST] = 0x7fffffff;
@@ -1772,7 +1778,7 @@ __global__ void k_group_append(GroupRecs gr, const unsigned long long* __restric
                                uint64_t g0, Bounds bd, double range, int cmax, double* A, int32_t* Apar,
                                uint8_t* Acand, int64_t TA, double* Bt, int32_t* Bpar, uint8_t* Bcand, int64_t TB,
                                int a_start, int32_t* chain_end, int* status) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i = (int64_t)rp_bid() * rp_bdim() + rp_tid();
     if (i >= B || status[ST_STOP]) return;
     const int32_t* rc = gr.rec(i);
     if (rc[0] < 0) return;
@@ -1796,7 +1802,7 @@ __global__ void k_group_finalize(const unsigned long long* __restrict__ incl, in
     const int fi = status[ST_FIRSTI];
     const unsigned long long v = (B > 0 && !status[ST_STOP]) ? incl[fi != 0x7fffffff ? fi : B - 1] : 0ull;
     __syncthreads();   // (every lane has read the words before lane 0 rewrites ST_NACC)
-    if (threadIdx.x == 0) {
+    if (rp_tid() == 0) {
         status[ST_NACC] = (int)(v >> GCOUNT_SHIFT);
         if (sg_edge >= 0) status[ST_SG] = sg_flags(valid, sg_edge, sg_stride);
     }
@@ -1807,9 +1813,9 @@ __global__ void k_group_finalize(const unsigned long long* __restrict__ incl, in
 // segments in parallel, the sum by lane 0. All lanes call it; block-uniform result.
 __device__ double path_length_blk(const double* P, int n, double* seg) {
     __shared__ double L;
-    for (int i = threadIdx.x; i + 1 < n; i += blockDim.x) seg[i] = sqrt(dist2(P + i * NQ, P + (i + 1) * NQ));
+    for (int i = rp_tid(); i + 1 < n; i += rp_bdim()) seg[i] = sqrt(dist2(P + i * NQ, P + (i + 1) * NQ));
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (rp_tid() == 0) {
         double t = 0.0;
         for (int i = 0; i + 1 < n; ++i) t = t + seg[i];
         L = t;
@@ -1837,7 +1843,7 @@ __global__ __launch_bounds__(256) void k_simp(int ops, int level, int dev_max, d
     __shared__ short keep[SPMAX];
     __shared__ int st[ST_WORDS], n_raw_s, mk;
     __shared__ unsigned long long part[64];
-    const int tid = threadIdx.x, nt = blockDim.x;
+    const int tid = rp_tid(), nt = rp_bdim();
     const bool pub = (ops & (OP_OUT | OP_STATUS)) != 0;
     RP_TSTAMP(1, 0);
     // ---- fetch 1: head (wave 0), PlanIO words (wave 1), counter partials (wave 2)
@@ -2064,30 +2070,30 @@ __global__ void k_argmin1(const double* __restrict__ T, const uint8_t* __restric
                           Bounds goalb, DI* partial) {
     __shared__ DI red[256];
     DI best = {__builtin_inf(), -1};
-    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t j = (int64_t)rp_bid() * rp_bdim() + rp_tid(); j < n; j += (int64_t)rp_gdim() * rp_bdim()) {
         if (!cand[j]) continue;
         DI c = {dist2(T + j * NQ, goalb.lo), j};
         best = di_min(best, c);
     }
-    red[threadIdx.x] = best;
+    red[rp_tid()] = best;
     __syncthreads();
     for (int s = 128; s > 0; s >>= 1) {
-        if (threadIdx.x < s) red[threadIdx.x] = di_min(red[threadIdx.x], red[threadIdx.x + s]);
+        if (rp_tid() < s) red[rp_tid()] = di_min(red[rp_tid()], red[rp_tid() + s]);
         __syncthreads();
     }
-    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+    if (rp_tid() == 0) partial[rp_bid()] = red[0];
 }
 __global__ void k_argmin2(const DI* __restrict__ partial, int n, DI* out) {
     __shared__ DI red[256];
     DI best = {__builtin_inf(), -1};
-    for (int j = threadIdx.x; j < n; j += blockDim.x) best = di_min(best, partial[j]);
-    red[threadIdx.x] = best;
+    for (int j = rp_tid(); j < n; j += rp_bdim()) best = di_min(best, partial[j]);
+    red[rp_tid()] = best;
     __syncthreads();
     for (int s = 128; s > 0; s >>= 1) {
-        if (threadIdx.x < s) red[threadIdx.x] = di_min(red[threadIdx.x], red[threadIdx.x + s]);
+        if (rp_tid() < s) red[rp_tid()] = di_min(red[rp_tid()], red[rp_tid() + s]);
         __syncthreads();
     }
-    if (threadIdx.x == 0) *out = red[0];
+    if (rp_tid() == 0) *out = red[0];
 }
 
 // diagnostics: collision pairs of one state (single lane)
@@ -2125,7 +2131,7 @@ __device__ void contacts_pairs(const Capsules& k, const DevScene* sc, int32_t* o
 }
 __global__ void k_contacts(const double* __restrict__ qd, const DevScene* __restrict__ sc, int32_t* out,
                            int cap, int* n_out) {
-    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    if (rp_bid() != 0 || rp_tid() != 0) return;
     float q[NQ];
     for (int i = 0; i < NQ; ++i) q[i] = (float)qd[i];
     Capsules k;
@@ -2138,7 +2144,7 @@ __global__ void k_contacts(const double* __restrict__ qd, const DevScene* __rest
 
 // numerics self-test: f64 sqrt / division / ceil and f64->f32 rounding on device
 __global__ void k_selftest(const double* __restrict__ x, int64_t n, double* __restrict__ out) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i = (int64_t)rp_bid() * rp_bdim() + rp_tid();
     if (i >= n) return;
     const double v = x[i];
     out[4 * i + 0] = sqrt(v < 0 ? -v : v);

@@ -87,7 +87,6 @@ enum { TR_NONE = 0, TR_HOST = 1, TR_RCCL = 2, TR_SHM = 3 };   // rank-group tran
     } while (0)
 
 constexpr int PATH_CAP = 1 << 16;   // states of a raw solution path (device buffer)
-constexpr int GRID_MIN_BOXES = 16;  // scenes with more boxes use the axis-grid broad phase
 
 }  // namespace
 
@@ -276,7 +275,7 @@ bool base_fixed(const DevScene& sc) {
 
 template <bool BF>
 void launch_validity_bf(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, hipStream_t s) {
-    const dim3 g(blocks_for(n, VBLOCK)), b(VBLOCK);
+    const dim3 g(blocks_for(n, VTHREADS)), b(VTHREADS);
 #define RP_VAL(N) hipLaunchKernelGGL((k_validity<N, BF>), g, b, 0, s, q, n, flags, c->d_scene)
     switch (ncl_bucket(c->scene)) {
         case NCL_GRID: RP_VAL(NCL_GRID); break;
@@ -1797,6 +1796,32 @@ int rp_create(rp_ctx** out, int device, const rp_robot_desc* robot) {
 
 void rp_destroy(rp_ctx* c) { delete c; }
 
+// Capsules no box of the scene can touch while the joints are inside the limits:
+// bit C set when every box's world AABB is farther than REACH[C] + 1e-4 m from the
+// capsule's reach centre (rp_model.h). The margin dwarfs the float32 FK error
+// (~1e-6 m), so every box test of such a capsule reports no contact (its narrow
+// phase distance exceeds the radius) and k_validity skips them in waves whose
+// states are all inside the limits. RBE_ENV_FAR=0 turns it off (tests, A/B).
+unsigned env_far_mask(const DevScene& sc, const float base[3]) {
+    if (const char* e = std::getenv("RBE_ENV_FAR"); e && *e && std::atoi(e) == 0) return 0u;
+    unsigned mask = 0u;
+    for (int cap = 0; cap < NCAP; ++cap) {
+        const double ctr[3] = {base[0], base[1], base[2] + (cap == 0 ? 0.0 : (double)SHOULDER_Z)};
+        bool far = true;
+        for (int j = 0; j < sc.n_boxes && far; ++j) {
+            double d2 = 0.0;
+            for (int k = 0; k < 3; ++k) {
+                const double lo = sc.box[j][8 + k], hi = sc.box[j][11 + k];
+                const double g = std::max({lo - ctr[k], 0.0, ctr[k] - hi});
+                d2 += g * g;
+            }
+            far = std::sqrt(d2) > (double)REACH[cap] + 1e-4;
+        }
+        if (far) mask |= 1u << cap;
+    }
+    return mask;
+}
+
 int rp_set_scene(rp_ctx* c, const rp_box* boxes, int32_t n, float plane_z, const float base[3]) {
     if (!c || n < 0 || n > MAX_BOXES || (n > 0 && !boxes)) return RP_ERR_ARG;
     RP_GUARD_BEGIN
@@ -1910,6 +1935,7 @@ int rp_set_scene(rp_ctx* c, const rp_box* boxes, int32_t n, float plane_z, const
     c->scene.plane_z = plane_z;
     if (base)
         for (int k = 0; k < 3; ++k) c->scene.base[k] = base[k];
+    c->scene.env_far = env_far_mask(c->scene, c->scene.base);
     upload_scene(c);
     c->have_scene = true;
     return RP_OK;

@@ -34,7 +34,7 @@ __device__ __forceinline__ void stamp(int k) {
     unsigned long long t;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
     __builtin_amdgcn_sched_barrier(0);
-    const unsigned w = blockIdx.x;
+    const unsigned w = rp_bid();
     if (w < STAMP_WAVES && __lane_id() == __builtin_amdgcn_readfirstlane(__lane_id())) g_stamps[w * STAMP_K + k] = t;
 }
 #define RP_STAMP(k) stamp(k)
@@ -47,7 +47,7 @@ __device__ __forceinline__ void tstamp(int kid, int k) {
     unsigned long long t;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
     __builtin_amdgcn_sched_barrier(0);
-    if (threadIdx.x == 0 && blockIdx.x == 0) g_tstamps[kid * TSTAMP_K + k] = t;
+    if (rp_tid() == 0 && rp_bid() == 0) g_tstamps[kid * TSTAMP_K + k] = t;
 }
 #define RP_TSTAMP(kid, k) tstamp(kid, k)
 // per-block stamps of a multi-block plan kernel (k_edges_ml: one wave per block)
@@ -58,7 +58,7 @@ __device__ __forceinline__ void estamp(int k) {
     unsigned long long t;
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
     __builtin_amdgcn_sched_barrier(0);
-    if (threadIdx.x == 0 && blockIdx.x < ESTAMP_BLOCKS) g_estamps[blockIdx.x * ESTAMP_K + k] = t;
+    if (rp_tid() == 0 && rp_bid() < ESTAMP_BLOCKS) g_estamps[rp_bid() * ESTAMP_K + k] = t;
 }
 #define RP_ESTAMP(k) estamp(k)
 #else
@@ -504,27 +504,59 @@ __device__ __forceinline__ bool pairs_ending_at(const Capsules& k) {
 // chain they drain the rest.
 // The set of tests and their arithmetic are unchanged, so results are identical.
 // All queue operations sit in wave-uniform control flow (ballot + mbcnt).
-#ifdef RP_QPAD
-// items padded to 16-B multiples (16 / 12 floats), 16-B aligned: enqueues and pops
-// move them with 128-bit LDS accesses (WaveQ = 70 x 112 B + 256 B = 8096 B)
+#if defined(RP_Q13)
+// self-pair items of 13 words in 64-B slots (a1 b1 a2 b2, tag; the radii come from
+// the wave's per-pair table): three 128-bit LDS writes and one 32-bit write per item
 #ifndef RP_QCAP
-#define RP_QCAP 70
+#define RP_QCAP 59
+#endif
+constexpr int QSS = 16, QSB = 11;
+#elif defined(RP_QPAD)
+// items padded to 16-B multiples (16 / 12 floats), 16-B aligned: enqueues and pops
+// move them with 128-bit LDS accesses (WaveQ = 66 x 112 B + 256 B = 7648 B)
+#ifndef RP_QCAP
+#define RP_QCAP 66
 #endif
 constexpr int QSS = 16, QSB = 12;
 #else
+// 59 items: WaveQ = 59 x 104 B + 256 B = 6392 B. Measured residency of one-wave
+// workgroups (tools/occupancy_probe.hip, wave start / end stamps + HW_ID): at most
+// 18 waves per CU with 8,192 B of LDS each (the 76-item queue's 8,160 B: the fifth
+// wave per SIMD the register budget allows never came), 21 at 6,656-7,680 B, 25 at
+// 5,632-6,144 B. With 59 items the register budget (5 per SIMD) binds, not LDS:
+// SQ_WAVE_CYCLES says 4.5 resident waves per SIMD on average against 3.9 (+5 %
+// goal3 4M states, profiles/r03/occupancy_ab.txt).
 #ifndef RP_QCAP
-#define RP_QCAP 76
+#define RP_QCAP 59
 #endif
 constexpr int QSS = 15, QSB = 11;
 #endif
-constexpr int QCAP = RP_QCAP;   // items per queue (WaveQ = 76 x 104 B + 256 B = 8160 B: 20 waves per CU)
+constexpr int QCAP = RP_QCAP;   // items per queue
+
+// (r_i, r_j) of each self pair (the 13-word queue items carry only the pair index)
+__constant__ constexpr float PAIR_RAD[NPAIR][2] = {
+#define RP_PR(p) {CAP_GEOM[PAIRS[p][0]][6], CAP_GEOM[PAIRS[p][1]][6]}
+    RP_PR(0), RP_PR(1), RP_PR(2), RP_PR(3), RP_PR(4), RP_PR(5), RP_PR(6), RP_PR(7), RP_PR(8), RP_PR(9),
+    RP_PR(10), RP_PR(11), RP_PR(12), RP_PR(13), RP_PR(14), RP_PR(15), RP_PR(16), RP_PR(17), RP_PR(18), RP_PR(19),
+    RP_PR(20), RP_PR(21), RP_PR(22), RP_PR(23), RP_PR(24), RP_PR(25), RP_PR(26), RP_PR(27), RP_PR(28), RP_PR(29),
+    RP_PR(30), RP_PR(31), RP_PR(32), RP_PR(33), RP_PR(34)
+#undef RP_PR
+};
 
 struct WaveQ {
     alignas(16) float ss[QCAP][QSS];   // self pair: a1 b1 a2 b2 (12), owner lane | pair << 8, r_i, r_j
     alignas(16) float sb[QCAP][QSB];   // capsule-box: pa pb (box frame) h (9), r^2, owner lane
     int hit[64];                       // per-lane collision found by a drained item
+#ifdef RP_Q13
+    float2 prad[NPAIR];                // (r_i, r_j) of self pair P
+#endif
+#ifdef RP_BOX_LDS
+    // broad-phase words of the cluster scenes' boxes (lo.xyz, exempt bits | hi.xyz, -),
+    // one spare entry for the loop's read-ahead
+    float4 bp[GRID_MIN_BOXES + 1][2];
+#endif
 };
-static_assert(sizeof(WaveQ) <= 8192, "WaveQ must fit 20 one-wave workgroups per CU");
+static_assert(sizeof(WaveQ) <= 7680, "WaveQ must let 20 one-wave workgroups share a CU");
 
 __device__ __forceinline__ int rank_in(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -554,6 +586,8 @@ struct QueueState {
     unsigned hand_near;   // bit I: the sphere test of pair (capsule I, hand) passed (this lane)
     int lane;
     float plane_z;
+    unsigned env_far;   // DevScene::env_far if the wave is inside the joint limits, else 0
+    bool box_lds;     // the scene's boxes fit the wave's LDS copy (RP_BOX_LDS)
     ClusterRegs<NCL> cl;
 };
 
@@ -573,7 +607,12 @@ __device__ __forceinline__ void pop_ss(S& s) {
         const V3 a1 = {it[0], it[1], it[2]}, b1 = {it[3], it[4], it[5]};
         const V3 a2 = {it[6], it[7], it[8]}, b2 = {it[9], it[10], it[11]};
         const int tag = __float_as_int(it[12]);
+#ifdef RP_Q13
+        const float2 rr2 = s.Q->prad[tag >> 8];
+        const float ri = rr2.x, rj = rr2.y;
+#else
         const float ri = it[13], rj = it[14];
+#endif
         const Aabb u = capsule_aabb(a1, b1, ri);
         const Aabb v = capsule_aabb(a2, b2, rj);
         if (!aabb_disjoint2(u, v)) {
@@ -643,6 +682,9 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
 #ifdef RP_ABLATE_ENV
     return false;
 #endif
+#ifndef RP_NO_ENV_FAR
+    if ((s.env_far >> C) & 1u) return false;   // no box within the capsule's reach (wave-uniform)
+#endif
     if constexpr (NCL == NCL_GRID) {
         // superset of the AABB-overlapping boxes from the axis grid (per-lane
         // gathers), then the exact AABB test on each candidate, one per lane per
@@ -686,17 +728,77 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
         // +1.6 % at 64k; -DRP_ENV_CMP builds the mask form)
         const float csep = aabb_sep(u, cr, cr + 4);
         if (!__any(csep <= 0.0f)) continue;
+#ifdef RP_ABLATE_BOX_LOOP
+        asm volatile("" ::"v"(csep));
+        continue;
+#endif
 #else
         const bool near_cl = !aabb_disjoint(u, cr, cr + 4);
         if (!__any(near_cl)) continue;
 #endif
         const int j0 = __float_as_int(cr[3]), nj = __float_as_int(cr[7]);
+#ifdef RP_BOX_LDS
+        // broad-phase words from the wave's LDS copy, the next box's read ahead of
+        // this box's test (LDS returns in order: no scalar-load round trip per box);
+        // scenes forced onto clusters with more boxes than the copy holds read the
+        // records below
+        if (s.box_lds) {
+        float4 A = s.Q->bp[j0][0], B = s.Q->bp[j0][1];
+        for (int j = j0; j < j0 + nj; ++j) {
+            const float4 nA = s.Q->bp[j + 1][0], nB = s.Q->bp[j + 1][1];
+            const float lo[3] = {A.x, A.y, A.z}, hi[3] = {B.x, B.y, B.z};
+            const float ex = ((__float_as_uint(A.w) >> C) & 1u) ? __builtin_inff() : -__builtin_inff();
+            const bool cand = fmaxr(fmaxr(csep, ex), aabb_sep(u, lo, hi)) <= 0.0f;
+            A = nA;
+            B = nB;
+            const unsigned long long m = __ballot(cand);
+            if (!m) continue;
+            room_sb(s, __popcll(m));
+            if (cand) enqueue_sb<C>(k, sc->box[j], r, s, m);
+            s.nsb += __popcll(m);
+        }
+        continue;
+        }
+#endif
+#ifdef RP_BOX_PIPE
+        // the next box's broad-phase words are loaded while this box is tested (a
+        // scalar-load round trip per box otherwise; the record past the cluster's
+        // last box is always inside DevScene and unused); the exempt bit is a
+        // scalar branch (wave-uniform), so the test is one compare and one branch
+        struct BRec { float lo[3], hi[3], ex; };
+        auto bload = [&](int jj) {
+            const float* b = sc->box[jj];
+            return BRec{{b[8], b[9], b[10]}, {b[11], b[12], b[13]}, b[14]};
+        };
+        BRec cur = bload(j0);
+        for (int j = j0; j < j0 + nj; ++j) {
+            const BRec nxt = bload(j + 1);
+            const bool exempt = (__float_as_uint(cur.ex) >> C) & 1u;
+            const bool cand = fmaxr(csep, aabb_sep(u, cur.lo, cur.hi)) <= 0.0f;
+            cur = nxt;
+            if (exempt) continue;
+            const unsigned long long m = __ballot(cand);
+            if (!m) continue;
+            room_sb(s, __popcll(m));
+            if (cand) enqueue_sb<C>(k, sc->box[j], r, s, m);
+            s.nsb += __popcll(m);
+        }
+        continue;
+#endif
         for (int j = j0; j < j0 + nj; ++j) {
             // the whole 64-B record in one scalar load; branch-free candidate test
             struct Rec { float v[16]; };
             const Rec rec = *reinterpret_cast<const Rec*>(sc->box[j]);
             const float* bx = rec.v;
-#ifndef RP_ENV_CMP
+#ifdef RP_EXEMPT_BRANCH
+            if ((__float_as_uint(bx[14]) >> C) & 1u) continue;   // wave-uniform
+            const bool cand = fmaxr(csep, aabb_sep(u, bx + 8, bx + 11)) <= 0.0f;
+            const unsigned long long m = __ballot(cand);
+            if (!m) continue;
+            room_sb(s, __popcll(m));
+            if (cand) enqueue_sb<C>(k, bx, r, s, m);
+            s.nsb += __popcll(m);
+#elif !defined(RP_ENV_CMP)
             const float ex = ((__float_as_uint(bx[14]) >> C) & 1u) ? __builtin_inff() : -__builtin_inff();
             const bool cand = fmaxr(fmaxr(csep, ex), aabb_sep(u, bx + 8, bx + 11)) <= 0.0f;
             const unsigned long long m = __ballot(cand);
@@ -759,9 +861,20 @@ template <int P, class S>
 __device__ __forceinline__ void pair_enqueue(const Capsules& k, S& s, bool cand, unsigned long long m) {
     constexpr int I = PAIRS[P][0], J = PAIRS[P][1];
     if (!m) return;
+#ifdef RP_ABLATE_SELF_ENQ
+    asm volatile("" ::"s"(m));
+    return;
+#endif
     room_ss(s, __popcll(m));
     if (cand) {
         float* it = s.Q->ss[s.nss + rank_in(m)];
+#ifdef RP_Q13
+        float4* it4 = reinterpret_cast<float4*>(it);
+        it4[0] = make_float4(k.a[I].x, k.a[I].y, k.a[I].z, k.b[I].x);
+        it4[1] = make_float4(k.b[I].y, k.b[I].z, k.a[J].x, k.a[J].y);
+        it4[2] = make_float4(k.a[J].z, k.b[J].x, k.b[J].y, k.b[J].z);
+        it[12] = __int_as_float(s.lane | (P << 8));
+#else
         it[0] = k.a[I].x; it[1] = k.a[I].y; it[2] = k.a[I].z;
         it[3] = k.b[I].x; it[4] = k.b[I].y; it[5] = k.b[I].z;
         it[6] = k.a[J].x; it[7] = k.a[J].y; it[8] = k.a[J].z;
@@ -769,6 +882,7 @@ __device__ __forceinline__ void pair_enqueue(const Capsules& k, S& s, bool cand,
         it[12] = __int_as_float(s.lane | (P << 8));
         it[13] = CAP_GEOM[I][6];
         it[14] = CAP_GEOM[J][6];
+#endif
     }
     s.nss += __popcll(m);
 }
@@ -906,11 +1020,35 @@ __device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene
         v.s.in_limits = !__any(!in);
     }
     v.s.plane_z = sc->plane_z;
+    v.s.env_far = v.s.in_limits ? sc->env_far : 0u;
     v.s.hand_near = 0u;
     v.s.cl.load(sc);
     Q.hit[v.s.lane] = 0;
+#ifdef RP_Q13
+    if (v.s.lane < NPAIR) Q.prad[v.s.lane] = make_float2(PAIR_RAD[v.s.lane][0], PAIR_RAD[v.s.lane][1]);
+#endif
+#ifdef RP_BOX_LDS
+    v.s.box_lds = sc->n_boxes <= GRID_MIN_BOXES;
+    if constexpr (NCL > 0) {
+        const int l = v.s.lane;
+        if (l < 2 * (GRID_MIN_BOXES + 1)) {
+            const float* bx = sc->box[l >> 1];
+            Q.bp[l >> 1][l & 1] = (l & 1) ? make_float4(bx[11], bx[12], bx[13], 0.0f)
+                                          : make_float4(bx[8], bx[9], bx[10], bx[14]);
+        }
+    }
+#endif
     __builtin_amdgcn_wave_barrier();
+#ifdef RP_SC_HOIST
+    // the 7 joint sin / cos first: independent chains, interleaved, instead of one
+    // exposed polynomial chain per link (the same function of q: the same bits)
+    JointsSC jt;
+#pragma unroll
+    for (int i = 0; i < 7; ++i) rp_sincos(q[i], &jt.s[i], &jt.c[i]);
+    if (fk_walk_j<QueuedVisit<NCL>, BF>(q, jt, sc->base, k, v)) return true;
+#else
     if (fk_walk<QueuedVisit<NCL>, BF>(q, sc, k, v)) return true;
+#endif
     if (!v.s.in_limits) never_pairs_outside_limits(q, sc, v.s);
     RP_STAMP(5);
     while (v.s.nsb > 0) pop_sb(v.s);
@@ -968,7 +1106,7 @@ struct SceneLds {
 };
 // all 64 lanes of the (one-wave) block; no wait (state_collides_ml waits)
 __device__ __forceinline__ void scene_to_lds(const DevScene* __restrict__ sc, SceneLds& L) {
-    const int t = (int)threadIdx.x;
+    const int t = (int)rp_tid();
     const float4* src = reinterpret_cast<const float4*>(&sc->box[0][0]);
     float4* dst = reinterpret_cast<float4*>(&L.box[0][0]);
 #pragma unroll

@@ -6,8 +6,22 @@
 // scratch memory on gfx950). rp_create rejects a descriptor whose structure
 // differs from this one.
 #pragma once
+#include <hip/hip_runtime.h>
 
 namespace rp {
+
+// Work-item / workgroup ids straight from the hardware registers and the dispatch
+// packet. HIP's threadIdx / blockIdx / blockDim / gridDim are device-library calls
+// (__ockl_get_local_id ...), and device-library functions are not inlined into
+// code built with -mno-amdgpu-ieee (their attributes differ): every use was an
+// s_swappc call (2,400 call sites in the library, two at the top of every
+// k_validity wave).
+__device__ __forceinline__ unsigned rp_tid() { return __builtin_amdgcn_workitem_id_x(); }
+__device__ __forceinline__ unsigned rp_bid() { return __builtin_amdgcn_workgroup_id_x(); }
+__device__ __forceinline__ unsigned rp_bid_y() { return __builtin_amdgcn_workgroup_id_y(); }
+__device__ __forceinline__ unsigned rp_bdim() { return __builtin_amdgcn_workgroup_size_x(); }
+// workgroups along x (HIP launches have uniform workgroups: grid = blocks x size)
+__device__ __forceinline__ unsigned rp_gdim() { return __builtin_amdgcn_grid_size_x() / __builtin_amdgcn_workgroup_size_x(); }
 
 constexpr int NQ = 9;       // 7 arm joints + 2 fingers (code/planning.py:143-150)
 constexpr int NCAP = 12;
@@ -53,6 +67,17 @@ constexpr bool pair_never(int p) {
     return false;
 }
 
+// Reach of each capsule while every joint is inside [Q_LO_F, Q_HI_F] (tools/
+// prove_reach.py, tests/golden/reach_proof.json): every point of capsule C lies
+// within REACH[C] metres of the robot base (C = 0, a fixed capsule) or of the
+// shoulder, base + (0, 0, 0.333) (every other capsule: on joint 1's axis, so q0
+// moves no point towards or away from it). Grid maximum + Lipschitz slack for the
+// capsules moved by <= 4 joints, the chain sum for the others; radius included;
+// rounded up to float.
+constexpr float REACH[NCAP] = {0.168167f, 0.253000f, 0.120006f, 0.306792f, 0.398614f, 0.681955f,
+                               0.802594f, 0.911263f, 0.999263f, 1.090294f, 1.136424f, 1.136424f};
+constexpr float SHOULDER_Z = 0.333f;
+
 // Capsule geometry (spec/franka_capsules.json): a(3), b(3), radius, in the link
 // frame. Compiled into the kernels (zero terms of the link->world transform fold
 // away, no scalar loads); rp_create rejects a descriptor with other numbers.
@@ -72,6 +97,7 @@ constexpr float CAP_GEOM[NCAP][7] = {
 };
 
 constexpr int MAX_BOXES = 64;
+constexpr int GRID_MIN_BOXES = 16;   // scenes with more boxes use the axis-grid broad phase
 constexpr int CLUSTER = 8;                       // boxes per broad-phase cluster
 constexpr int MAX_CLUSTERS = MAX_BOXES / CLUSTER;
 
@@ -98,6 +124,7 @@ struct DevScene {
     int n_boxes;
     int n_clusters;
     int grid;                    // 1: broad phase through the axis grid
+    unsigned env_far;            // bit C: capsule C can reach no box (REACH; rp_lib.hip env_far_mask)
     float grid_o[4];             // per-axis origin, pad
     float grid_s[4];             // per-axis cells per metre, pad
     unsigned long long grid_lo[3][GRID_CELLS];

@@ -119,7 +119,7 @@ __device__ __forceinline__ h8 b_frag(const NnMfma& P, const double* y, int ch) {
 // B operand images of tree nodes [t0, t1): img[node][32] f16 (64 B), made once per
 // node and plan (the searches read them; rp_lib.hip keeps a per-tree count)
 __global__ void k_nn_image(const double* __restrict__ tree, int64_t t0, int64_t t1, NnMfma P, h8* __restrict__ img) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i = (int64_t)rp_bid() * rp_bdim() + rp_tid();
     const int64_t node = t0 + (i >> 2);
     const int ch = (int)(i & 3);
     if (node >= t1) return;
@@ -139,7 +139,7 @@ __global__ void k_nn_image(const double* __restrict__ tree, int64_t t0, int64_t 
 // blocks of one tree range sit on one XCD and its L2 holds that range (the tree's
 // 72 B/node are re-read by every query block).
 __device__ __forceinline__ void nn_block_coords(int64_t qblocks, int64_t* qb, int64_t* y) {
-    const int64_t nwg = (int64_t)gridDim.x, lid = (int64_t)blockIdx.x;
+    const int64_t nwg = (int64_t)rp_gdim(), lid = (int64_t)rp_bid();
     const int64_t q = nwg / 8, r = nwg % 8, xcd = lid % 8;
     const int64_t wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + lid / 8;
     *y = wgid / qblocks;
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(64 * W) void k_nn_mfma(const double* __restrict__ q
     nn_block_coords(qblocks, &qb, &yr);
     const int64_t qb0 = qb * W * QW;
     if (qb0 >= n) return;   // whole block idle (uniform)
-    const int w = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63), ch = lane >> 4;
+    const int w = (int)(rp_tid() >> 6), lane = (int)(rp_tid() & 63), ch = lane >> 4;
     const int64_t t_lo = yr * chunk, t_hi = min(T, t_lo + chunk);
     const int64_t qw0 = qb0 + (int64_t)w * QW;
 
@@ -334,7 +334,7 @@ __global__ __launch_bounds__(64 * W) void k_nn_mfma(const double* __restrict__ q
 // the queries of a split search as f64 states (NNQ_SAMPLE / NNQ_STEER: Philox samples,
 // steered; nn_query of rp_kernels.h)
 __global__ void k_nn_queries(NnQuery Q, int64_t n, double* __restrict__ qx) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t k = (int64_t)rp_bid() * rp_bdim() + rp_tid();
     if (k >= n) return;
     double x[NQ];
     nn_query(Q, k, x);

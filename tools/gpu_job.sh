@@ -47,6 +47,7 @@ for s in "$@"; do
     ptests) step pytest_plan 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
     procs) step pytest_procs 900 python -u -m pytest tests/test_gpu_group_procs.py -m gpu -x -v --timeout 400 --timeout-method thread ;;
     small) step small 300 python tools/small_launch.py && step smallprof 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/smallprof -o kt -- python tools/small_launch.py "" ;;
+    vpmc) for v in abvariants/*.so; do n=$(basename $v .so); step vpmc_$n 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY --output-format csv -d gpurun_out/vpmc_$n -o v -- python tools/variant_bench.py $v --rounds 1 --iters 3 && python tools/pmc_summary.py gpurun_out/vpmc_$n > gpurun_out/vpmc_$n.txt; done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

@@ -97,12 +97,14 @@ __device__ __forceinline__ void rp_sincos(float x, float* sn, float* cs) {
     const float pc = fma_(fma_(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f);
     const float cr = fma_(z * z, pc, fma_(-0.5f, z, 1.0f));
     const int qd = ((int)k) & 3;
-    float s = sr, c = cr;
-    if (qd == 1) { s = cr; c = -sr; }
-    else if (qd == 2) { s = -sr; c = -cr; }
-    else if (qd == 3) { s = -cr; c = sr; }
-    *sn = s;
-    *cs = c;
+    // quadrant by bits: odd quadrants swap sin and cos, quadrants 2 and 3 negate sin,
+    // 1 and 2 negate cos (the oracle's case analysis, the same values; as selects and
+    // sign-bit XORs instead of a branchy case analysis: -63 SALU, -35 VALU per wave,
+    // +4 % goal3)
+    const bool odd = qd & 1;
+    const float s0 = odd ? cr : sr, c0 = odd ? sr : cr;
+    *sn = __uint_as_float(__float_as_uint(s0) ^ ((unsigned)(qd & 2) << 30));
+    *cs = __uint_as_float(__float_as_uint(c0) ^ ((unsigned)((qd + 1) & 2) << 30));
 }
 
 // A rigid frame: rotation columns c0, c1, c2 and origin p (world).
@@ -596,8 +598,13 @@ struct QueueState {
 // passes run full; the walk's end pops until empty. Room is guaranteed: a batch has
 // at most as many items as there are active lanes. (Draining whenever more than
 // QCAP - 64 items were pending ran more, emptier passes and needed a larger queue.)
+#ifdef RP_POP_NOINLINE
+#define RP_POP_INLINE __attribute__((noinline))
+#else
+#define RP_POP_INLINE __forceinline__
+#endif
 template <class S>
-__device__ __forceinline__ void pop_ss(S& s) {
+__device__ RP_POP_INLINE void pop_ss(S& s) {
     const unsigned long long act = __ballot(1);
     const int nact = __popcll(act), r = rank_in(act);
     const int take = s.nss < nact ? s.nss : nact;
@@ -630,7 +637,7 @@ __device__ __forceinline__ void pop_ss(S& s) {
     s.nss -= take;
 }
 template <class S>
-__device__ __forceinline__ void pop_sb(S& s) {
+__device__ RP_POP_INLINE void pop_sb(S& s) {
     const unsigned long long act = __ballot(1);
     const int nact = __popcll(act), r = rank_in(act);
     const int take = s.nsb < nact ? s.nsb : nact;
@@ -677,6 +684,14 @@ template <int C, int NCL>
 __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __restrict__ sc,
                                            QueueState<NCL>& s) {
     constexpr float r = CAP_GEOM[C][6];
+#ifdef RP_AABB_LATE
+    // the plane test needs only lo.z; the rest of the AABB after the reach skip
+    if (fminr(k.a[C].z, k.b[C].z) - r <= s.plane_z) return true;   // capsule vs ground plane
+#ifndef RP_NO_ENV_FAR
+    if ((s.env_far >> C) & 1u) return false;   // no box within the capsule's reach (wave-uniform)
+#endif
+    const Aabb u = capsule_aabb(k.a[C], k.b[C], r);
+#else
     const Aabb u = capsule_aabb(k.a[C], k.b[C], r);
     if (u.lo.z <= s.plane_z) return true;  // capsule vs ground plane
 #ifdef RP_ABLATE_ENV
@@ -684,6 +699,7 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
 #endif
 #ifndef RP_NO_ENV_FAR
     if ((s.env_far >> C) & 1u) return false;   // no box within the capsule's reach (wave-uniform)
+#endif
 #endif
     if constexpr (NCL == NCL_GRID) {
         // superset of the AABB-overlapping boxes from the axis grid (per-lane
@@ -860,7 +876,9 @@ __device__ __forceinline__ bool pair_sphere(const Capsules& k) {
 template <int P, class S>
 __device__ __forceinline__ void pair_enqueue(const Capsules& k, S& s, bool cand, unsigned long long m) {
     constexpr int I = PAIRS[P][0], J = PAIRS[P][1];
+#ifndef RP_PAIR_NOBRANCH
     if (!m) return;
+#endif
 #ifdef RP_ABLATE_SELF_ENQ
     asm volatile("" ::"s"(m));
     return;

@@ -10,18 +10,26 @@
 
 namespace rp {
 
-// Work-item / workgroup ids straight from the hardware registers and the dispatch
-// packet. HIP's threadIdx / blockIdx / blockDim / gridDim are device-library calls
-// (__ockl_get_local_id ...), and device-library functions are not inlined into
-// code built with -mno-amdgpu-ieee (their attributes differ): every use was an
-// s_swappc call (2,400 call sites in the library, two at the top of every
-// k_validity wave).
+// Work-item / workgroup ids straight from the hardware registers. HIP's threadIdx /
+// blockIdx / blockDim / gridDim are device-library calls (__ockl_get_local_id ...),
+// and device-library functions are not inlined into code built with
+// -mno-amdgpu-ieee (their attributes differ): every use was an s_swappc call (2,400
+// call sites in the library, two at the top of every k_validity wave).
 __device__ __forceinline__ unsigned rp_tid() { return __builtin_amdgcn_workitem_id_x(); }
 __device__ __forceinline__ unsigned rp_bid() { return __builtin_amdgcn_workgroup_id_x(); }
 __device__ __forceinline__ unsigned rp_bid_y() { return __builtin_amdgcn_workgroup_id_y(); }
-__device__ __forceinline__ unsigned rp_bdim() { return __builtin_amdgcn_workgroup_size_x(); }
-// workgroups along x (HIP launches have uniform workgroups: grid = blocks x size)
-__device__ __forceinline__ unsigned rp_gdim() { return __builtin_amdgcn_grid_size_x() / __builtin_amdgcn_workgroup_size_x(); }
+// Block size and workgroup count from the hidden kernel arguments (code object v5:
+// hidden_block_count_x at offset 0, hidden_group_size_x at 12 — what HIP's gridDim /
+// blockDim read), NOT from the dispatch packet: the packet lives in the AQL queue in
+// host memory, so every wave reading it paid a PCIe round trip (the latency kernels'
+// grid-stride loops: k_edges_ml<16> 11 -> 24 us per launch, C3 RRT-forced plans
+// 0.040 -> 0.065 ms; tools/plan_trace.py A/B, profiles/r03/ids_ab.txt).
+__device__ __forceinline__ unsigned rp_bdim() {
+    return ((const unsigned short*)__builtin_amdgcn_implicitarg_ptr())[6];
+}
+__device__ __forceinline__ unsigned rp_gdim() {
+    return ((const unsigned*)__builtin_amdgcn_implicitarg_ptr())[0];
+}
 
 constexpr int NQ = 9;       // 7 arm joints + 2 fingers (code/planning.py:143-150)
 constexpr int NCAP = 12;

@@ -9,11 +9,13 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from rbe550_final_project_amd import _abi, model, scenes  # noqa: E402
+from rbe550_final_project_amd import _abi, model, native, scenes  # noqa: E402
 from rbe550_final_project_amd.native import Context  # noqa: E402
 
 
 def main():
+    if len(sys.argv) > 1 and sys.argv[1].endswith(".so"):   # a library build to trace (A/B)
+        native.LIB_PATH = os.path.abspath(sys.argv.pop(1))
     name = sys.argv[1] if len(sys.argv) > 1 else "goal3_tallest_10box"
     batch = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
     batch_min = batch if (len(sys.argv) > 3 and sys.argv[3] == "full") else 0

@@ -527,6 +527,20 @@ struct PlanIO {
 __device__ __forceinline__ void publish_seq(PlanIO* hio, int seq) {
     __hip_atomic_store(&hio->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// Block-wide publication: every lane's PlanIO stores, then ONE lane's system-scope
+// release store of the sequence number (publish_seq). The workgroup barrier orders
+// the other lanes' stores before that release (fences and barriers are cumulative in
+// the HIP / HSA model: the release makes visible everything that happens-before it),
+// so no per-lane system fence is needed. A __threadfence_system() in every lane made
+// each of a 1024-lane block's 16 waves write back L2 (buffer_wbl2 sc0 sc1 + wait +
+// invalidate) before the barrier: ~3 us at the end of every solving accept kernel.
+// -DRP_FENCE_ALL builds the per-lane fences (A/B).
+__device__ __forceinline__ void publish_after_barrier() {
+#ifdef RP_FENCE_ALL
+    __threadfence_system();
+#endif
+    __syncthreads();
+}
 
 // Straight-first check in one launch: lane 0 = start, lane 1 = goal, lanes
 // 2..nd = the interior slots 1..nd-1 of start -> goal (checkMotion mode 0, the
@@ -1418,8 +1432,7 @@ __device__ void tail_finish_straight(const PathArgs& pa, const int* st, const un
         hio->simp_edges = 1;
         hio->out = 1;
     }
-    __threadfence_system();
-    __syncthreads();
+    publish_after_barrier();
     if (t == 0) publish_seq(hio, pa.seq);
 }
 
@@ -1533,6 +1546,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
     // side (a_start: extension near -> new; chain next -> prev), else `from`
     const double* ext_node = a_start ? eto : efrom;
     const double* chain_node = a_start ? efrom : eto;
+    RP_TSTAMP(0, 9);   // (kernel entry)
     if (rp_tid() == 64) {   // (another wave)
         if (sg_edge >= 0) sgv = sg_flags(valid, sg_edge, sg_stride);
         slv = io->status[ST_SL];
@@ -1636,6 +1650,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
     const TailLds ov{l_apar, TA, nA, l_bpar, TB, nbw, l_cend, nA, first, slv,
                      st0, cpart, l_P, l_asrc, l_bsrc, ext_node, chain_node};
     iteration_tail(status, nB, TA, a_start, Apar, Bpar, chain_end, pa, io, &ov);
+    RP_TSTAMP(0, 10);   // (kernel exit of lane 0)
 }
 
 // solution path for host-chosen join nodes (approximate solutions)
@@ -2052,8 +2067,7 @@ __global__ __launch_bounds__(256) void k_simp(int ops, int level, int dev_max, d
             hio->simp_edges = h.edges_total;
             hio->out = out ? 1 : 0;
         }
-        __threadfence_system();
-        __syncthreads();
+        publish_after_barrier();
         if (tid == 0) publish_seq(hio, seq);
     }
     RP_TSTAMP(1, 4);

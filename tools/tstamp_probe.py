@@ -34,7 +34,8 @@ def main():
             sc = scenes.Scene.from_json(q["scene"])
             ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
             ctx.set_attached(q["attached"])
-            p = _abi.make_params(seed=i, batch=batch, n_waypoints=150, timeout_s=10.0, tree_capacity=1 << 24)
+            p = _abi.make_params(seed=i, batch=batch, n_waypoints=150, timeout_s=10.0, tree_capacity=1 << 24,
+                                 straight_first=os.environ.get("RBE_TRACE_STRAIGHT", "0") == "1")
             ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
             assert L.rp_debug_tstamps(buf.ctypes.data_as(C.c_void_p)) == 0
             assert L.rp_debug_estamps(ebuf.ctypes.data_as(C.c_void_p)) == 0
@@ -44,7 +45,7 @@ def main():
     r = np.stack(rows)
     for kid, kname in KERNELS.items():
         s = r[:, kid, :]
-        npts = int((s[0] > 0).sum())
+        npts = int((s[0, :9] > 0).sum()) if kid == 0 else int((s[0] > 0).sum())
         if npts < 2:
             continue
         print(f"{kname}: {len(s)} plans, stamps 0..{npts - 1} (us, median)")
@@ -55,6 +56,9 @@ def main():
                 print(f"   {k - 1}->{k}: {np.median(d):7.2f}  (p90 {np.percentile(d, 90):6.2f}, n {len(d)})")
         ok = (s[:, npts - 1] > 0) & (s[:, 0] > 0)
         print(f"   total {np.median((s[ok, npts - 1] - s[ok, 0]) / 100.0):7.2f}")
+        if kid == 0 and (s[:, 9] > 0).all() and (s[:, 10] > 0).all():   # entry (9) and exit (10) stamps
+            print(f"   entry->0 {np.median((s[:, 0] - s[:, 9]) / 100.0):7.2f}   8->exit "
+                  f"{np.median((s[:, 10] - s[:, 8]) / 100.0):7.2f}   entry->exit {np.median((s[:, 10] - s[:, 9]) / 100.0):7.2f}")
     # last k_edges_ml launch of each plan (stamps 0 entry, 1 scene in LDS, 2 edge
     # words loaded, 3 state built, 4 collision done, 5 exit), blocks that ran a state
     names = ["scene->LDS", "edge loads", "interp", "collides", "tail"]

@@ -547,6 +547,14 @@ void shm_barrier(rp_ctx* c, int64_t k) {
 }
 
 void upload_scene(rp_ctx* c) {
+    DevScene& sc = c->scene;
+    int n = 0;
+    for (int p = 0; p < NPAIR; ++p)
+        if (!pair_never(p)) sc.ml_unit[n++] = (unsigned short)p;
+    for (int cap = 0; cap < NCAP; ++cap)
+        if (!((sc.env_far >> cap) & 1u))
+            for (int j = 0; j < sc.n_boxes; ++j) sc.ml_unit[n++] = (unsigned short)(NPAIR + cap * sc.n_boxes + j);
+    sc.ml_n = n;
     HIP_TRY(hipMemcpyAsync(c->d_scene, &c->scene, sizeof(DevScene), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
 }

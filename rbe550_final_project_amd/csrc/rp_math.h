@@ -1122,7 +1122,8 @@ struct SceneLds {
     int pi[NPAIR], pj[NPAIR];
     float rad[NCAP];
     float plane_z, base[3];
-    int nb;
+    int nb, un;
+    alignas(16) unsigned short ul[ML_UNITS_PAD];   // DevScene::ml_unit (un of them)
 };
 // all 64 lanes of the (one-wave) block; no wait (state_collides_ml waits)
 __device__ __forceinline__ void scene_to_lds(const DevScene* __restrict__ sc, SceneLds& L) {
@@ -1136,9 +1137,15 @@ __device__ __forceinline__ void scene_to_lds(const DevScene* __restrict__ sc, Sc
         L.pj[t] = ML_PAIR_J[t];
     }
     if (t < NCAP) L.rad[t] = ML_RADIUS[t];
+    {
+        const uint4* us = reinterpret_cast<const uint4*>(sc->ml_unit);
+        uint4* ud = reinterpret_cast<uint4*>(L.ul);
+        for (int k = t; k < ML_UNITS_PAD / 8; k += 64) ud[k] = us[k];
+    }
     if (t == 0) {
         L.plane_z = sc->plane_z;
         L.nb = sc->n_boxes;
+        L.un = sc->ml_n;
     }
     if (t < 3) L.base[t] = sc->base[t];
 }
@@ -1188,12 +1195,22 @@ __device__ __forceinline__ bool state_collides_ml(const float q[NQ], bool run, c
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     if constexpr (GL == 16) RP_ESTAMP(11);
     const int nb = sc.nb;
-    const int units = NPAIR + NCAP * nb;
     const bool active = run && !hit;   // uniform within the group
+    // every running state of the wave inside the joint limits: the scene's reduced
+    // unit list (no never pairs, no box tests of capsules that reach no box: both
+    // proven for such states, DevScene::ml_unit), else every unit
+    bool reduced;
+    {
+        float ex = -__builtin_inff();
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) ex = fmaxr(ex, fmaxr(Q_LO_F[j] - q[j], q[j] - Q_HI_F[j]));
+        reduced = !__any(active && !(ex <= 0.0f));
+    }
+    const int units = reduced ? sc.un : NPAIR + NCAP * nb;
     for (int u0 = 0; u0 < units; u0 += GL) {
-        const int u = u0 + gl;
+        const int u = reduced ? (int)sc.ul[u0 + gl < units ? u0 + gl : 0] : u0 + gl;
         bool h = false;
-        if (active && u < units) {
+        if (active && u0 + gl < units) {
             if (u < NPAIR) {
                 const int i = sc.pi[u], j = sc.pj[u];
                 const float* pi = cs.v[i];

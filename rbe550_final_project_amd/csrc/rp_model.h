@@ -124,6 +124,7 @@ constexpr int MAX_CLUSTERS = MAX_BOXES / CLUSTER;
 //   the widening absorbs any host/device rounding difference), so the exact AABB
 //   test on that superset finds exactly the boxes the full scan would.
 constexpr int GRID_CELLS = 64;
+constexpr int ML_UNITS_PAD = (NPAIR + NCAP * MAX_BOXES + 7) / 8 * 8;   // 808: whole 16-B words
 struct DevScene {
     float box[MAX_BOXES][16];
     float cluster[MAX_CLUSTERS][8];
@@ -137,6 +138,13 @@ struct DevScene {
     float grid_s[4];             // per-axis cells per metre, pad
     unsigned long long grid_lo[3][GRID_CELLS];
     unsigned long long grid_hi[3][GRID_CELLS];
+    // test units of the lane-group kernels (rp_math.h state_collides_ml) for waves
+    // whose states are all inside the joint limits: the self pairs that are not never
+    // pairs, then capsule x box for the capsules that can reach a box (env_far clear);
+    // unit u < NPAIR is self pair u, else capsule (u - NPAIR) / n_boxes vs box
+    // (u - NPAIR) % n_boxes (rp_lib.hip upload_scene)
+    int ml_n;
+    alignas(16) unsigned short ml_unit[ML_UNITS_PAD];
 };
 
 // cell of coordinate v on an axis with origin o and scale s (cells per metre),

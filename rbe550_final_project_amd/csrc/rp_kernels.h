@@ -1634,12 +1634,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
     const int first = firstpk == ~0ull ? 0x7fffffff : (int)(firstpk >> 32);
     const int nA = firstpk == ~0ull ? (int)(tot >> 32) : first + 1;
     const int nB = firstpk == ~0ull ? totalB : (int)(firstpk & 0xffffffffu);
-    // the chain nodes' states: one parallel copy (not a serial chain per sample)
     const int nbw = nB < TAIL_LB ? nB : TAIL_LB;
-    for (int k = rp_tid(); k < nbw * NQ; k += FUSE_THREADS) {
-        const int j = k / NQ, d = k - j * NQ;
-        Bt[(TB + j) * NQ + d] = chain_node[(int64_t)l_bsrc[j] * NQ + d];
-    }
     if (rp_tid() == 0) {
         status[ST_NACC] = nA;
         status[ST_FIRST] = first;
@@ -1650,6 +1645,14 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
     const TailLds ov{l_apar, TA, nA, l_bpar, TB, nbw, l_cend, nA, first, slv,
                      st0, cpart, l_P, l_asrc, l_bsrc, ext_node, chain_node};
     iteration_tail(status, nB, TA, a_start, Apar, Bpar, chain_end, pa, io, &ov);
+    // the chain nodes' states (one parallel copy, not a serial chain per sample), after
+    // the tail: the tail reads them from their edge records (TailLds::state), so a
+    // plan this iteration finishes is published before this copy's loads return;
+    // later kernels see it at the kernel boundary
+    for (int k = rp_tid(); k < nbw * NQ; k += FUSE_THREADS) {
+        const int j = k / NQ, d = k - j * NQ;
+        Bt[(TB + j) * NQ + d] = chain_node[(int64_t)l_bsrc[j] * NQ + d];
+    }
     RP_TSTAMP(0, 10);   // (kernel exit of lane 0)
 }
 

@@ -34,6 +34,7 @@ def main():
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     sc = {"goal3": scenes.goal3_tallest(), "empty": scenes.Scene(),
+          "goal1_5box": scenes.Scene(boxes=scenes.goal1_scattered(0).boxes[:5]),
           "clutter64": scenes.Scene.from_json(json.load(open(os.path.join(
               ROOT, "tests/golden/workloads/clutter64.json")))["queries"][0]["scene"])}[a.scene]
     g = torch.Generator(device=dev)

@@ -847,12 +847,12 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-// exclusive scan of one value per thread over a FUSE_THREADS block; *total = sum.
+// exclusive scan of one value per thread over an NT-thread block; *total = sum.
 // Wave scans, then every lane sums the wave totals below it (independent LDS reads,
 // not one lane's serial pass); LDS-only barriers.
-template <typename T>
+template <typename T, int NT = FUSE_THREADS>
 __device__ __forceinline__ T block_scan_excl(T v, T* lds, T* total) {
-    constexpr int NW = FUSE_THREADS / 64;
+    constexpr int NW = NT / 64;
     const int lane = rp_tid() & 63, w = rp_tid() >> 6;
     T x = v;
 #pragma unroll
@@ -1529,14 +1529,16 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_conn_accept_small(
 // node is the checked endpoint of edge k * G, chain node s that of edge k * G + 1 +
 // s), not recomputed.
 constexpr int TAIL_LB = 4096;   // tree-B nodes an accept kernel keeps the parents of in LDS
-template <int ITEMS>
-__global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
+// NT threads (256 for iterations of <= 256 samples: 4 waves' barriers and scan
+// instead of 16; the tail needs >= 192 lanes), ITEMS samples per thread
+template <int ITEMS, int NT = FUSE_THREADS>
+__global__ __launch_bounds__(NT) void k_iter_accept_small(
     const int* __restrict__ gfail, const int32_t* __restrict__ near, const int32_t* __restrict__ y,
     const int32_t* __restrict__ m, int64_t B, int G, const double* __restrict__ efrom,
     const double* __restrict__ eto, double* A, int32_t* Apar, uint8_t* Acand, int64_t TA, double* Bt,
     int32_t* Bpar, uint8_t* Bcand, int64_t TB, int a_start, int32_t* chain_end, int* status,
     const uint8_t* valid, int64_t sg_edge, int sg_stride, PathArgs pa, PlanIO* io) {
-    __shared__ unsigned long long lds64[FUSE_THREADS / 64];
+    __shared__ unsigned long long lds64[NT / 64];
     __shared__ int sgv, slv, st0[ST_WORDS];
     __shared__ unsigned long long firstpk;   // first REACHED: (target << 32) | tree-B nodes up to it
     __shared__ unsigned long long cpart[64];
@@ -1585,7 +1587,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
     RP_TSTAMP(0, 1);
     // both scans in one: accepted extensions (high word), chain nodes (low word)
     unsigned long long tot;
-    const unsigned long long ex = block_scan_excl(((unsigned long long)na << 32) | (unsigned)nl, lds64, &tot);
+    const unsigned long long ex = block_scan_excl<unsigned long long, NT>(((unsigned long long)na << 32) | (unsigned)nl, lds64, &tot);
     const int exA = (int)(ex >> 32), exB = (int)(ex & 0xffffffffu);
     const int totalB = (int)(tot & 0xffffffffu);
     if (rp_tid() == 0) firstpk = ~0ull;
@@ -1649,7 +1651,7 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_iter_accept_small(
     // the tail: the tail reads them from their edge records (TailLds::state), so a
     // plan this iteration finishes is published before this copy's loads return;
     // later kernels see it at the kernel boundary
-    for (int k = rp_tid(); k < nbw * NQ; k += FUSE_THREADS) {
+    for (int k = rp_tid(); k < nbw * NQ; k += NT) {
         const int j = k / NQ, d = k - j * NQ;
         Bt[(TB + j) * NQ + d] = chain_node[(int64_t)l_bsrc[j] * NQ + d];
     }

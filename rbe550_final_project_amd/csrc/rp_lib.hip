@@ -322,6 +322,16 @@ void launch_validity(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, hipSt
 // Thresholds measured on MI355X (tools/ml_tune.py): a validity launch of dense
 // states gains below ~4k states; an edge launch's bound (edges x slots, mostly
 // idle lanes: short edges, finished chains) gains up to ~64k.
+// 256-thread accept kernels for iterations of <= 256 samples (RBE_ACCEPT_SMALL=0:
+// always 1024 threads, A/B and tests)
+bool accept_small_block() {
+    static const bool on = [] {
+        const char* e = std::getenv("RBE_ACCEPT_SMALL");
+        return !(e && *e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+
 int ml_lanes(int64_t states, bool edges) {
     const char* e = std::getenv("RBE_ML_LANES");
     const int forced = (e && *e) ? std::atoi(e) : 0;
@@ -1473,14 +1483,15 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                              c->gfail.p, c->stream, nullptr, 1, 0, nullptr, 0,
                              (first_launch && ride.slots > 0) ? &ride : nullptr, true);
                 pa.seq = seq;   // (an iteration that finishes the plan publishes it)
-#define RP_ITER_SMALL(IT)                                                                                           \
-    hipLaunchKernelGGL(k_iter_accept_small<IT>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, (const int*)c->gfail.p,   \
+#define RP_ITER_SMALL(IT, NT)                                                                                       \
+    hipLaunchKernelGGL((k_iter_accept_small<IT, NT>), dim3(1), dim3(NT), 0, c->stream, (const int*)c->gfail.p,        \
                        (const int32_t*)c->near_.p, (const int32_t*)c->yv.p, (const int32_t*)c->mv.p, C, G,          \
                        (const double*)c->efrom.p, (const double*)c->eto.p, A.q.p, A.par.p, A.cand.p, An, Bt.q.p,    \
                        Bt.par.p, Bt.cand.p, Bn, a_start, c->chain_end.p, status, (const uint8_t*)c->valid.p, sg,    \
                        sg_stride, pa, io)
-                if (C <= FUSE_THREADS) RP_ITER_SMALL(1);
-                else RP_ITER_SMALL(4);
+                if (C <= 256 && accept_small_block()) RP_ITER_SMALL(1, 256);
+                else if (C <= FUSE_THREADS) RP_ITER_SMALL(1, FUSE_THREADS);
+                else RP_ITER_SMALL(4, FUSE_THREADS);
 #undef RP_ITER_SMALL
                 HIP_TRY(hipGetLastError());
                 run_program(0, tail_steps, seq, true);

@@ -30,6 +30,7 @@ for s in "$@"; do
     tstamps) RBE_LIB_PATH=abvariants/lib_stamps.so step tstamps 300 python tools/tstamp_probe.py ;;
     mllanes) for g in 1 8 16 32; do RBE_ML_LANES=$g step mllanes_$g 300 python tools/variant_bench.py abvariants/lib_new.so --scene goal1_5box --states 65536 --iters 50 && RBE_ML_LANES=$g step mllanes3_$g 300 python tools/variant_bench.py abvariants/lib_new.so --scene goal3 --states 65536 --iters 50 && RBE_ML_LANES=$g step mllanes16k_$g 300 python tools/variant_bench.py abvariants/lib_new.so --scene goal3 --states 16384 --iters 50; done ;;
     acceptab) for r in 1 2; do for v in 0 1; do RBE_ACCEPT_SMALL=$v step acceptab_${v}_$r 300 python tools/plan_bench.py goal3_tallest_10box 4096; done; done && RBE_ACCEPT_SMALL=1 step ptab_small 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ptab_small -o pt -- python tools/plan_trace.py && python tools/trace_summary.py gpurun_out/ptab_small/pt_kernel_trace.csv > gpurun_out/ptab_small_summary.txt ;;
+    frontab) for r in 1 2; do for v in 0 8 16; do RBE_ML_LANES_FRONT=$v step frontab_${v}_$r 300 python tools/plan_bench.py goal3_tallest_10box 4096; done; done ;;
     rates) step rates 600 python tools/scene_rates.py ;;
     stamps) step stamps 300 python tools/stamp_probe.py abvariants/lib_stamps.so ;;
     sweep) step sweep 600 python tools/plan_sweep.py goal3_tallest_10box 4096 32 64 128 256 512 && step sweep4 600 python tools/plan_sweep.py goal4_pentagon_10box 4096 32 64 128 256 512 ;;

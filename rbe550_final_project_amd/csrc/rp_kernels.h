@@ -54,8 +54,21 @@ __global__ __launch_bounds__(VTHREADS, NCL == NCL_GRID ? RP_VALIDITY_WAVES_GRID 
     const int64_t i = (int64_t)rp_bid() * VTHREADS + rp_tid();
     if (i >= n) return;
     float qq[NQ];
+#ifndef RP_QLOAD1
+    // the state's 36 bytes as three 12-byte structs: the compiler merges them into
+    // two 16-byte loads and one 4-byte load per lane (gfx950 global loads need only
+    // dword alignment) instead of nine dword loads (A/B +1 % goal3, ±0 clutter64)
+    struct F3 { float x, y, z; };
+    const F3* q3 = reinterpret_cast<const F3*>(q + i * NQ);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const F3 v = q3[k];
+        qq[3 * k] = v.x; qq[3 * k + 1] = v.y; qq[3 * k + 2] = v.z;
+    }
+#else
 #pragma unroll
     for (int k = 0; k < NQ; ++k) qq[k] = q[i * NQ + k];
+#endif
 #ifdef RP_STAMPS
     asm volatile("" ::"v"(qq[0]), "v"(qq[8]));
     RP_STAMP(1);

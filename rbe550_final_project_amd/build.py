@@ -33,11 +33,12 @@ LIBS = ["-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
 
 def validity_source_hash():
     """Hash of what k_validity's machine code is made from (rp_math.h, rp_model.h,
-    the compiler flags): PMC measurements of that kernel (profiles/pmc_validity.json)
-    carry it, and bench.py uses them only while it still matches."""
+    rp_kernels.h where its body is, the compiler flags): PMC measurements of that
+    kernel (profiles/pmc_validity.json) carry it, and bench.py uses them only while
+    it still matches."""
     import hashlib
     h = hashlib.sha256()
-    for f in ("rp_math.h", "rp_model.h"):
+    for f in ("rp_math.h", "rp_model.h", "rp_kernels.h"):
         h.update(open(os.path.join(_HERE, "csrc", f), "rb").read())
     h.update(" ".join(FLAGS).encode())
     return h.hexdigest()[:16]

@@ -118,6 +118,54 @@ def run_plans(ctx, wl, batch, seed, group, batch_min=0, tree_capacity=0, stats_o
     return times, states, statuses
 
 
+def run_plan_path(ctx, wl, seed, straight_first=True):
+    """End-to-end wall time of the reference's own call, per query (ms):
+    `PlannerInterface.plan_path(qpos_goal=goal, num_waypoints=150,
+    attached_object=held, timeout=10.0)` (code/motion_primitives.py:144), through the
+    Genesis stand-in of the CPU tests (tests/mock_genesis.py: box entities with
+    get_pos / get_quat torch tensors, a robot with get_qpos / set_qpos / q_limit).
+    One PlannerInterface per workload, on the bench's context (one context per
+    process, as motion_primitives.py:38 keeps one planner); before each query the
+    blocks are moved to the query's poses and the robot to its start (the
+    simulation's state when the caller plans). Timed: the whole plan_path call —
+    scene ingestion, rp_plan, the 150 waypoint tensors, restoring qpos."""
+    import contextlib
+    import io
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import mock_genesis as M
+    from rbe550_final_project_amd import planning
+    q0 = scenes.Scene.from_json(wl["queries"][0]["scene"])
+    sim = M.Scene(q0.boxes)
+    pi = planning.PlannerInterface(sim.robot, sim)
+    pi._ctx = ctx
+    planning.configure(seed=seed, batch=4096, straight_first=straight_first)
+    times, parts, statuses, states = [], {"scene_ms": [], "rp_plan_ms": [], "other_ms": []}, [], 0
+    sink = io.StringIO()   # plan_path prints "Number of waypoints in path" (planning.py:200)
+    try:
+        for q in wl["queries"]:
+            sc = scenes.Scene.from_json(q["scene"])
+            for ent, (c, h, yaw) in zip(sim.entities[1:], sc.boxes):
+                ent.set_pos(c)
+                ent._quat = np.array([np.cos(yaw / 2), 0.0, 0.0, np.sin(yaw / 2)])
+            sim.robot.q = torch.tensor(q["start"], dtype=torch.float32)
+            held = sim.entities[1 + q["attached"]] if q["attached"] >= 0 else None
+            goal = np.array(q["goal"], dtype=float)
+            with contextlib.redirect_stdout(sink):
+                t0 = time.perf_counter()
+                wps = pi.plan_path(qpos_goal=goal, num_waypoints=150, attached_object=held, timeout=10.0)
+                times.append(1e3 * (time.perf_counter() - t0))
+            sink.seek(0)
+            sink.truncate()
+            statuses.append(pi.last_status)
+            states += int(pi.last_stats["states_checked"])
+            for k in parts:
+                parts[k].append(pi.last_timing[k])
+            assert len(wps) == 150, (q["label"], len(wps))
+    finally:
+        planning.configure(straight_first=True)
+    return times, states, statuses, {k: round(float(np.median(v)), 4) for k, v in parts.items()}
+
+
 def max_over_ranks(x, dev, distributed):
     """max of a float over the ranks (device tensor on RCCL, host tensor on gloo)"""
     if not distributed:
@@ -396,6 +444,20 @@ def main():
             t3, s3, st3 = run_plans(ctx, wl, args.plan_batch, 0, group, straight_first=False)
             plan["C3_rrt"] = plan_record(t3, s3, st3, args.plan_batch, dev, distributed,
                                          {"mode": "RRT-Connect forced (straight_first off)"})
+            # the same queries through the reference's API end to end:
+            # PlannerInterface.plan_path with the call site's arguments (run_plan_path)
+            for key, wname, sf in (("C3_plan_path", "goal3_tallest_10box", True),
+                                   ("C3_plan_path_rrt", "goal3_tallest_10box", False),
+                                   ("C1_plan_path", "goal1_scattered_6box", True),
+                                   ("C1_plan_path_rrt", "goal1_scattered_6box", False)):
+                w = wl if wname == "goal3_tallest_10box" else wl1
+                run_plan_path(ctx, w, 100, sf)   # warm-up pass (untimed)
+                tp, sp, stp, parts = run_plan_path(ctx, w, 0, sf)
+                plan[key] = plan_record(tp, sp, stp, args.plan_batch, dev, distributed,
+                                        {"mode": "PlannerInterface.plan_path(qpos_goal, num_waypoints=150, "
+                                                 "attached_object, timeout=10.0) through tests/mock_genesis.py"
+                                                 + ("" if sf else "; RRT-Connect forced"),
+                                         "median_parts_ms": parts})
         except Exception as ex:  # report, keep the primary metric
             plan = {"error": repr(ex)[:300]}
         # configured-batch workloads: C4 (262,144-sample iterations) and C5

@@ -130,7 +130,20 @@ typedef struct rp_plan_params {
                                the sub-batching); on trees of >= 4,096 nodes the first
                                sub-batch is at least a quarter of the iteration. 0 =
                                default 64; < 0 = the whole iteration as one batch        */
+    int64_t group_repl;     /* rank groups (rp_group_init*): sub-batches (see chunk) of at
+                               most this many samples run replicated — every rank computes
+                               the whole sub-batch, nothing is exchanged (same trees: the
+                               planner is deterministic); larger ones are sharded with one
+                               record all-gather each. Timeout vote: an iteration whose
+                               first sub-batch is sharded votes through that exchange; one
+                               that opens replicated first exchanges the ranks' timeout
+                               flags alone when k % RP_GROUP_VOTE_EVERY ==
+                               RP_GROUP_VOTE_EVERY - 1 (all stop if any timed out).
+                               0 = RP_GROUP_REPL_DEFAULT; < 0 = always shard            */
 } rp_plan_params;
+
+#define RP_GROUP_REPL_DEFAULT 4096
+#define RP_GROUP_VOTE_EVERY 8
 
 /* rp_ik parameters (defaults follow Genesis inverse_kinematics). Zero / negative
  * fields take the default shown. */

@@ -162,6 +162,34 @@ class OracleScene:
             raise RuntimeError(f"ro_plan rc={rc}")
         return out[:n.value].copy(), status.value, st.as_dict()
 
+    def plan_group(self, start, goal, lo, hi, params, world, path_cap=4096):
+        """The rank-group protocol with `world` ranks as threads of this process (a
+        barrier all-gather between them); every rank must return the same plan.
+        Returns rank 0's (path, status, stats)."""
+        import threading
+        stage = [None] * world
+        bar = threading.Barrier(world, timeout=600)
+
+        def make(rank):
+            def allgather(_user, send, recv, nbytes):
+                stage[rank] = C.string_at(send, nbytes)
+                bar.wait()
+                C.memmove(recv, b"".join(stage), nbytes * world)
+                bar.wait()
+                return 0
+            return allgather
+        res = [None] * world
+
+        def run(r):
+            res[r] = self.plan(start, goal, lo, hi, params, rank=r, world=world, allgather=make(r), path_cap=path_cap)
+        th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+        [t.start() for t in th]
+        [t.join() for t in th]
+        for r in range(1, world):
+            if res[r] is None or not np.array_equal(res[r][0], res[0][0]) or res[r][1] != res[0][1]:
+                raise RuntimeError(f"oracle rank {r} disagrees with rank 0")
+        return res[0]
+
 
 def sincos64(x):
     s, c = C.c_double(), C.c_double()

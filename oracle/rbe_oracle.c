@@ -573,17 +573,24 @@ static void kd_insert(kd_tree* k, const double* pts, int32_t id) {
             }
             if (hi - lo > spread) { spread = hi - lo; dim = d; }
         }
-        double cs[KD_LEAF];
-        if (dim >= 0 && L->cnt == KD_LEAF) {
+        if (dim >= 0) {
+            /* (a leaf that grew past KD_LEAF while its points were identical splits
+             * too, as soon as they are not: searches stay logarithmic) */
+            double* cs = (double*)malloc(sizeof(double) * L->cnt);
             for (int i = 0; i < L->cnt; ++i) cs[i] = pts[NQ * (int64_t)L->idx[i] + dim];
             qsort(cs, L->cnt, sizeof(double), cmp_double);
             double split = cs[L->cnt / 2];
             if (!(split > cs[0])) split = cs[L->cnt - 1];   /* both sides non-empty */
+            free(cs);
             const int32_t a = kd_new_leaf(k), b = kd_new_leaf(k);
             L = &k->nodes[v];   /* (realloc) */
             for (int i = 0; i < L->cnt; ++i) {
                 const int32_t j = L->idx[i];
                 kd_node* C = &k->nodes[pts[NQ * (int64_t)j + dim] >= split ? b : a];
+                if (C->cnt == C->cap) {
+                    C->cap *= 2;
+                    C->idx = (int32_t*)realloc(C->idx, sizeof(int32_t) * C->cap);
+                }
                 C->idx[C->cnt++] = j;
             }
             free(L->idx);
@@ -895,6 +902,18 @@ int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], co
     if (p.batch_min > p.batch) p.batch_min = p.batch;
     p.batch_min = ((p.batch_min + world - 1) / world) * world;
     const int cmax = (int)ceil(max_extent / p.range) + 1;
+    /* rank groups (include/rbe_planner.h group_repl): iterations of at most `repl`
+     * samples are replicated here (every rank computes all of it, no exchange), larger
+     * ones sharded. rp_lib.hip decides per sub-batch instead (an execution detail:
+     * the trees are the same); what both share is the timeout vote, which follows the
+     * GPU's first sub-batch of the iteration (chunk0 = rp_plan_params.chunk, default
+     * 64; at least a quarter of the iteration on trees of >= 4,096 nodes): when it is
+     * sharded the vote rides on the iteration's first exchange, when it is replicated
+     * the group exchanges the flags alone every RP_GROUP_VOTE_EVERY iterations */
+    int64_t repl = p.group_repl > 0 ? p.group_repl : p.group_repl < 0 ? 0 : RP_GROUP_REPL_DEFAULT;
+    if (world == 1) repl = 0;
+    int64_t chunk0 = p.chunk > 0 ? p.chunk : p.chunk < 0 ? INT64_MAX : 64;
+    if (chunk0 != INT64_MAX) chunk0 = ((chunk0 + world - 1) / world) * world;
 
     /* PlannerInputStates: invalid start / goal are skipped -> status */
     if (out_of_bounds(start, lo, hi) || !valid_d(s, start)) {
@@ -949,7 +968,7 @@ int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], co
     int64_t B = p.batch_min;
     uint64_t gbase = 0;
     int32_t* res = (int32_t*)malloc(sizeof(int32_t) * BMAX);
-    int32_t* mine = (int32_t*)malloc(sizeof(int32_t) * (BMAX / world + 1));
+    int32_t* mine = (int32_t*)malloc(sizeof(int32_t) * (BMAX + 1));
     int32_t* rbuf = (int32_t*)malloc(sizeof(int32_t) * (BMAX / world + 1) * world);
     int64_t* tnode = (int64_t*)malloc(sizeof(int64_t) * BMAX);
     int32_t* trec = (int32_t*)malloc(sizeof(int32_t) * 2 * (BMAX + world));
@@ -965,19 +984,38 @@ int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], co
          * all ranks leave the loop at the same iteration */
         const int tflag = (now_s() - t_solve) >= p.timeout_s;
         if (world == 1 && tflag) break;
+        const int repl_it = world > 1 && B <= repl;
         const int a_start = (iter % 2) == 0;
         tree_t* A = a_start ? &T[0] : &T[1];
         tree_t* Bt = a_start ? &T[1] : &T[0];
         if (A->n + B > A->cap || Bt->n + B * cmax > Bt->cap) break;
         const int64_t TA = A->n, TB = Bt->n;
+        /* the timeout vote (rp_lib.hip plan_impl, group_vote) */
+        int64_t c_first = B < chunk0 ? B : chunk0;
+        if (TA + TB >= 4096) {
+            const int64_t quarter = ((B / 4 + world - 1) / world) * world;
+            if (quarter > c_first) c_first = quarter;
+            if (c_first > B) c_first = B;
+        }
+        const int vote_first = world > 1 && c_first > repl;
+        if (world > 1 && !vote_first && iter % RP_GROUP_VOTE_EVERY == RP_GROUP_VOTE_EVERY - 1) {
+            double te = now_s();
+            mine[0] = tflag;
+            if (fn(user, mine, rbuf, (int64_t)sizeof(int32_t))) { solved = -1; break; }
+            st.exchange_ms += 1e3 * (now_s() - te);
+            int any = 0;
+            for (int r = 0; r < world; ++r) any |= rbuf[r];
+            if (any) break;
+        }
         const uint64_t g0 = gbase;
-        const int64_t per = B / world;
+        const int64_t per = repl_it ? B : B / world;
+        const int64_t off = repl_it ? 0 : rank * per;
         /* extension: my slice of the batch (samples are independent: OpenMP over
          * them for large batches, same results as the serial loop) */
         int64_t ext_states = 0;
 #pragma omp parallel for schedule(dynamic, 64) reduction(+ : ext_states) if (per >= OMP_MIN_ITEMS)
         for (int64_t k = 0; k < per; ++k) {
-            const int64_t i = rank * per + k;
+            const int64_t i = off + k;
             double qr[NQ], qn[NQ];
             int reach;
             sample_state(p.seed, g0 + (uint64_t)i, lo, hi, qr);
@@ -989,9 +1027,9 @@ int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], co
         }
         st.states_checked += ext_states;
         st.edges_checked += per;
-        if (world > 1) {
+        if (world > 1 && !repl_it) {
             double te = now_s();
-            mine[per] = tflag;
+            mine[per] = vote_first ? tflag : 0;
             if (fn(user, mine, rbuf, (int64_t)(sizeof(int32_t) * (per + 1)))) { solved = -1; break; }
             st.exchange_ms += 1e3 * (now_s() - te);
             int any = 0;
@@ -1015,11 +1053,12 @@ int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], co
         }
         st.samples += B;
         /* connect: my slice of the accepted targets (independent: OpenMP) */
-        const int64_t pt = (nacc + world - 1) / world;
+        const int64_t pt = repl_it ? nacc : (nacc + world - 1) / world;
+        const int64_t toff = repl_it ? 0 : rank * pt;
         int64_t con_states = 0, con_edges = 0;
 #pragma omp parallel for schedule(dynamic, 16) reduction(+ : con_states, con_edges) if (pt >= OMP_MIN_ITEMS)
         for (int64_t k = 0; k < pt; ++k) {
-            const int64_t t = rank * pt + k;
+            const int64_t t = toff + k;
             tmine[2 * k] = -1;
             tmine[2 * k + 1] = 0;
             if (t >= nacc) continue;
@@ -1043,7 +1082,7 @@ int ro_plan(const ro_scene* s, const double start[NQ], const double goal[NQ], co
         }
         st.states_checked += con_states;
         st.edges_checked += con_edges;
-        if (world > 1) {
+        if (world > 1 && !repl_it) {
             double te = now_s();
             if (fn(user, tmine, trec, (int64_t)(sizeof(int32_t) * 2 * pt))) { solved = -1; break; }
             st.exchange_ms += 1e3 * (now_s() - te);

@@ -38,7 +38,8 @@ class PlanParams(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("batch", C.c_int64), ("batch_min", C.c_int64), ("range", C.c_double),
                 ("resolution", C.c_double), ("timeout_s", C.c_double), ("max_iters", C.c_int64),
                 ("n_waypoints", C.c_int32), ("simplify", C.c_int32), ("tree_capacity", C.c_int64),
-                ("straight_first", C.c_int32), ("chunk", C.c_int32)]
+                ("straight_first", C.c_int32), ("chunk", C.c_int32),
+                ("group_repl", C.c_int64)]
 
 
 class IkParams(C.Structure):
@@ -91,7 +92,7 @@ def make_boxes(boxes):
 
 
 def make_params(seed=0, batch=4096, range_=0.0, resolution=0.0, timeout_s=5.0, max_iters=0, batch_min=0,
-                n_waypoints=100, simplify=True, tree_capacity=0, straight_first=True, chunk=0):
+                n_waypoints=100, simplify=True, tree_capacity=0, straight_first=True, chunk=0, group_repl=0):
     p = PlanParams()
     p.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     p.batch = int(batch)
@@ -105,4 +106,5 @@ def make_params(seed=0, batch=4096, range_=0.0, resolution=0.0, timeout_s=5.0, m
     p.tree_capacity = int(tree_capacity)
     p.straight_first = 0 if straight_first else -1   # 0 = default (on with simplification)
     p.chunk = int(chunk)   # first sub-batch of an iteration (execution only; 0 = 64, < 0 = none)
+    p.group_repl = int(group_repl)   # rank groups: replicated iterations up to this size (0 = 4096, < 0 = none)
     return p

@@ -24,7 +24,10 @@ HEADERS.append(os.path.join(os.path.dirname(_HERE), "include", "rbe_planner.h"))
 #   -fno-slp-vectorize: no v_pk_add/v_pk_mul pairs that need v_mov shuffles to
 #     line up their operands (4238 -> 3857 static VALU); +9 %
 DEVICE_FLAGS = ["-Xarch_device", "-fno-honor-nans", "-Xarch_device", "-mno-amdgpu-ieee", "-fno-slp-vectorize"]
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
+# -mcode-object-version=6: rp_bdim / rp_gdim (rp_model.h) read the hidden kernel
+#   arguments at the v5/v6 offsets; pinned so a toolchain default cannot move them
+#   (rp_create also checks them on the device)
+FLAGS = ["--offload-arch=gfx950", "-mcode-object-version=6", "-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off",
          "-fno-fast-math", "-Wall", "-Wno-unused-result"] + DEVICE_FLAGS
 # RCCL (rank-group all-gather on the context stream, rp_group_init_rccl); when torch
 # is loaded first its bundled librccl.so.1 (same SONAME) satisfies the dependency

@@ -54,7 +54,6 @@ __global__ __launch_bounds__(VTHREADS, NCL == NCL_GRID ? RP_VALIDITY_WAVES_GRID 
     const int64_t i = (int64_t)rp_bid() * VTHREADS + rp_tid();
     if (i >= n) return;
     float qq[NQ];
-#ifndef RP_QLOAD1
     // the state's 36 bytes as three 12-byte structs: the compiler merges them into
     // two 16-byte loads and one 4-byte load per lane (gfx950 global loads need only
     // dword alignment) instead of nine dword loads (A/B +1 % goal3, ±0 clutter64)
@@ -65,10 +64,6 @@ __global__ __launch_bounds__(VTHREADS, NCL == NCL_GRID ? RP_VALIDITY_WAVES_GRID 
         const F3 v = q3[k];
         qq[3 * k] = v.x; qq[3 * k + 1] = v.y; qq[3 * k + 2] = v.z;
     }
-#else
-#pragma unroll
-    for (int k = 0; k < NQ; ++k) qq[k] = q[i * NQ + k];
-#endif
 #ifdef RP_STAMPS
     asm volatile("" ::"v"(qq[0]), "v"(qq[8]));
     RP_STAMP(1);
@@ -547,11 +542,12 @@ __device__ __forceinline__ void publish_seq(PlanIO* hio, int seq) {
 // so no per-lane system fence is needed. A __threadfence_system() in every lane made
 // each of a 1024-lane block's 16 waves write back L2 (buffer_wbl2 sc0 sc1 + wait +
 // invalidate) before the barrier: ~3 us at the end of every solving accept kernel.
-// -DRP_FENCE_ALL builds the per-lane fences (A/B).
+// What the barrier does not give is completion: a wave's stores may still be in
+// flight when it reaches the barrier, so every wave first waits for its own
+// (s_waitcnt vmcnt(0): vmcnt 0, expcnt 7, lgkmcnt 15 in the gfx9 encoding), and lane
+// 0's release then covers stores that have all reached the cache hierarchy.
 __device__ __forceinline__ void publish_after_barrier() {
-#ifdef RP_FENCE_ALL
-    __threadfence_system();
-#endif
+    __builtin_amdgcn_s_waitcnt(0x0F70);
     __syncthreads();
 }
 
@@ -2183,6 +2179,23 @@ __global__ void k_selftest(const double* __restrict__ x, int64_t n, double* __re
     out[4 * i + 1] = 0.13037 / (v == 0 ? 1.0 : v);
     out[4 * i + 2] = ceil(v * 7.0);
     out[4 * i + 3] = (double)(float)v;
+}
+
+// Scene upload (rp_lib.hip flush_scene): one block copies the record from the pinned
+// host staging copy (zero-copy reads over PCIe) into the device record, in stream
+// order with the kernels that read it (no DMA-engine hand-off)
+__global__ __launch_bounds__(256) void k_scene_copy(const uint4* __restrict__ src, uint4* __restrict__ dst, int n16) {
+    for (int i = (int)rp_tid(); i < n16; i += 256) dst[i] = src[i];
+}
+
+// rp_bdim / rp_gdim read the hidden kernel arguments at the code-object v5/v6
+// offsets (rp_model.h); rp_create launches this once and refuses to run if they do
+// not return the launch's own block size and grid.
+__global__ void k_dims_probe(int* __restrict__ out) {
+    if (rp_bid() == 0 && rp_tid() == 0) {
+        out[0] = (int)rp_bdim();
+        out[1] = (int)rp_gdim();
+    }
 }
 
 }  // namespace rp

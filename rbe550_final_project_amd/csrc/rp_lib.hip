@@ -106,6 +106,15 @@ struct rp_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     DevScene scene{};
     DevScene* d_scene = nullptr;
+    // scene uploads (upload_scene / flush_scene): rp_set_scene / rp_set_attached only
+    // mark the host record dirty; the next call that launches a scene-reading kernel
+    // copies it from a pinned staging record, asynchronously on the context stream,
+    // and only if it differs from what the device already holds
+    DevScene* h_scene_stage = nullptr;   // pinned
+    DevScene uploaded{};                 // the record d_scene holds (valid if have_uploaded)
+    bool have_uploaded = false;
+    bool scene_dirty = false;
+    hipEvent_t scene_ev = nullptr;       // the last upload's copy (staging reusable after it)
     bool have_scene = false;
     std::vector<int> slot_of;            // caller box index -> stored (cluster-sorted) slot
     rp_robot_desc robot{};
@@ -160,6 +169,7 @@ struct rp_ctx {
     int32_t* h_send = nullptr;           // host transport staging (pinned)
     int32_t* h_recv = nullptr;
     int64_t h_cap = 0;                   // int32 words per rank slot in the staging
+    int32_t* h_vote = nullptr;           // RCCL timeout vote: mine, then every rank's (pinned)
     DevBuf<unsigned long long> g_cnt, g_incl;
     hipEvent_t gx0 = nullptr, gx1 = nullptr;
     // shared-memory transport (ranks of one node sharing a host segment): per-rank
@@ -192,6 +202,8 @@ struct rp_ctx {
         shm = shm_dev = nullptr;
         shm_bytes = shm_k = 0;
         free_staging();
+        if (h_vote) (void)hipHostFree(h_vote);
+        h_vote = nullptr;
         rank = 0;
         world = 1;
         transport = 0;
@@ -215,6 +227,8 @@ struct rp_ctx {
         if (gx0) (void)hipEventDestroy(gx0);
         if (gx1) (void)hipEventDestroy(gx1);
         if (h_io) (void)hipHostFree(h_io);
+        if (scene_ev) (void)hipEventSynchronize(scene_ev), (void)hipEventDestroy(scene_ev);
+        if (h_scene_stage) (void)hipHostFree(h_scene_stage);
         if (d_scene) (void)hipFree(d_scene);
         if (ev0) (void)hipEventDestroy(ev0);
         if (ev1) (void)hipEventDestroy(ev1);
@@ -528,6 +542,40 @@ void group_exchange(rp_ctx* c, int64_t words) {
     HIP_TRY(hipMemcpyAsync(c->g_recv.p, c->h_recv, bytes * c->world, hipMemcpyHostToDevice, c->stream));
 }
 
+// Timeout vote of a rank group outside the record exchanges (replicated iterations):
+// every rank's flag, OR-ed; true = some rank timed out. RCCL: a one-word all-gather
+// and a read-back; shared memory: the words in this exchange's region and the
+// arrival barrier; host transport: the callback.
+int shm_vote(rp_ctx* c, int tflag);
+int group_vote(rp_ctx* c, int tflag) {
+    int any = 0;
+    if (c->transport == TR_SHM) return shm_vote(c, tflag);
+    if (!c->h_vote) HIP_TRY(hipHostMalloc((void**)&c->h_vote, sizeof(int32_t) * (c->world + 1), hipHostMallocDefault));
+    const double t0 = now_s();
+    if (c->transport == TR_RCCL) {
+        c->h_vote[0] = tflag;
+        HIP_TRY(hipMemcpyAsync(c->g_send.p, c->h_vote, sizeof(int32_t), hipMemcpyHostToDevice, c->stream));
+        NCCL_TRY(ncclAllGather(c->g_send.p, c->g_recv.p, 1, ncclInt32, c->comm, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->h_vote + 1, c->g_recv.p, sizeof(int32_t) * c->world, hipMemcpyDeviceToHost,
+                               c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        for (int r = 0; r < c->world; ++r) any |= c->h_vote[1 + r];
+    } else {
+        if (c->h_cap < 1) {
+            c->free_staging();
+            HIP_TRY(hipHostMalloc((void**)&c->h_send, sizeof(int32_t), hipHostMallocDefault));
+            HIP_TRY(hipHostMalloc((void**)&c->h_recv, sizeof(int32_t) * c->world, hipHostMallocDefault));
+            c->h_cap = 1;
+        }
+        c->h_send[0] = tflag;
+        if (c->g_fn(c->g_user, c->h_send, c->h_recv, (int64_t)sizeof(int32_t)) != 0)
+            throw HipError{"group all-gather callback failed"};
+        for (int r = 0; r < c->world; ++r) any |= c->h_recv[r];
+    }
+    c->stats.exchange_ms += 1e3 * (now_s() - t0);
+    return any != 0;
+}
+
 // shared-memory transport layout: SHM_HDR bytes of per-rank sequence words (one
 // 64-B line each), then two regions of `region` bytes (exchange k uses region k & 1:
 // a rank writes region (k+2) & 1 only after every rank has arrived at exchange k+1,
@@ -555,6 +603,18 @@ void shm_barrier(rp_ctx* c, int64_t k) {
     }
     (void)seq;
 }
+int shm_vote(rp_ctx* c, int tflag) {
+    const int64_t k = ++c->shm_k;
+    (void)shm_records(c, k, 1);   // (size check)
+    int32_t* words = reinterpret_cast<int32_t*>(c->shm + SHM_HDR + (k & 1) * shm_region(c));
+    __atomic_store_n(words + c->rank, tflag, __ATOMIC_RELAXED);
+    const double t0 = now_s();
+    shm_barrier(c, k);
+    c->stats.exchange_ms += 1e3 * (now_s() - t0);
+    int any = 0;
+    for (int r = 0; r < c->world; ++r) any |= __atomic_load_n(words + r, __ATOMIC_RELAXED);
+    return any != 0;
+}
 
 void upload_scene(rp_ctx* c) {
     DevScene& sc = c->scene;
@@ -565,8 +625,31 @@ void upload_scene(rp_ctx* c) {
         if (!((sc.env_far >> cap) & 1u))
             for (int j = 0; j < sc.n_boxes; ++j) sc.ml_unit[n++] = (unsigned short)(NPAIR + cap * sc.n_boxes + j);
     sc.ml_n = n;
-    HIP_TRY(hipMemcpyAsync(c->d_scene, &c->scene, sizeof(DevScene), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->scene_dirty = true;
+}
+
+// Make d_scene hold c->scene before a launch on stream s: a copy from the pinned
+// staging record on the context stream when the record changed since the last
+// upload (no host synchronisation: a query whose scene is unchanged costs nothing,
+// a changed one one asynchronous 9 KB copy); a launch on another stream waits for it.
+void flush_scene(rp_ctx* c, hipStream_t s) {
+    if (c->scene_dirty) {
+        c->scene_dirty = false;
+        if (!c->have_uploaded || std::memcmp(&c->uploaded, &c->scene, sizeof(DevScene)) != 0) {
+            HIP_TRY(hipEventSynchronize(c->scene_ev));   // the previous copy has left the staging record
+            std::memcpy(c->h_scene_stage, &c->scene, sizeof(DevScene));
+            // a one-block copy kernel, not hipMemcpyAsync: same latency in A/B (goal3 RRT
+            // plans 0.042 ms either way) without a DMA-engine hand-off in the stream
+            static_assert(sizeof(DevScene) % 16 == 0, "the scene copy moves 16-byte words");
+            hipLaunchKernelGGL(k_scene_copy, dim3(1), dim3(256), 0, c->stream, (const uint4*)c->h_scene_stage,
+                               (uint4*)c->d_scene, (int)(sizeof(DevScene) / 16));
+            HIP_TRY(hipGetLastError());
+            HIP_TRY(hipEventRecord(c->scene_ev, c->stream));
+            std::memcpy(&c->uploaded, &c->scene, sizeof(DevScene));
+            c->have_uploaded = true;
+        }
+    }
+    if (s != c->stream) HIP_TRY(hipStreamWaitEvent(s, c->scene_ev, 0));
 }
 
 // Edge validity for arbitrary host edges (API and simplification): out[i].
@@ -852,8 +935,9 @@ bool nn_big(int64_t n, int64_t T) {
 // images of tree nodes [t.n_img, T) for the matrix-core search (once per node and plan)
 const h8* tree_images(rp_ctx* c, Tree& t, int64_t T) {
     if (t.n_img < T) {
-        t.img.ensure((size_t)t.q.n / NQ * 4);
-        hipLaunchKernelGGL(k_nn_image, dim3(blocks_for((T - t.n_img) * 4, 256)), dim3(256), 0, c->stream,
+        t.img.ensure(((size_t)t.q.n / NQ + NNM_PAD) * 4);   // + the dead pad slots
+        const int64_t tpad = (T + NNM_PAD - 1) / NNM_PAD * NNM_PAD;
+        hipLaunchKernelGGL(k_nn_image, dim3(blocks_for((tpad - t.n_img) * 4, 256)), dim3(256), 0, c->stream,
                            (const double*)t.q.p, t.n_img, T, c->nnm, t.img.p);
         t.n_img = T;
     }
@@ -990,6 +1074,14 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     bool grouped = c->transport != TR_NONE;
     if (const char* e = std::getenv("RBE_PLAN_GROUPED"))
         if (*e && world == 1 && std::atoi(e) != 0) grouped = true;
+    // rank groups: sub-batches of at most `repl` samples run replicated — every rank
+    // computes the whole sub-batch with the single-rank kernels (the same trees: the
+    // computation is deterministic) and nothing is exchanged; only larger sub-batches
+    // are sharded (rp_plan_params.group_repl; RBE_GROUP_REPL overrides)
+    int64_t repl = p.group_repl > 0 ? p.group_repl : p.group_repl < 0 ? 0 : RP_GROUP_REPL_DEFAULT;
+    if (const char* e = std::getenv("RBE_GROUP_REPL"))
+        if (*e) repl = std::max<int64_t>(0, std::atoll(e));
+    if (c->transport == TR_NONE) repl = 0;
 
     // workspace
     const int64_t cap = p.tree_capacity;
@@ -1058,7 +1150,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     // single-rank iterations of <= FUSE_MAX samples run speculatively (extension
     // and connect edges in one launch, k_ext_conn_nn); RBE_PLAN_SPECULATE=0 keeps
     // the two-phase iteration (same trees; the parity tests run both)
-    bool speculate = !grouped;
+    bool speculate = !grouped || repl > 0;
     if (const char* e = std::getenv("RBE_PLAN_SPECULATE"))
         if (*e) speculate = speculate && std::atoi(e) != 0;
     const int G = cmax + 1;   // edges per sample in a speculative launch
@@ -1086,7 +1178,8 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     if (const char* e = std::getenv("RBE_CHUNK_GROWTH"))
         if (*e) chunk_growth = std::max<int64_t>(1, std::atoll(e));
     const int64_t C00 = std::min<int64_t>(p.batch_min, chunk0);   // the plan's first sub-batch
-    const bool spec0 = speculate && C00 <= FUSE_MAX;
+    const bool shard0 = grouped && C00 > repl;                     // ... sharded over the group
+    const bool spec0 = speculate && C00 <= FUSE_MAX && !shard0;
     const int level = p.simplify < 0 ? 0 : p.simplify > 2 ? 1 : p.simplify;
     // straight-first (rp_plan_params.straight_first): with simplification on, a valid
     // straight edge start -> goal is the path the shortcut stage (REDUCE's greedy
@@ -1178,11 +1271,11 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     }
     // (a rank group rides them along its first front too, after its slice's groups,
     // unless that launch is work-compacted)
-    const bool grouped_sg = grouped && !packed((C00 / world) * G);
-    int64_t sg_edge = (!straight && !oob && (!grouped || grouped_sg))
-                          ? (spec0 ? C00 * G : grouped ? (C00 / world) * G : C00)
+    const bool grouped_sg = shard0 && !packed((C00 / world) * G);
+    int64_t sg_edge = (!straight && !oob && (!shard0 || grouped_sg))
+                          ? (spec0 ? C00 * G : shard0 ? (C00 / world) * G : C00)
                           : -1;
-    const int sg_stride = (spec0 || grouped) ? G : 1;
+    const int sg_stride = (spec0 || shard0) ? G : 1;
     // the prologue (k_plan_init): its own launch, or block 0 of the first
     // speculative front when that is the plan's next GPU work (one launch fewer on
     // the latency path); RBE_FUSE_INIT=0 keeps it separate (tests)
@@ -1223,7 +1316,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         HIP_TRY(hipGetLastError());
         init_pending = false;
     };
-    bool fuse_init = (spec0 || grouped) && !(sg_edge < 0 && !sg_known);
+    bool fuse_init = (spec0 || shard0) && !(sg_edge < 0 && !sg_known);
     if (const char* e = std::getenv("RBE_NN_SPLIT"))   // (a forced split search reads the trees first)
         if (*e && std::atoi(e) != 0) fuse_init = false;
     if (const char* e = std::getenv("RBE_FUSE_INIT"))
@@ -1325,7 +1418,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     uint64_t gbase = 0;
     for (; iter < p.max_iters; ++iter, gbase += (uint64_t)B, B = std::min(BMAX, 2 * B)) {
         const int tflag = (now_s() - t_solve) >= p.timeout_s;
-        if (!grouped && tflag) break;   // (a group votes through its exchange)
+        if (!grouped && tflag) break;
         const int a_start = (iter % 2) == 0;
         Tree& A = c->tree[a_start ? 0 : 1];
         Tree& Bt = c->tree[a_start ? 1 : 0];
@@ -1345,6 +1438,13 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         // least a quarter of the iteration there (RBE_CHUNK_TREE: the node count)
         int64_t C = std::min(B, chunk0);
         if (TA + TB >= chunk_tree) C = std::min(B, std::max(C, ((B / 4 + world - 1) / world) * world));
+        // timeout vote of a group: on the first exchange of an iteration whose first
+        // sub-batch is sharded; an iteration that opens replicated (no exchange) votes
+        // on its own every RP_GROUP_VOTE_EVERY iterations. Every rank stops at the same
+        // iteration (the oracle's rule, oracle/rbe_oracle.c ro_plan).
+        const bool vote_first = grouped && C > repl;
+        if (grouped && !vote_first && iter % RP_GROUP_VOTE_EVERY == RP_GROUP_VOTE_EVERY - 1 && group_vote(c, tflag))
+            break;
         // next sub-batch: x chunk_growth, but at least a quarter of what is left, so an
         // iteration that does not solve runs at most ~4 sub-batches (each one a round
         // trip and nearest-node launches over the whole snapshot)
@@ -1359,9 +1459,10 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             const bool first_launch = iter == 0 && done == 0;
             const int64_t sg = first_launch ? sg_edge : -1;   // start / goal ride along
             const int64_t per = C / world;
-            if (!(grouped || (speculate && C <= FUSE_MAX))) launch_init();
+            const bool shard = grouped && C > repl;
+            if (!(shard || (speculate && C <= FUSE_MAX))) launch_init();
             c->stats.samples += C;
-            if (grouped) {
+            if (shard) {
                 // ---- rank group: the speculative front on my slice, ONE all-gather of
                 // sample records, every rank appends the same nodes, one host round trip
                 const int seq = ++c->seq;
@@ -1400,7 +1501,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                 // the timeout vote rides on an iteration's first exchange (the oracle's rule)
                 hipLaunchKernelGGL(k_group_pack, dim3(blocks_for(per, 256)), dim3(256), 0, c->stream,
                                    (const int*)c->gfail.p, (const int32_t*)c->near_.p, (const int32_t*)c->yv.p,
-                                   (const int32_t*)c->mv.p, per, done == 0 ? tflag : 0, own);
+                                   (const int32_t*)c->mv.p, per, (done == 0 && vote_first) ? tflag : 0, own);
                 HIP_TRY(hipGetLastError());
                 if (c->transport == TR_SHM) {
                     HIP_TRY(hipStreamSynchronize(c->stream));   // my records are in the segment
@@ -1791,6 +1892,9 @@ int rp_create(rp_ctx** out, int device, const rp_robot_desc* robot) {
         HIP_TRY(hipEventCreate(&c->ev0));
         HIP_TRY(hipEventCreate(&c->ev1));
         HIP_TRY(hipMalloc(&c->d_scene, sizeof(DevScene)));
+        HIP_TRY(hipHostMalloc((void**)&c->h_scene_stage, sizeof(DevScene), hipHostMallocDefault));
+        HIP_TRY(hipEventCreateWithFlags(&c->scene_ev, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(c->scene_ev, c->stream));
         c->robot = *robot;
         c->scene.base[0] = 0.0f;
         c->scene.base[1] = 0.0f;
@@ -1803,6 +1907,18 @@ int rp_create(rp_ctx** out, int device, const rp_robot_desc* robot) {
         HIP_TRY(hipMemsetAsync(c->sync.p, 0, 2 * sizeof(unsigned), c->stream));
     }
         c->scalar.ensure(16);
+        // the hidden-argument offsets rp_bdim / rp_gdim read (rp_model.h) are those of
+        // code objects v5 / v6: check them once against a known launch
+        {
+            constexpr int kB = 96, kG = 3;
+            int dims[2] = {0, 0};
+            hipLaunchKernelGGL(k_dims_probe, dim3(kG), dim3(kB), 0, c->stream, c->scalar.p);
+            HIP_TRY(hipMemcpyAsync(dims, c->scalar.p, sizeof dims, hipMemcpyDeviceToHost, c->stream));
+            HIP_TRY(hipStreamSynchronize(c->stream));
+            if (dims[0] != kB || dims[1] != kG)
+                throw HipError{"hidden kernel-argument layout is not code object v5/v6 (block size " +
+                               std::to_string(dims[0]) + ", grid " + std::to_string(dims[1]) + ")"};
+        }
         upload_scene(c);
     } catch (const HipError& e) {
         g_create_error = e.msg;
@@ -1973,6 +2089,10 @@ int rp_set_attached(rp_ctx* c, int32_t box, uint32_t link_mask) {
         std::memcpy(&c->scene.box[c->slot_of[box]][14], &bits, 4);
     }
     upload_scene(c);
+    // the attachment completes a query's scene (rp_set_scene, then rp_set_attached):
+    // start its upload now, so it overlaps the caller's work before the next launch
+    // instead of opening that launch's dependency chain (goal3 RRT plans)
+    flush_scene(c, c->stream);
     return RP_OK;
     RP_GUARD_END(c)
 }
@@ -1984,6 +2104,7 @@ int rp_check_states(rp_ctx* c, const float* q, int64_t n, uint8_t* flags_out) {
     HIP_TRY(hipSetDevice(c->device));
     c->q32.ensure((size_t)n * NQ);
     c->flags.ensure(n);
+    flush_scene(c, c->stream);
     HIP_TRY(hipMemcpyAsync(c->q32.p, q, sizeof(float) * NQ * n, hipMemcpyHostToDevice, c->stream));
     launch_validity(c, c->q32.p, n, c->flags.p, c->stream);
     HIP_TRY(hipMemcpyAsync(flags_out, c->flags.p, n, hipMemcpyDeviceToHost, c->stream));
@@ -1998,6 +2119,7 @@ int rp_check_states_device(rp_ctx* c, const float* q, int64_t n, uint8_t* flags,
     if (n == 0) return RP_OK;
     RP_GUARD_BEGIN
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    flush_scene(c, s);
     // the timing events only when profiling is on: two more API calls per launch make
     // back-to-back small launches host-bound
     if (c->profiling) HIP_TRY(hipEventRecord(c->ev0, s));
@@ -2032,6 +2154,7 @@ int rp_check_edges(rp_ctx* c, const double* qa, const double* qb, int64_t n, dou
     RP_GUARD_BEGIN
     HIP_TRY(hipSetDevice(c->device));
     c->stats = rp_stats{};
+    flush_scene(c, c->stream);
     c->stats.states_checked = check_edges_host(c, qa, qb, n, res, out);
     c->stats.edges_checked = n;
     return RP_OK;
@@ -2044,6 +2167,7 @@ int rp_check_edges_device(rp_ctx* c, const double* qa, const double* qb, int64_t
     if (n == 0) return RP_OK;
     RP_GUARD_BEGIN
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    flush_scene(c, s);
     c->end_nd.ensure(n);
     c->scalar.ensure(16);
     HIP_TRY(hipMemsetAsync(c->scalar.p, 0, sizeof(int), s));
@@ -2065,6 +2189,7 @@ int rp_state_contacts(rp_ctx* c, const double q[RP_NQ], int32_t* pairs_out, int3
     c->scalar.ensure(16);
     DevBuf<int32_t> out;
     out.ensure(2 * (size_t)std::max(cap, 1));
+    flush_scene(c, c->stream);
     HIP_TRY(hipMemcpyAsync(c->ea.p, q, sizeof(double) * NQ, hipMemcpyHostToDevice, c->stream));
     hipLaunchKernelGGL(k_contacts, dim3(1), dim3(64), 0, c->stream, c->ea.p, c->d_scene, out.p, cap, c->scalar.p);
     HIP_TRY(hipGetLastError());
@@ -2091,6 +2216,7 @@ int rp_plan(rp_ctx* c, const double start[RP_NQ], const double goal[RP_NQ], cons
         c->err = "rank group broken by an earlier failed plan on this rank; initialise the group again";
         return RP_ERR_EXCHANGE;
     }
+    flush_scene(c, c->stream);
     c->prof = rp_profile{};
     c->pused = 0;
     c->in_plan = true;
@@ -2237,6 +2363,7 @@ int rp_ik(rp_ctx* c, int32_t n_targets, const double* pos, const double* quat, c
     if (n_targets == 0) return RP_OK;
     RP_GUARD_BEGIN
     HIP_TRY(hipSetDevice(c->device));
+    flush_scene(c, c->stream);
     if (!c->have_scene) {
         c->err = "rp_ik before rp_set_scene";
         return RP_ERR_STATE;
@@ -2380,8 +2507,8 @@ int rp_selftest_nn(rp_ctx* c, const double* q, int64_t n, const double* tree, in
             return RP_ERR_ARG;
         }
         DevBuf<h8> dimg;
-        dimg.ensure((size_t)T * 4);
-        hipLaunchKernelGGL(k_nn_image, dim3(blocks_for(T * 4, 256)), dim3(256), 0, c->stream, (const double*)dt.p,
+        dimg.ensure((size_t)(T + NNM_PAD) * 4);
+        hipLaunchKernelGGL(k_nn_image, dim3(blocks_for((T + NNM_PAD) * 4, 256)), dim3(256), 0, c->stream, (const double*)dt.p,
                            (int64_t)0, T, c->nnm, dimg.p);
         if (mode >= 8) launch_nn_mfma<8>(c, dq.p, n, Q, dt.p, dimg.p, T);
         else if (mode >= 4) launch_nn_mfma<4>(c, dq.p, n, Q, dt.p, dimg.p, T);

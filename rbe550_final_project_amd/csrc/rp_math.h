@@ -70,15 +70,9 @@ __device__ __forceinline__ void estamp(int k) {
 // min / max / clamp as single instructions (v_min_f32, v_max_f32, v_med3_f32). The
 // oracle writes them as compares; for the finite operands here the two agree except
 // possibly in the sign of a zero result, which no later comparison or square sees.
-#ifndef RP_OPT_SELECT
 __device__ __forceinline__ float fminr(float a, float b) { return __builtin_fminf(a, b); }
 __device__ __forceinline__ float fmaxr(float a, float b) { return __builtin_fmaxf(a, b); }
 __device__ __forceinline__ float clampr(float x, float lo, float hi) { return __builtin_amdgcn_fmed3f(x, lo, hi); }
-#else
-__device__ __forceinline__ float fminr(float a, float b) { return a < b ? a : b; }
-__device__ __forceinline__ float fmaxr(float a, float b) { return a > b ? a : b; }
-__device__ __forceinline__ float clampr(float x, float lo, float hi) { return x < lo ? lo : (x > hi ? hi : x); }
-#endif
 __device__ __forceinline__ float clamp01(float x) { return clampr(x, 0.0f, 1.0f); }
 __device__ __forceinline__ float fma_(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
 // (u . v) = fma(uz, vz, fma(uy, vy, ux * vx))
@@ -295,7 +289,6 @@ __device__ __forceinline__ float aabb_sep(const Aabb& u, const float* lo, const 
     const float a = fmaxr(fmaxr(u.lo.x - hi[0], lo[0] - u.hi.x), fmaxr(u.lo.y - hi[1], lo[1] - u.hi.y));
     return fmaxr(a, fmaxr(u.lo.z - hi[2], lo[2] - u.hi.z));
 }
-#ifndef RP_AABB_CMP
 // The six interval tests as one max of differences: for finite (or infinite, never
 // NaN) operands with subnormals kept, x - y > 0 <=> x > y (x != y => x - y != 0), so
 // the result is the same bool. One compare instead of six compares whose lane masks
@@ -312,16 +305,6 @@ __device__ __forceinline__ bool aabb_disjoint2(const Aabb& u, const Aabb& v) {
     const float b = fmaxr(u.lo.z - v.hi.z, v.lo.z - u.hi.z);
     return fmaxr(a, b) > 0.0f;
 }
-#else
-__device__ __forceinline__ bool aabb_disjoint(const Aabb& u, const float* lo, const float* hi) {
-    return (u.lo.x > hi[0]) | (u.hi.x < lo[0]) | (u.lo.y > hi[1]) | (u.hi.y < lo[1]) |
-           (u.lo.z > hi[2]) | (u.hi.z < lo[2]);
-}
-__device__ __forceinline__ bool aabb_disjoint2(const Aabb& u, const Aabb& v) {
-    return (u.lo.x > v.hi.x) | (u.hi.x < v.lo.x) | (u.lo.y > v.hi.y) | (u.hi.y < v.lo.y) |
-           (u.lo.z > v.hi.z) | (u.hi.z < v.lo.z);
-}
-#endif
 
 // g(t) = q(t) . d with q the excess of a + t d over the box [-h, h]; also |q|^2.
 __device__ __forceinline__ float excess_dot(V3 a, V3 d, V3 h, float t, float* f2) {
@@ -455,11 +438,7 @@ __device__ __forceinline__ bool capsule_hits_env(const Capsules& k, const DevSce
             const float* bx = sc->box[j];
             if ((__float_as_uint(bx[14]) >> C) & 1u) continue;
             if (aabb_disjoint(u, bx + 8, bx + 11)) continue;
-#ifndef RP_ABLATE_BOX_NARROW
             if (capsule_box_narrow(k.a[C], k.b[C], r, bx)) return true;
-#else
-            return true;
-#endif
         }
     }
     return false;
@@ -472,9 +451,6 @@ __device__ __forceinline__ bool pair_hits(const Capsules& k) {
     const Aabb u = capsule_aabb(k.a[I], k.b[I], ri);
     const Aabb v = capsule_aabb(k.a[J], k.b[J], rj);
     if (aabb_disjoint2(u, v)) return false;
-#ifdef RP_ABLATE_SELF_NARROW
-    return true;
-#endif
     constexpr float rr = ri + rj;
     return segment_segment_dist2(k.a[I], k.b[I], k.a[J], k.b[J]) <= rr * rr;
 }
@@ -506,57 +482,22 @@ __device__ __forceinline__ bool pairs_ending_at(const Capsules& k) {
 // chain they drain the rest.
 // The set of tests and their arithmetic are unchanged, so results are identical.
 // All queue operations sit in wave-uniform control flow (ballot + mbcnt).
-#if defined(RP_Q13)
-// self-pair items of 13 words in 64-B slots (a1 b1 a2 b2, tag; the radii come from
-// the wave's per-pair table): three 128-bit LDS writes and one 32-bit write per item
-#ifndef RP_QCAP
-#define RP_QCAP 59
-#endif
-constexpr int QSS = 16, QSB = 11;
-#elif defined(RP_QPAD)
-// items padded to 16-B multiples (16 / 12 floats), 16-B aligned: enqueues and pops
-// move them with 128-bit LDS accesses (WaveQ = 66 x 112 B + 256 B = 7648 B)
-#ifndef RP_QCAP
-#define RP_QCAP 66
-#endif
-constexpr int QSS = 16, QSB = 12;
-#else
-// 59 items: WaveQ = 59 x 104 B + 256 B = 6392 B. Measured residency of one-wave
-// workgroups (tools/occupancy_probe.hip, wave start / end stamps + HW_ID): at most
-// 18 waves per CU with 8,192 B of LDS each (the 76-item queue's 8,160 B: the fifth
-// wave per SIMD the register budget allows never came), 21 at 6,656-7,680 B, 25 at
-// 5,632-6,144 B. With 59 items the register budget (5 per SIMD) binds, not LDS:
-// SQ_WAVE_CYCLES says 4.5 resident waves per SIMD on average against 3.9 (+5 %
-// goal3 4M states, profiles/r03/occupancy_ab.txt).
-#ifndef RP_QCAP
-#define RP_QCAP 59
-#endif
+// 64 items: WaveQ = 64 x 104 B + 256 B = 6912 B. A batch has at most 64 items (one
+// per active lane) and a full-queue pop frees min(pending, active lanes) slots, so
+// QCAP >= 64 is what makes "pop one pass, then enqueue" never overflow: with
+// pending < active lanes the pop empties the queue and the batch can hold up to 64.
+// Measured residency of one-wave workgroups (tools/occupancy_probe.hip, wave start /
+// end stamps + HW_ID): at most 18 waves per CU with 8,192 B of LDS each, 21 at
+// 6,656-7,680 B, 25 at 5,632-6,144 B; the register budget (5 waves per SIMD = 20
+// per CU) binds at 6,912 B, not LDS.
 constexpr int QSS = 15, QSB = 11;
-#endif
-constexpr int QCAP = RP_QCAP;   // items per queue
-
-// (r_i, r_j) of each self pair (the 13-word queue items carry only the pair index)
-__constant__ constexpr float PAIR_RAD[NPAIR][2] = {
-#define RP_PR(p) {CAP_GEOM[PAIRS[p][0]][6], CAP_GEOM[PAIRS[p][1]][6]}
-    RP_PR(0), RP_PR(1), RP_PR(2), RP_PR(3), RP_PR(4), RP_PR(5), RP_PR(6), RP_PR(7), RP_PR(8), RP_PR(9),
-    RP_PR(10), RP_PR(11), RP_PR(12), RP_PR(13), RP_PR(14), RP_PR(15), RP_PR(16), RP_PR(17), RP_PR(18), RP_PR(19),
-    RP_PR(20), RP_PR(21), RP_PR(22), RP_PR(23), RP_PR(24), RP_PR(25), RP_PR(26), RP_PR(27), RP_PR(28), RP_PR(29),
-    RP_PR(30), RP_PR(31), RP_PR(32), RP_PR(33), RP_PR(34)
-#undef RP_PR
-};
+constexpr int QCAP = 64;   // items per queue
+static_assert(QCAP >= 64, "a batch of one item per lane must fit after one pop pass");
 
 struct WaveQ {
     alignas(16) float ss[QCAP][QSS];   // self pair: a1 b1 a2 b2 (12), owner lane | pair << 8, r_i, r_j
     alignas(16) float sb[QCAP][QSB];   // capsule-box: pa pb (box frame) h (9), r^2, owner lane
     int hit[64];                       // per-lane collision found by a drained item
-#ifdef RP_Q13
-    float2 prad[NPAIR];                // (r_i, r_j) of self pair P
-#endif
-#ifdef RP_BOX_LDS
-    // broad-phase words of the cluster scenes' boxes (lo.xyz, exempt bits | hi.xyz, -),
-    // one spare entry for the loop's read-ahead
-    float4 bp[GRID_MIN_BOXES + 1][2];
-#endif
 };
 static_assert(sizeof(WaveQ) <= 7680, "WaveQ must let 20 one-wave workgroups share a CU");
 
@@ -589,7 +530,6 @@ struct QueueState {
     int lane;
     float plane_z;
     unsigned env_far;   // DevScene::env_far if the wave is inside the joint limits, else 0
-    bool box_lds;     // the scene's boxes fit the wave's LDS copy (RP_BOX_LDS)
     ClusterRegs<NCL> cl;
 };
 
@@ -598,13 +538,8 @@ struct QueueState {
 // passes run full; the walk's end pops until empty. Room is guaranteed: a batch has
 // at most as many items as there are active lanes. (Draining whenever more than
 // QCAP - 64 items were pending ran more, emptier passes and needed a larger queue.)
-#ifdef RP_POP_NOINLINE
-#define RP_POP_INLINE __attribute__((noinline))
-#else
-#define RP_POP_INLINE __forceinline__
-#endif
 template <class S>
-__device__ RP_POP_INLINE void pop_ss(S& s) {
+__device__ __forceinline__ void pop_ss(S& s) {
     const unsigned long long act = __ballot(1);
     const int nact = __popcll(act), r = rank_in(act);
     const int take = s.nss < nact ? s.nss : nact;
@@ -614,30 +549,21 @@ __device__ RP_POP_INLINE void pop_ss(S& s) {
         const V3 a1 = {it[0], it[1], it[2]}, b1 = {it[3], it[4], it[5]};
         const V3 a2 = {it[6], it[7], it[8]}, b2 = {it[9], it[10], it[11]};
         const int tag = __float_as_int(it[12]);
-#ifdef RP_Q13
-        const float2 rr2 = s.Q->prad[tag >> 8];
-        const float ri = rr2.x, rj = rr2.y;
-#else
         const float ri = it[13], rj = it[14];
-#endif
         const Aabb u = capsule_aabb(a1, b1, ri);
         const Aabb v = capsule_aabb(a2, b2, rj);
         if (!aabb_disjoint2(u, v)) {
             const float rr = ri + rj;
-#ifndef RP_HIT_STORE
             // an LDS OR (ds_or_b32) from every popping lane instead of a store under a
             // per-lane branch: no exec-mask save / restore (+2.9 % goal3 A/B)
             atomicOr(&s.Q->hit[tag & 63], (int)(segment_segment_dist2(a1, b1, a2, b2) <= rr * rr));
-#else
-            if (segment_segment_dist2(a1, b1, a2, b2) <= rr * rr) s.Q->hit[tag & 63] = 1;
-#endif
         }
     }
     __builtin_amdgcn_wave_barrier();
     s.nss -= take;
 }
 template <class S>
-__device__ RP_POP_INLINE void pop_sb(S& s) {
+__device__ __forceinline__ void pop_sb(S& s) {
     const unsigned long long act = __ballot(1);
     const int nact = __popcll(act), r = rank_in(act);
     const int take = s.nsb < nact ? s.nsb : nact;
@@ -645,11 +571,7 @@ __device__ RP_POP_INLINE void pop_sb(S& s) {
     if (r < take) {
         const float* it = s.Q->sb[s.nsb - 1 - r];
         const V3 pa = {it[0], it[1], it[2]}, pb = {it[3], it[4], it[5]}, h = {it[6], it[7], it[8]};
-#ifndef RP_HIT_STORE
         atomicOr(&s.Q->hit[__float_as_int(it[10])], (int)(segment_box_dist2(pa, pb, h) <= it[9]));
-#else
-        if (segment_box_dist2(pa, pb, h) <= it[9]) s.Q->hit[__float_as_int(it[10])] = 1;
-#endif
     }
     __builtin_amdgcn_wave_barrier();
     s.nsb -= take;
@@ -684,23 +606,9 @@ template <int C, int NCL>
 __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __restrict__ sc,
                                            QueueState<NCL>& s) {
     constexpr float r = CAP_GEOM[C][6];
-#ifdef RP_AABB_LATE
-    // the plane test needs only lo.z; the rest of the AABB after the reach skip
-    if (fminr(k.a[C].z, k.b[C].z) - r <= s.plane_z) return true;   // capsule vs ground plane
-#ifndef RP_NO_ENV_FAR
-    if ((s.env_far >> C) & 1u) return false;   // no box within the capsule's reach (wave-uniform)
-#endif
-    const Aabb u = capsule_aabb(k.a[C], k.b[C], r);
-#else
     const Aabb u = capsule_aabb(k.a[C], k.b[C], r);
     if (u.lo.z <= s.plane_z) return true;  // capsule vs ground plane
-#ifdef RP_ABLATE_ENV
-    return false;
-#endif
-#ifndef RP_NO_ENV_FAR
     if ((s.env_far >> C) & 1u) return false;   // no box within the capsule's reach (wave-uniform)
-#endif
-#endif
     if constexpr (NCL == NCL_GRID) {
         // superset of the AABB-overlapping boxes from the axis grid (per-lane
         // gathers), then the exact AABB test on each candidate, one per lane per
@@ -717,14 +625,10 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
             if (m) {
                 bx = sc->box[__builtin_ctzll(m)];
                 m &= m - 1;
-#ifndef RP_GRID_CMP
                 // exempt bit and box test as one separation value (one lane mask;
                 // A/B clutter64 +9.7 %; -DRP_GRID_CMP builds the mask form)
                 const float ex = ((__float_as_uint(bx[14]) >> C) & 1u) ? __builtin_inff() : -__builtin_inff();
                 cand = fmaxr(ex, aabb_sep(u, bx + 8, bx + 11)) <= 0.0f;
-#else
-                cand = !((__float_as_uint(bx[14]) >> C) & 1u) && !aabb_disjoint(u, bx + 8, bx + 11);
-#endif
             }
             const unsigned long long bm = __ballot(cand);
             if (!bm) continue;
@@ -737,84 +641,18 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
 #pragma unroll
     for (int cl = 0; cl < NCL; ++cl) {
         const float* cr = s.cl.c[cl];
-#ifndef RP_ENV_CMP
         // cluster test, box test and exempt bit folded into one separation value:
         // candidate iff max(cluster sep, box sep, exempt ? inf : -inf) <= 0 (one lane
         // mask per box instead of three combined by scalar ops: A/B +1.9 % goal3 4M,
         // +1.6 % at 64k; -DRP_ENV_CMP builds the mask form)
         const float csep = aabb_sep(u, cr, cr + 4);
         if (!__any(csep <= 0.0f)) continue;
-#ifdef RP_ABLATE_BOX_LOOP
-        asm volatile("" ::"v"(csep));
-        continue;
-#endif
-#else
-        const bool near_cl = !aabb_disjoint(u, cr, cr + 4);
-        if (!__any(near_cl)) continue;
-#endif
         const int j0 = __float_as_int(cr[3]), nj = __float_as_int(cr[7]);
-#ifdef RP_BOX_LDS
-        // broad-phase words from the wave's LDS copy, the next box's read ahead of
-        // this box's test (LDS returns in order: no scalar-load round trip per box);
-        // scenes forced onto clusters with more boxes than the copy holds read the
-        // records below
-        if (s.box_lds) {
-        float4 A = s.Q->bp[j0][0], B = s.Q->bp[j0][1];
-        for (int j = j0; j < j0 + nj; ++j) {
-            const float4 nA = s.Q->bp[j + 1][0], nB = s.Q->bp[j + 1][1];
-            const float lo[3] = {A.x, A.y, A.z}, hi[3] = {B.x, B.y, B.z};
-            const float ex = ((__float_as_uint(A.w) >> C) & 1u) ? __builtin_inff() : -__builtin_inff();
-            const bool cand = fmaxr(fmaxr(csep, ex), aabb_sep(u, lo, hi)) <= 0.0f;
-            A = nA;
-            B = nB;
-            const unsigned long long m = __ballot(cand);
-            if (!m) continue;
-            room_sb(s, __popcll(m));
-            if (cand) enqueue_sb<C>(k, sc->box[j], r, s, m);
-            s.nsb += __popcll(m);
-        }
-        continue;
-        }
-#endif
-#ifdef RP_BOX_PIPE
-        // the next box's broad-phase words are loaded while this box is tested (a
-        // scalar-load round trip per box otherwise; the record past the cluster's
-        // last box is always inside DevScene and unused); the exempt bit is a
-        // scalar branch (wave-uniform), so the test is one compare and one branch
-        struct BRec { float lo[3], hi[3], ex; };
-        auto bload = [&](int jj) {
-            const float* b = sc->box[jj];
-            return BRec{{b[8], b[9], b[10]}, {b[11], b[12], b[13]}, b[14]};
-        };
-        BRec cur = bload(j0);
-        for (int j = j0; j < j0 + nj; ++j) {
-            const BRec nxt = bload(j + 1);
-            const bool exempt = (__float_as_uint(cur.ex) >> C) & 1u;
-            const bool cand = fmaxr(csep, aabb_sep(u, cur.lo, cur.hi)) <= 0.0f;
-            cur = nxt;
-            if (exempt) continue;
-            const unsigned long long m = __ballot(cand);
-            if (!m) continue;
-            room_sb(s, __popcll(m));
-            if (cand) enqueue_sb<C>(k, sc->box[j], r, s, m);
-            s.nsb += __popcll(m);
-        }
-        continue;
-#endif
         for (int j = j0; j < j0 + nj; ++j) {
             // the whole 64-B record in one scalar load; branch-free candidate test
             struct Rec { float v[16]; };
             const Rec rec = *reinterpret_cast<const Rec*>(sc->box[j]);
             const float* bx = rec.v;
-#ifdef RP_EXEMPT_BRANCH
-            if ((__float_as_uint(bx[14]) >> C) & 1u) continue;   // wave-uniform
-            const bool cand = fmaxr(csep, aabb_sep(u, bx + 8, bx + 11)) <= 0.0f;
-            const unsigned long long m = __ballot(cand);
-            if (!m) continue;
-            room_sb(s, __popcll(m));
-            if (cand) enqueue_sb<C>(k, bx, r, s, m);
-            s.nsb += __popcll(m);
-#elif !defined(RP_ENV_CMP)
             const float ex = ((__float_as_uint(bx[14]) >> C) & 1u) ? __builtin_inff() : -__builtin_inff();
             const bool cand = fmaxr(fmaxr(csep, ex), aabb_sep(u, bx + 8, bx + 11)) <= 0.0f;
             const unsigned long long m = __ballot(cand);
@@ -822,16 +660,6 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
             room_sb(s, __popcll(m));
             if (cand) enqueue_sb<C>(k, bx, r, s, m);
             s.nsb += __popcll(m);
-#else
-            const bool exempt = (__float_as_uint(bx[14]) >> C) & 1u;
-            const bool apart = aabb_disjoint(u, bx + 8, bx + 11);   // both evaluated: no branch
-            const bool cand = near_cl && !exempt && !apart;
-            const unsigned long long m = __ballot(cand);
-            if (!m) continue;
-            room_sb(s, __popcll(m));
-            if (cand) enqueue_sb<C>(k, bx, r, s, m);
-            s.nsb += __popcll(m);
-#endif
         }
     }
     return false;
@@ -860,14 +688,9 @@ template <int P>
 __device__ __forceinline__ bool pair_sphere(const Capsules& k) {
     constexpr int I = PAIRS[P][0], J = PAIRS[P][1];
     constexpr float RS = sphere_radius<I>() + sphere_radius<J>();
-#ifndef RP_SPHERE_PAIRSUM
     // the centres' sums made once per capsule (place): -6 VALU per pair, 25 pairs per
     // state; the same values (the same two adds), so the same bools
     const V3 d = {k.m[I].x - k.m[J].x, k.m[I].y - k.m[J].y, k.m[I].z - k.m[J].z};
-#else
-    const V3 d = {(k.a[I].x + k.b[I].x) - (k.a[J].x + k.b[J].x), (k.a[I].y + k.b[I].y) - (k.a[J].y + k.b[J].y),
-                  (k.a[I].z + k.b[I].z) - (k.a[J].z + k.b[J].z)};
-#endif
     // |centre_I - centre_J| <= RS  <=>  |2 centre_I - 2 centre_J|^2 <= (2 RS)^2
     return dot3(d, d) <= (2.0f * RS) * (2.0f * RS);
 }
@@ -876,23 +699,10 @@ __device__ __forceinline__ bool pair_sphere(const Capsules& k) {
 template <int P, class S>
 __device__ __forceinline__ void pair_enqueue(const Capsules& k, S& s, bool cand, unsigned long long m) {
     constexpr int I = PAIRS[P][0], J = PAIRS[P][1];
-#ifndef RP_PAIR_NOBRANCH
     if (!m) return;
-#endif
-#ifdef RP_ABLATE_SELF_ENQ
-    asm volatile("" ::"s"(m));
-    return;
-#endif
     room_ss(s, __popcll(m));
     if (cand) {
         float* it = s.Q->ss[s.nss + rank_in(m)];
-#ifdef RP_Q13
-        float4* it4 = reinterpret_cast<float4*>(it);
-        it4[0] = make_float4(k.a[I].x, k.a[I].y, k.a[I].z, k.b[I].x);
-        it4[1] = make_float4(k.b[I].y, k.b[I].z, k.a[J].x, k.a[J].y);
-        it4[2] = make_float4(k.a[J].z, k.b[J].x, k.b[J].y, k.b[J].z);
-        it[12] = __int_as_float(s.lane | (P << 8));
-#else
         it[0] = k.a[I].x; it[1] = k.a[I].y; it[2] = k.a[I].z;
         it[3] = k.b[I].x; it[4] = k.b[I].y; it[5] = k.b[I].z;
         it[6] = k.a[J].x; it[7] = k.a[J].y; it[8] = k.a[J].z;
@@ -900,7 +710,6 @@ __device__ __forceinline__ void pair_enqueue(const Capsules& k, S& s, bool cand,
         it[12] = __int_as_float(s.lane | (P << 8));
         it[13] = CAP_GEOM[I][6];
         it[14] = CAP_GEOM[J][6];
-#endif
     }
     s.nss += __popcll(m);
 }
@@ -932,26 +741,6 @@ __device__ __forceinline__ void pairs_each(const Capsules& k, S& s) {
         // limits test them afterwards (never_pairs_outside_limits)
         if constexpr (!pair_never(L.p[T])) {
             constexpr int P = L.p[T], I = PAIRS[P][0];
-#ifdef RP_HAND_CONTAIN
-            // Inside the joint limits the finger capsules lie inside the hand capsule's
-            // bounding sphere (finger tips <= 0.0882 m from the hand capsule's centre at
-            // finger travel <= 0.04; the sphere is 0.0901 m: 1.9 mm to spare, far above
-            // rounding), so a capsule whose sphere misses the hand's misses the
-            // fingers: their pairs are candidates only after (I, hand) passed, and a
-            // wave where no lane's (I, hand) passed skips the finger tests. Exact
-            // reject: same flags.
-            if constexpr (J == C_HAND) {
-                const bool cand = pair_sphere<P>(k);
-                s.hand_near |= (cand ? 1u : 0u) << I;
-                pair_enqueue<P>(k, s, cand, __ballot(cand));
-            } else if constexpr (J == C_LFINGER || J == C_RFINGER) {
-                const bool near = ((s.hand_near >> I) & 1u) != 0u;
-                if (!s.in_limits || __any(near)) {
-                    const bool cand = (near || !s.in_limits) && pair_sphere<P>(k);
-                    pair_enqueue<P>(k, s, cand, __ballot(cand));
-                }
-            } else
-#endif
             {
                 const bool cand = pair_sphere<P>(k);
                 pair_enqueue<P>(k, s, cand, __ballot(cand));
@@ -980,9 +769,7 @@ struct QueuedVisit {
         if constexpr (C == C_LINK6) RP_STAMP(3);
         if constexpr (C == C_HAND) RP_STAMP(4);
         if (env_queued<C>(k, sc, s)) return true;
-#ifndef RP_ABLATE_SELF
         pairs_queued<C>(k, s);
-#endif
         return false;
     }
 };
@@ -1023,18 +810,12 @@ __device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene
     v.s.nsb = 0;
     v.s.lane = (int)__lane_id();
     {
-#ifndef RP_LIM_CMP
         // q_j in [lo_j, hi_j] for all j <=> max_j max(lo_j - q_j, q_j - hi_j) <= 0 (the
         // aabb_disjoint argument; one lane mask instead of 18 ANDed: +1.9 % goal3 A/B)
         float ex = -__builtin_inff();
 #pragma unroll
         for (int j = 0; j < NQ; ++j) ex = fmaxr(ex, fmaxr(Q_LO_F[j] - q[j], q[j] - Q_HI_F[j]));
         const bool in = ex <= 0.0f;
-#else
-        bool in = true;
-#pragma unroll
-        for (int j = 0; j < NQ; ++j) in = in && q[j] >= Q_LO_F[j] && q[j] <= Q_HI_F[j];
-#endif
         v.s.in_limits = !__any(!in);
     }
     v.s.plane_z = sc->plane_z;
@@ -1042,22 +823,7 @@ __device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene
     v.s.hand_near = 0u;
     v.s.cl.load(sc);
     Q.hit[v.s.lane] = 0;
-#ifdef RP_Q13
-    if (v.s.lane < NPAIR) Q.prad[v.s.lane] = make_float2(PAIR_RAD[v.s.lane][0], PAIR_RAD[v.s.lane][1]);
-#endif
-#ifdef RP_BOX_LDS
-    v.s.box_lds = sc->n_boxes <= GRID_MIN_BOXES;
-    if constexpr (NCL > 0) {
-        const int l = v.s.lane;
-        if (l < 2 * (GRID_MIN_BOXES + 1)) {
-            const float* bx = sc->box[l >> 1];
-            Q.bp[l >> 1][l & 1] = (l & 1) ? make_float4(bx[11], bx[12], bx[13], 0.0f)
-                                          : make_float4(bx[8], bx[9], bx[10], bx[14]);
-        }
-    }
-#endif
     __builtin_amdgcn_wave_barrier();
-#ifndef RP_SC_WALK
     // the 7 joint sin / cos first: independent chains, interleaved, instead of one
     // exposed polynomial chain per link (the same function of q: the same bits;
     // A/B +5 % goal3 4M states, +1.5 % at 64k, clutter64 +-0; -DRP_SC_WALK builds
@@ -1066,9 +832,6 @@ __device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene
 #pragma unroll
     for (int i = 0; i < 7; ++i) rp_sincos(q[i], &jt.s[i], &jt.c[i]);
     if (fk_walk_j<QueuedVisit<NCL>, BF>(q, jt, sc->base, k, v)) return true;
-#else
-    if (fk_walk<QueuedVisit<NCL>, BF>(q, sc, k, v)) return true;
-#endif
     if (!v.s.in_limits) never_pairs_outside_limits(q, sc, v.s);
     RP_STAMP(5);
     while (v.s.nsb > 0) pop_sb(v.s);

@@ -51,6 +51,11 @@ __device__ __forceinline__ void split16(double v, _Float16& hi, _Float16& lo) {
     lo = (_Float16)(vf - (float)hi);
 }
 
+// rank of this lane among the set lanes of m (ballot + mbcnt)
+__device__ __forceinline__ int rank_lanes(unsigned long long m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // LDS ordering between the lanes of one wave (stores, then other lanes' loads)
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -79,9 +84,13 @@ __device__ __forceinline__ h8 a_frag(const NnMfma& P, const double* x, bool live
     thr_slots(P, __builtin_inf(), na, hh, hl);
     const _Float16 z = (_Float16)0.0f, mg = (_Float16)(-P.G2);
     h8 a;
-    if (!live) {   // no query: Q = -65504 * 2^H < 0 for every node
+    if (!live) {   // no query: Q = -2^G |y'|^2 S^2 / 2 - 65504 * 2^H < 0 for every node (dead pads too)
         a = h8{z, z, z, z, z, z, z, z};
-        if (ch == 3) a[5] = (_Float16)(-65504.0f);
+        if (ch == 3) {
+            a[3] = mg;
+            a[4] = mg;
+            a[5] = (_Float16)(-65504.0f);
+        }
     } else if (ch == 0) {
         a = h8{xh[0], xh[1], xh[2], xh[3], xh[4], xh[5], xh[6], xh[7]};
     } else if (ch == 1) {
@@ -117,12 +126,22 @@ __device__ __forceinline__ h8 b_frag(const NnMfma& P, const double* y, int ch) {
 }
 
 // B operand images of tree nodes [t0, t1): img[node][32] f16 (64 B), made once per
-// node and plan (the searches read them; rp_lib.hip keeps a per-tree count)
+// node and plan (the searches read them; rp_lib.hip keeps a per-tree count). The
+// slots [t1, round_up(t1, NNM_PAD)) get a dead image that no query passes (norm slots
+// 65504 against -2^G, no threshold slots: Q = -2^(G+1) 65504 < 0), so the search's
+// tiles need no bounds test; the buffer holds NNM_PAD spare nodes.
+constexpr int NNM_PAD = 64;
 __global__ void k_nn_image(const double* __restrict__ tree, int64_t t0, int64_t t1, NnMfma P, h8* __restrict__ img) {
     const int64_t i = (int64_t)rp_bid() * rp_bdim() + rp_tid();
     const int64_t node = t0 + (i >> 2);
     const int ch = (int)(i & 3);
-    if (node >= t1) return;
+    const int64_t tpad = (t1 + NNM_PAD - 1) / NNM_PAD * NNM_PAD;
+    if (node >= tpad) return;
+    if (node >= t1) {
+        const _Float16 z = (_Float16)0.0f, big = (_Float16)65504.0f;
+        img[node * 4 + ch] = ch == 3 ? h8{z, z, z, big, big, z, z, z} : h8{z, z, z, z, z, z, z, z};
+        return;
+    }
     double y[NQ];
 #pragma unroll
     for (int d = 0; d < NQ; ++d) y[d] = tree[node * NQ + d];
@@ -155,6 +174,17 @@ __device__ unsigned long long g_nncount[4];
 #define RP_NNC(i, v) do { } while (0)
 #endif
 
+// Exact path: the (row, node) pairs that pass the filter are
+// appended to a per-wave LDS list (a ballot and a prefix count per round, no
+// barrier); the list is evaluated 64 pairs at a time (one per lane: the exact f64
+// distance and the lexicographic (distance, index) update of the row, three wave
+// LDS syncs per 64 pairs) when it holds NNM_FLUSH pairs and at the end of the range,
+// and only then are the rows' threshold slots tightened. The deferred tightening
+// lets a few more nodes through; the result does not depend on the order in which
+// a row's candidates are evaluated (the range's lexicographic minimum).
+constexpr int NNM_FLUSH = 64;
+constexpr int NNM_CAND = NNM_FLUSH + 64;   // a round appends at most one pair per lane
+
 template <int RB, int W>
 __global__ __launch_bounds__(64 * W) void k_nn_mfma(const double* __restrict__ qx, int64_t n,
                                                           const int* status, int64_t t0,
@@ -166,6 +196,7 @@ __global__ __launch_bounds__(64 * W) void k_nn_mfma(const double* __restrict__ q
     __shared__ unsigned long long s_best[W][QW];            // exact best distance (f64 bits; >= 0)
     __shared__ int s_bi[W][QW];                             // its node (lowest index among equal)
     __shared__ int s_ti[W][QW];                             // a round's lowest node at the new best
+    __shared__ int2 s_cand[W][NNM_CAND];                    // passing (row, node) pairs, not yet evaluated
     if (status) n = min(n, (int64_t)status[0] - t0);
     int64_t qb, yr;
     nn_block_coords(qblocks, &qb, &yr);
@@ -225,103 +256,111 @@ __global__ __launch_bounds__(64 * W) void k_nn_mfma(const double* __restrict__ q
             a[rb][6] = hl;
         }
     }
+    int ncand = 0;   // wave-uniform
+    // evaluate the listed pairs, then tighten the rows' threshold slots
+    auto flush = [&]() {
+        wave_lds_sync();   // the list's writes
+        for (int b0 = 0; b0 < ncand; b0 += 64) {
+            RP_NNC(2, 1);
+            const int k = b0 + lane;
+            const bool has = k < ncand;
+            int row = 0, node = 0;
+            unsigned long long prev = 0, db = 0;
+            if (has) {
+                const int2 cnd = s_cand[w][k];
+                row = cnd.x;
+                node = cnd.y;
+                prev = s_best[w][row];
+                s_ti[w][row] = 0x7fffffff;
+                db = (unsigned long long)__double_as_longlong(dist2(tree + (int64_t)node * NQ, &s_q[w][row][0]));
+            }
+            wave_lds_sync();
+            if (has) atomicMin(&s_best[w][row], db);
+            wave_lds_sync();
+            const unsigned long long cur = has ? s_best[w][row] : 0ull;
+            if (has && db == cur) atomicMin(&s_ti[w][row], node);
+            wave_lds_sync();
+            if (has && db == cur && s_ti[w][row] == node) {   // the row's lowest node at its new best
+                if (cur < prev) s_bi[w][row] = node;
+                else if (node < s_bi[w][row]) s_bi[w][row] = node;
+            }
+            wave_lds_sync();
+        }
+        ncand = 0;
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) {
+            const int r = rb * 16 + (lane & 15);
+            const double bnow = __longlong_as_double((long long)s_best[w][r]);
+            if (ch == 3 && bnow != curb[rb]) {
+                curb[rb] = bnow;
+                _Float16 hh, hl;
+                thr_slots(P, bnow, na[rb], hh, hl);
+                a[rb][5] = hh;
+                a[rb][6] = hl;
+            }
+        }
+    };
     // Each wave streams its range's node images itself, B fragments straight from
-    // global memory (L2: the XCD-grouped blocks of a range read the same lines)
-    // prefetched PF column tiles ahead; there is no block barrier, so a wave in its
-    // exact path holds up no other wave.
-    // (Measured and not kept: the f64 states of the tile staged in LDS for the exact
-    // path, and 4-wave LDS staging of the images behind block barriers: the same
-    // rate, more registers.)
+    // global memory (L2: the XCD-grouped blocks of a range read the same lines),
+    // PF column tiles ahead: every load lands in a fixed register that the MFMAs of
+    // its tile read PF tiles later (no register rotation, which made the compiler
+    // wait for each tile's freshly issued load), and loads past the range re-read its
+    // last tile (unconditional: static vmcnt waits). Tiles need no bounds test: the
+    // image's pad slots and dead query rows never pass (k_nn_image, a_frag).
     constexpr int PF = 4;
     const int64_t ntiles = (t_hi - t_lo + 15) / 16;
     const int col = lane & 15;   // this lane's column of every tile
-    const h8 hz = {};
+    const h8* ib = img + (t_lo + col) * 4 + ch;   // tile t: ib[t * 64]
     h8 bq[PF];
 #pragma unroll
-    for (int u = 0; u < PF; ++u) {
-        const int64_t j = t_lo + (int64_t)u * 16 + col;
-        bq[u] = j < t_hi ? img[j * 4 + ch] : hz;
-    }
+    for (int u = 0; u < PF; ++u) bq[u] = ib[min<int64_t>(u, ntiles - 1) * 64];
     const f4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
-    for (int64_t tb = 0; tb < ntiles; tb += PF) {
+    auto tile_step = [&](int64_t tile, const h8& b) {
+        f4 acc[RB];
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rb], b, zero, 0, 0, 0);
+        // this lane's column: acc[rb][e] = row rb * 16 + 4 ch + e
+        float m = fmaxf(fmaxf(acc[0][0], acc[0][1]), fmaxf(acc[0][2], acc[0][3]));
+#pragma unroll
+        for (int rb = 1; rb < RB; ++rb) m = fmaxf(m, fmaxf(fmaxf(acc[rb][0], acc[rb][1]), fmaxf(acc[rb][2], acc[rb][3])));
+        RP_NNC(0, 1);
+        if (!__any(m >= 0.0f)) return;
+        RP_NNC(1, 1);
+        unsigned pm = 0;
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) pm |= (acc[rb][e] >= 0.0f ? 1u : 0u) << (rb * 4 + e);
+        const int node = (int)(t_lo + tile * 16 + col);
+#ifdef RP_NN_COUNT
+        {
+            unsigned tot = __popc(pm);
+            for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+            RP_NNC(3, tot);
+        }
+#endif
+        while (__any(pm != 0)) {
+            const bool has = pm != 0;
+            const int e = has ? __builtin_ctz(pm) : 0;
+            pm &= pm - 1;
+            const unsigned long long bm = __ballot(has);
+            if (has) s_cand[w][ncand + rank_lanes(bm)] = int2{(e >> 2) * 16 + ch * 4 + (e & 3), node};
+            ncand += __popcll(bm);
+            if (ncand >= NNM_FLUSH) flush();
+        }
+    };
+    int64_t tb = 0;
+    for (; tb + PF <= ntiles; tb += PF) {
 #pragma unroll
         for (int u = 0; u < PF; ++u) {
-            const int64_t tile = tb + u;
-            if (tile >= ntiles) break;   // (uniform)
-            const h8 b = bq[u];
-            {
-                const int64_t j = t_lo + (tile + PF) * 16 + col;
-                bq[u] = j < t_hi ? img[j * 4 + ch] : hz;
-            }
-            const int64_t base = t_lo + tile * 16;
-            const bool live = base + col < t_hi;
-            f4 acc[RB];
-#pragma unroll
-            for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rb], b, zero, 0, 0, 0);
-            // this lane's column: acc[rb][e] = row rb * 16 + 4 ch + e
-            float m = -1.0f;
-            if (live) {
-#pragma unroll
-                for (int rb = 0; rb < RB; ++rb) m = fmaxf(m, fmaxf(fmaxf(acc[rb][0], acc[rb][1]), fmaxf(acc[rb][2], acc[rb][3])));
-            }
-            RP_NNC(0, 1);
-            if (!__any(m >= 0.0f)) continue;
-            RP_NNC(1, 1);
-            // ---- exact path: the passing (row, node) pairs, in rounds of one per lane
-            unsigned pm = 0;
-            if (live) {
-#pragma unroll
-                for (int rb = 0; rb < RB; ++rb)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e) pm |= (acc[rb][e] >= 0.0f ? 1u : 0u) << (rb * 4 + e);
-            }
-            const int node = (int)(base + col);
-#ifdef RP_NN_COUNT
-            {
-                unsigned tot = __popc(pm);
-                for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
-                RP_NNC(3, tot);
-            }
-#endif
-            while (__any(pm != 0)) {
-                RP_NNC(2, 1);
-                const bool has = pm != 0;
-                const int e = has ? __builtin_ctz(pm) : 0;
-                pm &= pm - 1;
-                const int row = (e >> 2) * 16 + ch * 4 + (e & 3);
-                unsigned long long prev = 0, db = 0;
-                if (has) {
-                    prev = s_best[w][row];
-                    s_ti[w][row] = 0x7fffffff;
-                    db = (unsigned long long)__double_as_longlong(dist2(tree + (int64_t)node * NQ, &s_q[w][row][0]));
-                }
-                wave_lds_sync();
-                if (has) atomicMin(&s_best[w][row], db);
-                wave_lds_sync();
-                const unsigned long long cur = has ? s_best[w][row] : 0ull;
-                if (has && db == cur) atomicMin(&s_ti[w][row], node);
-                wave_lds_sync();
-                if (has && db == cur && s_ti[w][row] == node) {   // the row's lowest node at its new best
-                    if (cur < prev) s_bi[w][row] = node;
-                    else if (node < s_bi[w][row]) s_bi[w][row] = node;
-                }
-                wave_lds_sync();
-            }
-            // rows whose best improved: new threshold slots (chunk-3 lanes)
-#pragma unroll
-            for (int rb = 0; rb < RB; ++rb) {
-                const int r = rb * 16 + (lane & 15);
-                const double bnow = __longlong_as_double((long long)s_best[w][r]);
-                if (ch == 3 && bnow != curb[rb]) {
-                    curb[rb] = bnow;
-                    _Float16 hh, hl;
-                    thr_slots(P, bnow, na[rb], hh, hl);
-                    a[rb][5] = hh;
-                    a[rb][6] = hl;
-                }
-            }
+            tile_step(tb + u, bq[u]);
+            bq[u] = ib[min<int64_t>(tb + u + PF, ntiles - 1) * 64];
         }
     }
+#pragma unroll
+    for (int u = 0; u < PF; ++u)
+        if (tb + u < ntiles) tile_step(tb + u, bq[u]);
+    if (ncand > 0) flush();
     wave_lds_sync();
     for (int r = lane; r < QW; r += 64) {
         const int64_t q = qw0 + r;

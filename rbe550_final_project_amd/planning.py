@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import logging
 import os
+import time
 from typing import Any
 
 import numpy as np
@@ -179,8 +180,10 @@ class PlannerInterface:
         self.scene = scene
         self.attached_object = None
         self._ctx = None
+        self._scene_cache = {}
         self.last_status = None
         self.last_stats = None
+        self.last_timing = None
 
     # -- GPU context -----------------------------------------------------------
     def _context(self):
@@ -191,7 +194,7 @@ class PlannerInterface:
     def _sync_scene(self):
         """Push the current obstacle geometry (boxes at their simulated poses) and
         the attached box to the GPU context."""
-        sc = scenes.from_genesis(self.scene, self.robot)
+        sc = scenes.from_genesis(self.scene, self.robot, cache=self._scene_cache)
         ctx = self._context()
         ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
         idx = -1
@@ -233,6 +236,7 @@ class PlannerInterface:
     # -- the query (planning.py:59-207) -----------------------------------------
     def plan_path(self, qpos_goal, qpos_start=None, timeout=5.0, smooth_path=True, num_waypoints=100,
                   attached_object=None, planner="RRTConnect"):
+        t_enter = time.perf_counter()
         if planner not in SUPPORTED_PLANNERS:
             _raise(f"Planner {planner} is not supported. Supported planners: {SUPPORTED_PLANNERS}.")
         if planner != "RRTConnect":
@@ -260,6 +264,7 @@ class PlannerInterface:
         self.attached_object = attached_object
         ctx = self._context()
         self._sync_scene()
+        t_scene = time.perf_counter()
 
         si = _SpaceInfo(lo, hi)
         eps = np.finfo(np.float64).eps
@@ -271,29 +276,32 @@ class PlannerInterface:
         if not goal_in:
             _logger().warning("OMPL goal state out of bounds")
             self.diagnose_bounds_violation(si, qpos_goal)
-        flags = ctx.check_states(np.stack([qpos_start, qpos_goal]).astype(np.float32))
-        if not flags[0]:
-            _logger().warning("OMPL start state invalid")
-            self.diagnose_valid_violation(qpos_start)
-        if not flags[1]:
-            _logger().warning("OMPL goal state invalid")
-            self.diagnose_valid_violation(qpos_goal)
 
         params = _abi.make_params(seed=_next_seed(), batch=_batch(), timeout_s=float(timeout),
                                   n_waypoints=int(num_waypoints) if num_waypoints else 0,
                                   simplify=bool(smooth_path), tree_capacity=_CONFIG["tree_capacity"] or 0,
                                   straight_first=_straight_first())
         cap = max(4096, int(num_waypoints or 0) + 16)
+        t_plan0 = time.perf_counter()
         try:
             path, status = ctx.plan(qpos_start, qpos_goal, lo, hi, params, path_cap=cap)
+            t_plan1 = time.perf_counter()
             self.last_stats = ctx.stats()
         except NativeError as ex:
             # the reference never raises on a failed plan (planning.py:190-202):
             # a library error (capacity, HIP) is reported and planning "fails"
             _logger().warning(f"MI355X planner error: {ex}")
             path, status = None, _abi.STATUS_NONE
+            t_plan1 = time.perf_counter()
             self.last_stats = None
         self.last_status = status
+        # planning.py:174-183 validity diagnostics. rp_plan checks the start and the
+        # goal itself (INVALID_START / INVALID_GOAL, as OMPL's planner does), so a
+        # separate check launch is only needed when one of them can be invalid: the
+        # plan reported it, a bound is violated, or the plan did not run
+        if status in (_abi.STATUS_INVALID_START, _abi.STATUS_INVALID_GOAL) or path is None \
+                or not (start_in and goal_in):
+            self._diagnose_start_goal(ctx, qpos_start, qpos_goal)
 
         waypoints = []
         if status in (_abi.STATUS_EXACT, _abi.STATUS_APPROXIMATE):
@@ -304,7 +312,27 @@ class PlannerInterface:
             _logger().warning("Path planning failed. Returning empty path.")
 
         self.robot.set_qpos(qpos_cur)
+        t_exit = time.perf_counter()
+        # where the call's wall time went (ms): scene ingestion (entity poses -> boxes,
+        # rp_set_scene / rp_set_attached), rp_plan itself, and everything else (argument
+        # checks, bounds, diagnostics, the waypoint tensors, restoring qpos)
+        self.last_timing = {"total_ms": 1e3 * (t_exit - t_enter), "scene_ms": 1e3 * (t_scene - t_enter),
+                            "rp_plan_ms": 1e3 * (t_plan1 - t_plan0),
+                            "other_ms": 1e3 * ((t_exit - t_enter) - (t_scene - t_enter) - (t_plan1 - t_plan0))}
         return waypoints
+
+    def _diagnose_start_goal(self, ctx, qpos_start, qpos_goal):
+        try:
+            flags = ctx.check_states(np.stack([qpos_start, qpos_goal]).astype(np.float32))
+        except NativeError as ex:
+            _logger().warning(f"MI355X planner error: {ex}")
+            return
+        if not flags[0]:
+            _logger().warning("OMPL start state invalid")
+            self.diagnose_valid_violation(qpos_start)
+        if not flags[1]:
+            _logger().warning("OMPL goal state invalid")
+            self.diagnose_valid_violation(qpos_goal)
 
     # -- goal configurations (motion_primitives.py:131-134) ----------------------
     def inverse_kinematics(self, pos, quat, init_qpos=None, n_seeds=256, iters=64, attached_object=None):
@@ -356,7 +384,10 @@ class PlannerInterface:
 
     @staticmethod
     def _states_to_tensor_list(path):
-        return [torch.tensor(row, dtype=torch.float32) for row in np.asarray(path)]
+        """planning.py:232-242: one float32 CPU tensor (n_qs,) per waypoint. The
+        rows are views of one (n, n_qs) tensor made with a single conversion (150
+        torch.tensor constructions cost ~0.8 ms, the views ~0.2 ms)."""
+        return list(torch.from_numpy(np.ascontiguousarray(path, dtype=np.float32)).unbind(0))
 
     def _ompl_state_to_tensor(self, state):
         return torch.tensor([float(state[i]) for i in range(self.robot.n_qs)], dtype=torch.float32)

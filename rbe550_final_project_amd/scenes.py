@@ -162,47 +162,86 @@ def _to_np(x):
     return np.asarray(x, dtype=float).reshape(-1)
 
 
+def _floats(x, n):
+    """The first n values of a pose vector as Python floats: one .tolist() for a
+    torch tensor (one device read when it lives on the GPU), else via numpy."""
+    if hasattr(x, "tolist") and not isinstance(x, np.ndarray):
+        v = x.tolist()
+        if len(v) >= n and not isinstance(v[0], list):
+            return [float(a) for a in v[:n]]
+    return [float(a) for a in _to_np(x)[:n]]
+
+
 def yaw_of_quat(q):
     """Rotation about world z of a (w, x, y, z) quaternion (tilt is ignored)."""
     w, x, y, z = (float(v) for v in q)
     return math.atan2(2.0 * (w * z + x * y), 1.0 - 2.0 * (y * y + z * z))
 
 
-def from_genesis(scene, robot=None):
-    """Boxes of a Genesis scene: every entity whose morph is a Box, at its current
-    pose (entity.get_pos / get_quat). Planes are taken as the ground at z = 0."""
-    s = Scene()
-    entities = getattr(scene, "entities", None)
-    if entities is None and hasattr(scene, "sim"):
-        entities = scene.sim.entities
-    base = BASE
-    plane_z = 0.0
-    raw_robot = getattr(robot, "robot", robot)
-    for ent in entities or []:
+def _entity_table(entities, raw_robot, robot):
+    """Per-entity static data: ("robot" | "plane" | "box" | None, payload). The box
+    payload is (half extents, entity index); the plane's is its height."""
+    table = []
+    for ent in entities:
         morph = getattr(ent, "morph", None)
         kind = type(morph).__name__ if morph is not None else ""
         if ent is raw_robot or ent is robot:
+            table.append(("robot", None))
+        elif kind == "Plane":
+            table.append(("plane", float(_to_np(getattr(morph, "pos", (0.0, 0.0, 0.0)))[2])))
+        elif kind == "Box":
+            size = getattr(morph, "size", None)
+            if size is None:
+                lo, hi = np.asarray(morph.lower, float), np.asarray(morph.upper, float)
+                size = hi - lo
+            half = tuple(float(v) / 2.0 for v in _to_np(size)[:3])
+            table.append(("box", (half, getattr(ent, "idx", None))))
+        else:
+            table.append((None, None))
+    return table
+
+
+def from_genesis(scene, robot=None, cache=None):
+    """Boxes of a Genesis scene: every entity whose morph is a Box, at its current
+    pose (entity.get_pos / get_quat). Planes are taken as the ground at z = 0.
+
+    cache: a dict owned by the caller (one per PlannerInterface). The entities'
+    static data (morph kind, box size, plane height) is kept there while the
+    scene's entity list is the same objects, so a call reads only the poses."""
+    entities = getattr(scene, "entities", None)
+    if entities is None and hasattr(scene, "sim"):
+        entities = scene.sim.entities
+    entities = list(entities or [])
+    raw_robot = getattr(robot, "robot", robot)
+    table = None
+    if cache is not None:
+        ents = cache.get("entities")
+        if ents is not None and len(ents) == len(entities) and cache.get("robot") is raw_robot \
+                and all(a is b for a, b in zip(ents, entities)):
+            table = cache["table"]
+    if table is None:
+        table = _entity_table(entities, raw_robot, robot)
+        if cache is not None:
+            cache.update(entities=entities, robot=raw_robot, table=table)
+    s = Scene()
+    base = BASE
+    plane_z = 0.0
+    for ent, (kind, data) in zip(entities, table):
+        if kind == "box":
+            half, idx = data
+            pos = _floats(ent.get_pos(), 3)
+            quat = _floats(ent.get_quat(), 4) if hasattr(ent, "get_quat") else (1.0, 0.0, 0.0, 0.0)
+            s.boxes.append((tuple(pos), half, yaw_of_quat(quat)))
+            s.names.append(str(idx if idx is not None else len(s.names)))
+            s.entity_idx.append(idx)
+        elif kind == "robot":
             if hasattr(ent, "get_pos"):
-                base = tuple(_to_np(ent.get_pos())[:3])
-            continue
-        if kind == "Plane":
-            plane_z = float(_to_np(getattr(morph, "pos", (0.0, 0.0, 0.0)))[2])
-            continue
-        if kind != "Box":
-            continue
-        size = getattr(morph, "size", None)
-        if size is None:
-            lo, hi = np.asarray(morph.lower, float), np.asarray(morph.upper, float)
-            size = hi - lo
-        half = tuple(float(v) / 2.0 for v in _to_np(size)[:3])
-        pos = _to_np(ent.get_pos())[:3]
-        quat = _to_np(ent.get_quat())[:4] if hasattr(ent, "get_quat") else (1.0, 0.0, 0.0, 0.0)
-        s.boxes.append((tuple(float(v) for v in pos), half, yaw_of_quat(quat)))
-        s.names.append(str(getattr(ent, "idx", len(s.names))))
-        s.entity_idx.append(getattr(ent, "idx", None))
+                base = tuple(_floats(ent.get_pos(), 3))
+        elif kind == "plane":
+            plane_z = data
     if robot is not None and hasattr(robot, "get_pos"):
         try:
-            base = tuple(_to_np(robot.get_pos())[:3])
+            base = tuple(_floats(robot.get_pos(), 3))
         except Exception:
             pass
     s.base = base

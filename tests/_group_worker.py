@@ -54,7 +54,7 @@ def main():
             ctx.set_attached(q["attached"])
             p = _abi.make_params(seed=c["seed"], batch=c["batch"], batch_min=c.get("batch_min", 0), n_waypoints=150,
                                  timeout_s=3600.0, straight_first=False, tree_capacity=1 << 23,
-                                 max_iters=c.get("max_iters", 0))
+                                 max_iters=c.get("max_iters", 0), group_repl=c.get("group_repl", 0))
             log(f"{tag} {c['name']} ...")
             path, st = ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
             s = ctx.stats()
@@ -76,8 +76,10 @@ def main():
         sc = scenes.Scene.from_json(q["scene"])
         ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
         ctx.set_attached(q["attached"])
+        # every iteration sharded (group_repl < 0): a rank planning alone waits at the
+        # first exchange
         p = _abi.make_params(seed=c["seed"], batch=c["batch"], n_waypoints=150, timeout_s=3600.0,
-                             straight_first=False)
+                             straight_first=False, group_repl=-1)
         dist.barrier()
         if rank == 0:
             os.environ["RBE_WAIT_WATCHDOG_S"] = "2"

@@ -120,3 +120,40 @@ def test_validity_robot_base(gpu_ctx, oracle_lib, base, name):
     o = _pair(gpu_ctx, oracle_lib, sc)
     q = (model.Q_LO + (model.Q_HI - model.Q_LO) * np.random.default_rng(8).random((1 << 17, 9))).astype(np.float32)
     assert np.array_equal(gpu_ctx.check_states(q), o.check_states(q))
+
+
+def _clusters(rng, n_clusters, jitter):
+    """n_clusters groups of 64 near-identical states (one wave each): whenever a
+    broad phase passes for one lane it passes for all 64 at once, so every queue
+    batch is a full wave (a 64-item batch after a pop pass)."""
+    base = model.Q_LO + (model.Q_HI - model.Q_LO) * rng.random((n_clusters, 1, 9))
+    q = base + jitter * rng.standard_normal((n_clusters, 64, 9))
+    return np.clip(q, model.Q_LO, model.Q_HI).reshape(-1, 9).astype(np.float32)
+
+
+@pytest.mark.parametrize("name", ["goal3", "clutter64"])
+@pytest.mark.parametrize("jitter", [0.0, 1e-4, 2e-3])
+def test_wave_saturated_queues(gpu_ctx, oracle_lib, name, jitter):
+    """Waves whose 64 states are (near-)identical: box and self-pair candidates
+    arrive 64 at a time, so the narrow-phase queues take full-wave batches right
+    after a pop pass. Flags bit-exact (single states and edges)."""
+    import json
+    import os
+    if name == "goal3":
+        sc = scenes.goal3_tallest()
+    else:
+        gold = os.path.join(os.path.dirname(__file__), "golden", "workloads", "clutter64.json")
+        sc = scenes.Scene.from_json(json.load(open(gold))["queries"][0]["scene"])
+    o = _pair(gpu_ctx, oracle_lib, sc, attached=3)
+    rng = np.random.default_rng(int(jitter * 1e5) + len(name))
+    q = _clusters(rng, 2048, jitter)
+    g = gpu_ctx.check_states(q)
+    c = o.check_states(q)
+    assert np.array_equal(g, c), f"{(g != c).sum()} of {len(q)} flags differ"
+    # both outcomes occur, so a corrupted hit word would show
+    assert 0 < c.sum() < len(c)
+    a = _clusters(rng, 256, jitter).astype(np.float64)
+    b = a + 0.02 * rng.standard_normal(a.shape)
+    b = np.clip(b, model.Q_LO, model.Q_HI)
+    res = 0.01 * model.max_extent()
+    assert np.array_equal(gpu_ctx.check_edges(a, b, res), o.check_edges(a, b, res))

@@ -43,16 +43,23 @@ class ThreadGroup:
 
 @pytest.mark.parametrize("wl,qi,batch", [("goal4_pentagon_10box", 2, 64), ("goal3_tallest_10box", 5, 256),
                                          ("clutter64", 0, 128)])
-@pytest.mark.parametrize("packed,world,straight", [("", 2, False), ("1", 2, False), ("", 4, False), ("", 2, True)])
-def test_two_rank_plan_equals_single(oracle_lib, wl, qi, batch, packed, world, straight, monkeypatch):
+@pytest.mark.parametrize("packed,world,straight,repl", [("", 2, False, -1), ("1", 2, False, -1), ("", 4, False, -1),
+                                                        ("", 2, True, -1), ("", 2, False, 0), ("", 4, False, 0),
+                                                        ("", 2, False, 64)])
+def test_two_rank_plan_equals_single(oracle_lib, wl, qi, batch, packed, world, straight, repl, monkeypatch):
     """World 2 and 4 (ranks as threads on one GPU); packed "1": the ranks' connect
     launches are work-compacted (k_edges_packed); straight: the product default
-    (straight edge first: every rank decides alone, no exchange when it is valid)."""
+    (straight edge first: every rank decides alone, no exchange when it is valid);
+    repl: rp_plan_params.group_repl — -1 shards every iteration (one exchange each),
+    0 (default: up to 4,096 samples) replicates these small iterations on every rank
+    with no exchange but the timeout vote every 8th iteration, 64 replicates only the
+    first iteration."""
     if packed:
         monkeypatch.setenv("RBE_EDGE_PACKED", packed)
     q = json.load(open(os.path.join(GOLD, "workloads", wl + ".json")))["queries"][qi]
     sc = scenes.Scene.from_json(q["scene"])
-    p = _abi.make_params(seed=13, batch=batch, n_waypoints=150, timeout_s=60, straight_first=straight)
+    p = _abi.make_params(seed=13, batch=batch, n_waypoints=150, timeout_s=60, straight_first=straight,
+                         group_repl=repl)
     g = ThreadGroup(world)
     ctxs = []
     for r in range(world):
@@ -78,9 +85,56 @@ def test_two_rank_plan_equals_single(oracle_lib, wl, qi, batch, packed, world, s
     o.set_scene(sc.boxes, sc.plane_z, sc.base)
     o.set_attached(q["attached"])
     ref_cpu, st_cpu, _ = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
-    assert g.calls >= (0 if straight else 1)
+    its = ctxs[0].stats()["iterations"]
+    if repl == 0:   # all replicated: only the timeout votes exchange
+        assert g.calls == its // 8
+    elif repl > 0:   # iteration 0 replicated, the others sharded
+        assert g.calls >= its - 1 - (its - 1) // 8
+    else:
+        assert g.calls >= (0 if straight else its)
     for path, status in out:
         assert status == st == st_cpu == _abi.STATUS_EXACT
         assert np.array_equal(path, ref) and np.array_equal(path, ref_cpu)
     for c in ctxs + [single]:
+        c.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_replicated_timeout_vote(oracle_lib, world):
+    """Replicated iterations exchange nothing but a timeout vote every 8th iteration
+    (include/rbe_planner.h group_repl): with an already-expired budget on every rank
+    the group runs iterations 0-6, votes at iteration 7 and stops there on every
+    rank; the APPROXIMATE path equals the oracle's group protocol (ranks as threads)."""
+    q = json.load(open(os.path.join(GOLD, "workloads", "clutter64_well.json")))["queries"][0]
+    sc = scenes.Scene.from_json(q["scene"])
+    p = _abi.make_params(seed=3, batch=1152, n_waypoints=150, timeout_s=1e-9, straight_first=False)
+    g = ThreadGroup(world)
+    ctxs = []
+    for r in range(world):
+        c = Context(device=0, robot=model.robot_desc())
+        c.set_scene(sc.boxes, sc.plane_z, sc.base)
+        c.set_attached(q["attached"])
+        c.group_init(r, world, g.fn(r))
+        ctxs.append(c)
+    out = [None] * world
+
+    def run(r):
+        out[r] = ctxs[r].plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    [t.start() for t in th]
+    [t.join(timeout=300) for t in th]
+    assert all(o is not None for o in out), "a rank did not finish"
+    assert g.calls == 1
+    stats = [c.stats() for c in ctxs]
+    assert all(s["iterations"] == 7 for s in stats), [s["iterations"] for s in stats]
+    o = oracle_lib.OracleScene()
+    o.set_scene(sc.boxes, sc.plane_z, sc.base)
+    o.set_attached(q["attached"])
+    ref, st_ref, ost = o.plan_group(q["start"], q["goal"], model.Q_LO, model.Q_HI, p, world)
+    assert ost["iterations"] == 7
+    for path, status in out:
+        assert status == st_ref == _abi.STATUS_APPROXIMATE
+        assert np.array_equal(path, ref)
+    for c in ctxs:
         c.close()

@@ -47,6 +47,11 @@ for s in "$@"; do
     nntest) step pytest_nn 600 python -u -m pytest tests/test_gpu_nn.py -m gpu -x -v --timeout 120 --timeout-method thread ;;
     wellab) step wellab 600 python tools/well_ab.py ;;
     wellprof) step wellprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/wellprof -o kt -- python tools/well_ab.py mfma=RBE_NN_MFMA:4,RBE_PLAN_CHUNK:-1 part=RBE_NN_MFMA:0,RBE_PLAN_CHUNK:-1 ;;
+    satq) RBE_LIB_PATH=abvariants/lib_q59.so step satq59 300 python -u -m pytest tests/test_gpu_edge_cases.py -k saturated -m gpu -v --timeout 120 --timeout-method thread ;;
+    sceneab) for r in 1 2; do step sab_head_$r 300 python tools/plan_bench.py abvariants/lib_head.so goal3_tallest_10box 4096 && for v in 1 0; do RBE_SCENE_COPY=$v step sab_new_${v}_$r 300 python tools/plan_bench.py rbe550_final_project_amd/librbe_mi355x.so goal3_tallest_10box 4096; done; done; cat gpurun_out/sab_*.log | grep median ;;
+    nnab) for v in abvariants/lib_head.so rbe550_final_project_amd/librbe_mi355x.so; do n=$(basename $v .so); step nnab_$n 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/nnab_$n -o kt -- python tools/nn_bench.py $v --check --tree walk && step nnabu_$n 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/nnabu_$n -o kt -- python tools/nn_bench.py $v --check --tree uniform; done; for d in gpurun_out/nnab*_*/; do echo $d; grep -h "k_nn_mfma\|k_nn_part" $d/*kernel_stats.csv | cut -c1-200; done ;;
+    counters) rocprofv3 -L > gpurun_out/counters.txt 2>&1; grep -i "mfma\|SQ_INSTS_VALU\b\|VALU_MFMA" gpurun_out/counters.txt | head -40 ;;
+    edgepmc) step epmc_a 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH --output-format csv -d gpurun_out/epmc_a -o a -- python tools/c5_profile.py pmc && step epmc_b 300 rocprofv3 --pmc SQ_WAVES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/epmc_b -o b -- python tools/c5_profile.py pmc && python tools/pmc_summary.py gpurun_out/epmc_a gpurun_out/epmc_b --kernel k_edges --exclude packed --json gpurun_out/edges_pmc.json > gpurun_out/edges_pmc.txt && python tools/pmc_summary.py gpurun_out/epmc_a gpurun_out/epmc_b --kernel k_edges_packed --json gpurun_out/edges_packed_pmc.json > gpurun_out/edges_packed_pmc.txt && python tools/pmc_summary.py gpurun_out/epmc_a gpurun_out/epmc_b --kernel k_nn_mfma --json gpurun_out/nn_pmc.json > gpurun_out/nn_pmc.txt && cat gpurun_out/edges_pmc.txt gpurun_out/edges_packed_pmc.txt gpurun_out/nn_pmc.txt ;;
     nncount) step nncount 300 python tools/nn_count.py abvariants/lib_nncount.so 4 8 ;;
     chunks) step chunks 600 python tools/chunk_sweep.py -1 16 64 256 ;;
     ptests) step pytest_plan 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -m gpu -x -q --timeout 300 --timeout-method thread ;;

@@ -21,9 +21,10 @@ def main():
     wl = json.load(open(os.path.join(ROOT, "tests", "golden", "workloads", name + ".json")))
     ctx = native.Context(0, model.robot_desc())
     for rep in range(3):
-        t = []
+        t, tw = [], []
         for i, q in enumerate(wl["queries"]):
             sc = scenes.Scene.from_json(q["scene"])
+            tw0 = time.perf_counter()
             ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
             ctx.set_attached(q["attached"])
             p = _abi.make_params(seed=i, batch=batch, batch_min=batch_min, n_waypoints=150, timeout_s=10.0,
@@ -31,8 +32,10 @@ def main():
             t0 = time.perf_counter()
             ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
             t.append(1e3 * (time.perf_counter() - t0))
-        print(f"{os.path.basename(native.LIB_PATH)} {name} batch {batch}: total {sum(t):.2f} ms median "
-              f"{np.median(t):.3f} ms", flush=True)
+            tw.append(1e3 * (time.perf_counter() - tw0))
+        print(f"{os.path.basename(native.LIB_PATH)} {os.environ.get('RBE_SCENE_COPY', '')} {name} batch {batch}: "
+              f"total {sum(t):.2f} ms median {np.median(t):.3f} ms; with set_scene + set_attached: "
+              f"median {np.median(tw):.3f} ms", flush=True)
 
 
 if __name__ == "__main__":

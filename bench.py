@@ -190,7 +190,8 @@ def config_scenes():
     """BASELINE.md configs other than the headline C3: (name, scene, states per launch)."""
     c4 = load_workload("goal4_pentagon_10box")["queries"][14]["scene"]
     c5 = load_workload("clutter64")["queries"][0]["scene"]
-    return [("C2_goal1_5box_64k", scenes.Scene(boxes=scenes.goal1_scattered(0).boxes[:5]), 1 << 16),
+    return [("C3_goal3_10box_4M", scenes.goal3_tallest(), 1 << 22),   # (the round 1-3 headline batch)
+            ("C2_goal1_5box_64k", scenes.Scene(boxes=scenes.goal1_scattered(0).boxes[:5]), 1 << 16),
             ("C4_goal4_pentagon_256k", scenes.Scene.from_json(c4), 1 << 18),
             ("C5_clutter64_1M", scenes.Scene.from_json(c5), 1 << 20)]
 
@@ -309,7 +310,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--states", type=int, default=1 << 22, help="states per GPU per step")
+    # 2^24 states (604 MB of HBM) per GPU and step: at 4M the launch's last partial
+    # round of waves and the launch gap cost ~5 % (34.2 vs 35.9 G states/s, same box,
+    # profiles/r04/validity_batch_size.txt); the 4M rate is kept in per_config
+    ap.add_argument("--states", type=int, default=1 << 24, help="states per GPU per step")
     ap.add_argument("--plan-batch", type=int, default=4096, help="RRT-Connect samples per iteration (global)")
     ap.add_argument("--no-plan", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
@@ -399,20 +403,35 @@ def main():
     plan = None
     rank_group = None
     if not args.no_plan:
-        # the rank group is built outside the per-workload error handling: at N > 1 a
-        # plan number without the group would be a single-rank number, so a failure
-        # here ends the run (non-zero exit) instead of being reported as N-GPU
+        # the rank group: at N > 1 a plan number without the group would be a
+        # single-rank number, so if any rank fails to join it every rank skips the plan
+        # workloads (the ranks agree on that first) and the line reports the error;
+        # the validity metric above stands on its own
         group = None
+        group_err = None
         if distributed:
             from rbe550_final_project_amd.distributed import Group
-            group = Group(ctx, transport="shm" if args.backend == "gloo" else "rccl")
-            # what the transport itself reports on every rank (RCCL: ncclCommUserRank /
-            # ncclCommCount of the library's communicator)
-            views = [None] * world
-            dist.all_gather_object(views, ctx.group_info())
-            rank_group = {"transport": views[0]["transport"], "ranks": views,
-                          "consistent": all(v["world"] == world and v["rank"] == r for r, v in enumerate(views))}
+            try:
+                group = Group(ctx, transport="shm" if args.backend == "gloo" else "rccl")
+            except Exception as ex:
+                group_err = f"rank {rank}: {ex!r}"[:300]
+            errs = [None] * world
+            dist.all_gather_object(errs, group_err)
+            if any(errs):
+                if group is not None:
+                    group.leave()
+                group = None
+                rank_group = {"error": [e for e in errs if e]}
+            else:
+                # what the transport itself reports on every rank (RCCL: ncclCommUserRank /
+                # ncclCommCount of the library's communicator)
+                views = [None] * world
+                dist.all_gather_object(views, ctx.group_info())
+                rank_group = {"transport": views[0]["transport"], "ranks": views,
+                              "consistent": all(v["world"] == world and v["rank"] == r for r, v in enumerate(views))}
         try:
+            if distributed and group is None:
+                raise RuntimeError(f"no rank group: {rank_group['error']}")
             # warm-up: one untimed pass over the whole C3 workload in both modes (a
             # 2-query warm-up left the first timed workload at 2x its median on one box)
             run_plans(ctx, wl, args.plan_batch, 100, group)
@@ -467,12 +486,12 @@ def main():
         # configured batch) on the same queries
         well = load_workload("clutter64_well")
         wellx = {"queries": well["queries"] * 4}
-        for key, wl_c, batch, bmin, seeds_from, max_iters in (
+        for key, wl_c, batch, bmin, seeds_from, max_iters in ([] if (distributed and group is None) else (
                 ("C4_pentagon", load_workload("goal4_pentagon_10box"), C4_BATCH, C4_BATCH, 0, 0),
                 ("C4_pentagon_sched", load_workload("goal4_pentagon_10box"), C4_BATCH, 0, 0, 0),
                 ("C5_clutter64", load_workload("clutter64"), C5_BATCH, C5_BATCH, 0, 0),
                 ("C5_well", wellx, C5_BATCH, C5_BATCH, 1, 8),
-                ("C5_well_sched", wellx, C5_BATCH, 0, 1, 8)):
+                ("C5_well_sched", wellx, C5_BATCH, 0, 1, 8))):
             try:
                 extra = {}
                 tq, sq, stq = run_plans(ctx, wl_c, batch, seeds_from, group, batch_min=bmin, tree_capacity=1 << 23,

@@ -23,7 +23,10 @@ HEADERS.append(os.path.join(os.path.dirname(_HERE), "include", "rbe_planner.h"))
 #     (no NaN is ever produced or tested); +2.7 %
 #   -fno-slp-vectorize: no v_pk_add/v_pk_mul pairs that need v_mov shuffles to
 #     line up their operands (4238 -> 3857 static VALU); +9 %
-DEVICE_FLAGS = ["-Xarch_device", "-fno-honor-nans", "-Xarch_device", "-mno-amdgpu-ieee", "-fno-slp-vectorize"]
+#   -mllvm -amdgpu-mfma-vgpr-form: MFMA results in VGPRs, not AGPRs (k_nn_mfma's
+#     epilogue read every accumulator back with v_accvgpr_read: 16 per 16-node tile)
+DEVICE_FLAGS = ["-Xarch_device", "-fno-honor-nans", "-Xarch_device", "-mno-amdgpu-ieee", "-fno-slp-vectorize",
+                "-mllvm", "-amdgpu-mfma-vgpr-form"]
 # -mcode-object-version=6: rp_bdim / rp_gdim (rp_model.h) read the hidden kernel
 #   arguments at the v5/v6 offsets; pinned so a toolchain default cannot move them
 #   (rp_create also checks them on the device)

@@ -29,6 +29,9 @@ constexpr int VBLOCK = 64;      // validity / edge block size: one wave (its LDS
 #ifndef RP_EDGE_WAVES
 #define RP_EDGE_WAVES 4
 #endif
+#ifndef RP_EDGE_WAVES_CL
+#define RP_EDGE_WAVES_CL 4
+#endif
 constexpr int NNBLOCK = 256;    // NN block size
 constexpr int NNTILE = 256;     // tree nodes per LDS tile (256 x 72 B = 18 KiB)
 
@@ -97,8 +100,8 @@ __device__ __forceinline__ unsigned long long counter_sum(const unsigned long lo
     return s;
 }
 
-template <int NCL>
-__global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_edges(const double* __restrict__ from,
+template <int NCL, bool BF = false>
+__global__ __launch_bounds__(VBLOCK, NCL == NCL_GRID ? RP_EDGE_WAVES : RP_EDGE_WAVES_CL) void k_edges(const double* __restrict__ from,
                                                   const double* __restrict__ to,
                                                   const int* __restrict__ nd, int64_t n_edges,
                                                   int kmax, int mode, uint8_t* valid, int group,
@@ -150,7 +153,7 @@ __global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_edges(const double* _
             float qq[NQ];
 #pragma unroll
             for (int k = 0; k < NQ; ++k) qq[k] = (float)st[k];
-            if (state_collides<NCL>(qq, sc, wq)) {
+            if (state_collides<NCL, BF>(qq, sc, wq)) {
                 valid[e] = 0;
                 if (gfail) {
                     const int g = (int)(e / group), s = (int)(e - (int64_t)g * group);
@@ -195,8 +198,8 @@ __global__ void k_chunk_first(const int32_t* __restrict__ incl, int64_t n_edges,
 // lanes map its 64 items to edges through LDS (each of the next 64 edges writes
 // its index into the item slots it covers; empty edges cover none, so a pass may
 // take another round of 64 edges).
-template <int NCL>
-__global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_edges_packed(
+template <int NCL, bool BF = false>
+__global__ __launch_bounds__(VBLOCK, NCL == NCL_GRID ? RP_EDGE_WAVES : RP_EDGE_WAVES_CL) void k_edges_packed(
     const double* __restrict__ from, const double* __restrict__ to, const int* __restrict__ nd, int64_t n_edges,
     int mode, uint8_t* valid, int group, int* gfail, unsigned long long* counter, const DevScene* __restrict__ sc,
     const int32_t* __restrict__ incl, const int32_t* __restrict__ chunk_first) {
@@ -253,7 +256,7 @@ __global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_edges_packed(
             float qq[NQ];
 #pragma unroll
             for (int k = 0; k < NQ; ++k) qq[k] = (float)st[k];
-            if (state_collides<NCL>(qq, sc, wq)) {
+            if (state_collides<NCL, BF>(qq, sc, wq)) {
                 valid[e] = 0;
                 if (gfail) {
                     const int g = (int)(e / group), s = (int)(e - (int64_t)g * group);

@@ -407,8 +407,15 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
     if (max_blocks && nb > max_blocks) nb = max_blocks;   // grid-stride (gated launches)
     const dim3 g(nb), b(VBLOCK);
     const int ps = prof_begin(c, s);
-#define RP_EDGES(N) hipLaunchKernelGGL(k_edges<N>, g, b, 0, s, from, to, nd, n, kmax, mode, valid, group, gfail, \
-                                       c->counter.p, c->d_scene, dcount, per_item, dkmax)
+    // (the reference's robot base folded in as a constant, as for k_validity)
+    const bool bf = base_fixed(c->scene);
+#define RP_EDGES(N)                                                                                                \
+    do {                                                                                                           \
+        if (bf) hipLaunchKernelGGL((k_edges<N, true>), g, b, 0, s, from, to, nd, n, kmax, mode, valid, group, gfail, \
+                                   c->counter.p, c->d_scene, dcount, per_item, dkmax);                             \
+        else hipLaunchKernelGGL((k_edges<N, false>), g, b, 0, s, from, to, nd, n, kmax, mode, valid, group, gfail,   \
+                                c->counter.p, c->d_scene, dcount, per_item, dkmax);                                \
+    } while (0)
     switch (ncl_bucket(c->scene)) {
         case NCL_GRID: RP_EDGES(NCL_GRID); break;
         case 0: RP_EDGES(0); break;
@@ -473,9 +480,15 @@ void launch_edges_packed(rp_ctx* c, const double* from, const double* to, const 
                        c->echunk.p);
     debug_wait(c, "k_chunk_first");
     const dim3 g(std::min<unsigned>(blocks_for(n * (int64_t)kmax, VBLOCK), 8192u)), b(VBLOCK);
-#define RP_EDGESP(N) hipLaunchKernelGGL(k_edges_packed<N>, g, b, 0, s, from, to, nd, n, mode, valid, group, gfail, \
-                                        c->counter.p, c->d_scene, (const int32_t*)c->eincl.p,   \
-                                        (const int32_t*)c->echunk.p)
+    const bool bf = base_fixed(c->scene);
+#define RP_EDGESP(N)                                                                                               \
+    do {                                                                                                           \
+        if (bf) hipLaunchKernelGGL((k_edges_packed<N, true>), g, b, 0, s, from, to, nd, n, mode, valid, group,     \
+                                   gfail, c->counter.p, c->d_scene, (const int32_t*)c->eincl.p,                    \
+                                   (const int32_t*)c->echunk.p);                                                   \
+        else hipLaunchKernelGGL((k_edges_packed<N, false>), g, b, 0, s, from, to, nd, n, mode, valid, group, gfail, \
+                                c->counter.p, c->d_scene, (const int32_t*)c->eincl.p, (const int32_t*)c->echunk.p); \
+    } while (0)
     switch (ncl_bucket(c->scene)) {
         case NCL_GRID: RP_EDGESP(NCL_GRID); break;
         case 0: RP_EDGESP(0); break;
@@ -905,7 +918,9 @@ void launch_nn_mfma_w(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, 
     int64_t S0 = std::max<int64_t>(1, std::min<int64_t>(want, stages / 32));
     if (const char* e = std::getenv("RBE_NN_RANGES"))   // (A/B: cap on the tree ranges)
         if (*e) S0 = std::max<int64_t>(1, std::min<int64_t>(S0, std::atoll(e)));
-    const int64_t chunk = ((stages + S0 - 1) / S0) * NNM_STAGE;
+    int64_t chunk = ((stages + S0 - 1) / S0) * NNM_STAGE;
+    if (const char* e = std::getenv("RBE_NN_RANGE_MAX"))   // (A/B: nodes per range at most)
+        if (*e) chunk = std::max<int64_t>(NNM_STAGE, std::min<int64_t>(chunk, std::atoll(e) / NNM_STAGE * NNM_STAGE));
     const int S = (int)((T + chunk - 1) / chunk);
     c->nn_part.ensure((size_t)S * n);
     hipLaunchKernelGGL((k_nn_mfma<RB, W>), dim3((unsigned)(qblocks * S)), dim3(64 * W), 0, c->stream, qx, n,

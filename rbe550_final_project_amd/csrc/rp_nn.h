@@ -350,6 +350,14 @@ __global__ __launch_bounds__(64 * W) void k_nn_mfma(const double* __restrict__ q
         }
     };
     int64_t tb = 0;
+    const h8* nx = ib + PF * 64;   // the next group's first tile
+    for (; tb + 2 * PF <= ntiles; tb += PF, nx += PF * 64) {   // (every prefetch in range)
+#pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            tile_step(tb + u, bq[u]);
+            bq[u] = nx[u * 64];
+        }
+    }
     for (; tb + PF <= ntiles; tb += PF) {
 #pragma unroll
         for (int u = 0; u < PF; ++u) {

@@ -88,14 +88,19 @@ def test_configured_batch_group_iteration_world1(gpu_ctx, name, monkeypatch):
 
 
 @pytest.mark.parametrize("name", ["C2_q1_s1", "C5_well_s4"])
-def test_rccl_transport_world1(name):
+@pytest.mark.parametrize("repl", ["0", ""])
+def test_rccl_transport_world1(name, repl, monkeypatch):
     """The RCCL transport end to end on one GPU (a 1-rank communicator: the
-    records go through ncclAllGather on the planner stream)."""
+    records go through ncclAllGather on the planner stream). RBE_GROUP_REPL=0 shards
+    every sub-batch (every one exchanges); the default replicates sub-batches of up to
+    4,096 samples (the 64-sample first one of these plans: no exchange)."""
+    monkeypatch.setenv("RBE_GROUP_REPL", repl)
     ctx = Context(device=0, robot=model.robot_desc())
     try:
         ctx.group_init_rccl(0, 1, native.rccl_unique_id())
         s = _check(ctx, name)
-        assert s["exchange_ms"] > 0.0
+        if repl == "0":
+            assert s["exchange_ms"] > 0.0
         ctx.group_leave()
         _check(ctx, name)
     finally:

@@ -40,7 +40,7 @@ for s in "$@"; do
     lat) step lat 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/lat -o lt -- python tools/latency_probe.py && python tools/latency_probe.py --summarize gpurun_out/lat/lt_kernel_trace.csv > gpurun_out/lat_summary.txt ;;
     prof) step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o kt -- python bench.py --steps 20 --no-cpu --no-plan --no-configs ;;
     pmc) step pmc_sq 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH --output-format csv -d gpurun_out/pmc_sq -o sq -- python bench.py --steps 3 --warmup 1 --no-cpu --no-plan --no-configs && step pmc_sq2 600 rocprofv3 --pmc SQ_WAVES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_sq2 -o sq2 -- python bench.py --steps 3 --warmup 1 --no-cpu --no-plan --no-configs && step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o f -- python bench.py --steps 3 --warmup 1 --no-cpu --no-plan --no-configs && step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o w -- python bench.py --steps 3 --warmup 1 --no-cpu --no-plan --no-configs ;;
-    pmcsum) python tools/pmc_summary.py gpurun_out/pmc_sq gpurun_out/pmc_sq2 --json gpurun_out/validity_pmc_sq.json > gpurun_out/validity_pmc_sq.txt && python tools/make_pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write 4194304 gpurun_out/pmc_validity.json > /dev/null && echo pmcsum ok ;;
+    pmcsum) python tools/pmc_summary.py gpurun_out/pmc_sq gpurun_out/pmc_sq2 --json gpurun_out/validity_pmc_sq.json > gpurun_out/validity_pmc_sq.txt && python tools/make_pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write 16777216 gpurun_out/pmc_validity.json > /dev/null && echo pmcsum ok ;;
     c5prof) step c5prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c5prof -o kt -- python tools/c5_profile.py ;;
     nnpmc) step nnpmc_a 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH --output-format csv -d gpurun_out/nnpmc_a -o a -- python tools/c5_profile.py pmc && step nnpmc_b 300 rocprofv3 --pmc SQ_WAVES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/nnpmc_b -o b -- python tools/c5_profile.py pmc && python tools/pmc_summary.py gpurun_out/nnpmc_a gpurun_out/nnpmc_b --kernel k_nn_mfma --json gpurun_out/nn_pmc.json > gpurun_out/nn_pmc.txt ;;
     c5stats) step c5stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c5stats -o kt -- python tools/c5_profile.py ;;
@@ -52,7 +52,13 @@ for s in "$@"; do
     nnab) for v in abvariants/lib_head.so rbe550_final_project_amd/librbe_mi355x.so; do n=$(basename $v .so); step nnab_$n 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/nnab_$n -o kt -- python tools/nn_bench.py $v --check --tree walk && step nnabu_$n 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/nnabu_$n -o kt -- python tools/nn_bench.py $v --check --tree uniform; done; for d in gpurun_out/nnab*_*/; do echo $d; grep -h "k_nn_mfma\|k_nn_part" $d/*kernel_stats.csv | cut -c1-200; done ;;
     counters) rocprofv3 -L > gpurun_out/counters.txt 2>&1; grep -i "mfma\|SQ_INSTS_VALU\b\|VALU_MFMA" gpurun_out/counters.txt | head -40 ;;
     edgepmc) step epmc_a 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH --output-format csv -d gpurun_out/epmc_a -o a -- python tools/c5_profile.py pmc && step epmc_b 300 rocprofv3 --pmc SQ_WAVES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/epmc_b -o b -- python tools/c5_profile.py pmc && python tools/pmc_summary.py gpurun_out/epmc_a gpurun_out/epmc_b --kernel k_edges --exclude packed --json gpurun_out/edges_pmc.json > gpurun_out/edges_pmc.txt && python tools/pmc_summary.py gpurun_out/epmc_a gpurun_out/epmc_b --kernel k_edges_packed --json gpurun_out/edges_packed_pmc.json > gpurun_out/edges_packed_pmc.txt && python tools/pmc_summary.py gpurun_out/epmc_a gpurun_out/epmc_b --kernel k_nn_mfma --json gpurun_out/nn_pmc.json > gpurun_out/nn_pmc.txt && cat gpurun_out/edges_pmc.txt gpurun_out/edges_packed_pmc.txt gpurun_out/nn_pmc.txt ;;
-    nncount) step nncount 300 python tools/nn_count.py abvariants/lib_nncount.so 4 8 ;;
+    edgebench) for sc in clutter64 goal3; do step eb_$sc 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/eb_$sc -o kt -- python tools/edge_bench.py --scene $sc && grep -h "k_edges\|k_validity\|k_edge_prep" gpurun_out/eb_$sc/*kernel_stats.csv | cut -c1-160; done ;;
+    edgeab) for v in abvariants/lib_head.so abvariants/lib_ew5.so rbe550_final_project_amd/librbe_mi355x.so; do n=$(basename $v .so); for sc in clutter64 goal3; do step eab_${n}_$sc 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/eab_${n}_$sc -o kt -- python tools/edge_bench.py $v --scene $sc && grep -h "k_edges" gpurun_out/eab_${n}_$sc/*kernel_stats.csv | awk -F'",' '{print "'$n' '$sc'", substr($1,1,30), $2}'; done; done ;;
+    nnpmc2) step nnp_a 300 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/nnp_a -o a -- python tools/nn_bench.py --reps 2 && step nnp_b 300 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/nnp_b -o b -- python tools/nn_bench.py --reps 2 && python tools/pmc_summary.py gpurun_out/nnp_a gpurun_out/nnp_b --kernel k_nn_mfma --json gpurun_out/nn_pmc_bench.json > gpurun_out/nn_pmc_bench.txt && cat gpurun_out/nn_pmc_bench.txt ;;
+    vsize) for n in 4194304 16777216 4194304 16777216; do step vsize_$n 300 python bench.py --states $n --steps 30 --no-plan --no-cpu --no-configs && grep -o '"value": [0-9.]*\|"frac": [0-9.]*\|"kernel_ms": [0-9.]*' gpurun_out/vsize_$n.log | head -3 | tr '\n' ' '; echo; done ;;
+    nnrange) for r in 0 65536 32768 16384 8192; do RBE_NN_RANGE_MAX=$([ $r = 0 ] && echo "" || echo $r) step nnrange_$r 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/nnrange_$r -o kt -- python tools/nn_bench.py && grep -h "k_nn_mfma\|k_nn_reduce" gpurun_out/nnrange_$r/*kernel_stats.csv | awk -F'",' '{print "range '$r'", substr($1,1,30), $2}'; done ;;
+    nncount) step nncount 300 python tools/nn_count.py abvariants/lib_nncount.so 4 8 && cat gpurun_out/nncount.log ;;
+    nnrb) for m in 4 8 2; do step nnrb_$m 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/nnrb_$m -o kt -- python tools/nn_bench.py --mode $m && grep -h "k_nn_mfma" gpurun_out/nnrb_$m/*kernel_stats.csv | awk -F'",' '{print "mode '$m'", substr($1,1,30), $2}'; done ;;
     chunks) step chunks 600 python tools/chunk_sweep.py -1 16 64 256 ;;
     ptests) step pytest_plan 900 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_configs.py -m gpu -x -q --timeout 300 --timeout-method thread ;;
     procs) step pytest_procs 900 python -u -m pytest tests/test_gpu_group_procs.py -m gpu -x -v --timeout 400 --timeout-method thread ;;

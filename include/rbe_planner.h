@@ -258,6 +258,18 @@ int rp_plan(rp_ctx* ctx, const double start[RP_NQ], const double goal[RP_NQ],
             const double lo[RP_NQ], const double hi[RP_NQ], const rp_plan_params* params,
             double* path_out, int32_t path_cap, int32_t* n_out, int32_t* status_out);
 
+/* rp_plan split in two (same arguments, same results): rp_plan_async copies the
+ * inputs and hands the query to the context's planner thread, which runs rp_plan;
+ * it returns at once, so the caller's own per-query work (planning.py builds the
+ * waypoint tensors, code/planning.py:232-242, and restores qpos, :205) overlaps the
+ * GPU's. path_out, n_out and status_out must stay valid until rp_plan_wait, which
+ * blocks until the query is done and returns rp_plan's code. Every other call on the
+ * context while a query is in flight is RP_ERR_STATE. */
+int rp_plan_async(rp_ctx* ctx, const double start[RP_NQ], const double goal[RP_NQ],
+                  const double lo[RP_NQ], const double hi[RP_NQ], const rp_plan_params* params,
+                  double* path_out, int32_t path_cap, int32_t* n_out, int32_t* status_out);
+int rp_plan_wait(rp_ctx* ctx);
+
 /* Batched IK of the hand link: for each of n_targets poses (pos[3], quat[4] as
  * w, x, y, z; world frame, robot base from rp_set_scene) run n_seeds damped-least-
  * squares restarts on the 7 arm joints at once (restart 0 from init[t], the others

@@ -91,6 +91,18 @@ def make_boxes(boxes):
     return arr, len(boxes)
 
 
+def set_params(p, seed, batch, timeout_s, n_waypoints, simplify, tree_capacity, straight_first):
+    """Refill the per-query fields of a reused PlanParams (planning.plan_path)."""
+    p.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+    p.batch = int(batch)
+    p.timeout_s = float(timeout_s)
+    p.n_waypoints = int(n_waypoints or 0)
+    p.simplify = 1 if simplify else 0
+    p.tree_capacity = int(tree_capacity)
+    p.straight_first = 0 if straight_first else -1
+    return p
+
+
 def make_params(seed=0, batch=4096, range_=0.0, resolution=0.0, timeout_s=5.0, max_iters=0, batch_min=0,
                 n_waypoints=100, simplify=True, tree_capacity=0, straight_first=True, chunk=0, group_repl=0):
     p = PlanParams()

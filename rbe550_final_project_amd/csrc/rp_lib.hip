@@ -9,13 +9,17 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <chrono>
 #include <climits>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/rbe_planner.h"
@@ -100,8 +104,31 @@ struct Tree {
     void release() { q.release(); par.release(); cand.release(); img.release(); }
 };
 
+// rp_plan_async / rp_plan_wait: one query handed to the context's planner thread
+struct PlanJob {
+    double start[RP_NQ], goal[RP_NQ], lo[RP_NQ], hi[RP_NQ];
+    rp_plan_params params;
+    double* path_out;
+    int32_t path_cap;
+    int32_t* n_out;
+    int32_t* status_out;
+    int rc;
+};
+
+struct PlanWorker {
+    enum { IDLE = 0, POSTED = 1, DONE = 2, QUIT = 3 };
+    std::thread th;
+    std::atomic<int> state{IDLE};
+    std::mutex m;
+    std::condition_variable cv;
+    PlanJob job{};
+    double spin_s = 0.005;   // after a query the thread spins this long before it sleeps
+};
+
 struct rp_ctx {
     int device = 0;
+    PlanWorker* worker = nullptr;        // created by the first rp_plan_async
+    bool busy = false;                   // a rp_plan_async query is in flight
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     DevScene scene{};
@@ -212,7 +239,24 @@ struct rp_ctx {
         g_user = nullptr;
     }
 
+    void stop_worker() {
+        if (!worker) return;
+        {
+            // a query still in flight finishes first (the thread only looks at QUIT
+            // between queries)
+            while (worker->state.load(std::memory_order_acquire) == PlanWorker::POSTED) std::this_thread::yield();
+            std::lock_guard<std::mutex> lk(worker->m);
+            worker->state.store(PlanWorker::QUIT, std::memory_order_release);
+        }
+        worker->cv.notify_one();
+        worker->th.join();
+        delete worker;
+        worker = nullptr;
+        busy = false;
+    }
+
     ~rp_ctx() {
+        stop_worker();
         (void)hipSetDevice(device);
         for (auto& t : tree) t.release();
         q32.release(); flags.release(); ea.release(); eb.release(); end_nd.release(); eval.release();
@@ -1836,6 +1880,12 @@ bool structure_matches(const rp_robot_desc& r) {
 // C-ABI
 // ===========================================================================
 
+// calls that use the context's stream or state are refused while a rp_plan_async
+// query is in flight (its thread owns them until rp_plan_wait)
+#define RP_IDLE(c)                                                          \
+    do {                                                                    \
+        if ((c)->busy) return RP_ERR_STATE;                                 \
+    } while (0)
 #define RP_GUARD_BEGIN try {
 #define RP_GUARD_END(c)                          \
     }                                            \
@@ -1974,6 +2024,7 @@ unsigned env_far_mask(const DevScene& sc, const float base[3]) {
 
 int rp_set_scene(rp_ctx* c, const rp_box* boxes, int32_t n, float plane_z, const float base[3]) {
     if (!c || n < 0 || n > MAX_BOXES || (n > 0 && !boxes)) return RP_ERR_ARG;
+    RP_IDLE(c);
     RP_GUARD_BEGIN
     HIP_TRY(hipSetDevice(c->device));
     // box records in the caller's order (cos/sin of yaw in double, rounded once;
@@ -2094,6 +2145,7 @@ int rp_set_scene(rp_ctx* c, const rp_box* boxes, int32_t n, float plane_z, const
 
 int rp_set_attached(rp_ctx* c, int32_t box, uint32_t link_mask) {
     if (!c || box >= c->scene.n_boxes) return RP_ERR_ARG;
+    RP_IDLE(c);
     RP_GUARD_BEGIN
     HIP_TRY(hipSetDevice(c->device));
     for (int j = 0; j < c->scene.n_boxes; ++j) c->scene.box[j][14] = 0.0f;
@@ -2114,6 +2166,7 @@ int rp_set_attached(rp_ctx* c, int32_t box, uint32_t link_mask) {
 
 int rp_check_states(rp_ctx* c, const float* q, int64_t n, uint8_t* flags_out) {
     if (!c || n < 0 || (n > 0 && (!q || !flags_out))) return RP_ERR_ARG;
+    RP_IDLE(c);
     if (n == 0) return RP_OK;
     RP_GUARD_BEGIN
     HIP_TRY(hipSetDevice(c->device));
@@ -2131,6 +2184,7 @@ int rp_check_states(rp_ctx* c, const float* q, int64_t n, uint8_t* flags_out) {
 
 int rp_check_states_device(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, void* stream) {
     if (!c || n < 0 || (n > 0 && (!q || !flags))) return RP_ERR_ARG;
+    RP_IDLE(c);
     if (n == 0) return RP_OK;
     RP_GUARD_BEGIN
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
@@ -2150,6 +2204,7 @@ int rp_check_states_device(rp_ctx* c, const float* q, int64_t n, uint8_t* flags,
 
 int rp_last_kernel_ms(rp_ctx* c, double* ms) {
     if (!c || !ms) return RP_ERR_ARG;
+    RP_IDLE(c);
     if (!c->timed) {
         c->err = "no timed rp_check_states_device call (rp_set_profiling on first)";
         return RP_ERR_ARG;
@@ -2165,6 +2220,7 @@ int rp_last_kernel_ms(rp_ctx* c, double* ms) {
 
 int rp_check_edges(rp_ctx* c, const double* qa, const double* qb, int64_t n, double res, uint8_t* out) {
     if (!c || n < 0 || (n > 0 && (!qa || !qb || !out)) || !(res > 0)) return RP_ERR_ARG;
+    RP_IDLE(c);
     if (n == 0) return RP_OK;
     RP_GUARD_BEGIN
     HIP_TRY(hipSetDevice(c->device));
@@ -2179,6 +2235,7 @@ int rp_check_edges(rp_ctx* c, const double* qa, const double* qb, int64_t n, dou
 int rp_check_edges_device(rp_ctx* c, const double* qa, const double* qb, int64_t n, double res, uint8_t* out,
                           void* stream) {
     if (!c || n < 0 || (n > 0 && (!qa || !qb || !out)) || !(res > 0)) return RP_ERR_ARG;
+    RP_IDLE(c);
     if (n == 0) return RP_OK;
     RP_GUARD_BEGIN
     hipStream_t s = stream ? (hipStream_t)stream : c->stream;
@@ -2198,6 +2255,7 @@ int rp_check_edges_device(rp_ctx* c, const double* qa, const double* qb, int64_t
 
 int rp_state_contacts(rp_ctx* c, const double q[RP_NQ], int32_t* pairs_out, int32_t cap) {
     if (!c || !q || cap < 0 || (cap > 0 && !pairs_out)) return RP_ERR_ARG;
+    RP_IDLE(c);
     RP_GUARD_BEGIN
     HIP_TRY(hipSetDevice(c->device));
     c->ea.ensure(NQ);
@@ -2219,12 +2277,17 @@ int rp_state_contacts(rp_ctx* c, const double q[RP_NQ], int32_t* pairs_out, int3
     RP_GUARD_END(c)
 }
 
-int rp_plan(rp_ctx* c, const double start[RP_NQ], const double goal[RP_NQ], const double lo[RP_NQ],
-            const double hi[RP_NQ], const rp_plan_params* params, double* path_out, int32_t path_cap,
-            int32_t* n_out, int32_t* status_out) {
-    if (!c || !start || !goal || !lo || !hi || !params || !n_out || !status_out || path_cap < 0 ||
-        (path_cap > 0 && !path_out))
-        return RP_ERR_ARG;
+static int plan_args_bad(rp_ctx* c, const double* start, const double* goal, const double* lo, const double* hi,
+                         const rp_plan_params* params, double* path_out, int32_t path_cap, int32_t* n_out,
+                         int32_t* status_out) {
+    return !c || !start || !goal || !lo || !hi || !params || !n_out || !status_out || path_cap < 0 ||
+           (path_cap > 0 && !path_out);
+}
+
+// the query itself (rp_plan, and the planner thread of rp_plan_async)
+static int plan_entry(rp_ctx* c, const double start[RP_NQ], const double goal[RP_NQ], const double lo[RP_NQ],
+                      const double hi[RP_NQ], const rp_plan_params* params, double* path_out, int32_t path_cap,
+                      int32_t* n_out, int32_t* status_out) {
     RP_GUARD_BEGIN
     HIP_TRY(hipSetDevice(c->device));
     if (c->transport != TR_NONE && c->group_broken) {
@@ -2253,6 +2316,103 @@ int rp_plan(rp_ctx* c, const double start[RP_NQ], const double goal[RP_NQ], cons
     RP_GUARD_END(c)
 }
 
+int rp_plan(rp_ctx* c, const double start[RP_NQ], const double goal[RP_NQ], const double lo[RP_NQ],
+            const double hi[RP_NQ], const rp_plan_params* params, double* path_out, int32_t path_cap,
+            int32_t* n_out, int32_t* status_out) {
+    if (plan_args_bad(c, start, goal, lo, hi, params, path_out, path_cap, n_out, status_out)) return RP_ERR_ARG;
+    RP_IDLE(c);
+    return plan_entry(c, start, goal, lo, hi, params, path_out, path_cap, n_out, status_out);
+}
+
+// The planner thread: runs posted queries; between queries it spins for
+// PlanWorker::spin_s (back-to-back queries are handed over without a wake-up), then
+// sleeps on the condition variable.
+static void plan_worker_main(rp_ctx* c) {
+    PlanWorker& w = *c->worker;
+    double last = now_s();
+    for (uint64_t spin = 0;; ++spin) {
+        const int s = w.state.load(std::memory_order_acquire);
+        if (s == PlanWorker::POSTED) {
+            PlanJob& j = w.job;
+            j.rc = plan_entry(c, j.start, j.goal, j.lo, j.hi, &j.params, j.path_out, j.path_cap, j.n_out,
+                              j.status_out);
+            w.state.store(PlanWorker::DONE, std::memory_order_release);
+            last = now_s();
+            continue;
+        }
+        if (s == PlanWorker::QUIT) return;
+        if ((spin & 255) != 0 || now_s() - last < w.spin_s) {
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+            __builtin_ia32_pause();
+#endif
+            continue;
+        }
+        std::unique_lock<std::mutex> lk(w.m);
+        w.cv.wait(lk, [&] {
+            const int t = w.state.load(std::memory_order_acquire);
+            return t == PlanWorker::POSTED || t == PlanWorker::QUIT;
+        });
+        last = now_s();
+    }
+}
+
+int rp_plan_async(rp_ctx* c, const double start[RP_NQ], const double goal[RP_NQ], const double lo[RP_NQ],
+                  const double hi[RP_NQ], const rp_plan_params* params, double* path_out, int32_t path_cap,
+                  int32_t* n_out, int32_t* status_out) {
+    if (plan_args_bad(c, start, goal, lo, hi, params, path_out, path_cap, n_out, status_out)) return RP_ERR_ARG;
+    RP_IDLE(c);
+    try {
+        if (!c->worker) {
+            c->worker = new PlanWorker();
+            if (const char* e = std::getenv("RBE_PLAN_SPIN_US"))
+                if (*e) c->worker->spin_s = std::max(0.0, std::atof(e)) * 1e-6;
+            c->worker->th = std::thread(plan_worker_main, c);
+        }
+    } catch (const std::exception& e) {
+        delete c->worker;
+        c->worker = nullptr;
+        c->err = std::string("planner thread: ") + e.what();
+        return RP_ERR_DEVICE;
+    }
+    PlanWorker& w = *c->worker;
+    PlanJob& j = w.job;
+    std::memcpy(j.start, start, sizeof j.start);
+    std::memcpy(j.goal, goal, sizeof j.goal);
+    std::memcpy(j.lo, lo, sizeof j.lo);
+    std::memcpy(j.hi, hi, sizeof j.hi);
+    j.params = *params;
+    j.path_out = path_out;
+    j.path_cap = path_cap;
+    j.n_out = n_out;
+    j.status_out = status_out;
+    j.rc = RP_OK;
+    c->busy = true;
+    {
+        std::lock_guard<std::mutex> lk(w.m);
+        w.state.store(PlanWorker::POSTED, std::memory_order_release);
+    }
+    w.cv.notify_one();
+    return RP_OK;
+}
+
+int rp_plan_wait(rp_ctx* c) {
+    if (!c) return RP_ERR_ARG;
+    if (!c->busy || !c->worker) {
+        c->err = "rp_plan_wait without a query in flight";
+        return RP_ERR_STATE;
+    }
+    PlanWorker& w = *c->worker;
+    while (w.state.load(std::memory_order_acquire) != PlanWorker::DONE) {
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+        __builtin_ia32_pause();
+#endif
+    }
+    const int rc = w.job.rc;
+    w.state.store(PlanWorker::IDLE, std::memory_order_release);
+    c->busy = false;
+    return rc;
+}
+
 int rp_get_stream(rp_ctx* c, void** out) {
     if (!c || !out) return RP_ERR_ARG;
     *out = (void*)c->stream;
@@ -2261,18 +2421,21 @@ int rp_get_stream(rp_ctx* c, void** out) {
 
 int rp_set_profiling(rp_ctx* c, int32_t on) {
     if (!c) return RP_ERR_ARG;
+    RP_IDLE(c);
     c->profiling = on != 0;
     return RP_OK;
 }
 
 int rp_get_profile(rp_ctx* c, rp_profile* out) {
     if (!c || !out) return RP_ERR_ARG;
+    RP_IDLE(c);
     *out = c->prof;
     return RP_OK;
 }
 
 int rp_group_init(rp_ctx* c, int32_t rank, int32_t world, rp_allgather_fn fn, void* user) {
     if (!c || world < 1 || rank < 0 || rank >= world || (world > 1 && !fn)) return RP_ERR_ARG;
+    RP_IDLE(c);
     RP_GUARD_BEGIN
     HIP_TRY(hipSetDevice(c->device));
     c->leave_group();
@@ -2290,6 +2453,7 @@ int rp_group_init(rp_ctx* c, int32_t rank, int32_t world, rp_allgather_fn fn, vo
 int rp_group_init_shm(rp_ctx* c, int32_t rank, int32_t world, void* base, int64_t bytes) {
     if (!c || !base || world < 1 || world > 64 || rank < 0 || rank >= world || bytes < SHM_HDR + 2 * 4096)
         return RP_ERR_ARG;
+    RP_IDLE(c);
     RP_GUARD_BEGIN
     HIP_TRY(hipSetDevice(c->device));
     c->leave_group();
@@ -2327,6 +2491,7 @@ int rp_group_rccl_unique_id(uint8_t out[RP_RCCL_ID_BYTES]) {
 
 int rp_group_init_rccl(rp_ctx* c, int32_t rank, int32_t world, const uint8_t id[RP_RCCL_ID_BYTES]) {
     if (!c || !id || world < 1 || rank < 0 || rank >= world) return RP_ERR_ARG;
+    RP_IDLE(c);
     RP_GUARD_BEGIN
     HIP_TRY(hipSetDevice(c->device));
     c->leave_group();
@@ -2344,6 +2509,7 @@ int rp_group_init_rccl(rp_ctx* c, int32_t rank, int32_t world, const uint8_t id[
 
 int rp_group_info(rp_ctx* c, int32_t* rank, int32_t* world, int32_t* transport) {
     if (!c || !rank || !world || !transport) return RP_ERR_ARG;
+    RP_IDLE(c);
     RP_GUARD_BEGIN
     static_assert(TR_NONE == RP_TRANSPORT_NONE && TR_HOST == RP_TRANSPORT_HOST && TR_RCCL == RP_TRANSPORT_RCCL &&
                       TR_SHM == RP_TRANSPORT_SHM, "transport codes");
@@ -2363,11 +2529,16 @@ int rp_group_info(rp_ctx* c, int32_t* rank, int32_t* world, int32_t* transport) 
 
 int rp_get_stats(rp_ctx* c, rp_stats* out) {
     if (!c || !out) return RP_ERR_ARG;
+    RP_IDLE(c);
     *out = c->stats;
     return RP_OK;
 }
 
-const char* rp_last_error(rp_ctx* c) { return c ? c->err.c_str() : g_create_error.c_str(); }
+const char* rp_last_error(rp_ctx* c) {
+    // (while a query is in flight its thread owns c->err)
+    if (c && c->busy) return "a rp_plan_async query is in flight (rp_plan_wait)";
+    return c ? c->err.c_str() : g_create_error.c_str();
+}
 
 int rp_ik(rp_ctx* c, int32_t n_targets, const double* pos, const double* quat, const double* init,
           const double lo[RP_NQ], const double hi[RP_NQ], const rp_ik_params* params, double* q_out,
@@ -2375,6 +2546,7 @@ int rp_ik(rp_ctx* c, int32_t n_targets, const double* pos, const double* quat, c
     if (!c || n_targets < 0 || !params || !lo || !hi ||
         (n_targets > 0 && (!pos || !quat || !init || !q_out || !status_out)))
         return RP_ERR_ARG;
+    RP_IDLE(c);
     if (n_targets == 0) return RP_OK;
     RP_GUARD_BEGIN
     HIP_TRY(hipSetDevice(c->device));
@@ -2472,6 +2644,7 @@ int rp_debug_tstamps(unsigned long long* out) {
 // device sqrt / div / ceil / f64->f32 of x[i] -> out[4*i..4*i+3].
 int rp_selftest_f64(rp_ctx* c, const double* x, int64_t n, double* out) {
     if (!c || n <= 0 || !x || !out) return RP_ERR_ARG;
+    RP_IDLE(c);
     RP_GUARD_BEGIN
     HIP_TRY(hipSetDevice(c->device));
     DevBuf<double> dx, dy;
@@ -2496,6 +2669,7 @@ int rp_selftest_f64(rp_ctx* c, const double* x, int64_t n, double* out) {
 int rp_selftest_nn(rp_ctx* c, const double* q, int64_t n, const double* tree, int64_t T, const double lo[RP_NQ],
                    const double hi[RP_NQ], int32_t mode, int32_t* out) {
     if (!c || n <= 0 || T <= 0 || !q || !tree || !lo || !hi || !out) return RP_ERR_ARG;
+    RP_IDLE(c);
     if (T >= ((int64_t)1 << 31)) return RP_ERR_ARG;
     RP_GUARD_BEGIN
     HIP_TRY(hipSetDevice(c->device));

@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("RBE_LIB_PATH") or os.path.join(_HERE, LIB_NAME)
 # every symbol include/rbe_planner.h declares
 EXPORTS = ("rp_version", "rp_default_robot", "rp_create", "rp_destroy", "rp_set_scene", "rp_set_attached",
            "rp_check_states", "rp_check_states_device", "rp_check_edges", "rp_check_edges_device",
-           "rp_state_contacts", "rp_plan", "rp_group_init", "rp_group_init_shm", "rp_group_rccl_unique_id", "rp_group_init_rccl",
+           "rp_state_contacts", "rp_plan", "rp_plan_async", "rp_plan_wait", "rp_group_init", "rp_group_init_shm", "rp_group_rccl_unique_id", "rp_group_init_rccl",
            "rp_get_stats", "rp_last_error", "rp_last_kernel_ms", "rp_selftest_f64", "rp_ik", "rp_set_profiling",
            "rp_get_profile", "rp_get_stream", "rp_group_info", "rp_selftest_nn")
 
@@ -49,7 +49,7 @@ def load():
     L.rp_create.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(_abi.RobotDesc)]
     L.rp_destroy.argtypes = [vp]
     L.rp_destroy.restype = None
-    L.rp_set_scene.argtypes = [vp, C.POINTER(_abi.Box), i32, f32, C.POINTER(f32)]
+    L.rp_set_scene.argtypes = [vp, vp, i32, f32, C.POINTER(f32)]   # rp_box* (ctypes array or address)
     L.rp_set_attached.argtypes = [vp, i32, u32]
     L.rp_check_states.argtypes = [vp, vp, i64, vp]
     L.rp_check_states_device.argtypes = [vp, vp, i64, vp, vp]
@@ -57,6 +57,8 @@ def load():
     L.rp_check_edges_device.argtypes = [vp, vp, vp, i64, f64, vp, vp]
     L.rp_state_contacts.argtypes = [vp, vp, vp, i32]
     L.rp_plan.argtypes = [vp, vp, vp, vp, vp, C.POINTER(_abi.PlanParams), vp, i32, C.POINTER(i32), C.POINTER(i32)]
+    L.rp_plan_async.argtypes = L.rp_plan.argtypes
+    L.rp_plan_wait.argtypes = [vp]
     L.rp_group_init.argtypes = [vp, i32, i32, vp, vp]
     L.rp_group_rccl_unique_id.argtypes = [vp]
     L.rp_group_init_shm.argtypes = [vp, i32, i32, vp, i64]
@@ -106,6 +108,7 @@ class Context:
         if rc != 0:
             raise NativeError(f"rp_create failed ({rc}): {L.rp_last_error(None).decode()}")
         self.device = device
+        self.scene_gen = 0   # bumped by every set_scene / set_attached (callers that cache a scene)
         self._cb = None
         self._group_bufs = None
 
@@ -129,9 +132,20 @@ class Context:
     def set_scene(self, boxes, plane_z=0.0, base=(0.0, 0.0, 0.01)):
         arr, n = _abi.make_boxes(boxes)
         b = (C.c_float * 3)(*[float(v) for v in base])
+        self.scene_gen += 1
         self._check(load().rp_set_scene(self._h, arr, n, float(plane_z), b), "rp_set_scene")
 
+    def set_scene_array(self, rec, plane_z=0.0, base=(0.0, 0.0, 0.01)):
+        """set_scene from an (n, 7) C-contiguous float32 array of rp_box records
+        (center xyz, half extents xyz, yaw): no per-box ctypes conversion."""
+        assert rec.dtype == np.float32 and rec.ndim == 2 and rec.shape[1] == 7 and rec.flags.c_contiguous
+        b = (C.c_float * 3)(*base)
+        self.scene_gen += 1
+        self._check(load().rp_set_scene(self._h, rec.ctypes.data if len(rec) else None, len(rec), float(plane_z), b),
+                    "rp_set_scene")
+
     def set_attached(self, box_index, link_mask=_abi.ATTACH_EXEMPT_MASK):
+        self.scene_gen += 1
         self._check(load().rp_set_attached(self._h, int(box_index), int(link_mask)), "rp_set_attached")
 
     # -- validity ------------------------------------------------------------
@@ -183,7 +197,7 @@ class Context:
         return out
 
     # -- planning ------------------------------------------------------------
-    def plan(self, start, goal, lo, hi, params, path_cap=4096):
+    def _plan_buffers(self, path_cap):
         # A plan of a few tens of microseconds: the call's own overhead matters, so the
         # inputs go into one reused buffer whose address (and the output's) is taken
         # once (ndarray.ctypes costs microseconds per use)
@@ -193,19 +207,50 @@ class Context:
             out = np.empty((path_cap, _abi.NQ), dtype=np.float64)
             n, status = C.c_int32(0), C.c_int32(0)
             a = inp.ctypes.data
-            b = self._plan_bufs = {"inp": inp, "out": out, "n": n, "status": status, "fn": load().rp_plan,
+            L = load()
+            b = self._plan_bufs = {"inp": inp, "out": out, "n": n, "status": status, "fn": L.rp_plan,
+                                   "fn_async": L.rp_plan_async, "fn_wait": L.rp_plan_wait,
                                    "args": (a, a + 8 * _abi.NQ, a + 16 * _abi.NQ, a + 24 * _abi.NQ),
                                    "out_addr": out.ctypes.data, "rn": C.byref(n), "rs": C.byref(status)}
+        return b
+
+    def _plan_call(self, fn, start, goal, lo, hi, params, path_cap):
+        b = self._plan_buffers(path_cap)
         inp, nq = b["inp"], _abi.NQ
         inp[0:nq] = start
         inp[nq:2 * nq] = goal
         inp[2 * nq:3 * nq] = lo
         inp[3 * nq:4 * nq] = hi
         a0, a1, a2, a3 = b["args"]
-        rc = b["fn"](self._h, a0, a1, a2, a3, C.byref(params), b["out_addr"], path_cap, b["rn"], b["rs"])
+        rc = b[fn](self._h, a0, a1, a2, a3, C.byref(params), b["out_addr"], path_cap, b["rn"], b["rs"])
+        if rc < 0:
+            self._check(rc, "rp_plan" if fn == "fn" else "rp_plan_async")
+        return b
+
+    def plan(self, start, goal, lo, hi, params, path_cap=4096):
+        """rp_plan: (path (n, 9) float64, status)."""
+        b = self._plan_call("fn", start, goal, lo, hi, params, path_cap)
+        return b["out"][:b["n"].value].copy(), b["status"].value
+
+    def plan_async(self, start, goal, lo, hi, params, path_cap=4096):
+        """rp_plan_async: hand the query to the context's planner thread and return
+        at once; plan_wait() returns what plan() would. The params struct is copied."""
+        self._plan_call("fn_async", start, goal, lo, hi, params, path_cap)
+
+    def plan_wait(self, out=None):
+        """rp_plan_wait: (path, status) of the query in flight. With `out` (an (m, 9)
+        float array, e.g. the numpy view of a float32 tensor) a path of exactly m
+        states is written into it (float64 -> float32 rounds once, as astype) and
+        `out` is returned; otherwise a float64 copy."""
+        b = self._plan_bufs
+        rc = b["fn_wait"](self._h)
         if rc < 0:
             self._check(rc, "rp_plan")
-        return b["out"][:b["n"].value].copy(), b["status"].value
+        n = b["n"].value
+        if out is not None and len(out) == n:
+            np.copyto(out, b["out"][:n], casting="same_kind")
+            return out, b["status"].value
+        return b["out"][:n].copy(), b["status"].value
 
     def ik(self, pos, quat, init, lo, hi, params=None):
         """Batched hand-link IK (rp_ik): pos (T, 3), quat (T, 4) as w, x, y, z, init

@@ -174,16 +174,26 @@ class _SpaceInfo:
         return self._b
 
 
+def _f64(x):
+    """float64 copy of a qpos (torch tensor or array-like); tensor_to_array + asarray."""
+    if isinstance(x, torch.Tensor):
+        return x.detach().cpu().numpy().astype(np.float64)
+    return np.array(x, dtype=np.float64)
+
+
 class PlannerInterface:
     def __init__(self, robot: Any, scene: Any):
         self.robot = _ensure_adapter(robot, scene)
         self.scene = scene
         self.attached_object = None
         self._ctx = None
-        self._scene_cache = {}
+        self._reader = None      # scenes.GenesisReader of self.scene
+        self._pushed = None      # (ctx.scene_gen, box poses, base, attached box) last pushed
+        self._qlim = None        # (robot.q_limit object, lo, hi)
+        self._params = None
+        self._stats_ctx = None
+        self._times = None
         self.last_status = None
-        self.last_stats = None
-        self.last_timing = None
 
     # -- GPU context -----------------------------------------------------------
     def _context(self):
@@ -192,22 +202,65 @@ class PlannerInterface:
         return self._ctx
 
     def _sync_scene(self):
-        """Push the current obstacle geometry (boxes at their simulated poses) and
-        the attached box to the GPU context."""
-        sc = scenes.from_genesis(self.scene, self.robot, cache=self._scene_cache)
+        """Push the obstacle geometry (boxes at their simulated poses) and the attached
+        box to the GPU context. The poses are read on every call (the simulation may
+        have moved a block); the context is updated only when they, the attachment or
+        the context's scene (someone else set one) changed."""
+        rd = self._reader
+        if rd is None or not rd.valid_for(self.scene, self.robot):
+            rd = self._reader = scenes.GenesisReader(self.scene, self.robot)
+            self._pushed = None
+            self._scene_names = rd.names
+        poses, base = rd.poses()
         ctx = self._context()
-        ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
         idx = -1
         att = self.attached_object
         if att:
-            ent_idx = getattr(att, "idx", None)
-            for k, e in enumerate(sc.entity_idx):
-                if e is not None and e == ent_idx:
-                    idx = k
-                    break
+            idx = rd.box_of_entity.get(getattr(att, "idx", None), -1)
+        gen = getattr(ctx, "scene_gen", None)
+        pushed = self._pushed
+        if gen is not None and pushed is not None and pushed[0] == gen and pushed[1] == poses \
+                and pushed[2] == base:
+            if pushed[3] != idx:
+                ctx.set_attached(idx)
+                self._pushed = (ctx.scene_gen, poses, base, idx)
+            return
+        if hasattr(ctx, "set_scene_array"):
+            ctx.set_scene_array(rd.box_array(poses), rd.plane_z, base)
+        else:
+            ctx.set_scene(rd.boxes(poses), rd.plane_z, base)
         ctx.set_attached(idx)
-        self._scene_names = sc.names
-        return sc
+        self._pushed = (getattr(ctx, "scene_gen", None), poses, base, idx)
+
+    def _bounds(self):
+        """planning.py:139-150: bounds = the robot's q_limit as float64 (of the stored
+        float32 values); converted once per q_limit object."""
+        ql = self.robot.q_limit
+        c = self._qlim
+        if c is None or c[0] is not ql:
+            lo = np.asarray(tensor_to_array(ql[0]), dtype=float)
+            hi = np.asarray(tensor_to_array(ql[1]), dtype=float)
+            c = self._qlim = (ql, lo, hi)
+        return c[1], c[2]
+
+    @property
+    def last_stats(self):
+        """rp_get_stats of this planner's last query (None if it failed in the library)."""
+        return self._stats_ctx.stats() if self._stats_ctx is not None else None
+
+    @property
+    def last_timing(self):
+        """Where the last plan_path call's wall time went (ms): scene ingestion (entity
+        poses -> boxes, rp_set_scene / rp_set_attached when they changed), rp_plan
+        (from rp_plan_async to rp_plan_wait's return: the GPU query, with the waypoint
+        tensors and the qpos restore overlapped), and everything else (argument
+        checks, bounds, diagnostics, the output list)."""
+        if self._times is None:
+            return None
+        t0, t1, t2, t3, t4 = self._times
+        total = 1e3 * (t4 - t0)
+        return {"total_ms": total, "scene_ms": 1e3 * (t1 - t0), "rp_plan_ms": 1e3 * (t3 - t2),
+                "other_ms": total - 1e3 * (t1 - t0) - 1e3 * (t3 - t2)}
 
     # -- diagnostics (planning.py:32-57) ----------------------------------------
     def diagnose_bounds_violation(self, si, state):
@@ -237,89 +290,99 @@ class PlannerInterface:
     def plan_path(self, qpos_goal, qpos_start=None, timeout=5.0, smooth_path=True, num_waypoints=100,
                   attached_object=None, planner="RRTConnect"):
         t_enter = time.perf_counter()
-        if planner not in SUPPORTED_PLANNERS:
-            _raise(f"Planner {planner} is not supported. Supported planners: {SUPPORTED_PLANNERS}.")
         if planner != "RRTConnect":
+            if planner not in SUPPORTED_PLANNERS:
+                _raise(f"Planner {planner} is not supported. Supported planners: {SUPPORTED_PLANNERS}.")
             _logger().warning(f"Planner {planner} is served by the MI355X batched RRT-Connect.")
-        solver = getattr(self.robot, "_solver", None)
+        robot = self.robot
+        solver = getattr(robot, "_solver", None)
         if solver is not None and getattr(solver, "n_envs", 0) > 0:
             _raise("Motion planning is not supported for batched envs (yet).")
-        if self.robot.n_qs != self.robot.n_dofs:
+        n_qs = robot.n_qs
+        if n_qs != robot.n_dofs:
             _raise("Motion planning is not yet supported for rigid entities with free joints.")
 
-        qpos_cur = self.robot.get_qpos()
-        if qpos_start is None:
-            qpos_start = self.robot.get_qpos()
-        qpos_start = np.asarray(tensor_to_array(qpos_start), dtype=np.float64)
-        qpos_goal = np.asarray(tensor_to_array(qpos_goal), dtype=np.float64)
-        n_qs = self.robot.n_qs
+        # planning.py:129-133 reads get_qpos() twice (current, and the start when none
+        # is given): one read serves both
+        qpos_cur = robot.get_qpos()
+        qpos_start = _f64(qpos_cur if qpos_start is None else qpos_start)
+        qpos_goal = _f64(qpos_goal)
         if qpos_start.shape != (n_qs,) or qpos_goal.shape != (n_qs,):
             _raise("Invalid shape for `qpos_start` or `qpos_goal`.")
         if n_qs != _abi.NQ:
             _raise(f"The MI355X planner is built for the 9-D Franka Panda (got n_qs={n_qs}).")
-
-        lo = np.asarray(tensor_to_array(self.robot.q_limit[0]), dtype=float)
-        hi = np.asarray(tensor_to_array(self.robot.q_limit[1]), dtype=float)
+        lo, hi = self._bounds()
 
         self.attached_object = attached_object
         ctx = self._context()
         self._sync_scene()
         t_scene = time.perf_counter()
 
-        si = _SpaceInfo(lo, hi)
-        eps = np.finfo(np.float64).eps
-        start_in = bool(np.all(qpos_start - eps <= hi) and np.all(qpos_start + eps >= lo))
-        if not start_in:
-            _logger().warning("OMPL start state out of bounds")
-            self.diagnose_bounds_violation(si, qpos_start)
-        goal_in = bool(np.all(qpos_goal - eps <= hi) and np.all(qpos_goal + eps >= lo))
-        if not goal_in:
-            _logger().warning("OMPL goal state out of bounds")
-            self.diagnose_bounds_violation(si, qpos_goal)
-
-        params = _abi.make_params(seed=_next_seed(), batch=_batch(), timeout_s=float(timeout),
-                                  n_waypoints=int(num_waypoints) if num_waypoints else 0,
-                                  simplify=bool(smooth_path), tree_capacity=_CONFIG["tree_capacity"] or 0,
-                                  straight_first=_straight_first())
-        cap = max(4096, int(num_waypoints or 0) + 16)
+        p = self._params
+        if p is None:
+            p = self._params = _abi.make_params()
+        _abi.set_params(p, seed=_next_seed(), batch=_batch(), timeout_s=float(timeout),
+                        n_waypoints=int(num_waypoints) if num_waypoints else 0, simplify=bool(smooth_path),
+                        tree_capacity=_CONFIG["tree_capacity"] or 0, straight_first=_straight_first())
+        nwp = p.n_waypoints
+        cap = max(4096, nwp + 16)
         t_plan0 = time.perf_counter()
+        path = out = None
+        status = _abi.STATUS_NONE
+        restored = False
+        self._stats_ctx = None
         try:
-            path, status = ctx.plan(qpos_start, qpos_goal, lo, hi, params, path_cap=cap)
-            t_plan1 = time.perf_counter()
-            self.last_stats = ctx.stats()
+            ctx.plan_async(qpos_start, qpos_goal, lo, hi, p, path_cap=cap)
+            # while the GPU plans: the waypoint tensors of the expected path (an
+            # interpolated solution has exactly num_waypoints states) and the restore
+            # of the robot's qpos (planning.py:205; the planner never moves the robot)
+            views = None
+            try:
+                if nwp > 0:
+                    buf = torch.empty((nwp, n_qs), dtype=torch.float32)
+                    views = buf.unbind(0)
+                    out = buf.numpy()
+                robot.set_qpos(qpos_cur)
+                restored = True
+            finally:
+                path, status = ctx.plan_wait(out)
+            self._stats_ctx = ctx
         except NativeError as ex:
             # the reference never raises on a failed plan (planning.py:190-202):
             # a library error (capacity, HIP) is reported and planning "fails"
             _logger().warning(f"MI355X planner error: {ex}")
             path, status = None, _abi.STATUS_NONE
-            t_plan1 = time.perf_counter()
-            self.last_stats = None
+        t_plan1 = time.perf_counter()
         self.last_status = status
-        # planning.py:174-183 validity diagnostics. rp_plan checks the start and the
-        # goal itself (INVALID_START / INVALID_GOAL, as OMPL's planner does), so a
-        # separate check launch is only needed when one of them can be invalid: the
-        # plan reported it, a bound is violated, or the plan did not run
-        if status in (_abi.STATUS_INVALID_START, _abi.STATUS_INVALID_GOAL) or path is None \
-                or not (start_in and goal_in):
-            self._diagnose_start_goal(ctx, qpos_start, qpos_goal)
+
+        if status in (_abi.STATUS_INVALID_START, _abi.STATUS_INVALID_GOAL) or path is None:
+            self._diagnose(ctx, qpos_start, qpos_goal, lo, hi)
 
         waypoints = []
         if status in (_abi.STATUS_EXACT, _abi.STATUS_APPROXIMATE):
             _logger().info("Path solution found successfully.")
             print("Number of waypoints in path:", len(path))
-            waypoints = self._states_to_tensor_list(path)
+            waypoints = list(views) if path is out and out is not None else self._states_to_tensor_list(path)
         else:
             _logger().warning("Path planning failed. Returning empty path.")
-
-        self.robot.set_qpos(qpos_cur)
-        t_exit = time.perf_counter()
-        # where the call's wall time went (ms): scene ingestion (entity poses -> boxes,
-        # rp_set_scene / rp_set_attached), rp_plan itself, and everything else (argument
-        # checks, bounds, diagnostics, the waypoint tensors, restoring qpos)
-        self.last_timing = {"total_ms": 1e3 * (t_exit - t_enter), "scene_ms": 1e3 * (t_scene - t_enter),
-                            "rp_plan_ms": 1e3 * (t_plan1 - t_plan0),
-                            "other_ms": 1e3 * ((t_exit - t_enter) - (t_scene - t_enter) - (t_plan1 - t_plan0))}
+        if not restored:
+            robot.set_qpos(qpos_cur)
+        self._times = (t_enter, t_scene, t_plan0, t_plan1, time.perf_counter())
         return waypoints
+
+    def _diagnose(self, ctx, qpos_start, qpos_goal, lo, hi):
+        """planning.py:164-183: bound and validity diagnostics of start and goal, run
+        when the plan reports an invalid start / goal (rp_plan applies OMPL's bound
+        and validity checks to both itself) or did not run."""
+        si = _SpaceInfo(lo, hi)
+        eps = np.finfo(np.float64).eps
+        if not bool(np.all(qpos_start - eps <= hi) and np.all(qpos_start + eps >= lo)):
+            _logger().warning("OMPL start state out of bounds")
+            self.diagnose_bounds_violation(si, qpos_start)
+        if not bool(np.all(qpos_goal - eps <= hi) and np.all(qpos_goal + eps >= lo)):
+            _logger().warning("OMPL goal state out of bounds")
+            self.diagnose_bounds_violation(si, qpos_goal)
+        self._diagnose_start_goal(ctx, qpos_start, qpos_goal)
 
     def _diagnose_start_goal(self, ctx, qpos_start, qpos_goal):
         try:

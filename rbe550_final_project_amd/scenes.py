@@ -201,52 +201,146 @@ def _entity_table(entities, raw_robot, robot):
     return table
 
 
-def from_genesis(scene, robot=None, cache=None):
-    """Boxes of a Genesis scene: every entity whose morph is a Box, at its current
-    pose (entity.get_pos / get_quat). Planes are taken as the ground at z = 0.
-
-    cache: a dict owned by the caller (one per PlannerInterface). The entities'
-    static data (morph kind, box size, plane height) is kept there while the
-    scene's entity list is the same objects, so a call reads only the poses."""
+def _entities(scene):
     entities = getattr(scene, "entities", None)
     if entities is None and hasattr(scene, "sim"):
         entities = scene.sim.entities
-    entities = list(entities or [])
-    raw_robot = getattr(robot, "robot", robot)
-    table = None
-    if cache is not None:
-        ents = cache.get("entities")
-        if ents is not None and len(ents) == len(entities) and cache.get("robot") is raw_robot \
-                and all(a is b for a, b in zip(ents, entities)):
-            table = cache["table"]
-    if table is None:
-        table = _entity_table(entities, raw_robot, robot)
-        if cache is not None:
-            cache.update(entities=entities, robot=raw_robot, table=table)
-    s = Scene()
-    base = BASE
-    plane_z = 0.0
-    for ent, (kind, data) in zip(entities, table):
-        if kind == "box":
-            half, idx = data
+    return entities if entities is not None else []
+
+
+def _rows(x, n, k):
+    """An (n, k) pose block (torch tensor / array, possibly with a leading env axis of
+    1) as n lists of k Python floats, with one .tolist()."""
+    if hasattr(x, "detach"):
+        x = x.detach()
+    if hasattr(x, "tolist") and not isinstance(x, np.ndarray):
+        v = x.tolist()
+    else:
+        v = np.asarray(x, dtype=float).tolist()
+    while len(v) == 1 and n != 1 and isinstance(v[0], list) and isinstance(v[0][0], list):
+        v = v[0]
+    if n == 1 and not isinstance(v[0], list):
+        v = [v]
+    return [[float(a) for a in r[:k]] for r in v[:n]]
+
+
+class GenesisReader:
+    """Reads the collider-relevant state of a live Genesis scene: every Box entity's
+    pose, the robot base and the ground height (code/scenes.py builds them; the
+    reference's collider sees them through set_qpos + detect_collision,
+    code/planning.py:209-219).
+
+    The entities' static data (morph kind, box half extents, plane height) is read
+    once while the scene's entity list is the same objects. Poses are read per query:
+    when the scene's rigid solver offers `get_links_pos` / `get_links_quat` and every
+    box has a `base_link_idx`, with one call each for all boxes and the robot base
+    (Genesis serves each entity.get_pos() with its own solver read); otherwise per
+    entity with `get_pos()` / `get_quat()`."""
+
+    def __init__(self, scene, robot=None):
+        self.scene = scene
+        entities = _entities(scene)
+        self._ents_obj = entities
+        self._ents = list(entities)
+        raw_robot = getattr(robot, "robot", robot)
+        self._raw_robot = raw_robot
+        self._robot = robot
+        table = _entity_table(self._ents, raw_robot, robot)
+        self.box_ents, self.halves, self.entity_idx = [], [], []
+        self.robot_ent = None
+        self.plane_z = 0.0
+        for ent, (kind, data) in zip(self._ents, table):
+            if kind == "box":
+                self.box_ents.append(ent)
+                self.halves.append(data[0])
+                self.entity_idx.append(data[1])
+            elif kind == "robot":
+                self.robot_ent = ent
+            elif kind == "plane":
+                self.plane_z = data
+        self.box_of_entity = {e: k for k, e in enumerate(self.entity_idx) if e is not None}
+        self.names = [str(e if e is not None else k) for k, e in enumerate(self.entity_idx)]
+        self._links = None
+        solver = getattr(scene, "rigid_solver", None)
+        if solver is not None and hasattr(solver, "get_links_pos") and hasattr(solver, "get_links_quat"):
+            rsrc = self._raw_robot if self._raw_robot is not None else self.robot_ent
+            links = [getattr(e, "base_link_idx", None) for e in self.box_ents]
+            if rsrc is not None:
+                links.append(getattr(rsrc, "base_link_idx", None))
+            if all(isinstance(x, (int, np.integer)) for x in links):
+                self._solver = solver
+                self._nb = len(self.box_ents)
+                self._with_base = rsrc is not None
+                self._links = [int(x) for x in links]
+
+    def valid_for(self, scene, robot):
+        """Same scene, robot and entity objects as when the static data was read."""
+        if scene is not self.scene or getattr(robot, "robot", robot) is not self._raw_robot:
+            return False
+        ents = _entities(scene)
+        if ents is self._ents_obj and len(ents) == len(self._ents):
+            return True
+        ents = list(ents)
+        return len(ents) == len(self._ents) and all(a is b for a, b in zip(ents, self._ents))
+
+    def poses(self):
+        """(box poses: per box [x, y, z, qw, qx, qy, qz], robot base (x, y, z))."""
+        if self._links is not None:
+            n = len(self._links)
+            P = _rows(self._solver.get_links_pos(self._links), n, 3)
+            Q = _rows(self._solver.get_links_quat(self._links), n, 4)
+            boxes = [p + q for p, q in zip(P[:self._nb], Q[:self._nb])]
+            base = tuple(P[self._nb]) if self._with_base else BASE
+            return boxes, base
+        boxes = []
+        for ent in self.box_ents:
             pos = _floats(ent.get_pos(), 3)
-            quat = _floats(ent.get_quat(), 4) if hasattr(ent, "get_quat") else (1.0, 0.0, 0.0, 0.0)
-            s.boxes.append((tuple(pos), half, yaw_of_quat(quat)))
-            s.names.append(str(idx if idx is not None else len(s.names)))
-            s.entity_idx.append(idx)
-        elif kind == "robot":
-            if hasattr(ent, "get_pos"):
-                base = tuple(_floats(ent.get_pos(), 3))
-        elif kind == "plane":
-            plane_z = data
-    if robot is not None and hasattr(robot, "get_pos"):
-        try:
-            base = tuple(_floats(robot.get_pos(), 3))
-        except Exception:
-            pass
-    s.base = base
-    s.plane_z = plane_z
-    return s
+            quat = _floats(ent.get_quat(), 4) if hasattr(ent, "get_quat") else [1.0, 0.0, 0.0, 0.0]
+            boxes.append(pos + quat)
+        base = BASE
+        if self.robot_ent is not None and hasattr(self.robot_ent, "get_pos"):
+            base = tuple(_floats(self.robot_ent.get_pos(), 3))
+        robot = self._robot
+        if robot is not None and robot is not self.robot_ent and hasattr(robot, "get_pos"):
+            try:
+                base = tuple(_floats(robot.get_pos(), 3))
+            except Exception:
+                pass
+        return boxes, base
+
+    def boxes(self, poses):
+        """Box records (center, half, yaw) of box poses from poses()."""
+        return [((p[0], p[1], p[2]), h, yaw_of_quat(p[3:7])) for p, h in zip(poses, self.halves)]
+
+    def box_array(self, poses):
+        """The rp_box records of box poses from poses() as an (n, 7) float32 array
+        (center, half extents, yaw: the values boxes() gives, rounded to float32
+        once, as the ctypes path of _abi.make_boxes)."""
+        n = len(poses)
+        rec = np.empty((n, 7), dtype=np.float32)
+        if n:
+            rec[:, 0:3] = np.array(poses, dtype=np.float64)[:, 0:3]
+            rec[:, 3:6] = self.halves
+            rec[:, 6] = [math.atan2(2.0 * (w * z + x * y), 1.0 - 2.0 * (y * y + z * z))
+                         for _, _, _, w, x, y, z in poses]
+        return rec
+
+    def read(self):
+        """The scene as a Scene record."""
+        poses, base = self.poses()
+        return Scene(self.boxes(poses), list(self.names), self.plane_z, base, list(self.entity_idx))
+
+
+def from_genesis(scene, robot=None, cache=None):
+    """Boxes of a Genesis scene: every entity whose morph is a Box, at its current
+    pose (GenesisReader). cache: a dict owned by the caller (one per
+    PlannerInterface) that keeps the reader while the scene's entities stay the same."""
+    rd = cache.get("reader") if cache is not None else None
+    if rd is None or not rd.valid_for(scene, robot):
+        rd = GenesisReader(scene, robot)
+        if cache is not None:
+            cache["reader"] = rd
+    return rd.read()
 
 
 def load_json(path):

@@ -1,6 +1,8 @@
 """Genesis-free mock robot/scene exposing exactly what planning.py reads
 (SURVEY.md §4 item 5): n_qs, n_dofs, q_limit, get_qpos/set_qpos, get_pos,
-_solver.n_envs, and scene.entities with Box/Plane morphs and poses."""
+_solver.n_envs, and scene.entities with Box/Plane morphs and poses; with
+`rigid_solver=True` also Genesis' batched link-pose reads
+(scene.rigid_solver.get_links_pos / get_links_quat over entity.base_link_idx)."""
 import math
 
 import numpy as np
@@ -28,6 +30,7 @@ class MJCF:
 class Entity:
     def __init__(self, idx, morph, yaw=0.0):
         self.idx = idx
+        self.base_link_idx = idx   # one link per entity here (the robot's base link)
         self.morph = morph
         self._pos = np.array(getattr(morph, "pos", (0, 0, 0)), dtype=float)
         self._quat = np.array([math.cos(yaw / 2), 0.0, 0.0, math.sin(yaw / 2)])
@@ -61,12 +64,30 @@ class Robot(Entity):
         self.q = torch.as_tensor(q, dtype=torch.float32).clone()
 
 
+class RigidSolver:
+    """scene.rigid_solver's link-pose reads: one (n, 3) / (n, 4) float32 tensor per
+    call, as Genesis returns for n links of an unbatched scene."""
+
+    def __init__(self, scene):
+        self._scene = scene
+
+    def get_links_pos(self, links_idx=None):
+        ents = self._scene.entities
+        return torch.tensor(np.stack([ents[i]._pos for i in links_idx]), dtype=torch.float32)
+
+    def get_links_quat(self, links_idx=None):
+        ents = self._scene.entities
+        return torch.tensor(np.stack([ents[i]._quat for i in links_idx]), dtype=torch.float32)
+
+
 class Scene:
     """plane (entity 0), boxes (1..n), robot (n+1) — the order of code/scenes.py."""
 
-    def __init__(self, boxes, **robot_kw):
+    def __init__(self, boxes, rigid_solver=True, **robot_kw):
         self.entities = [Entity(0, Plane())]
         for i, (c, h, yaw) in enumerate(boxes):
             self.entities.append(Entity(i + 1, Box([2 * v for v in h], c), yaw))
         self.robot = Robot(len(self.entities), **robot_kw)
         self.entities.append(self.robot)
+        if rigid_solver:
+            self.rigid_solver = RigidSolver(self)

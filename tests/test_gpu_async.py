@@ -1,0 +1,108 @@
+"""rp_plan_async / rp_plan_wait (the planner thread) and the drop-in plan_path built
+on it, against the CPU oracle: the same paths, statuses and trees as rp_plan, every
+other call refused while a query is in flight."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from rbe550_final_project_amd import _abi, model, planning, scenes
+from rbe550_final_project_amd.native import NativeError
+import mock_genesis as M
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _wl(name):
+    return json.load(open(os.path.join(GOLD, "workloads", name + ".json")))
+
+
+@pytest.mark.parametrize("straight_first", [True, False])
+def test_async_equals_oracle_every_goal3_query(gpu_ctx, oracle_lib, straight_first):
+    for qi, q in enumerate(_wl("goal3_tallest_10box")["queries"]):
+        sc = scenes.Scene.from_json(q["scene"])
+        o = oracle_lib.OracleScene()
+        o.set_scene(sc.boxes, sc.plane_z, sc.base)
+        o.set_attached(q["attached"])
+        gpu_ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+        gpu_ctx.set_attached(q["attached"])
+        p = _abi.make_params(seed=qi, batch=4096, n_waypoints=150, timeout_s=60, straight_first=straight_first)
+        ref, st_ref, stats_ref = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+        gpu_ctx.plan_async(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+        out = np.empty((150, 9), dtype=np.float32)
+        path, st = gpu_ctx.plan_wait(out)
+        assert st == st_ref == _abi.STATUS_EXACT and path is out, (qi, st)
+        assert np.array_equal(path, ref.astype(np.float32)), qi
+        g = gpu_ctx.stats()
+        assert (g["start_tree_size"], g["goal_tree_size"], g["iterations"]) == \
+            (stats_ref["start_tree_size"], stats_ref["goal_tree_size"], stats_ref["iterations"]), qi
+        # float64 output (no buffer) equals rp_plan's
+        gpu_ctx.plan_async(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+        path64, st64 = gpu_ctx.plan_wait()
+        assert st64 == st_ref and np.array_equal(path64, ref), qi
+
+
+def test_calls_refused_while_in_flight(gpu_ctx):
+    sc = scenes.goal3_tallest()
+    gpu_ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+    gpu_ctx.set_attached(-1)
+    q = _wl("goal3_tallest_10box")["queries"][3]
+    p = _abi.make_params(seed=1, batch=4096, n_waypoints=150, timeout_s=60, straight_first=False)
+    gpu_ctx.plan_async(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+    refused = 0
+    for call in (lambda: gpu_ctx.check_states(np.zeros((4, 9), np.float32)),
+                 lambda: gpu_ctx.set_attached(-1),
+                 lambda: gpu_ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)):
+        try:
+            call()
+        except NativeError as e:
+            refused += 1
+            assert "in flight" in str(e)
+    path, st = gpu_ctx.plan_wait()
+    # the query may have finished before a call was made: a call is refused until
+    # rp_plan_wait returns, whatever the GPU's progress
+    assert refused == 3 and st == _abi.STATUS_EXACT and len(path) == 150
+    with pytest.raises(NativeError, match="without a query in flight"):
+        gpu_ctx.plan_wait()
+    assert gpu_ctx.check_states(np.zeros((4, 9), np.float32)).shape == (4,)
+
+
+@pytest.mark.parametrize("straight_first", [True, False])
+def test_plan_path_equals_oracle(gpu_ctx, oracle_lib, straight_first):
+    """PlannerInterface.plan_path with the call site's arguments
+    (code/motion_primitives.py:144) through the Genesis mock: the waypoints are the
+    oracle's path for the scene the reader ingests (float32 entity poses), rounded
+    to float32; the scene is pushed only when a block moved."""
+    wl = _wl("goal3_tallest_10box")
+    q0 = scenes.Scene.from_json(wl["queries"][0]["scene"])
+    sim = M.Scene(q0.boxes)
+    pi = planning.PlannerInterface(sim.robot, sim)
+    pi._ctx = gpu_ctx
+    planning.configure(seed=0, batch=4096, straight_first=straight_first)
+    try:
+        for qi, q in enumerate(wl["queries"]):
+            sc = scenes.Scene.from_json(q["scene"])
+            for ent, (c, h, yaw) in zip(sim.entities[1:], sc.boxes):
+                ent.set_pos(c)
+                ent._quat = np.array([np.cos(yaw / 2), 0.0, 0.0, np.sin(yaw / 2)])
+            sim.robot.q = torch.tensor(q["start"], dtype=torch.float32)
+            held = sim.entities[1 + q["attached"]] if q["attached"] >= 0 else None
+            goal = np.array(q["goal"], dtype=float)
+            wps = pi.plan_path(qpos_goal=goal, num_waypoints=150, attached_object=held, timeout=10.0)
+            ing = scenes.from_genesis(sim, pi.robot)
+            o = oracle_lib.OracleScene()
+            o.set_scene(ing.boxes, ing.plane_z, ing.base)
+            o.set_attached(q["attached"])
+            start = sim.robot.q.numpy().astype(np.float64)
+            p = _abi.make_params(seed=qi, batch=4096, n_waypoints=150, timeout_s=10.0, straight_first=straight_first)
+            lo, hi = pi._bounds()
+            ref, st_ref, _ = o.plan(start, goal, lo, hi, p)
+            assert pi.last_status == st_ref == _abi.STATUS_EXACT, qi
+            assert len(wps) == 150 and all(w.dtype == torch.float32 and tuple(w.shape) == (9,) for w in wps)
+            assert np.array_equal(torch.stack(wps).numpy(), ref.astype(np.float32)), qi
+            assert torch.equal(sim.robot.set_calls[-1], torch.tensor(q["start"], dtype=torch.float32))
+    finally:
+        planning.configure(straight_first=True)

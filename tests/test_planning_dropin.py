@@ -143,7 +143,10 @@ class _FakeContext:
     def check_states(self, q):
         return np.ones(len(np.asarray(q).reshape(-1, 9)), dtype=np.uint8)
 
-    def plan(self, *a, **k):
+    def plan_async(self, *a, **k):
+        pass
+
+    def plan_wait(self, out=None):
         raise NativeError("rp_plan failed (-5): path_cap too small")
 
     def stats(self):

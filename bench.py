@@ -98,6 +98,9 @@ def run_plans(ctx, wl, batch, seed, group, batch_min=0, tree_capacity=0, stats_o
     straight_first=False forces RRT-Connect on every query (the product default
     first checks the straight edge start -> goal)."""
     times, states, statuses = [], 0, []
+    # the workspace for this batch / tree size, allocated before the timed queries
+    # (rp_reserve; the product's PlannerInterface does the same when it opens a context)
+    ctx.reserve(batch, tree_capacity)
     for i, q in enumerate(wl["queries"]):
         sc = scenes.Scene.from_json(q["scene"])
         ctx.set_scene(sc.boxes, sc.plane_z, sc.base)

@@ -18,6 +18,10 @@
  *                               interpolated path: RealVectorStateSpace bounds,
  *                               RRTConnect solve, simplifySolution,
  *                               path.interpolate(num_waypoints)                   code/planning.py:139-200
+ *   rp_plan_async / rp_plan_wait rp_plan on the context's planner thread, so the
+ *                               caller's tensor-list conversion and qpos restore
+ *                               overlap the query                                 code/planning.py:200-205,232-242
+ *   rp_reserve                  (new) workspace sizing ahead of the first query
  *   rp_ik                       robot.inverse_kinematics(link=hand, pos, quat) that
  *                               makes plan_path's goals (Genesis, batched restarts)  code/motion_primitives.py:131-134
  *   rp_group_*                  (new) data-parallel sharding of each RRT-Connect
@@ -269,6 +273,13 @@ int rp_plan_async(rp_ctx* ctx, const double start[RP_NQ], const double goal[RP_N
                   const double lo[RP_NQ], const double hi[RP_NQ], const rp_plan_params* params,
                   double* path_out, int32_t path_cap, int32_t* n_out, int32_t* status_out);
 int rp_plan_wait(rp_ctx* ctx);
+
+/* Size the planner's device workspace for queries of up to `batch` samples per
+ * iteration on trees of `tree_capacity` nodes (0: the rp_plan_params defaults), so
+ * that the first such query allocates nothing (hipMalloc / hipFree synchronise the
+ * device: milliseconds inside the query otherwise). Buffers only grow; rp_plan
+ * grows them itself for anything larger. */
+int rp_reserve(rp_ctx* ctx, int64_t batch, int64_t tree_capacity);
 
 /* Batched IK of the hand link: for each of n_targets poses (pos[3], quat[4] as
  * w, x, y, z; world frame, robot base from rp_set_scene) run n_seeds damped-least-

@@ -1089,6 +1089,59 @@ void wait_seq(rp_ctx* c, int seq) {
 // the batched RRT-Connect solve
 // ---------------------------------------------------------------------------
 
+// The planner's device workspace for iterations of up to BMAX samples on trees of
+// `cap` nodes (plan_impl; rp_reserve sizes it ahead of the first query, so no
+// hipMalloc / hipFree, which synchronise the device, lands inside a timed plan).
+// Buffers only grow.
+void plan_workspace(rp_ctx* c, int64_t BMAX, int world, int cmax, int64_t cap, bool grouped) {
+    const int64_t PMAX = BMAX / world;
+    for (auto& t : c->tree) {
+        t.q.ensure((size_t)cap * NQ);
+        t.par.ensure(cap);
+        t.cand.ensure(cap);
+    }
+    const int64_t ne = std::max<int64_t>({PMAX + 2, ((BMAX + world - 1) / world) * cmax, (int64_t)SPMAX * SPMAX / 2,
+                                          (std::min<int64_t>(BMAX, FUSE_MAX) + 2) * (cmax + 1),
+                                          grouped ? (PMAX + 2) * (cmax + 1) : 0});
+    c->efrom.ensure(ne * NQ);
+    c->eto.ensure(ne * NQ);
+    c->nd.ensure(ne);
+    c->valid.ensure(ne);
+    c->near_.ensure(BMAX);
+    c->res.ensure(BMAX);
+    c->acc.ensure(BMAX);
+    c->incl.ensure(BMAX);
+    c->yv.ensure(BMAX);
+    c->mv.ensure(BMAX);
+    c->rec.ensure(2 * (BMAX + world));
+    c->Lv.ensure(BMAX);
+    c->chain_end.ensure(BMAX);
+    // + 2: k_plan_init marks the start / goal edges' groups at batch_min and
+    // batch_min + 1 (two-phase: batch_min = BMAX at the configured sizes)
+    c->gfail.ensure(std::max<int64_t>(BMAX, FUSE_MAX) + 2);
+    if (grouped) {
+        c->g_send.ensure((size_t)GREC * PMAX + 1);
+        c->g_recv.ensure((size_t)world * (GREC * PMAX + 1));
+        c->g_cnt.ensure(BMAX);
+        c->g_incl.ensure(BMAX);
+    }
+    c->scalar.ensure(16);
+    c->counter.ensure(COUNTER_SLOTS);
+    if (!c->sync.p) {
+        c->sync.ensure(2);
+        HIP_TRY(hipMemsetAsync(c->sync.p, 0, 2 * sizeof(unsigned), c->stream));
+    }
+    c->io.ensure(1);
+    c->simp.ensure(1);
+    if (!c->h_io) {
+        HIP_TRY(hipHostMalloc((void**)&c->h_io, sizeof(PlanIO), hipHostMallocCoherent));
+        c->h_io->seq = c->seq;
+    }
+    c->q32.ensure(2 * NQ);
+    c->flags.ensure(2);
+    c->path.ensure((size_t)PATH_CAP * NQ);
+}
+
 int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* lo, const double* hi,
               const rp_plan_params* pp, double* path_out, int32_t path_cap, int32_t* n_out,
               int32_t* status_out) {
@@ -1144,53 +1197,11 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
 
     // workspace
     const int64_t cap = p.tree_capacity;
+    plan_workspace(c, BMAX, world, cmax, cap, grouped);
     for (auto& t : c->tree) {
-        t.q.ensure((size_t)cap * NQ);
-        t.par.ensure(cap);
-        t.cand.ensure(cap);
         t.n = 0;
         t.n_img = 0;
     }
-    const int64_t ne = std::max<int64_t>({PMAX + 2, ((BMAX + world - 1) / world) * cmax, (int64_t)SPMAX * SPMAX / 2,
-                                          (std::min<int64_t>(BMAX, FUSE_MAX) + 2) * (cmax + 1),
-                                          grouped ? (PMAX + 2) * (cmax + 1) : 0});
-    c->efrom.ensure(ne * NQ);
-    c->eto.ensure(ne * NQ);
-    c->nd.ensure(ne);
-    c->valid.ensure(ne);
-    c->near_.ensure(BMAX);
-    c->res.ensure(BMAX);
-    c->acc.ensure(BMAX);
-    c->incl.ensure(BMAX);
-    c->yv.ensure(BMAX);
-    c->mv.ensure(BMAX);
-    c->rec.ensure(2 * (BMAX + world));
-    c->Lv.ensure(BMAX);
-    c->chain_end.ensure(BMAX);
-    // + 2: k_plan_init marks the start / goal edges' groups at batch_min and
-    // batch_min + 1 (two-phase: batch_min = BMAX at the configured sizes)
-    c->gfail.ensure(std::max<int64_t>(BMAX, FUSE_MAX) + 2);
-    if (grouped) {
-        c->g_send.ensure((size_t)GREC * PMAX + 1);
-        c->g_recv.ensure((size_t)world * (GREC * PMAX + 1));
-        c->g_cnt.ensure(BMAX);
-        c->g_incl.ensure(BMAX);
-    }
-    c->scalar.ensure(16);
-    c->counter.ensure(COUNTER_SLOTS);
-    if (!c->sync.p) {
-        c->sync.ensure(2);
-        HIP_TRY(hipMemsetAsync(c->sync.p, 0, 2 * sizeof(unsigned), c->stream));
-    }
-    c->io.ensure(1);
-    c->simp.ensure(1);
-    if (!c->h_io) {
-        HIP_TRY(hipHostMalloc((void**)&c->h_io, sizeof(PlanIO), hipHostMallocCoherent));
-        c->h_io->seq = c->seq;
-    }
-    c->q32.ensure(2 * NQ);
-    c->flags.ensure(2);
-    c->path.ensure((size_t)PATH_CAP * NQ);
 
     PlanIO* io = c->io.p;
     int* status = io->status;
@@ -2411,6 +2422,36 @@ int rp_plan_wait(rp_ctx* c) {
     w.state.store(PlanWorker::IDLE, std::memory_order_release);
     c->busy = false;
     return rc;
+}
+
+int rp_reserve(rp_ctx* c, int64_t batch, int64_t tree_capacity) {
+    if (!c || batch < 0 || tree_capacity < 0) return RP_ERR_ARG;
+    RP_IDLE(c);
+    RP_GUARD_BEGIN
+    HIP_TRY(hipSetDevice(c->device));
+    const int64_t B = batch > 0 ? batch : 4096;
+    const int64_t cap = tree_capacity > 0 ? tree_capacity : (int64_t)1 << 22;
+    // the default range (0.2 x the bounds' extent) and resolution (0.01 x): connect
+    // chains of ceil(5) + 1 steps, ceil(20) + 2 slots per edge (+ 1 each for rounding)
+    const int cmax = 7, kmax = 23;
+    plan_workspace(c, B, c->world, cmax, cap, c->transport != TR_NONE);
+    // buffers that large launches grow on first use: node images of the matrix-core
+    // nearest-node search, the work-compacted edge launch's slot counts / scan / chunk
+    // map, the hipCUB scratch of its scans, the materialised queries
+    for (auto& t : c->tree) t.img.ensure(((size_t)t.q.n / NQ + NNM_PAD) * 4);
+    const int64_t ne = (int64_t)c->nd.n;
+    c->eslot.ensure(ne);
+    c->eincl.ensure(ne);
+    c->echunk.ensure(blocks_for(ne * (int64_t)kmax, VBLOCK) + 1);
+    size_t b32 = 0, b64 = 0;
+    HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b32, (const int32_t*)nullptr, (int32_t*)nullptr, (int)ne,
+                                             c->stream));
+    HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b64, (const unsigned long long*)nullptr,
+                                             (unsigned long long*)nullptr, (int)B, c->stream));
+    c->cub_tmp.ensure(std::max(b32, b64) + 16);
+    c->nn_qx.ensure((size_t)B * NQ);
+    return RP_OK;
+    RP_GUARD_END(c)
 }
 
 int rp_get_stream(rp_ctx* c, void** out) {

@@ -19,7 +19,7 @@ LIB_PATH = os.environ.get("RBE_LIB_PATH") or os.path.join(_HERE, LIB_NAME)
 # every symbol include/rbe_planner.h declares
 EXPORTS = ("rp_version", "rp_default_robot", "rp_create", "rp_destroy", "rp_set_scene", "rp_set_attached",
            "rp_check_states", "rp_check_states_device", "rp_check_edges", "rp_check_edges_device",
-           "rp_state_contacts", "rp_plan", "rp_plan_async", "rp_plan_wait", "rp_group_init", "rp_group_init_shm", "rp_group_rccl_unique_id", "rp_group_init_rccl",
+           "rp_state_contacts", "rp_plan", "rp_plan_async", "rp_plan_wait", "rp_reserve", "rp_group_init", "rp_group_init_shm", "rp_group_rccl_unique_id", "rp_group_init_rccl",
            "rp_get_stats", "rp_last_error", "rp_last_kernel_ms", "rp_selftest_f64", "rp_ik", "rp_set_profiling",
            "rp_get_profile", "rp_get_stream", "rp_group_info", "rp_selftest_nn")
 
@@ -59,6 +59,7 @@ def load():
     L.rp_plan.argtypes = [vp, vp, vp, vp, vp, C.POINTER(_abi.PlanParams), vp, i32, C.POINTER(i32), C.POINTER(i32)]
     L.rp_plan_async.argtypes = L.rp_plan.argtypes
     L.rp_plan_wait.argtypes = [vp]
+    L.rp_reserve.argtypes = [vp, i64, i64]
     L.rp_group_init.argtypes = [vp, i32, i32, vp, vp]
     L.rp_group_rccl_unique_id.argtypes = [vp]
     L.rp_group_init_shm.argtypes = [vp, i32, i32, vp, i64]
@@ -231,6 +232,10 @@ class Context:
         """rp_plan: (path (n, 9) float64, status)."""
         b = self._plan_call("fn", start, goal, lo, hi, params, path_cap)
         return b["out"][:b["n"].value].copy(), b["status"].value
+
+    def reserve(self, batch=0, tree_capacity=0):
+        """rp_reserve: size the planner workspace ahead of the first query."""
+        self._check(load().rp_reserve(self._h, int(batch), int(tree_capacity)), "rp_reserve")
 
     def plan_async(self, start, goal, lo, hi, params, path_cap=4096):
         """rp_plan_async: hand the query to the context's planner thread and return

@@ -191,6 +191,7 @@ class PlannerInterface:
         self._pushed = None      # (ctx.scene_gen, box poses, base, attached box) last pushed
         self._qlim = None        # (robot.q_limit object, lo, hi)
         self._params = None
+        self._reserved = None
         self._stats_ctx = None
         self._times = None
         self.last_status = None
@@ -200,6 +201,14 @@ class PlannerInterface:
         if self._ctx is None:
             self._ctx = Context(device=_device(), robot=model.robot_desc())
         return self._ctx
+
+    def _reserve(self, ctx, batch, cap):
+        """Workspace for this batch / tree capacity sized once (rp_reserve), so the
+        first query does not allocate device memory inside the plan."""
+        key = (id(ctx), batch, cap)
+        if self._reserved != key and hasattr(ctx, "reserve"):
+            ctx.reserve(batch, cap)
+            self._reserved = key
 
     def _sync_scene(self):
         """Push the obstacle geometry (boxes at their simulated poses) and the attached
@@ -324,6 +333,7 @@ class PlannerInterface:
         _abi.set_params(p, seed=_next_seed(), batch=_batch(), timeout_s=float(timeout),
                         n_waypoints=int(num_waypoints) if num_waypoints else 0, simplify=bool(smooth_path),
                         tree_capacity=_CONFIG["tree_capacity"] or 0, straight_first=_straight_first())
+        self._reserve(ctx, p.batch, p.tree_capacity)
         nwp = p.n_waypoints
         cap = max(4096, nwp + 16)
         t_plan0 = time.perf_counter()

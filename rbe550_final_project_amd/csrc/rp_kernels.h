@@ -1,7 +1,7 @@
 // rp_kernels.h — HIP kernels of the planner hot path (gfx950).
 //
 //   k_validity    one lane per state: FK + plane/box/self collision    (planning.py:209-230)
-//   k_edges       one lane per (edge, interpolation slot)             (OMPL checkMotion)
+//   k_edges       one lane per (edge, interpolation slot), wave-compacted (OMPL checkMotion)
 //   k_ext_nn      one lane per sample: Philox sample, brute-force NN over the
 //                 tree (LDS tiles), steering                          (RRTConnect growTree)
 //   k_conn_nn     one lane per connect target: NN + connect chain     (RRTConnect connect)
@@ -100,6 +100,41 @@ __device__ __forceinline__ unsigned long long counter_sum(const unsigned long lo
     return s;
 }
 
+// Inclusive scans across the 64 lanes of a wave on the DPP network: shifts within
+// rows of 16 (row_shr 1, 2, 4, 8), then row 15 -> rows 1, 3 and row 31 -> rows 2, 3
+// (row_bcast 15 / 31). Lanes outside a source row keep the identity (`old`).
+__device__ __forceinline__ int wave_incl_add(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);
+    return v;
+}
+__device__ __forceinline__ int wave_incl_max(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x111, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x112, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x114, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x118, 0xf, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x142, 0xa, 0xf, false));
+    v = max(v, __builtin_amdgcn_update_dpp(-1, v, 0x143, 0xc, 0xf, false));
+    return v;
+}
+
+// Wave-compacted (edge, slot) items: the launch covers groups of 64 consecutive
+// edges with kmax waves each (the dense grid's size: kmax slot rounds of 64 lanes
+// per group); a wave scans its group's slot counts (lane j: edge 64 g + j, 0 for an
+// empty edge; from nd only, so that every wave of a group sees the same list while
+// the launch's own failures change valid / gfail) and runs round r of the group's
+// packed item list, item t = 64 r + lane -> the edge j whose [start_j, start_j +
+// cnt_j) holds t (the start marks of the round, max-scanned, plus the edge that
+// carries into the round), slot t - start_j. Every running wave but a group's last
+// has 64 busy lanes (a dense (edge, slot) grid idles the lanes past each edge's
+// slot count: a quarter of them for range-length RRT edges), and there is no
+// per-lane 64-bit index division. A wave with no round left exits after the scan;
+// an item of an edge already invalid (or past its prefix group's first failure) when
+// it is reached is skipped, as in the dense grid.
 template <int NCL, bool BF = false>
 __global__ __launch_bounds__(VBLOCK, NCL == NCL_GRID ? RP_EDGE_WAVES : RP_EDGE_WAVES_CL) void k_edges(const double* __restrict__ from,
                                                   const double* __restrict__ to,
@@ -110,54 +145,86 @@ __global__ __launch_bounds__(VBLOCK, NCL == NCL_GRID ? RP_EDGE_WAVES : RP_EDGE_W
                                                   const int* __restrict__ dcount, int per_item,
                                                   const int* __restrict__ dkmax) {
     __shared__ WaveQ wq;
+    __shared__ int mark[VBLOCK];
     // device-side edge count (planner iterations: dcount = accepted targets) and
     // slot count (rp_check_edges_device: k_edge_prep's max); the grid may be
-    // smaller than the work (gated launches): grid-stride over it
+    // smaller than the work (gated launches): grid-stride over (group, round)
     if (dcount) n_edges = min(n_edges, (int64_t)dcount[0] * per_item);
     if (dkmax) kmax = *dkmax;
-    const int64_t total = n_edges * kmax;
-    for (int64_t base = (int64_t)rp_bid() * VBLOCK; base < total; base += (int64_t)rp_gdim() * VBLOCK) {
-        const int64_t idx = base + rp_tid();
-        const int64_t e = idx / kmax;
-        const int slot = (int)(idx - e * kmax);
-        bool run = false;
-        int nde = -1;
-        int emode = mode;
+    kmax = max(kmax, 1);
+    const int lane = rp_tid();
+    const int64_t n_waves = (n_edges + VBLOCK - 1) / VBLOCK * kmax;
+    for (int64_t w = rp_bid(); w < n_waves; w += rp_gdim()) {
+        const int64_t g = w / kmax;
+        const int r = (int)(w - g * kmax);
+        const int64_t e = g * VBLOCK + lane;
+        int nde = -1, emode = mode, cnt = 0;
         if (e < n_edges) {
             nde = nd[e];
             if (mode == 2 && nde >= 0) {
                 emode = (nde & ND_FROM) ? 1 : 0;
                 nde &= ~ND_FROM;
             }
-            const int slots = nde > 1 ? nde : 1;
-            run = nde >= 0 && slot < slots && valid[e] != 0;
-            if (run && gfail) {
-                const int g = (int)(e / group), s = (int)(e - (int64_t)g * group);
-                run = gfail[g] > s;
-            }
+            // the layout depends on nd alone: valid / gfail change while the launch
+            // runs (this launch's own failures), and every wave of a group must see
+            // the same item list (they are read per item below)
+            cnt = nde >= 0 ? (nde > 1 ? nde : 1) : 0;
         }
-        const unsigned long long ballot = __ballot(run);
-        count_states(counter, ballot);
-        if (!ballot) continue;
-        if (run) {
-            double st[NQ];
-            const double* a = from + e * NQ;
-            const double* b = to + e * NQ;
-            if (slot == 0) {
-                const double* ep = emode ? a : b;
-#pragma unroll
-                for (int k = 0; k < NQ; ++k) st[k] = ep[k];
-            } else {
-                interp(a, b, (double)slot / (double)nde, st);
+        const int incl = wave_incl_add(cnt);
+        const int total = __builtin_amdgcn_readlane(incl, 63);
+        const int start = incl - cnt;
+        const int packed_nd = nde | (emode << 30);   // nde < 2^30 (ND_FROM stripped)
+        // rounds r, r + kmax, ... (a group holds at most 64 kmax items when every
+        // edge's slot count is <= kmax; the stride keeps any larger one exact)
+        for (int r0 = r * VBLOCK; r0 < total; r0 += kmax * VBLOCK) {
+            __builtin_amdgcn_wave_barrier();
+            mark[lane] = -1;
+            __builtin_amdgcn_wave_barrier();
+            if (cnt > 0 && start >= r0 && start < r0 + VBLOCK) mark[start - r0] = lane;
+            __builtin_amdgcn_wave_barrier();
+            // the edge covering item r0 that started in an earlier round (if any)
+            const unsigned long long cov = __ballot(cnt > 0 && start < r0 && r0 < start + cnt);
+            const int carry = cov ? (int)__builtin_ctzll(cov) : -1;
+            const int j = max(wave_incl_max(mark[lane]), carry);
+            const int sj = __shfl(start, j);
+            const int pj = __shfl(packed_nd, j);
+            const int64_t ej = g * VBLOCK + j;
+            const int t = r0 + lane;
+            bool run = t < total;
+            int slot = 0, nj = 0, mj = 0;
+            if (run) {
+                slot = t - sj;
+                nj = pj & ~(1 << 30);
+                mj = (pj >> 30) & 1;
+                run = valid[ej] != 0;
+                if (run && gfail) {
+                    const int gi = (int)(ej / group), si = (int)(ej - (int64_t)gi * group);
+                    run = gfail[gi] > si;
+                }
             }
-            float qq[NQ];
+            const unsigned long long ballot = __ballot(run);
+            count_states(counter, ballot);
+            if (!ballot) continue;
+            if (run) {
+                double st[NQ];
+                const double* a = from + ej * NQ;
+                const double* b = to + ej * NQ;
+                if (slot == 0) {
+                    const double* ep = mj ? a : b;
 #pragma unroll
-            for (int k = 0; k < NQ; ++k) qq[k] = (float)st[k];
-            if (state_collides<NCL, BF>(qq, sc, wq)) {
-                valid[e] = 0;
-                if (gfail) {
-                    const int g = (int)(e / group), s = (int)(e - (int64_t)g * group);
-                    atomicMin(&gfail[g], s);
+                    for (int k = 0; k < NQ; ++k) st[k] = ep[k];
+                } else {
+                    interp(a, b, (double)slot / (double)nj, st);
+                }
+                float qq[NQ];
+#pragma unroll
+                for (int k = 0; k < NQ; ++k) qq[k] = (float)st[k];
+                if (state_collides<NCL, BF>(qq, sc, wq)) {
+                    valid[ej] = 0;
+                    if (gfail) {
+                        const int gi = (int)(ej / group), si = (int)(ej - (int64_t)gi * group);
+                        atomicMin(&gfail[gi], si);
+                    }
                 }
             }
         }
@@ -278,8 +345,11 @@ __global__ void k_edge_prep(const double* __restrict__ from, const double* __res
         valid[e] = 1;
         v = c > 1 ? c : 1;
     }
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));   // wave max: one atomic per wave
-    if ((rp_tid() & 63) == 0 && v > 0) atomicMax(kmax, v);
+    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));   // wave max
+    // one atomic per wave, and only while it can raise the maximum (thousands of
+    // waves' atomics on one word serialise: 50 us for 262,144 edges)
+    if ((rp_tid() & 63) == 0 && v > __hip_atomic_load(kmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMax(kmax, v);
 }
 
 // ---------------------------------------------------------------------------

@@ -447,7 +447,8 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
         prof_end(c, ps, 1, s);
         return;
     }
-    unsigned nb = blocks_for(threads, VBLOCK);
+    // k_edges: kmax one-wave blocks per group of 64 edges (its slot rounds)
+    unsigned nb = (unsigned)std::min<int64_t>((int64_t)blocks_for(n, VBLOCK) * kmax, (int64_t)1 << 30);
     if (max_blocks && nb > max_blocks) nb = max_blocks;   // grid-stride (gated launches)
     const dim3 g(nb), b(VBLOCK);
     const int ps = prof_begin(c, s);
@@ -1180,7 +1181,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     const int cmax = (int)std::ceil(max_extent / p.range) + 1;
     const int kmax = (int)std::ceil(p.range / p.resolution) + 2;
     const int kfull = (int)std::ceil(max_extent / p.resolution) + 2;   // any in-bounds edge
-    const int64_t BMAX = p.batch, PMAX = BMAX / world;
+    const int64_t BMAX = p.batch;
     // rank groups (and RBE_PLAN_GROUPED=1 at world 1, the same iteration without an
     // exchange) run the one-exchange speculative iteration at every batch size
     bool grouped = c->transport != TR_NONE;
@@ -1700,8 +1701,14 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             prof_end(c, pn1, 0, c->stream);
             c->prof.nn_pairs += (double)C * (double)TA;
             debug_wait(c, "k_ext_nn");
-            launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, C + (sg >= 0 ? 2 : 0), kmax, a_start ? 0 : 1, c->valid.p,
-                         1, nullptr, c->stream);
+            // extension edges: steers shorter than the range (samples near the tree)
+            // leave most of a dense (edge, slot) grid's lanes idle on large trees
+            if (packed(C + (sg >= 0 ? 2 : 0)))
+                launch_edges_packed(c, c->efrom.p, c->eto.p, c->nd.p, C + (sg >= 0 ? 2 : 0), kmax, a_start ? 0 : 1,
+                                    c->valid.p, 1, nullptr, c->stream, nullptr, 1);
+            else
+                launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, C + (sg >= 0 ? 2 : 0), kmax, a_start ? 0 : 1,
+                             c->valid.p, 1, nullptr, c->stream);
             debug_wait(c, "ext edges");
             c->stats.edges_checked += C;
 

@@ -174,6 +174,13 @@ class Context:
                     "rp_check_edges")
         return out
 
+    def check_edges_device(self, qa_ptr, qb_ptr, n, resolution, out_ptr, stream=None):
+        """rp_check_edges_device on device buffers (N x 9 float64 endpoints, N uint8
+        flags), asynchronous on `stream` (None: the context stream)."""
+        self._check(load().rp_check_edges_device(self._h, C.c_void_p(qa_ptr), C.c_void_p(qb_ptr), int(n),
+                                                 float(resolution), C.c_void_p(out_ptr),
+                                                 C.c_void_p(stream) if stream else None), "rp_check_edges_device")
+
     def contacts(self, q, cap=64):
         q = np.ascontiguousarray(q, dtype=np.float64)
         out = np.zeros((cap, 2), dtype=np.int32)

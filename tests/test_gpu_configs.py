@@ -173,3 +173,15 @@ def test_validity_kernel_timing_needs_profiling():
         ctx.close()
         hip.hipFree(dq)
         hip.hipFree(df)
+
+
+@pytest.mark.parametrize("name", ["C2_q0_s0", "C4_q10", "C5_clutter64", "C5_well_s3", "C5_well_s0"])
+@pytest.mark.parametrize("packed", ["0", "1"])
+def test_configured_batch_edge_kernels(gpu_ctx, name, packed, monkeypatch):
+    """Every large edge launch through one kernel: RBE_EDGE_PACKED=0 the
+    wave-compacted (edge, slot) grid (k_edges: groups of 64 edges, kmax waves each,
+    grid-striding when the grid is capped), 1 the globally scanned item list
+    (k_edges_packed); whole iterations, so the launches are the configured sizes."""
+    monkeypatch.setenv("RBE_EDGE_PACKED", packed)
+    monkeypatch.setenv("RBE_PLAN_CHUNK", "-1")
+    _check(gpu_ctx, name)

@@ -38,7 +38,7 @@ def main():
     ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
     ctx.set_attached(q["attached"])
     ctx.set_profiling(True)
-    keys = ("RBE_NN_MFMA", "RBE_PLAN_CHUNK", "RBE_CHUNK_TREE", "RBE_NN_WAVES", "RBE_NN_RANGES")
+    keys = ("RBE_NN_MFMA", "RBE_PLAN_CHUNK", "RBE_CHUNK_TREE", "RBE_NN_WAVES", "RBE_NN_RANGES", "RBE_EDGE_PACKED")
     for rep in range(2):   # rep 0: warm-up
         for name, env in cfgs.items():
             for k in keys:
@@ -51,13 +51,14 @@ def main():
                 path, st = ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
                 s, pr = ctx.stats(), ctx.profile()
                 rows.append((s["total_ms"], pr["nn_ms"], pr["nn_launches"], pr["nn_pairs"], pr["edge_ms"],
-                             pr["edge_launches"], s["iterations"], s["samples"], float(path.sum())))
+                             pr["edge_launches"], s["iterations"], s["samples"], float(path.sum()), pr["edge_states"]))
             if rep == 0:
                 continue
             r = np.array(rows)
             print(f"{name:14s} total med {np.median(r[:, 0]):8.2f} ms (sum {r[:, 0].sum():8.2f}) | NN {r[:, 1].sum():8.2f} ms "
                   f"{int(r[:, 2].sum())} launches {r[:, 3].sum():.3g} pairs -> {r[:, 3].sum() / (r[:, 1].sum() * 1e-3):.3g} pairs/s"
-                  f" | edges {r[:, 4].sum():7.2f} ms {int(r[:, 5].sum())} launches | iters {r[:, 6].astype(int).tolist()} "
+                  f" | edges {r[:, 4].sum():7.2f} ms {int(r[:, 5].sum())} launches "
+                  f"{r[:, 9].sum() / (r[:, 4].sum() * 1e-3) / 1e9:.2f} G states/s | iters {r[:, 6].astype(int).tolist()} "
                   f"samples {int(r[:, 7].sum())} pathsum {r[:, 8].sum():.9g}", flush=True)
 
 

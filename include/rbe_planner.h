@@ -228,6 +228,16 @@ int rp_set_scene(rp_ctx* ctx, const rp_box* boxes, int32_t n_boxes, float plane_
  * box_index = -1 clears. The reference exempts hand | left_finger | right_finger. */
 int rp_set_attached(rp_ctx* ctx, int32_t box_index, uint32_t exempt_link_mask);
 
+/* rp_set_scene + rp_set_attached from the simulator's poses in one call (the
+ * drop-in planning.py's per-query scene ingestion): box j at position
+ * poses[7j .. 7j+2] with orientation quaternion (w, x, y, z) = poses[7j+3 .. 7j+6],
+ * half extents halves[3j .. 3j+2]; its yaw is atan2(2(wz + xy), 1 - 2(y^2 + z^2))
+ * in double (tilt ignored), then every value is rounded to float once, as
+ * rp_set_scene's records. base_pos: the robot base (double). */
+int rp_set_scene_poses(rp_ctx* ctx, const double* poses, const float* halves, int32_t n_boxes,
+                       float plane_z, const double base_pos[3], int32_t attached_box,
+                       uint32_t exempt_link_mask);
+
 /* Validity of N states (row-major N x 9 float32, host memory). flags_out[i] = 1 if
  * valid (collision free), 0 otherwise. */
 int rp_check_states(rp_ctx* ctx, const float* q, int64_t n, uint8_t* flags_out);

@@ -2161,11 +2161,9 @@ int rp_set_scene(rp_ctx* c, const rp_box* boxes, int32_t n, float plane_z, const
     RP_GUARD_END(c)
 }
 
-int rp_set_attached(rp_ctx* c, int32_t box, uint32_t link_mask) {
-    if (!c || box >= c->scene.n_boxes) return RP_ERR_ARG;
-    RP_IDLE(c);
-    RP_GUARD_BEGIN
-    HIP_TRY(hipSetDevice(c->device));
+// the attachment's exemption bits in the host scene record (uploaded by the next
+// flush_scene)
+static void set_attached_bits(rp_ctx* c, int32_t box, uint32_t link_mask) {
     for (int j = 0; j < c->scene.n_boxes; ++j) c->scene.box[j][14] = 0.0f;
     if (box >= 0) {
         uint32_t bits = 0;
@@ -2174,12 +2172,44 @@ int rp_set_attached(rp_ctx* c, int32_t box, uint32_t link_mask) {
         std::memcpy(&c->scene.box[c->slot_of[box]][14], &bits, 4);
     }
     upload_scene(c);
+}
+
+int rp_set_attached(rp_ctx* c, int32_t box, uint32_t link_mask) {
+    if (!c || box >= c->scene.n_boxes) return RP_ERR_ARG;
+    RP_IDLE(c);
+    RP_GUARD_BEGIN
+    HIP_TRY(hipSetDevice(c->device));
+    set_attached_bits(c, box, link_mask);
     // the attachment completes a query's scene (rp_set_scene, then rp_set_attached):
     // start its upload now, so it overlaps the caller's work before the next launch
     // instead of opening that launch's dependency chain (goal3 RRT plans)
     flush_scene(c, c->stream);
     return RP_OK;
     RP_GUARD_END(c)
+}
+
+int rp_set_scene_poses(rp_ctx* c, const double* poses, const float* halves, int32_t n, float plane_z,
+                       const double base[3], int32_t attached, uint32_t link_mask) {
+    if (!c || n < 0 || n > MAX_BOXES || (n > 0 && (!poses || !halves)) || !base || attached >= n) return RP_ERR_ARG;
+    RP_IDLE(c);
+    rp_box boxes[MAX_BOXES];
+    for (int j = 0; j < n; ++j) {
+        const double* p = poses + 7 * j;
+        const double w = p[3], x = p[4], y = p[5], z = p[6];
+        for (int k = 0; k < 3; ++k) {
+            boxes[j].center[k] = (float)p[k];
+            boxes[j].half[k] = halves[3 * j + k];
+        }
+        boxes[j].yaw = (float)std::atan2(2.0 * (w * z + x * y), 1.0 - 2.0 * (y * y + z * z));
+    }
+    const float b[3] = {(float)base[0], (float)base[1], (float)base[2]};
+    const int rc = rp_set_scene(c, boxes, n, plane_z, b);
+    if (rc != RP_OK) return rc;
+    // no upload here: the next query's first call (rp_plan's flush_scene, on the
+    // planner thread with rp_plan_async) copies the record, so the launch is not
+    // on the caller's path
+    set_attached_bits(c, attached, link_mask);
+    return RP_OK;
 }
 
 int rp_check_states(rp_ctx* c, const float* q, int64_t n, uint8_t* flags_out) {

@@ -17,7 +17,7 @@ LIB_NAME = "librbe_mi355x.so"
 LIB_PATH = os.environ.get("RBE_LIB_PATH") or os.path.join(_HERE, LIB_NAME)
 
 # every symbol include/rbe_planner.h declares
-EXPORTS = ("rp_version", "rp_default_robot", "rp_create", "rp_destroy", "rp_set_scene", "rp_set_attached",
+EXPORTS = ("rp_version", "rp_default_robot", "rp_create", "rp_destroy", "rp_set_scene", "rp_set_attached", "rp_set_scene_poses",
            "rp_check_states", "rp_check_states_device", "rp_check_edges", "rp_check_edges_device",
            "rp_state_contacts", "rp_plan", "rp_plan_async", "rp_plan_wait", "rp_reserve", "rp_group_init", "rp_group_init_shm", "rp_group_rccl_unique_id", "rp_group_init_rccl",
            "rp_get_stats", "rp_last_error", "rp_last_kernel_ms", "rp_selftest_f64", "rp_ik", "rp_set_profiling",
@@ -51,6 +51,7 @@ def load():
     L.rp_destroy.restype = None
     L.rp_set_scene.argtypes = [vp, vp, i32, f32, C.POINTER(f32)]   # rp_box* (ctypes array or address)
     L.rp_set_attached.argtypes = [vp, i32, u32]
+    L.rp_set_scene_poses.argtypes = [vp, vp, vp, i32, f32, vp, i32, u32]
     L.rp_check_states.argtypes = [vp, vp, i64, vp]
     L.rp_check_states_device.argtypes = [vp, vp, i64, vp, vp]
     L.rp_check_edges.argtypes = [vp, vp, vp, i64, f64, vp]
@@ -136,14 +137,17 @@ class Context:
         self.scene_gen += 1
         self._check(load().rp_set_scene(self._h, arr, n, float(plane_z), b), "rp_set_scene")
 
-    def set_scene_array(self, rec, plane_z=0.0, base=(0.0, 0.0, 0.01)):
-        """set_scene from an (n, 7) C-contiguous float32 array of rp_box records
-        (center xyz, half extents xyz, yaw): no per-box ctypes conversion."""
-        assert rec.dtype == np.float32 and rec.ndim == 2 and rec.shape[1] == 7 and rec.flags.c_contiguous
-        b = (C.c_float * 3)(*base)
+    def set_scene_poses(self, poses, halves, plane_z, base, attached=-1, link_mask=_abi.ATTACH_EXEMPT_MASK):
+        """rp_set_scene_poses: boxes from simulator poses (n, 7) float64 [x, y, z, qw,
+        qx, qy, qz] and half extents (n, 3) float32, the robot base (3,) float64 and
+        the attached box, in one call."""
+        assert poses.dtype == np.float64 and halves.dtype == np.float32 and base.dtype == np.float64
         self.scene_gen += 1
-        self._check(load().rp_set_scene(self._h, rec.ctypes.data if len(rec) else None, len(rec), float(plane_z), b),
-                    "rp_set_scene")
+        n = len(poses)
+        self._check(load().rp_set_scene_poses(self._h, poses.ctypes.data if n else None,
+                                              halves.ctypes.data if n else None, n, float(plane_z),
+                                              base.ctypes.data, int(attached), int(link_mask)),
+                    "rp_set_scene_poses")
 
     def set_attached(self, box_index, link_mask=_abi.ATTACH_EXEMPT_MASK):
         self.scene_gen += 1

@@ -234,11 +234,12 @@ class PlannerInterface:
                 ctx.set_attached(idx)
                 self._pushed = (ctx.scene_gen, poses, base, idx)
             return
-        if hasattr(ctx, "set_scene_array"):
-            ctx.set_scene_array(rd.box_array(poses), rd.plane_z, base)
+        if hasattr(ctx, "set_scene_poses"):   # one library call (rp_set_scene_poses)
+            ctx.set_scene_poses(np.array(poses, dtype=np.float64).reshape(-1, 7), rd.halves_f32, rd.plane_z,
+                                np.array(base, dtype=np.float64), idx)
         else:
             ctx.set_scene(rd.boxes(poses), rd.plane_z, base)
-        ctx.set_attached(idx)
+            ctx.set_attached(idx)
         self._pushed = (getattr(ctx, "scene_gen", None), poses, base, idx)
 
     def _bounds(self):

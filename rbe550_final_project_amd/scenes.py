@@ -258,6 +258,7 @@ class GenesisReader:
                 self.robot_ent = ent
             elif kind == "plane":
                 self.plane_z = data
+        self.halves_f32 = np.array(self.halves, dtype=np.float32).reshape(-1, 3)
         self.box_of_entity = {e: k for k, e in enumerate(self.entity_idx) if e is not None}
         self.names = [str(e if e is not None else k) for k, e in enumerate(self.entity_idx)]
         self._links = None
@@ -311,19 +312,6 @@ class GenesisReader:
     def boxes(self, poses):
         """Box records (center, half, yaw) of box poses from poses()."""
         return [((p[0], p[1], p[2]), h, yaw_of_quat(p[3:7])) for p, h in zip(poses, self.halves)]
-
-    def box_array(self, poses):
-        """The rp_box records of box poses from poses() as an (n, 7) float32 array
-        (center, half extents, yaw: the values boxes() gives, rounded to float32
-        once, as the ctypes path of _abi.make_boxes)."""
-        n = len(poses)
-        rec = np.empty((n, 7), dtype=np.float32)
-        if n:
-            rec[:, 0:3] = np.array(poses, dtype=np.float64)[:, 0:3]
-            rec[:, 3:6] = self.halves
-            rec[:, 6] = [math.atan2(2.0 * (w * z + x * y), 1.0 - 2.0 * (y * y + z * z))
-                         for _, _, _, w, x, y, z in poses]
-        return rec
 
     def read(self):
         """The scene as a Scene record."""

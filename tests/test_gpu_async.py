@@ -106,3 +106,25 @@ def test_plan_path_equals_oracle(gpu_ctx, oracle_lib, straight_first):
             assert torch.equal(sim.robot.set_calls[-1], torch.tensor(q["start"], dtype=torch.float32))
     finally:
         planning.configure(straight_first=True)
+
+
+def test_scene_poses_equal_scene_records(gpu_ctx, oracle_lib):
+    """rp_set_scene_poses (yaw from the quaternion in double, values rounded to float
+    once) gives the scene rp_set_scene gives for the ingested records: validity flags
+    bit-exact against the oracle on the yawed pentagon scene with an attached box."""
+    q = _wl("goal4_pentagon_10box")["queries"][14]
+    sc = scenes.Scene.from_json(q["scene"])
+    sim = M.Scene(sc.boxes)
+    rd = scenes.GenesisReader(sim, sim.robot)
+    poses, base = rd.poses()
+    o = oracle_lib.OracleScene()
+    ing = rd.read()
+    o.set_scene(ing.boxes, ing.plane_z, ing.base)
+    o.set_attached(3)
+    gpu_ctx.set_scene_poses(np.array(poses, dtype=np.float64).reshape(-1, 7), rd.halves_f32, rd.plane_z,
+                            np.array(base, dtype=np.float64), 3)
+    rng = np.random.default_rng(4)
+    qs = (model.Q_LO + (model.Q_HI - model.Q_LO) * rng.random((65536, 9))).astype(np.float32)
+    qs[:4096] = np.clip(np.asarray(q["start"])[None, :] + rng.normal(0, 0.2, (4096, 9)), model.Q_LO,
+                        model.Q_HI).astype(np.float32)
+    assert np.array_equal(gpu_ctx.check_states(qs), o.check_states(qs))

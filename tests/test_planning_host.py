@@ -2,6 +2,8 @@
 Genesis scene reader, the scene push only on change, the overlapped waypoint
 tensors and the qpos restore, driven through a stand-in of native.Context that
 follows rp_plan_async / rp_plan_wait's contract."""
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -22,10 +24,18 @@ class AsyncCtx:
         self.scenes, self.attached, self.calls = [], [], []
         self.in_flight = False
 
-    def set_scene_array(self, rec, plane_z, base):
-        assert not self.in_flight
+    def set_scene_poses(self, poses, halves, plane_z, base, attached=-1):
+        """rp_set_scene_poses' records: float32 of the centre, half extents and
+        atan2 yaw (double)"""
+        assert not self.in_flight and poses.dtype == np.float64 and halves.dtype == np.float32
         self.scene_gen += 1
-        self.scenes.append((rec.copy(), plane_z, tuple(base)))
+        rec = np.empty((len(poses), 7), np.float32)
+        for j, (x, y, z, w, qx, qy, qz) in enumerate(poses):
+            rec[j, :3] = (x, y, z)
+            rec[j, 3:6] = halves[j]
+            rec[j, 6] = math.atan2(2.0 * (w * qz + qx * qy), 1.0 - 2.0 * (qy * qy + qz * qz))
+        self.scenes.append((rec, plane_z, tuple(base)))
+        self.attached.append(attached)
 
     def set_attached(self, idx):
         assert not self.in_flight
@@ -66,7 +76,9 @@ def test_reader_matches_per_entity_scene(rigid_solver):
     rd = scenes.GenesisReader(sc, sc.robot)
     assert (rd._links is not None) == rigid_solver
     poses, base = rd.poses()
-    rec = rd.box_array(poses)
+    ctx = AsyncCtx(_path(2))
+    ctx.set_scene_poses(np.array(poses, dtype=np.float64), rd.halves_f32, rd.plane_z, base)
+    rec = ctx.scenes[-1][0]
     arr, n = _abi.make_boxes(rd.boxes(poses))
     assert n == 3 and np.array_equal(rec, np.frombuffer(arr, dtype=np.float32).reshape(-1, 7)[:n])
     assert np.allclose(rec[:, :3], [b[0] for b in BOXES]) and np.allclose(rec[:, 6], [b[2] for b in BOXES], atol=1e-6)
@@ -85,12 +97,12 @@ def test_scene_pushed_only_when_changed():
     # attaching box 2 (entity 2): only the attachment is pushed
     pi.plan_path(model.SAFE_HOME, num_waypoints=150, attached_object=sc.entities[2])
     assert len(ctx.scenes) == 1 and ctx.attached == [-1, 1]
-    # a block moved by the simulation: the scene is pushed again
+    # a block moved by the simulation: the scene is pushed again (with the attachment)
     sc.entities[1].set_pos((0.40, 0.2, 0.02))
     pi.plan_path(model.SAFE_HOME, num_waypoints=150, attached_object=sc.entities[2])
-    assert len(ctx.scenes) == 2 and abs(float(ctx.scenes[-1][0][0, 0]) - 0.40) < 1e-6
+    assert len(ctx.scenes) == 2 and abs(float(ctx.scenes[-1][0][0, 0]) - 0.40) < 1e-6 and ctx.attached[-1] == 1
     # someone else set a scene on the context: pushed again although the poses are the same
-    ctx.set_scene_array(np.zeros((0, 7), np.float32), 0.0, (0, 0, 0))
+    ctx.set_scene_poses(np.zeros((0, 7)), np.zeros((0, 3), np.float32), 0.0, (0, 0, 0))
     pi.plan_path(model.SAFE_HOME, num_waypoints=150, attached_object=sc.entities[2])
     assert len(ctx.scenes) == 4 and ctx.attached[-1] == 1
 

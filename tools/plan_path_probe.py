@@ -34,9 +34,9 @@ def main():
     pi = planning.PlannerInterface(sim.robot, sim)
     pi._ctx = ctx
     rd = scenes.GenesisReader(sim, pi.robot)
-    T = {k: [] for k in ("poses", "box_array", "set_scene_array", "set_attached", "unbind150", "get_qpos",
+    T = {k: [] for k in ("poses", "set_scene_poses", "set_attached", "unbind150", "get_qpos",
                          "set_qpos", "plan_sync", "plan_async_wait", "plan_async_unbind_wait", "plan_path",
-                         "plan_path_same_scene", "empty_call")}
+                         "plan_path_same_scene", "empty_call", "reference_tensor_list")}
     sink = io.StringIO()
     lo, hi = pi._bounds()
     for rep in range(12):
@@ -50,11 +50,9 @@ def main():
             poses, base = rd.poses()
             T["poses"].append(time.perf_counter() - t)
             t = time.perf_counter()
-            rec = rd.box_array(poses)
-            T["box_array"].append(time.perf_counter() - t)
-            t = time.perf_counter()
-            ctx.set_scene_array(rec, rd.plane_z, base)
-            T["set_scene_array"].append(time.perf_counter() - t)
+            ctx.set_scene_poses(np.array(poses, dtype=np.float64).reshape(-1, 7), rd.halves_f32, rd.plane_z,
+                                np.array(base, dtype=np.float64), q["attached"])
+            T["set_scene_poses"].append(time.perf_counter() - t)
             t = time.perf_counter()
             ctx.set_attached(q["attached"])
             T["set_attached"].append(time.perf_counter() - t)
@@ -95,6 +93,12 @@ def main():
             t = time.perf_counter()
             len(v)
             T["empty_call"].append(time.perf_counter() - t)
+            # the reference's own conversion of a 150-state path (code/planning.py:232-242:
+            # one torch.tensor of a 9-float list per state), for scale
+            path = np.linspace(0.0, 1.0, 150 * 9).reshape(150, 9)
+            t = time.perf_counter()
+            [torch.tensor([float(s[i]) for i in range(9)], dtype=torch.float32) for s in path]
+            T["reference_tensor_list"].append(time.perf_counter() - t)
             sink.seek(0)
             sink.truncate()
     planning.configure(straight_first=True)

@@ -74,6 +74,53 @@ __global__ __launch_bounds__(VTHREADS, NCL == NCL_GRID ? RP_VALIDITY_WAVES_GRID 
     flags[i] = state_collides<NCL, BF>(qq, sc, wq) ? 0 : 1;
 }
 
+// Mid-size launches (a few thousand to ~10^5 states: one wave per SIMD or fewer)
+// are as slow as one wave's dependency chain. NR waves share each group of 64
+// states, each walking the chain with a part of the tests (rp_math.h ROLE_*: NR = 2
+// env + the self pairs before SPLIT_J | the rest; NR = 3 env | pairs before SPLIT_J
+// | the rest); their hits meet in LDS. NR times the waves, each with a shorter
+// chain (the FK walk is done NR times); the same tests as k_validity, so the same
+// flags. Measured (tools/split_ab.py, profiles/r04/validity_split_ab.txt): 3 roles
+// best up to 64k states (C2's 64k launch 9.8 -> 7.6 us), 2 up to 128k, above that
+// the one-wave kernel (the extra FK walks cost more than the chains save).
+template <int NCL, bool BF, int SPLIT_NR>
+__global__ __launch_bounds__(64 * SPLIT_NR, SPLIT_NR) void k_validity_split(const float* __restrict__ q, int64_t n,
+                                                                          uint8_t* __restrict__ flags,
+                                                                          const DevScene* __restrict__ sc) {
+    static_assert(SPLIT_NR == 2 || SPLIT_NR == 3, "two or three roles");
+    __shared__ WaveQ wqs[SPLIT_NR];
+    __shared__ int hits[SPLIT_NR - 1][64];
+    const int w = rp_tid() >> 6, lane = rp_tid() & 63;
+    const int64_t i = (int64_t)rp_bid() * 64 + lane;
+    bool hit = false;
+    if (i < n) {
+        float qq[NQ];
+        struct F3 { float x, y, z; };
+        const F3* q3 = reinterpret_cast<const F3*>(q + i * NQ);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const F3 v = q3[k];
+            qq[3 * k] = v.x; qq[3 * k + 1] = v.y; qq[3 * k + 2] = v.z;
+        }
+        if constexpr (SPLIT_NR == 2) {
+            if (w == 0) hit = state_collides<NCL, BF, ROLE_ENV | ROLE_PA>(qq, sc, wqs[0]);
+            else hit = state_collides<NCL, BF, ROLE_PB>(qq, sc, wqs[1]);
+        } else {
+            if (w == 0) hit = state_collides<NCL, BF, ROLE_ENV>(qq, sc, wqs[0]);
+            else if (w == 1) hit = state_collides<NCL, BF, ROLE_PA>(qq, sc, wqs[1]);
+            else hit = state_collides<NCL, BF, ROLE_PB>(qq, sc, wqs[2]);
+        }
+    }
+    if (w > 0) hits[w - 1][lane] = hit;
+    __syncthreads();
+    if (w == 0 && i < n) {
+        bool any = hit;
+#pragma unroll
+        for (int r = 0; r < SPLIT_NR - 1; ++r) any = any || hits[r][lane] != 0;
+        flags[i] = any ? 0 : 1;
+    }
+}
+
 // ---------------------------------------------------------------------------
 // edge validity (DiscreteMotionValidator::checkMotion semantics)
 // ---------------------------------------------------------------------------
@@ -175,7 +222,9 @@ __global__ __launch_bounds__(VBLOCK, NCL == NCL_GRID ? RP_EDGE_WAVES : RP_EDGE_W
         const int start = incl - cnt;
         const int packed_nd = nde | (emode << 30);   // nde < 2^30 (ND_FROM stripped)
         // rounds r, r + kmax, ... (a group holds at most 64 kmax items when every
-        // edge's slot count is <= kmax; the stride keeps any larger one exact)
+        // edge's slot count is <= kmax; the stride keeps any larger one exact; the
+        // scan inside this loop instead, so that none of it lives across the state
+        // check, measured +3 % time: profiles/r04/edge_waves_ab.txt)
         for (int r0 = r * VBLOCK; r0 < total; r0 += kmax * VBLOCK) {
             __builtin_amdgcn_wave_barrier();
             mark[lane] = -1;

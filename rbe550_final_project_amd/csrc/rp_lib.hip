@@ -331,8 +331,38 @@ bool base_fixed(const DevScene& sc) {
     return sc.base[0] == BASE_FIXED[0] && sc.base[1] == BASE_FIXED[1] && sc.base[2] == BASE_FIXED[2];
 }
 
+// launches of (4096, 65536] states: k_validity_split with 3 roles, (65536,
+// split_max] with 2 (rp_kernels.h); RBE_SPLIT_MAX overrides the bound (0: off)
+int64_t split_max() {
+    static const int64_t v = [] {
+        const char* e = std::getenv("RBE_SPLIT_MAX");
+        return (e && *e) ? (int64_t)std::atoll(e) : (int64_t)131072;
+    }();
+    return v;
+}
+
+template <bool BF, int NR>
+void launch_validity_split(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, hipStream_t s) {
+    const dim3 g(blocks_for(n, 64)), b(64 * NR);
+#define RP_VALS(N) hipLaunchKernelGGL((k_validity_split<N, BF, NR>), g, b, 0, s, q, n, flags, c->d_scene)
+    switch (ncl_bucket(c->scene)) {
+        case NCL_GRID: RP_VALS(NCL_GRID); break;
+        case 0: RP_VALS(0); break;
+        case 1: RP_VALS(1); break;
+        case 2: RP_VALS(2); break;
+        case 4: RP_VALS(4); break;
+        default: RP_VALS(8); break;
+    }
+#undef RP_VALS
+}
+
 template <bool BF>
 void launch_validity_bf(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, hipStream_t s) {
+    if (n <= split_max()) {
+        if (n <= 65536) launch_validity_split<BF, 3>(c, q, n, flags, s);
+        else launch_validity_split<BF, 2>(c, q, n, flags, s);
+        return;
+    }
     const dim3 g(blocks_for(n, VTHREADS)), b(VTHREADS);
 #define RP_VAL(N) hipLaunchKernelGGL((k_validity<N, BF>), g, b, 0, s, q, n, flags, c->d_scene)
     switch (ncl_bucket(c->scene)) {

@@ -759,7 +759,18 @@ __device__ __forceinline__ void pairs_queued(const Capsules& k, S& s) {
     }
 }
 
-template <int NCL>
+// Work roles of a state check (k_validity_split: two or three waves share each
+// state), a bit set: ROLE_ENV the plane and box tests of every capsule, ROLE_PA the
+// self pairs completed before capsule SPLIT_J, ROLE_PB the self pairs completed at
+// SPLIT_J or later and the never pairs of waves outside the joint limits. The sets
+// partition ROLE_ALL's tests, so OR-ing the roles' results gives its result.
+enum { ROLE_ENV = 1, ROLE_PA = 2, ROLE_PB = 4, ROLE_ALL = 7 };
+#ifndef RP_SPLIT_J
+#define RP_SPLIT_J C_LINK6
+#endif
+constexpr int SPLIT_J = RP_SPLIT_J;
+
+template <int NCL, int ROLE = ROLE_ALL>
 struct QueuedVisit {
     const DevScene* __restrict__ sc;
     QueueState<NCL> s;
@@ -768,8 +779,11 @@ struct QueuedVisit {
         if constexpr (C == C_LINK4) RP_STAMP(2);
         if constexpr (C == C_LINK6) RP_STAMP(3);
         if constexpr (C == C_HAND) RP_STAMP(4);
-        if (env_queued<C>(k, sc, s)) return true;
-        pairs_queued<C>(k, s);
+        if constexpr ((ROLE & ROLE_ENV) != 0) {
+            if (env_queued<C>(k, sc, s)) return true;
+        }
+        if constexpr (((ROLE & ROLE_PA) != 0 && C < SPLIT_J) || ((ROLE & ROLE_PB) != 0 && C >= SPLIT_J))
+            pairs_queued<C>(k, s);
         return false;
     }
 };
@@ -800,10 +814,10 @@ __device__ __forceinline__ void never_pairs_outside_limits(const float q[NQ], co
 // box and self narrow phases are queued and drained wave-compacted. Every lane of
 // the wave that is still running must call this at the same point. NCL >= the
 // scene's cluster count (rp_lib.hip picks the instantiation).
-template <int NCL, bool BF = false>
+template <int NCL, bool BF = false, int ROLE = ROLE_ALL>
 __device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene* __restrict__ sc, WaveQ& Q) {
     Capsules k;
-    QueuedVisit<NCL> v;
+    QueuedVisit<NCL, ROLE> v;
     v.sc = sc;
     v.s.Q = &Q;
     v.s.nss = 0;
@@ -821,7 +835,7 @@ __device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene
     v.s.plane_z = sc->plane_z;
     v.s.env_far = v.s.in_limits ? sc->env_far : 0u;
     v.s.hand_near = 0u;
-    v.s.cl.load(sc);
+    if constexpr ((ROLE & ROLE_ENV) != 0) v.s.cl.load(sc);
     Q.hit[v.s.lane] = 0;
     __builtin_amdgcn_wave_barrier();
     // the 7 joint sin / cos first: independent chains, interleaved, instead of one
@@ -831,8 +845,9 @@ __device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene
     JointsSC jt;
 #pragma unroll
     for (int i = 0; i < 7; ++i) rp_sincos(q[i], &jt.s[i], &jt.c[i]);
-    if (fk_walk_j<QueuedVisit<NCL>, BF>(q, jt, sc->base, k, v)) return true;
-    if (!v.s.in_limits) never_pairs_outside_limits(q, sc, v.s);
+    if (fk_walk_j<QueuedVisit<NCL, ROLE>, BF>(q, jt, sc->base, k, v)) return true;
+    if constexpr ((ROLE & ROLE_PB) != 0)
+        if (!v.s.in_limits) never_pairs_outside_limits(q, sc, v.s);
     RP_STAMP(5);
     while (v.s.nsb > 0) pop_sb(v.s);
     RP_STAMP(6);

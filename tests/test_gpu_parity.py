@@ -438,3 +438,24 @@ def test_validity_flags_outside_joint_limits(gpu_ctx, oracle_lib, name, mode):
     g = gpu_ctx.check_states(q)
     c = o.check_states(q)
     assert np.array_equal(g, c), f"{(g != c).sum()} flags differ"
+
+
+@pytest.mark.parametrize("name", ["goal1", "goal3", "goal4_yawed", "clutter64"])
+@pytest.mark.parametrize("n", [4097, 8192, 65536, 65537, 131072, 131073])
+def test_validity_flags_every_launch_kernel(gpu_ctx, oracle_lib, name, n):
+    """The launch sizes at the kernels' boundaries: <= 4,096 states the lane-group
+    kernel, up to 65,536 the three-role split kernel, up to 131,072 the two-role one,
+    above it the one-wave k_validity (rp_lib.hip launch_validity). Uniform states,
+    states near the home pose, every 64th state outside the joint limits, box 0
+    attached:
+    flags bit-exact."""
+    sc = SCENES[name]
+    o = _both(gpu_ctx, oracle_lib, sc, attached=0)
+    rng = np.random.default_rng(n)
+    q = _uniform(n, n + 1)
+    q[: n // 10] = _near(model.SAFE_HOME, n // 10, n + 2, sigma=0.5)   # a tenth near the home pose
+    pad = np.array([0.6] * 7 + [0.02] * 2)
+    q[::64] = (model.Q_HI + pad * rng.random((len(q[::64]), 9))).astype(np.float32)
+    g = gpu_ctx.check_states(q)
+    r = o.check_states(q)
+    assert np.array_equal(g, r), f"{(g != r).sum()} of {n} flags differ"

@@ -128,3 +128,28 @@ def test_scene_poses_equal_scene_records(gpu_ctx, oracle_lib):
     qs[:4096] = np.clip(np.asarray(q["start"])[None, :] + rng.normal(0, 0.2, (4096, 9)), model.Q_LO,
                         model.Q_HI).astype(np.float32)
     assert np.array_equal(gpu_ctx.check_states(qs), o.check_states(qs))
+
+
+def test_async_error_and_close_in_flight(gpu_ctx):
+    """A library error inside an asynchronous query (a 150-waypoint path for a
+    10-state output buffer) comes back from rp_plan_wait, and the context plans again
+    afterwards; a context closed
+    with a query in flight finishes that query first (rp_destroy joins the planner
+    thread), then is gone."""
+    q = _wl("clutter64")["queries"][0]
+    sc = scenes.Scene.from_json(q["scene"])
+    gpu_ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+    gpu_ctx.set_attached(q["attached"])
+    p = _abi.make_params(seed=0, batch=4096, n_waypoints=150, timeout_s=60, straight_first=False)
+    gpu_ctx.plan_async(q["start"], q["goal"], model.Q_LO, model.Q_HI, p, path_cap=10)
+    with pytest.raises(NativeError, match="path_cap"):
+        gpu_ctx.plan_wait()
+    path, st = gpu_ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+    assert st == _abi.STATUS_EXACT and len(path) == 150
+    from rbe550_final_project_amd.native import Context
+    c2 = Context(device=0, robot=model.robot_desc())
+    c2.set_scene(sc.boxes, sc.plane_z, sc.base)
+    c2.set_attached(q["attached"])
+    c2.plan_async(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+    c2.close()
+    assert not c2._h

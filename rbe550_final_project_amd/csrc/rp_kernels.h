@@ -18,8 +18,9 @@ constexpr int VBLOCK = 64;      // validity / edge block size: one wave (its LDS
 // waves per SIMD requested from the register allocator. k_validity on cluster
 // scenes: 5 (96 VGPRs; the queue's LDS lets 20 one-wave workgroups share a CU,
 // rp_math.h QCAP): +4.5 % goal3 over 4 waves. Grid scenes
-// keep 4 (their broad phase spills at 96). The edge kernels: 4 (was uncapped at
-// 136 VGPRs = 3 waves): C4 262k-sample plans -12 %; 5 spills.
+// keep 4 (their broad phase spills at 96). The loop-free k_edges (the planner's
+// launches): 5, as k_validity; the grid-striding edge kernels (k_edges_packed,
+// k_edges<LOOP>): 4 (a loop around the state check spills at 96).
 #ifndef RP_VALIDITY_WAVES
 #define RP_VALIDITY_WAVES 5
 #endif
@@ -30,7 +31,10 @@ constexpr int VBLOCK = 64;      // validity / edge block size: one wave (its LDS
 #define RP_EDGE_WAVES 4
 #endif
 #ifndef RP_EDGE_WAVES_CL
-#define RP_EDGE_WAVES_CL 4
+#define RP_EDGE_WAVES_CL 5
+#endif
+#ifndef RP_EDGE_WAVES_LOOP
+#define RP_EDGE_WAVES_LOOP 4
 #endif
 constexpr int NNBLOCK = 256;    // NN block size
 constexpr int NNTILE = 256;     // tree nodes per LDS tile (256 x 72 B = 18 KiB)
@@ -182,100 +186,132 @@ __device__ __forceinline__ int wave_incl_max(int v) {
 // per-lane 64-bit index division. A wave with no round left exits after the scan;
 // an item of an edge already invalid (or past its prefix group's first failure) when
 // it is reached is skipped, as in the dense grid.
-template <int NCL, bool BF = false>
-__global__ __launch_bounds__(VBLOCK, NCL == NCL_GRID ? RP_EDGE_WAVES : RP_EDGE_WAVES_CL) void k_edges(const double* __restrict__ from,
-                                                  const double* __restrict__ to,
-                                                  const int* __restrict__ nd, int64_t n_edges,
-                                                  int kmax, int mode, uint8_t* valid, int group,
-                                                  int* gfail, unsigned long long* counter,
-                                                  const DevScene* __restrict__ sc,
-                                                  const int* __restrict__ dcount, int per_item,
-                                                  const int* __restrict__ dkmax) {
+// One (group, round) of a k_edges launch: the group's slot counts, scanned; the
+// round's items mapped to their edges; their states checked. Returns false when the
+// round is past the group's items.
+template <int NCL, bool BF>
+__device__ __forceinline__ bool edge_group_round(const double* __restrict__ from, const double* __restrict__ to,
+                                                 const int* __restrict__ nd, int64_t n_edges, int mode,
+                                                 uint8_t* valid, int group, int* gfail,
+                                                 unsigned long long* counter, const DevScene* __restrict__ sc,
+                                                 int64_t g, int r0, WaveQ& wq, int* mark) {
+    const int lane = rp_tid();
+    const int64_t e = g * VBLOCK + lane;
+    int nde = -1, emode = mode, cnt = 0;
+    if (e < n_edges) {
+        nde = nd[e];
+        if (mode == 2 && nde >= 0) {
+            emode = (nde & ND_FROM) ? 1 : 0;
+            nde &= ~ND_FROM;
+        }
+        // the layout depends on nd alone: valid / gfail change while the launch
+        // runs (this launch's own failures), and every wave of a group must see the
+        // same item list (they are read per item below)
+        cnt = nde >= 0 ? (nde > 1 ? nde : 1) : 0;
+    }
+    const int incl = wave_incl_add(cnt);
+    const int total = __builtin_amdgcn_readlane(incl, 63);
+    if (r0 >= total) return false;
+    const int start = incl - cnt;
+    const int packed_nd = nde | (emode << 30);   // nde < 2^30 (ND_FROM stripped)
+    __builtin_amdgcn_wave_barrier();
+    mark[lane] = -1;
+    __builtin_amdgcn_wave_barrier();
+    if (cnt > 0 && start >= r0 && start < r0 + VBLOCK) mark[start - r0] = lane;
+    __builtin_amdgcn_wave_barrier();
+    // the edge covering item r0 that started in an earlier round (if any)
+    const unsigned long long cov = __ballot(cnt > 0 && start < r0 && r0 < start + cnt);
+    const int carry = cov ? (int)__builtin_ctzll(cov) : -1;
+    const int j = max(wave_incl_max(mark[lane]), carry);
+    const int sj = __shfl(start, j);
+    const int pj = __shfl(packed_nd, j);
+    const int64_t ej = g * VBLOCK + j;
+    const int t = r0 + lane;
+    bool run = t < total;
+    int slot = 0, nj = 0, mj = 0;
+    if (run) {
+        slot = t - sj;
+        nj = pj & ~(1 << 30);
+        mj = (pj >> 30) & 1;
+        run = valid[ej] != 0;
+        if (run && gfail) {
+            const int gi = (int)(ej / group), si = (int)(ej - (int64_t)gi * group);
+            run = gfail[gi] > si;
+        }
+    }
+    const unsigned long long ballot = __ballot(run);
+    count_states(counter, ballot);
+    if (ballot && run) {
+        double st[NQ];
+        const double* a = from + ej * NQ;
+        const double* b = to + ej * NQ;
+        if (slot == 0) {
+            const double* ep = mj ? a : b;
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) st[k] = ep[k];
+        } else {
+            interp(a, b, (double)slot / (double)nj, st);
+        }
+        float qq[NQ];
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) qq[k] = (float)st[k];
+        if (state_collides<NCL, BF>(qq, sc, wq)) {
+            valid[ej] = 0;
+            if (gfail) {
+                const int gi = (int)(ej / group), si = (int)(ej - (int64_t)gi * group);
+                atomicMin(&gfail[gi], si);
+            }
+        }
+    }
+    return true;
+}
+
+// Wave-compacted (edge, slot) items: the launch covers groups of 64 consecutive
+// edges with kmax waves each (the dense grid's size: kmax slot rounds of 64 lanes
+// per group); a wave scans its group's slot counts (lane j: edge 64 g + j, 0 for an
+// empty edge; from nd only, so that every wave of a group sees the same list while
+// the launch's own failures change valid / gfail) and runs round r of the group's
+// packed item list, item t = 64 r + lane -> the edge j whose [start_j, start_j +
+// cnt_j) holds t (the start marks of the round, max-scanned, plus the edge that
+// carries into the round), slot t - start_j. Every running wave but a group's last
+// has 64 busy lanes (a dense (edge, slot) grid idles the lanes past each edge's
+// slot count: a quarter of them for range-length RRT edges), and there is no
+// per-lane 64-bit index division. A wave with no round left exits after the scan;
+// an item of an edge already invalid (or past its prefix group's first failure) when
+// it is reached is skipped, as in the dense grid.
+// LOOP = false (the planner's launches): one (group, round) per block — the grid is
+// groups x kmax and kmax bounds every edge's slot count (the steering range, or the
+// whole bounds' extent for shortcut edges). No loop around the state check lets it
+// keep k_validity's register budget (5 waves per SIMD at 96 VGPRs: a loop around it
+// hoists loop-invariant values and spills 29 VGPRs). LOOP = true (rp_check_edges_device:
+// the slot bound lives on the device, dkmax; capped grids): grid-stride over (group,
+// round) and rounds r, r + kmax, ...
+template <int NCL, bool BF = false, bool LOOP = false>
+__global__ __launch_bounds__(VBLOCK, LOOP ? RP_EDGE_WAVES_LOOP : (NCL == NCL_GRID ? RP_EDGE_WAVES : RP_EDGE_WAVES_CL)) void k_edges(
+    const double* __restrict__ from, const double* __restrict__ to, const int* __restrict__ nd, int64_t n_edges,
+    int kmax, int mode, uint8_t* valid, int group, int* gfail, unsigned long long* counter,
+    const DevScene* __restrict__ sc, const int* __restrict__ dcount, int per_item, const int* __restrict__ dkmax) {
     __shared__ WaveQ wq;
     __shared__ int mark[VBLOCK];
     // device-side edge count (planner iterations: dcount = accepted targets) and
-    // slot count (rp_check_edges_device: k_edge_prep's max); the grid may be
-    // smaller than the work (gated launches): grid-stride over (group, round)
+    // slot count (rp_check_edges_device: k_edge_prep's max)
     if (dcount) n_edges = min(n_edges, (int64_t)dcount[0] * per_item);
     if (dkmax) kmax = *dkmax;
     kmax = max(kmax, 1);
-    const int lane = rp_tid();
     const int64_t n_waves = (n_edges + VBLOCK - 1) / VBLOCK * kmax;
-    for (int64_t w = rp_bid(); w < n_waves; w += rp_gdim()) {
+    if constexpr (!LOOP) {
+        const int64_t w = rp_bid();
+        if (w >= n_waves) return;
         const int64_t g = w / kmax;
-        const int r = (int)(w - g * kmax);
-        const int64_t e = g * VBLOCK + lane;
-        int nde = -1, emode = mode, cnt = 0;
-        if (e < n_edges) {
-            nde = nd[e];
-            if (mode == 2 && nde >= 0) {
-                emode = (nde & ND_FROM) ? 1 : 0;
-                nde &= ~ND_FROM;
-            }
-            // the layout depends on nd alone: valid / gfail change while the launch
-            // runs (this launch's own failures), and every wave of a group must see
-            // the same item list (they are read per item below)
-            cnt = nde >= 0 ? (nde > 1 ? nde : 1) : 0;
-        }
-        const int incl = wave_incl_add(cnt);
-        const int total = __builtin_amdgcn_readlane(incl, 63);
-        const int start = incl - cnt;
-        const int packed_nd = nde | (emode << 30);   // nde < 2^30 (ND_FROM stripped)
-        // rounds r, r + kmax, ... (a group holds at most 64 kmax items when every
-        // edge's slot count is <= kmax; the stride keeps any larger one exact; the
-        // scan inside this loop instead, so that none of it lives across the state
-        // check, measured +3 % time: profiles/r04/edge_waves_ab.txt)
-        for (int r0 = r * VBLOCK; r0 < total; r0 += kmax * VBLOCK) {
-            __builtin_amdgcn_wave_barrier();
-            mark[lane] = -1;
-            __builtin_amdgcn_wave_barrier();
-            if (cnt > 0 && start >= r0 && start < r0 + VBLOCK) mark[start - r0] = lane;
-            __builtin_amdgcn_wave_barrier();
-            // the edge covering item r0 that started in an earlier round (if any)
-            const unsigned long long cov = __ballot(cnt > 0 && start < r0 && r0 < start + cnt);
-            const int carry = cov ? (int)__builtin_ctzll(cov) : -1;
-            const int j = max(wave_incl_max(mark[lane]), carry);
-            const int sj = __shfl(start, j);
-            const int pj = __shfl(packed_nd, j);
-            const int64_t ej = g * VBLOCK + j;
-            const int t = r0 + lane;
-            bool run = t < total;
-            int slot = 0, nj = 0, mj = 0;
-            if (run) {
-                slot = t - sj;
-                nj = pj & ~(1 << 30);
-                mj = (pj >> 30) & 1;
-                run = valid[ej] != 0;
-                if (run && gfail) {
-                    const int gi = (int)(ej / group), si = (int)(ej - (int64_t)gi * group);
-                    run = gfail[gi] > si;
-                }
-            }
-            const unsigned long long ballot = __ballot(run);
-            count_states(counter, ballot);
-            if (!ballot) continue;
-            if (run) {
-                double st[NQ];
-                const double* a = from + ej * NQ;
-                const double* b = to + ej * NQ;
-                if (slot == 0) {
-                    const double* ep = mj ? a : b;
-#pragma unroll
-                    for (int k = 0; k < NQ; ++k) st[k] = ep[k];
-                } else {
-                    interp(a, b, (double)slot / (double)nj, st);
-                }
-                float qq[NQ];
-#pragma unroll
-                for (int k = 0; k < NQ; ++k) qq[k] = (float)st[k];
-                if (state_collides<NCL, BF>(qq, sc, wq)) {
-                    valid[ej] = 0;
-                    if (gfail) {
-                        const int gi = (int)(ej / group), si = (int)(ej - (int64_t)gi * group);
-                        atomicMin(&gfail[gi], si);
-                    }
-                }
-            }
+        edge_group_round<NCL, BF>(from, to, nd, n_edges, mode, valid, group, gfail, counter, sc, g,
+                                  (int)(w - g * kmax) * VBLOCK, wq, mark);
+    } else {
+        for (int64_t w = rp_bid(); w < n_waves; w += rp_gdim()) {
+            const int64_t g = w / kmax;
+            for (int r0 = (int)(w - g * kmax) * VBLOCK;; r0 += kmax * VBLOCK)
+                if (!edge_group_round<NCL, BF>(from, to, nd, n_edges, mode, valid, group, gfail, counter, sc, g, r0,
+                                               wq, mark))
+                    break;
         }
     }
 }
@@ -315,7 +351,7 @@ __global__ void k_chunk_first(const int32_t* __restrict__ incl, int64_t n_edges,
 // its index into the item slots it covers; empty edges cover none, so a pass may
 // take another round of 64 edges).
 template <int NCL, bool BF = false>
-__global__ __launch_bounds__(VBLOCK, NCL == NCL_GRID ? RP_EDGE_WAVES : RP_EDGE_WAVES_CL) void k_edges_packed(
+__global__ __launch_bounds__(VBLOCK, NCL == NCL_GRID ? RP_EDGE_WAVES : RP_EDGE_WAVES_LOOP) void k_edges_packed(
     const double* __restrict__ from, const double* __restrict__ to, const int* __restrict__ nd, int64_t n_edges,
     int mode, uint8_t* valid, int group, int* gfail, unsigned long long* counter, const DevScene* __restrict__ sc,
     const int32_t* __restrict__ incl, const int32_t* __restrict__ chunk_first) {

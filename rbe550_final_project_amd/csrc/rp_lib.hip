@@ -477,19 +477,27 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
         prof_end(c, ps, 1, s);
         return;
     }
-    // k_edges: kmax one-wave blocks per group of 64 edges (its slot rounds)
+    // k_edges: kmax one-wave blocks per group of 64 edges (its slot rounds). The
+    // loop-free kernel needs the exact grid and kmax >= every slot count; a capped
+    // grid or a device-side slot bound (dkmax) takes the grid-striding one
     unsigned nb = (unsigned)std::min<int64_t>((int64_t)blocks_for(n, VBLOCK) * kmax, (int64_t)1 << 30);
+    const bool loop = dkmax != nullptr || (max_blocks && nb > max_blocks);
     if (max_blocks && nb > max_blocks) nb = max_blocks;   // grid-stride (gated launches)
     const dim3 g(nb), b(VBLOCK);
     const int ps = prof_begin(c, s);
     // (the reference's robot base folded in as a constant, as for k_validity)
     const bool bf = base_fixed(c->scene);
-#define RP_EDGES(N)                                                                                                \
+#define RP_EDGES_L(N, L)                                                                                           \
     do {                                                                                                           \
-        if (bf) hipLaunchKernelGGL((k_edges<N, true>), g, b, 0, s, from, to, nd, n, kmax, mode, valid, group, gfail, \
-                                   c->counter.p, c->d_scene, dcount, per_item, dkmax);                             \
-        else hipLaunchKernelGGL((k_edges<N, false>), g, b, 0, s, from, to, nd, n, kmax, mode, valid, group, gfail,   \
-                                c->counter.p, c->d_scene, dcount, per_item, dkmax);                                \
+        if (bf) hipLaunchKernelGGL((k_edges<N, true, L>), g, b, 0, s, from, to, nd, n, kmax, mode, valid, group,     \
+                                   gfail, c->counter.p, c->d_scene, dcount, per_item, dkmax);                      \
+        else hipLaunchKernelGGL((k_edges<N, false, L>), g, b, 0, s, from, to, nd, n, kmax, mode, valid, group,       \
+                                gfail, c->counter.p, c->d_scene, dcount, per_item, dkmax);                         \
+    } while (0)
+#define RP_EDGES(N)                         \
+    do {                                    \
+        if (loop) RP_EDGES_L(N, true);      \
+        else RP_EDGES_L(N, false);          \
     } while (0)
     switch (ncl_bucket(c->scene)) {
         case NCL_GRID: RP_EDGES(NCL_GRID); break;
@@ -500,6 +508,7 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
         default: RP_EDGES(8); break;
     }
 #undef RP_EDGES
+#undef RP_EDGES_L
     HIP_TRY(hipGetLastError());
     prof_end(c, ps, 1, s);
 }
@@ -1255,14 +1264,15 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     if (const char* e = std::getenv("RBE_PLAN_SPECULATE"))
         if (*e) speculate = speculate && std::atoi(e) != 0;
     const int G = cmax + 1;   // edges per sample in a speculative launch
-    // connect chains end early, so large connect launches are work-compacted
-    // (k_edges_packed); RBE_EDGE_PACKED=0/1 forces the choice (tests)
-    int packed_mode = -1;
+    // Edge launches are work-compacted (connect chains end early, steers are short
+    // on large trees). Round 4: the loop-free wave-compacted k_edges (groups of 64 edges x kmax waves,
+    // 5 waves per SIMD) beats the scanned list on every size measured (C5 covered-well
+    // plans 9.8 vs 10.4 ms of edge time, profiles/r04/edge_loopfree_ab.txt), so the
+    // packed path runs only when RBE_EDGE_PACKED=1 asks for it (tests)
+    int packed_mode = 0;
     if (const char* e = std::getenv("RBE_EDGE_PACKED"))
         if (*e) packed_mode = std::atoi(e) != 0;
-    auto packed = [&](int64_t n_edges) {
-        return packed_mode >= 0 ? packed_mode == 1 : n_edges * (int64_t)kmax >= ((int64_t)1 << 20);
-    };
+    auto packed = [&](int64_t) { return packed_mode == 1; };
     // sub-batches (rp_plan_params.chunk): an iteration runs as ordered sub-batches of
     // chunk0, chunk0 * chunk_growth, ... samples and ends after the one holding the
     // first REACHED sample; the trees do not depend on it (the oracle appends up to
@@ -1731,8 +1741,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             prof_end(c, pn1, 0, c->stream);
             c->prof.nn_pairs += (double)C * (double)TA;
             debug_wait(c, "k_ext_nn");
-            // extension edges: steers shorter than the range (samples near the tree)
-            // leave most of a dense (edge, slot) grid's lanes idle on large trees
+            // (extension edges: steers shorter than the range on large trees)
             if (packed(C + (sg >= 0 ? 2 : 0)))
                 launch_edges_packed(c, c->efrom.p, c->eto.p, c->nd.p, C + (sg >= 0 ? 2 : 0), kmax, a_start ? 0 : 1,
                                     c->valid.p, 1, nullptr, c->stream, nullptr, 1);

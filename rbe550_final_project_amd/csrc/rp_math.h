@@ -526,7 +526,6 @@ struct QueueState {
     WaveQ* Q;
     int nss, nsb;     // wave-uniform item counts
     bool in_limits;   // every state of the wave inside the joint limits (skip never pairs)
-    unsigned hand_near;   // bit I: the sphere test of pair (capsule I, hand) passed (this lane)
     int lane;
     float plane_z;
     unsigned env_far;   // DevScene::env_far if the wave is inside the joint limits, else 0
@@ -834,7 +833,6 @@ __device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene
     }
     v.s.plane_z = sc->plane_z;
     v.s.env_far = v.s.in_limits ? sc->env_far : 0u;
-    v.s.hand_near = 0u;
     if constexpr ((ROLE & ROLE_ENV) != 0) v.s.cl.load(sc);
     Q.hit[v.s.lane] = 0;
     __builtin_amdgcn_wave_barrier();

@@ -17,8 +17,8 @@ from rbe550_final_project_amd.build import validity_source_hash  # noqa: E402
 
 def main():
     fdir, wdir, n, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
-    f, meta = load([fdir], "k_validity", n)
-    w, _ = load([wdir], "k_validity", n)
+    f, meta, _, _ = load([fdir], "k_validity", n)
+    w, _, _, _ = load([wdir], "k_validity", n)
     read_b = 2.0 * f["FETCH_SIZE"] * 1024.0
     write_b = w["WRITE_SIZE"] * 1024.0
     d = {"kernel": "k_validity", "states_per_launch": n, "fetch_size_kb": f["FETCH_SIZE"],

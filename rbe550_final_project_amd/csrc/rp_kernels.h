@@ -419,22 +419,28 @@ __global__ __launch_bounds__(VBLOCK, NCL == NCL_GRID ? RP_EDGE_WAVES : RP_EDGE_W
     }
 }
 
-// nd for arbitrary edges (API / simplification) and the max over edges
-__global__ void k_edge_prep(const double* __restrict__ from, const double* __restrict__ to, int64_t n,
-                            double res, int* nd, uint8_t* valid, int* kmax) {
-    const int64_t e = (int64_t)rp_bid() * rp_bdim() + rp_tid();
+// nd for arbitrary edges (API / simplification) and the max over edges. A fixed
+// grid (EDGE_PREP_BLOCKS of 256 threads) strides over the edges and each block
+// raises the maximum once: atomics on one word serialise at ~11 ns each (one per
+// wave of a 262,144-edge launch: 45 us, rocprofv3 profiles/r04/edge_prep_ab.txt)
+constexpr int EDGE_PREP_BLOCKS = 256;
+__global__ __launch_bounds__(256) void k_edge_prep(const double* __restrict__ from, const double* __restrict__ to,
+                                                   int64_t n, double res, int* nd, uint8_t* valid, int* kmax) {
+    __shared__ int wmax[4];
     int v = 0;
-    if (e < n) {
+    for (int64_t e = (int64_t)rp_bid() * 256 + rp_tid(); e < n; e += (int64_t)rp_gdim() * 256) {
         const int c = segment_count(from + e * NQ, to + e * NQ, res);
         nd[e] = c;
         valid[e] = 1;
-        v = c > 1 ? c : 1;
+        v = max(v, c > 1 ? c : 1);
     }
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));   // wave max
-    // one atomic per wave, and only while it can raise the maximum (thousands of
-    // waves' atomics on one word serialise: 50 us for 262,144 edges)
-    if ((rp_tid() & 63) == 0 && v > __hip_atomic_load(kmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        atomicMax(kmax, v);
+    v = wave_incl_max(v);   // lane 63: the wave's max
+    if ((rp_tid() & 63) == 63) wmax[rp_tid() >> 6] = v;
+    __syncthreads();
+    if (rp_tid() == 0) {
+        v = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+        if (v > __hip_atomic_load(kmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(kmax, v);
+    }
 }
 
 // ---------------------------------------------------------------------------

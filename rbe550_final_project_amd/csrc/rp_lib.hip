@@ -762,7 +762,7 @@ int64_t check_edges_host(rp_ctx* c, const double* qa, const double* qb, int64_t 
     HIP_TRY(hipMemcpyAsync(c->eb.p, qb, sizeof(double) * NQ * n, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemsetAsync(c->scalar.p, 0, sizeof(int) * 16, c->stream));
     HIP_TRY(hipMemsetAsync(c->counter.p, 0, sizeof(unsigned long long) * COUNTER_SLOTS, c->stream));
-    hipLaunchKernelGGL(k_edge_prep, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, c->ea.p, c->eb.p, n, res,
+    hipLaunchKernelGGL(k_edge_prep, dim3((unsigned)std::min<int64_t>(blocks_for(n, 256), EDGE_PREP_BLOCKS)), dim3(256), 0, c->stream, c->ea.p, c->eb.p, n, res,
                        c->end_nd.p, c->eval.p, c->scalar.p);
     HIP_TRY(hipGetLastError());
     const int kmax = read_scalar(c, c->scalar.p);
@@ -2330,7 +2330,7 @@ int rp_check_edges_device(rp_ctx* c, const double* qa, const double* qb, int64_t
     c->end_nd.ensure(n);
     c->scalar.ensure(16);
     HIP_TRY(hipMemsetAsync(c->scalar.p, 0, sizeof(int), s));
-    hipLaunchKernelGGL(k_edge_prep, dim3(blocks_for(n, 256)), dim3(256), 0, s, qa, qb, n, res, c->end_nd.p, out,
+    hipLaunchKernelGGL(k_edge_prep, dim3((unsigned)std::min<int64_t>(blocks_for(n, 256), EDGE_PREP_BLOCKS)), dim3(256), 0, s, qa, qb, n, res, c->end_nd.p, out,
                        c->scalar.p);
     HIP_TRY(hipGetLastError());
     // fully asynchronous: the slot count (the longest edge's) stays on the device and

@@ -18,9 +18,11 @@ constexpr int VBLOCK = 64;      // validity / edge block size: one wave (its LDS
 // waves per SIMD requested from the register allocator. k_validity on cluster
 // scenes: 5 (96 VGPRs; the queue's LDS lets 20 one-wave workgroups share a CU,
 // rp_math.h QCAP): +4.5 % goal3 over 4 waves. Grid scenes
-// keep 4 (their broad phase spills at 96). The loop-free k_edges (the planner's
-// launches): 5, as k_validity; the grid-striding edge kernels (k_edges_packed,
-// k_edges<LOOP>): 4 (a loop around the state check spills at 96).
+// keep 4 (their broad phase spills at 96: k_validity measures the same at 5). The
+// loop-free k_edges (the planner's launches): 5, as k_validity, on grid scenes too
+// (base-fixed robot: 6 VGPRs spilled, −3.5 % edge time; 21 with a free base: 4); the grid-striding edge kernels
+// (k_edges_packed, k_edges<LOOP>) and k_straight: 4 (a loop around the state check
+// spills at 96).
 #ifndef RP_VALIDITY_WAVES
 #define RP_VALIDITY_WAVES 5
 #endif
@@ -32,6 +34,9 @@ constexpr int VBLOCK = 64;      // validity / edge block size: one wave (its LDS
 #endif
 #ifndef RP_EDGE_WAVES_CL
 #define RP_EDGE_WAVES_CL 5
+#endif
+#ifndef RP_EDGE_WAVES_GRID   // the loop-free k_edges of grid scenes, base-fixed robot: 96 VGPRs,
+#define RP_EDGE_WAVES_GRID 5 // 6 spilled; C5 well edges 9.8 -> 9.45 ms (profiles/r04/edge_grid_waves_ab.txt)
 #endif
 #ifndef RP_EDGE_WAVES_LOOP
 #define RP_EDGE_WAVES_LOOP 4
@@ -287,7 +292,7 @@ __device__ __forceinline__ bool edge_group_round(const double* __restrict__ from
 // the slot bound lives on the device, dkmax; capped grids): grid-stride over (group,
 // round) and rounds r, r + kmax, ...
 template <int NCL, bool BF = false, bool LOOP = false>
-__global__ __launch_bounds__(VBLOCK, LOOP ? RP_EDGE_WAVES_LOOP : (NCL == NCL_GRID ? RP_EDGE_WAVES : RP_EDGE_WAVES_CL)) void k_edges(
+__global__ __launch_bounds__(VBLOCK, LOOP ? RP_EDGE_WAVES_LOOP : (NCL == NCL_GRID ? (BF ? RP_EDGE_WAVES_GRID : RP_EDGE_WAVES) : RP_EDGE_WAVES_CL)) void k_edges(
     const double* __restrict__ from, const double* __restrict__ to, const int* __restrict__ nd, int64_t n_edges,
     int kmax, int mode, uint8_t* valid, int group, int* gfail, unsigned long long* counter,
     const DevScene* __restrict__ sc, const int* __restrict__ dcount, int per_item, const int* __restrict__ dkmax) {

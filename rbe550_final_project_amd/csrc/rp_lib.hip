@@ -765,7 +765,12 @@ int64_t check_edges_host(rp_ctx* c, const double* qa, const double* qb, int64_t 
     hipLaunchKernelGGL(k_edge_prep, dim3((unsigned)std::min<int64_t>(blocks_for(n, 256), EDGE_PREP_BLOCKS)), dim3(256), 0, c->stream, c->ea.p, c->eb.p, n, res,
                        c->end_nd.p, c->eval.p, c->scalar.p);
     HIP_TRY(hipGetLastError());
-    const int kmax = read_scalar(c, c->scalar.p);
+    int kmax = read_scalar(c, c->scalar.p);
+    static const int kpad = [] {   // (diagnostic: waves per group past the slot bound, tools/edge_pad.py)
+        const char* e = std::getenv("RBE_EDGE_KMAX_PAD");
+        return e && *e ? std::max(0, std::atoi(e)) : 0;
+    }();
+    kmax += kpad;
     launch_edges(c, c->ea.p, c->eb.p, c->end_nd.p, n, kmax, 0, c->eval.p, 1, nullptr, c->stream);
     HIP_TRY(hipMemcpyAsync(out, c->eval.p, n, hipMemcpyDeviceToHost, c->stream));
     return read_counter(c);

@@ -5,7 +5,7 @@ rp_check_edges_device, and the same interpolated states (materialised once) chec
 by rp_check_states_device. Run under rocprofv3 --kernel-trace --stats for the
 kernel times; prints wall-clock rates of both.
 
-    python tools/edge_bench.py [LIB.so] [--n 262144] [--scene clutter64|goal3] [--reps 10]
+    python tools/edge_bench.py [LIB.so] [--n 262144] [--scene clutter64|goal3] [--reps 10] [--host]
 """
 import argparse
 import json
@@ -27,6 +27,9 @@ def main():
     ap.add_argument("--n", type=int, default=262144)
     ap.add_argument("--scene", default="clutter64")
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--host", action="store_true",
+                    help="edges through rp_check_edges (host buffers; the loop-free k_edges with the read-back slot "
+                         "bound; RBE_EDGE_KMAX_PAD adds waves per group past it)")
     a = ap.parse_args()
     if a.lib:
         native.LIB_PATH = os.path.abspath(a.lib)
@@ -70,6 +73,9 @@ def main():
     h = ctx._h
 
     def edges():
+        if a.host:
+            fe.copy_(torch.from_numpy(ctx.check_edges(qa, qb, float(res)).astype(np.uint8)))
+            return
         ctx._check(L.rp_check_edges_device(h, ta.data_ptr(), tb.data_ptr(), a.n, float(res), fe.data_ptr(), None),
                    "rp_check_edges_device")
 

@@ -52,6 +52,7 @@ for s in "$@"; do
     nnab) for v in abvariants/lib_head.so rbe550_final_project_amd/librbe_mi355x.so; do n=$(basename $v .so); step nnab_$n 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/nnab_$n -o kt -- python tools/nn_bench.py $v --check --tree walk && step nnabu_$n 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/nnabu_$n -o kt -- python tools/nn_bench.py $v --check --tree uniform; done; for d in gpurun_out/nnab*_*/; do echo $d; grep -h "k_nn_mfma\|k_nn_part" $d/*kernel_stats.csv | cut -c1-200; done ;;
     counters) rocprofv3 -L > gpurun_out/counters.txt 2>&1; grep -i "mfma\|SQ_INSTS_VALU\b\|VALU_MFMA" gpurun_out/counters.txt | head -40 ;;
     edgepmc) step epmc_a 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_BRANCH --output-format csv -d gpurun_out/epmc_a -o a -- python tools/c5_profile.py pmc && step epmc_b 300 rocprofv3 --pmc SQ_WAVES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/epmc_b -o b -- python tools/c5_profile.py pmc && python tools/pmc_summary.py gpurun_out/epmc_a gpurun_out/epmc_b --kernel k_edges --exclude packed --json gpurun_out/edges_pmc.json > gpurun_out/edges_pmc.txt && python tools/pmc_summary.py gpurun_out/epmc_a gpurun_out/epmc_b --kernel k_edges_packed --json gpurun_out/edges_packed_pmc.json > gpurun_out/edges_packed_pmc.txt && python tools/pmc_summary.py gpurun_out/epmc_a gpurun_out/epmc_b --kernel k_nn_mfma --json gpurun_out/nn_pmc.json > gpurun_out/nn_pmc.txt && cat gpurun_out/edges_pmc.txt gpurun_out/edges_packed_pmc.txt gpurun_out/nn_pmc.txt ;;
+    edgepad) for pad in 0 20 60; do for sc in goal3 clutter64; do RBE_EDGE_KMAX_PAD=$pad step ep_${sc}_$pad 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/ep_${sc}_$pad -o kt -- python tools/edge_bench.py --scene $sc --host && grep -h "k_edges\|k_validity" gpurun_out/ep_${sc}_$pad/*kernel_stats.csv | awk -F'",' '{print "pad '$pad' '$sc'", substr($1,2,40), $2}'; done; done ;;
     edgebench) for sc in clutter64 goal3; do step eb_$sc 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/eb_$sc -o kt -- python tools/edge_bench.py --scene $sc && grep -h "k_edges\|k_validity\|k_edge_prep" gpurun_out/eb_$sc/*kernel_stats.csv | cut -c1-160; done ;;
     edgeab) for v in abvariants/lib_head.so abvariants/lib_ew5.so rbe550_final_project_amd/librbe_mi355x.so; do n=$(basename $v .so); for sc in clutter64 goal3; do step eab_${n}_$sc 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/eab_${n}_$sc -o kt -- python tools/edge_bench.py $v --scene $sc && grep -h "k_edges" gpurun_out/eab_${n}_$sc/*kernel_stats.csv | awk -F'",' '{print "'$n' '$sc'", substr($1,1,30), $2}'; done; done ;;
     nnpmc2) step nnp_a 300 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/nnp_a -o a -- python tools/nn_bench.py --reps 2 && step nnp_b 300 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_INSTS_BRANCH SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/nnp_b -o b -- python tools/nn_bench.py --reps 2 && python tools/pmc_summary.py gpurun_out/nnp_a gpurun_out/nnp_b --kernel k_nn_mfma --json gpurun_out/nn_pmc_bench.json > gpurun_out/nn_pmc_bench.txt && cat gpurun_out/nn_pmc_bench.txt ;;

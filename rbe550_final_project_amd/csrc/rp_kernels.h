@@ -295,25 +295,29 @@ template <int NCL, bool BF = false, bool LOOP = false>
 __global__ __launch_bounds__(VBLOCK, LOOP ? RP_EDGE_WAVES_LOOP : (NCL == NCL_GRID ? (BF ? RP_EDGE_WAVES_GRID : RP_EDGE_WAVES) : RP_EDGE_WAVES_CL)) void k_edges(
     const double* __restrict__ from, const double* __restrict__ to, const int* __restrict__ nd, int64_t n_edges,
     int kmax, int mode, uint8_t* valid, int group, int* gfail, unsigned long long* counter,
-    const DevScene* __restrict__ sc, const int* __restrict__ dcount, int per_item, const int* __restrict__ dkmax) {
+    const DevScene* __restrict__ sc, const int* __restrict__ dcount, int per_item, const int* __restrict__ dkmax,
+    int r_first) {
     __shared__ WaveQ wq;
     __shared__ int mark[VBLOCK];
     // device-side edge count (planner iterations: dcount = accepted targets) and
     // slot count (rp_check_edges_device: k_edge_prep's max)
     if (dcount) n_edges = min(n_edges, (int64_t)dcount[0] * per_item);
     if (dkmax) kmax = *dkmax;
-    kmax = max(kmax, 1);
-    const int64_t n_waves = (n_edges + VBLOCK - 1) / VBLOCK * kmax;
+    // rounds r_first .. kmax - 1 of every group (r_first > 0: the remainder after a
+    // loop-free launch over the first r_first rounds, rp_check_edges_device)
+    const int kk = max(kmax, 1) - r_first;
+    if (kk <= 0) return;
+    const int64_t n_waves = (n_edges + VBLOCK - 1) / VBLOCK * kk;
     if constexpr (!LOOP) {
         const int64_t w = rp_bid();
         if (w >= n_waves) return;
-        const int64_t g = w / kmax;
+        const int64_t g = w / kk;
         edge_group_round<NCL, BF>(from, to, nd, n_edges, mode, valid, group, gfail, counter, sc, g,
-                                  (int)(w - g * kmax) * VBLOCK, wq, mark);
+                                  (r_first + (int)(w - g * kk)) * VBLOCK, wq, mark);
     } else {
         for (int64_t w = rp_bid(); w < n_waves; w += rp_gdim()) {
-            const int64_t g = w / kmax;
-            for (int r0 = (int)(w - g * kmax) * VBLOCK;; r0 += kmax * VBLOCK)
+            const int64_t g = w / kk;
+            for (int r0 = (r_first + (int)(w - g * kk)) * VBLOCK;; r0 += kk * VBLOCK)
                 if (!edge_group_round<NCL, BF>(from, to, nd, n_edges, mode, valid, group, gfail, counter, sc, g, r0,
                                                wq, mark))
                     break;
@@ -429,6 +433,10 @@ __global__ __launch_bounds__(VBLOCK, NCL == NCL_GRID ? RP_EDGE_WAVES : RP_EDGE_W
 // raises the maximum once: atomics on one word serialise at ~11 ns each (one per
 // wave of a 262,144-edge launch: 45 us, rocprofv3 profiles/r04/edge_prep_ab.txt)
 constexpr int EDGE_PREP_BLOCKS = 256;
+// rp_check_edges_device: rounds of every group the loop-free k_edges covers before the
+// grid-striding remainder (range-length RRT edges have <= 22 slots: one round each
+// group of them needs at most 22)
+constexpr int EDGE_DEV_ROUNDS = 24;
 __global__ __launch_bounds__(256) void k_edge_prep(const double* __restrict__ from, const double* __restrict__ to,
                                                    int64_t n, double res, int* nd, uint8_t* valid, int* kmax) {
     __shared__ int wmax[4];

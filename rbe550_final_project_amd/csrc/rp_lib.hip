@@ -479,25 +479,35 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
     }
     // k_edges: kmax one-wave blocks per group of 64 edges (its slot rounds). The
     // loop-free kernel needs the exact grid and kmax >= every slot count; a capped
-    // grid or a device-side slot bound (dkmax) takes the grid-striding one
-    unsigned nb = (unsigned)std::min<int64_t>((int64_t)blocks_for(n, VBLOCK) * kmax, (int64_t)1 << 30);
-    const bool loop = dkmax != nullptr || (max_blocks && nb > max_blocks);
-    if (max_blocks && nb > max_blocks) nb = max_blocks;   // grid-stride (gated launches)
-    const dim3 g(nb), b(VBLOCK);
+    // grid takes the grid-striding one. A device-side slot bound (dkmax,
+    // rp_check_edges_device): the loop-free kernel over the first EDGE_DEV_ROUNDS
+    // rounds of every group, then the grid-striding one from that round on (its waves
+    // return at once when the bound is no larger)
+    const int64_t groups = blocks_for(n, VBLOCK);
+    const bool split = dkmax != nullptr && !dcount;
+    const int km0 = split ? EDGE_DEV_ROUNDS : kmax;
+    unsigned nb = (unsigned)std::min<int64_t>(groups * km0, (int64_t)1 << 30);
+    const bool loop = !split && (dkmax != nullptr || (max_blocks && nb > max_blocks));
+    if (!split && max_blocks && nb > max_blocks) nb = max_blocks;   // grid-stride (gated launches)
+    const unsigned nb_rest = (unsigned)std::min<int64_t>(groups * 4, max_blocks ? max_blocks : 8192);
+    const dim3 b(VBLOCK);
     const int ps = prof_begin(c, s);
     // (the reference's robot base folded in as a constant, as for k_validity)
     const bool bf = base_fixed(c->scene);
-#define RP_EDGES_L(N, L)                                                                                           \
+#define RP_EDGES_L(N, L, G, KM, DK, RF)                                                                           \
     do {                                                                                                           \
-        if (bf) hipLaunchKernelGGL((k_edges<N, true, L>), g, b, 0, s, from, to, nd, n, kmax, mode, valid, group,     \
-                                   gfail, c->counter.p, c->d_scene, dcount, per_item, dkmax);                      \
-        else hipLaunchKernelGGL((k_edges<N, false, L>), g, b, 0, s, from, to, nd, n, kmax, mode, valid, group,       \
-                                gfail, c->counter.p, c->d_scene, dcount, per_item, dkmax);                         \
+        if (bf) hipLaunchKernelGGL((k_edges<N, true, L>), dim3(G), b, 0, s, from, to, nd, n, KM, mode, valid,      \
+                                   group, gfail, c->counter.p, c->d_scene, dcount, per_item, DK, RF);              \
+        else hipLaunchKernelGGL((k_edges<N, false, L>), dim3(G), b, 0, s, from, to, nd, n, KM, mode, valid,        \
+                                group, gfail, c->counter.p, c->d_scene, dcount, per_item, DK, RF);                 \
     } while (0)
-#define RP_EDGES(N)                         \
-    do {                                    \
-        if (loop) RP_EDGES_L(N, true);      \
-        else RP_EDGES_L(N, false);          \
+#define RP_EDGES(N)                                                                       \
+    do {                                                                                  \
+        if (split) {                                                                      \
+            RP_EDGES_L(N, false, nb, km0, nullptr, 0);                                    \
+            RP_EDGES_L(N, true, nb_rest, km0, dkmax, EDGE_DEV_ROUNDS);                    \
+        } else if (loop) RP_EDGES_L(N, true, nb, kmax, dkmax, 0);                         \
+        else RP_EDGES_L(N, false, nb, kmax, dkmax, 0);                                    \
     } while (0)
     switch (ncl_bucket(c->scene)) {
         case NCL_GRID: RP_EDGES(NCL_GRID); break;

@@ -1,8 +1,9 @@
 """Edge-check launches (OMPL DiscreteMotionValidator::checkMotion semantics,
 code/planning.py:190) against the CPU oracle's check_edges, at sizes that take the
-wave-compacted k_edges grid (> 2,048 edges through rp_check_edges_device, whose grid
-is capped at 8,192 blocks and grid-strides over (group, round) waves) and the
-lane-group kernels below it: flags bit-exact."""
+wave-compacted k_edges grid (> 2,048 edges through rp_check_edges_device: the
+loop-free kernel over each group's first EDGE_DEV_ROUNDS = 24 rounds, then the
+grid-striding remainder — scale 3 and 10 give groups of ~30 and ~100 rounds) and
+the lane-group kernels below it: flags bit-exact."""
 import json
 import os
 
@@ -36,7 +37,8 @@ def _edges(n, seed, scale=1.0):
 
 
 @pytest.mark.parametrize("scene", ["goal3", "clutter64"])
-@pytest.mark.parametrize("n,scale", [(1000, 1.0), (2049, 1.0), (8192, 1.0), (40000, 1.0), (20000, 3.0)])
+@pytest.mark.parametrize("n,scale", [(1000, 1.0), (2049, 1.0), (8192, 1.0), (40000, 1.0), (20000, 3.0),
+                                     (20000, 10.0)])
 def test_device_edges_equal_oracle(gpu_ctx, oracle_lib, scene, n, scale):
     sc = _scene(scene)
     o = oracle_lib.OracleScene()

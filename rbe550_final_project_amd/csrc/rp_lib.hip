@@ -483,12 +483,15 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
     // rp_check_edges_device): the loop-free kernel over the first EDGE_DEV_ROUNDS
     // rounds of every group, then the grid-striding one from that round on (its waves
     // return at once when the bound is no larger)
-    const int64_t groups = blocks_for(n, VBLOCK);
-    const bool split = dkmax != nullptr && !dcount;
+    // A grid past EDGE_GRID_MAX blocks (2^30 threads) also takes the grid-striding one.
+    constexpr int64_t EDGE_GRID_MAX = (int64_t)1 << 24, EDGE_LOOP_BLOCKS = 65536;
+    const int64_t groups = (n + VBLOCK - 1) / VBLOCK;
+    const bool split = dkmax != nullptr && !dcount && groups * EDGE_DEV_ROUNDS <= EDGE_GRID_MAX;
     const int km0 = split ? EDGE_DEV_ROUNDS : kmax;
-    unsigned nb = (unsigned)std::min<int64_t>(groups * km0, (int64_t)1 << 30);
-    const bool loop = !split && (dkmax != nullptr || (max_blocks && nb > max_blocks));
-    if (!split && max_blocks && nb > max_blocks) nb = max_blocks;   // grid-stride (gated launches)
+    const int64_t nb_full = groups * (int64_t)km0;
+    const bool loop = !split && (dkmax != nullptr || (max_blocks && nb_full > max_blocks) || nb_full > EDGE_GRID_MAX);
+    const unsigned nb = (unsigned)(loop ? std::min<int64_t>(nb_full, max_blocks ? max_blocks : EDGE_LOOP_BLOCKS)
+                                        : nb_full);
     const unsigned nb_rest = (unsigned)std::min<int64_t>(groups * 4, max_blocks ? max_blocks : 8192);
     const dim3 b(VBLOCK);
     const int ps = prof_begin(c, s);

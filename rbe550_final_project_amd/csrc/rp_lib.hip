@@ -446,11 +446,21 @@ void launch_edges_ml(rp_ctx* c, const double* from, const double* to, const int*
                            group, gfail, c->counter.p, c->d_scene, dcount, per_item, dkmax, sr);
 }
 
+// rounds per group the loop-free kernel covers in a connect launch before one wave per
+// group takes the rest (RBE_EDGE_CONN_ROUNDS; 0: every round loop-free)
+int conn_rounds() {
+    static const int r = [] {
+        const char* e = std::getenv("RBE_EDGE_CONN_ROUNDS");
+        return e && *e ? std::max(0, std::atoi(e)) : 0;
+    }();
+    return r;
+}
+
 // sr: the straight edge riding along (rp_plan's first front; lane-group kernels only)
 void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd, int64_t n, int kmax,
                   int mode, uint8_t* valid, int group, int* gfail, hipStream_t s, const int* dcount = nullptr,
                   int per_item = 1, unsigned max_blocks = 0, const int* dkmax = nullptr, int64_t expect = 0,
-                  const StraightRide* sr = nullptr, bool front = false) {
+                  const StraightRide* sr = nullptr, bool front = false, int rounds_first = 0) {
     if (n <= 0) return;
     const int64_t threads = n * (int64_t)kmax;   // (dkmax: kmax is only the grid's size hint)
     StraightRide none{};
@@ -487,12 +497,18 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
     constexpr int64_t EDGE_GRID_MAX = (int64_t)1 << 24, EDGE_LOOP_BLOCKS = 65536;
     const int64_t groups = (n + VBLOCK - 1) / VBLOCK;
     const bool split = dkmax != nullptr && !dcount && groups * EDGE_DEV_ROUNDS <= EDGE_GRID_MAX;
-    const int km0 = split ? EDGE_DEV_ROUNDS : kmax;
+    // rounds_first (connect launches: groups of a few chain steps): the loop-free kernel
+    // over the first rounds_first rounds, then one wave per group for the rest
+    const bool first = !split && !dkmax && rounds_first > 0 && rounds_first < kmax &&
+                       !(max_blocks && groups * (int64_t)rounds_first > max_blocks);
+    const int km0 = split ? EDGE_DEV_ROUNDS : first ? rounds_first : kmax;
     const int64_t nb_full = groups * (int64_t)km0;
-    const bool loop = !split && (dkmax != nullptr || (max_blocks && nb_full > max_blocks) || nb_full > EDGE_GRID_MAX);
+    const bool loop = !split && !first &&
+                      (dkmax != nullptr || (max_blocks && nb_full > max_blocks) || nb_full > EDGE_GRID_MAX);
     const unsigned nb = (unsigned)(loop ? std::min<int64_t>(nb_full, max_blocks ? max_blocks : EDGE_LOOP_BLOCKS)
                                         : nb_full);
     const unsigned nb_rest = (unsigned)std::min<int64_t>(groups * 4, max_blocks ? max_blocks : 8192);
+    const unsigned nb_first = (unsigned)std::min<int64_t>(groups, EDGE_LOOP_BLOCKS);   // (one wave per group)
     const dim3 b(VBLOCK);
     const int ps = prof_begin(c, s);
     // (the reference's robot base folded in as a constant, as for k_validity)
@@ -509,6 +525,9 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
         if (split) {                                                                      \
             RP_EDGES_L(N, false, nb, km0, nullptr, 0);                                    \
             RP_EDGES_L(N, true, nb_rest, km0, dkmax, EDGE_DEV_ROUNDS);                    \
+        } else if (first) {                                                               \
+            RP_EDGES_L(N, false, nb, km0, nullptr, 0);                                    \
+            RP_EDGES_L(N, true, nb_first, km0 + 1, nullptr, km0);                         \
         } else if (loop) RP_EDGES_L(N, true, nb, kmax, dkmax, 0);                         \
         else RP_EDGES_L(N, false, nb, kmax, dkmax, 0);                                    \
     } while (0)
@@ -1811,7 +1830,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                                     cmax, c->gfail.p, c->stream, status, cmax);
             else
                 launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, C * cmax, kmax, a_start ? 1 : 0, c->valid.p, cmax,
-                             c->gfail.p, c->stream, status, cmax);
+                             c->gfail.p, c->stream, status, cmax, 0, nullptr, 0, nullptr, false, conn_rounds());
             debug_wait(c, "conn edges");
             if (fused) {
 #define RP_CONN_SMALL(IT)                                                                                        \

@@ -2370,8 +2370,9 @@ int rp_check_edges_device(rp_ctx* c, const double* qa, const double* qb, int64_t
     hipLaunchKernelGGL(k_edge_prep, dim3((unsigned)std::min<int64_t>(blocks_for(n, 256), EDGE_PREP_BLOCKS)), dim3(256), 0, s, qa, qb, n, res, c->end_nd.p, out,
                        c->scalar.p);
     HIP_TRY(hipGetLastError());
-    // fully asynchronous: the slot count (the longest edge's) stays on the device and
-    // a fixed grid strides over n x kmax (no host read-back, no stream wait)
+    // fully asynchronous: the slot count (the longest edge's) stays on the device (no
+    // host read-back, no stream wait): the loop-free kernel covers every group's first
+    // EDGE_DEV_ROUNDS rounds and a fixed grid strides over the rest (launch_edges)
     launch_edges(c, qa, qb, c->end_nd.p, n, 16, 0, out, 1, nullptr, s, nullptr, 1, 8192, c->scalar.p);
     return RP_OK;
     RP_GUARD_END(c)

@@ -169,6 +169,49 @@ def run_plan_path(ctx, wl, seed, straight_first=True):
     return times, states, statuses, {k: round(float(np.median(v)), 4) for k, v in parts.items()}
 
 
+def run_plan_path_devices(devices, seeds=(1, 2, 3, 4)):
+    """The C5 covered-well queries (131,072-sample iterations) through
+    PlannerInterface.plan_path with planning.configure(devices=devices): one process,
+    one context per device, one rank group (rp_group_init_local: RCCL between distinct
+    GPUs, the in-process shared segment when a device repeats). Per query wall time
+    (ms) of the whole call; one untimed warm-up query first."""
+    import contextlib
+    import io
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import mock_genesis as M
+    from rbe550_final_project_amd import planning
+    q = load_workload("clutter64_well")["queries"][0]
+    sc = scenes.Scene.from_json(q["scene"])
+    sim = M.Scene(sc.boxes)
+    times, statuses, states, info = [], [], 0, None
+    sink = io.StringIO()
+    try:
+        planning.configure(seed=seeds[0], batch=C5_BATCH, batch_min=C5_BATCH, straight_first=False,
+                           tree_capacity=1 << 23, devices=devices)
+        pi = planning.PlannerInterface(sim.robot, sim)
+        for k in range(len(seeds) + 1):
+            if k == 1:
+                planning.configure(seed=seeds[0])   # the timed queries: seeds[0], seeds[0] + 1, ...
+            with contextlib.redirect_stdout(sink):
+                t0 = time.perf_counter()
+                wps = pi.plan_path(qpos_goal=np.array(q["goal"]), qpos_start=np.array(q["start"]),
+                                   num_waypoints=150, timeout=10.0)
+                dt = 1e3 * (time.perf_counter() - t0)
+            sink.seek(0)
+            sink.truncate()
+            assert len(wps) == 150
+            if k > 0:
+                times.append(dt)
+                statuses.append(pi.last_status)
+                states += int(pi.last_stats["states_checked"])
+        info = [c.group_info() for c in pi._ctxs]
+        for c in pi._ctxs:
+            c.close()
+    finally:
+        planning.configure(seed=0, batch=4096, batch_min=0, straight_first=True, tree_capacity=0, devices=())
+    return times, states, statuses, info
+
+
 def max_over_ranks(x, dev, distributed):
     """max of a float over the ranks (device tensor on RCCL, host tensor on gloo)"""
     if not distributed:
@@ -508,6 +551,23 @@ def main():
                 plan[key] = plan_record(tq, sq, stq, batch, dev, distributed, extra)
             except Exception as ex:
                 plan[key] = {"error": repr(ex)[:300]}
+        # multi-GPU through the reference's own API in ONE process (the drop-in with
+        # planning.configure(devices=...)): every visible GPU, or two contexts on the
+        # one GPU of a single-GPU box (a rehearsal of the group: both share the chip)
+        if not distributed:
+            ndev = torch.cuda.device_count()
+            devs = tuple(range(ndev)) if ndev > 1 else (0, 0)
+            for key, dv in (("C5_well_plan_path", (local,)), ("C5_well_plan_path_devices", devs)):
+                try:
+                    tq, sq, stq, info = run_plan_path_devices(dv)
+                    plan[key] = plan_record(tq, sq, stq, C5_BATCH, dev, distributed, {
+                        "mode": "PlannerInterface.plan_path(qpos_goal, qpos_start, num_waypoints=150, timeout=10.0) "
+                                "through tests/mock_genesis.py, covered-well query, seeds 1-4, 131,072-sample "
+                                "iterations, planning.configure(devices=...)",
+                        "devices": list(dv), "ranks": info,
+                        "shares_gpu": len(set(dv)) < len(dv)})
+                except Exception as ex:
+                    plan[key] = {"error": repr(ex)[:300]}
         if group is not None:   # every rank done with the group's segment / communicator
             dist.barrier()
             group.leave()

@@ -5,8 +5,10 @@
  * What each entry point replaces in the reference (paths relative to /root/reference):
  *
  *   rp_create / rp_destroy      PlannerInterface.__init__ + _ensure_adapter      code/planning.py:14-30
- *   rp_set_scene                the Genesis scene the collider sees (plane, boxes,
- *                               raised robot base)                                code/scenes.py:29-34,49-85
+ *   rp_set_scene(_rot, _poses)  the Genesis scene the collider sees (plane, boxes
+ *                               at their poses, upright or toppled, raised robot
+ *                               base)                                             code/scenes.py:29-34,49-85,
+ *                                                                                 code/planning.py:211
  *   rp_set_attached             self.attached_object + the exemption of
  *                               collision_with_attached_object                    code/planning.py:153,221-230
  *   rp_check_states(_device)    _is_ompl_state_valid: set_qpos (FK) +
@@ -105,6 +107,16 @@ typedef struct rp_box {
     float yaw;
 } rp_box;
 
+/* Box obstacle with a full orientation: quaternion (w, x, y, z), the order of
+ * Genesis entity.get_quat(). A block that toppled or leans (goal3's "Stack
+ * collapsed! ... TAMP will re-plan", code/goal3_tallest.py:257) is tilted; x = y = 0
+ * is an upright box of yaw atan2(2(wz + xy), 1 - 2(y^2 + z^2)). */
+typedef struct rp_box_rot {
+    float center[3];
+    float half[3];
+    double quat[4];
+} rp_box_rot;
+
 /* rp_plan parameters. Zero / negative fields take the default shown. */
 typedef struct rp_plan_params {
     uint64_t seed;          /* Philox key; the reference is unseeded (scenes.py:9)          */
@@ -115,7 +127,12 @@ typedef struct rp_plan_params {
                                queries: 0.083 -> 0.072 ms vs 256, tools/plan_sweep.py)   */
     double range;           /* steering distance, default 0.2 * maxExtent (OMPL RRTConnect) */
     double resolution;      /* edge resolution, default 0.01 * maxExtent (OMPL default)     */
-    double timeout_s;       /* wall-clock budget of the solve, default 5.0 (planning.py:63) */
+    double timeout_s;       /* wall-clock budget of the solve, default 5.0 (planning.py:63);
+                               checked once per iteration, so a plan can overrun it by its
+                               last iteration. Rank groups: an iteration that opens
+                               replicated (see group_repl) only learns of a timeout at the
+                               next vote, up to RP_GROUP_VOTE_EVERY - 1 iterations later
+                               (the oracle applies the same rule)                          */
     int64_t max_iters;      /* iteration cap (deterministic tests), default unlimited        */
     int32_t n_waypoints;    /* path.interpolate(n) (planning.py:198), default 100; 0 = none */
     int32_t simplify;       /* smooth_path (planning.py:195-196): 0 = off; 1 = simplifyMax
@@ -206,6 +223,14 @@ typedef int (*rp_allgather_fn)(void* user, const void* send, void* recv, int64_t
 /* Library identity: returns a static string ("librbe_mi355x <version> gfx950"). */
 const char* rp_version(void);
 
+/* Layout version of the structs above (rp_plan_params, rp_box_rot, rp_stats, ...):
+ * bumped whenever one of them changes size or meaning (the structs carry no size
+ * field). A client checks rp_abi_version() == RP_ABI_VERSION once, before passing
+ * any struct (native.py load() does); a mismatch means the header and the library
+ * disagree and no call may be made. Version 5: rp_box_rot / rp_set_scene_rot. */
+#define RP_ABI_VERSION 5
+int rp_abi_version(void);
+
 /* Fill `out` with the built-in Franka Panda capsule model (spec/franka_capsules.json). */
 int rp_default_robot(rp_robot_desc* out);
 
@@ -223,17 +248,25 @@ void rp_destroy(rp_ctx* ctx);
 int rp_set_scene(rp_ctx* ctx, const rp_box* boxes, int32_t n_boxes, float plane_z,
                  const float base_pos[3]);
 
+/* rp_set_scene with full box orientations (the Genesis collider sees every box at
+ * its simulated pose, code/planning.py:211). A box with quat x = y = 0 gets exactly
+ * the record rp_set_scene makes for its yaw; any other box is tilted: the quaternion
+ * is normalised and turned into a rotation matrix in double, rounded to float once,
+ * and the collider tests the capsules against the rotated box (world AABB padded by
+ * 1e-6 m). RP_ERR_ARG for a zero quaternion. */
+int rp_set_scene_rot(rp_ctx* ctx, const rp_box_rot* boxes, int32_t n_boxes, float plane_z,
+                     const float base_pos[3]);
+
 /* Attached object (planning.py:221-230): contacts between box `box_index` and the
  * links set in `exempt_link_mask` (bit = 1 << RP_LINK*) are ignored.
  * box_index = -1 clears. The reference exempts hand | left_finger | right_finger. */
 int rp_set_attached(rp_ctx* ctx, int32_t box_index, uint32_t exempt_link_mask);
 
-/* rp_set_scene + rp_set_attached from the simulator's poses in one call (the
+/* rp_set_scene_rot + rp_set_attached from the simulator's poses in one call (the
  * drop-in planning.py's per-query scene ingestion): box j at position
- * poses[7j .. 7j+2] with orientation quaternion (w, x, y, z) = poses[7j+3 .. 7j+6],
- * half extents halves[3j .. 3j+2]; its yaw is atan2(2(wz + xy), 1 - 2(y^2 + z^2))
- * in double (tilt ignored), then every value is rounded to float once, as
- * rp_set_scene's records. base_pos: the robot base (double). */
+ * poses[7j .. 7j+2] (rounded to float) with orientation quaternion (w, x, y, z) =
+ * poses[7j+3 .. 7j+6] (upright or tilted, as rp_set_scene_rot), half extents
+ * halves[3j .. 3j+2]. base_pos: the robot base (double). */
 int rp_set_scene_poses(rp_ctx* ctx, const double* poses, const float* halves, int32_t n_boxes,
                        float plane_z, const double base_pos[3], int32_t attached_box,
                        uint32_t exempt_link_mask);
@@ -329,6 +362,18 @@ int rp_group_init(rp_ctx* ctx, int32_t rank, int32_t world, rp_allgather_fn fn, 
  * every rank's records from it (no copies, no callback). */
 int rp_group_init_shm(rp_ctx* ctx, int32_t rank, int32_t world, void* base, int64_t bytes);
 int rp_group_rccl_unique_id(uint8_t id_out[RP_RCCL_ID_BYTES]);
+/* rp_group_init_local: a rank group of `world` contexts of ONE process (the drop-in
+ * PlannerInterface with planning.configure(devices=[...]): the reference drives one
+ * planner from one process, code/motion_primitives.py:38, planning.py:121-122).
+ * ctxs[r] becomes rank r. transport RP_TRANSPORT_RCCL: one communicator per context
+ * from ncclCommInitAll over their devices (must be distinct; xGMI between the GPUs);
+ * RP_TRANSPORT_SHM: a pinned host segment of `bytes` bytes (0: 64 MiB) that the
+ * library allocates and every context reads and writes in place (contexts may share
+ * a device); RP_TRANSPORT_NONE: RCCL when the devices are distinct, else SHM.
+ * Each context plans from its own thread (rp_plan_async on every rank, then
+ * rp_plan_wait on every rank); world 1 returns the context to single-rank planning.
+ * The segment is freed when the last context leaves the group. */
+int rp_group_init_local(rp_ctx* const* ctxs, int32_t world, int32_t transport, int64_t bytes);
 int rp_group_init_rccl(rp_ctx* ctx, int32_t rank, int32_t world, const uint8_t id[RP_RCCL_ID_BYTES]);
 
 /* What the context's rank group is, as its transport sees it: for RCCL the

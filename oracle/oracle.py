@@ -32,6 +32,8 @@ def lib():
         L.ro_scene_create.argtypes = [C.POINTER(_abi.RobotDesc)]
         L.ro_scene_destroy.argtypes = [C.c_void_p]
         L.ro_scene_set.argtypes = [C.c_void_p, C.POINTER(_abi.Box), C.c_int32, C.c_float, C.POINTER(C.c_float)]
+        L.ro_scene_set_rot.argtypes = [C.c_void_p, C.POINTER(_abi.BoxRot), C.c_int32, C.c_float,
+                                       C.POINTER(C.c_float)]
         L.ro_scene_set_attached.argtypes = [C.c_void_p, C.c_int32, C.c_uint32]
         L.ro_state_valid.argtypes = [C.c_void_p, C.POINTER(C.c_float)]
         L.ro_check_states.restype = C.c_int64
@@ -85,9 +87,12 @@ class OracleScene:
             self.h = None
 
     def set_scene(self, boxes, plane_z=0.0, base=(0.0, 0.0, 0.01)):
-        arr, n = _abi.make_boxes(boxes)
+        """The same dispatch as native.Context.set_scene: upright boxes -> ro_scene_set,
+        any tilted box -> ro_scene_set_rot with every box as a quaternion."""
+        kind, arr, n = _abi.scene_boxes(boxes)
         b = (C.c_float * 3)(*base)
-        rc = lib().ro_scene_set(self.h, arr, n, float(plane_z), b)
+        fn = lib().ro_scene_set_rot if kind == "rot" else lib().ro_scene_set
+        rc = fn(self.h, arr, n, float(plane_z), b)
         if rc:
             raise ValueError(f"ro_scene_set rc={rc}")
 

@@ -31,6 +31,8 @@ struct ro_scene {
     int nbox;
     float box_c[RP_MAX_BOXES][3], box_h[RP_MAX_BOXES][3], box_cs[RP_MAX_BOXES], box_sn[RP_MAX_BOXES];
     float box_lo[RP_MAX_BOXES][3], box_hi[RP_MAX_BOXES][3];
+    int box_tilt[RP_MAX_BOXES];          /* 1: box_rt holds R^T rows (rp_set_scene_rot) */
+    float box_rt[RP_MAX_BOXES][9];
     uint32_t box_exempt[RP_MAX_BOXES];   /* capsule bits */
     float plane_z;
     float base[3];
@@ -86,6 +88,7 @@ int ro_scene_set(ro_scene* s, const rp_box* boxes, int32_t n, float plane_z, con
         }
         s->box_cs[j] = cs;
         s->box_sn[j] = sn;
+        s->box_tilt[j] = 0;
         s->box_exempt[j] = 0;
     }
     s->plane_z = plane_z;
@@ -93,6 +96,54 @@ int ro_scene_set(ro_scene* s, const rp_box* boxes, int32_t n, float plane_z, con
         s->base[0] = base[0];
         s->base[1] = base[1];
         s->base[2] = base[2];
+    }
+    return RP_OK;
+}
+
+/* Boxes with orientation quaternions (w, x, y, z): the product's rp_set_scene_rot
+ * restated. x = y = 0 is an upright box of yaw atan2(2(wz + xy), 1 - 2(y^2 + z^2));
+ * any other box is tilted: the normalised quaternion's rotation matrix R (world =
+ * R * box) in double, rounded to float once; the box frame of a world point p is
+ * R^T (p - c); world AABB half extents |R_k0| h0 + |R_k1| h1 + |R_k2| h2 + 1e-6. A
+ * toppled block is what goal3's collapse check re-plans around
+ * (code/goal3_tallest.py:257); Genesis' collider sees every box at its pose
+ * (code/planning.py:211). */
+int ro_scene_set_rot(ro_scene* s, const rp_box_rot* boxes, int32_t n, float plane_z, const float base[3]) {
+    if (!s || n < 0 || n > RP_MAX_BOXES || (n > 0 && !boxes)) return RP_ERR_ARG;
+    rp_box up[RP_MAX_BOXES];
+    memset(up, 0, sizeof up);
+    for (int j = 0; j < n; ++j) {
+        const rp_box_rot* b = &boxes[j];
+        for (int k = 0; k < 3; ++k) { up[j].center[k] = b->center[k]; up[j].half[k] = b->half[k]; }
+        double w = b->quat[0], x = b->quat[1], y = b->quat[2], z = b->quat[3];
+        if (x == 0.0 && y == 0.0 && w == 0.0 && z == 0.0) return RP_ERR_ARG;
+        up[j].yaw = (float)atan2(2.0 * (w * z + x * y), 1.0 - 2.0 * (y * y + z * z));
+    }
+    int rc = ro_scene_set(s, up, n, plane_z, base);
+    if (rc) return rc;
+    for (int j = 0; j < n; ++j) {
+        const rp_box_rot* b = &boxes[j];
+        double w = b->quat[0], x = b->quat[1], y = b->quat[2], z = b->quat[3];
+        if (x == 0.0 && y == 0.0) continue;
+        double nrm = sqrt(w * w + x * x + y * y + z * z);
+        w /= nrm; x /= nrm; y /= nrm; z /= nrm;
+        double R[3][3] = {{1.0 - 2.0 * (y * y + z * z), 2.0 * (x * y - w * z), 2.0 * (x * z + w * y)},
+                          {2.0 * (x * y + w * z), 1.0 - 2.0 * (x * x + z * z), 2.0 * (y * z - w * x)},
+                          {2.0 * (x * z - w * y), 2.0 * (y * z + w * x), 1.0 - 2.0 * (x * x + y * y)}};
+        float Rf[3][3];
+        for (int r = 0; r < 3; ++r)
+            for (int k = 0; k < 3; ++k) Rf[r][k] = (float)R[r][k];
+        for (int i = 0; i < 3; ++i)
+            for (int k = 0; k < 3; ++k) s->box_rt[j][3 * i + k] = Rf[k][i];
+        for (int k = 0; k < 3; ++k) {
+            float ext = fabsf(Rf[k][0]) * b->half[0] + fabsf(Rf[k][1]) * b->half[1] + fabsf(Rf[k][2]) * b->half[2] +
+                        1e-6f;
+            s->box_lo[j][k] = b->center[k] - ext;
+            s->box_hi[j][k] = b->center[k] + ext;
+        }
+        s->box_cs[j] = 0.0f;
+        s->box_sn[j] = 0.0f;
+        s->box_tilt[j] = 1;
     }
     return RP_OK;
 }
@@ -314,15 +365,27 @@ static float seg_seg_d2(v3 a1, v3 b1, v3 a2, v3 b2) {
     return dot(dd, dd);
 }
 
+/* world point P in the frame of box j: rotation by -yaw about z (upright), or
+ * R^T (P - c) with rows rt (tilted): o_i = fma(rt_i2, dz, fma(rt_i1, dy, rt_i0 dx)) */
+static void box_frame(const ro_scene* s, int j, v3 P, float o[3]) {
+    const float dx = P.x - s->box_c[j][0], dy = P.y - s->box_c[j][1], dz = P.z - s->box_c[j][2];
+    if (s->box_tilt[j]) {
+        const float* rt = s->box_rt[j];
+        for (int i = 0; i < 3; ++i) o[i] = fmaf(rt[3 * i + 2], dz, fmaf(rt[3 * i + 1], dy, rt[3 * i] * dx));
+    } else {
+        const float cs = s->box_cs[j], sn = s->box_sn[j];
+        o[0] = fmaf(cs, dx, sn * dy);
+        o[1] = fmaf(cs, dy, -(sn * dx));
+        o[2] = dz;
+    }
+}
+
 static int cap_vs_box(const ro_scene* s, int c, v3 A, v3 B, const aabb* u, int j) {
     if ((s->box_exempt[j] >> c) & 1u) return 0;
     if (disjoint(u, s->box_lo[j], s->box_hi[j])) return 0;
-    const float cs = s->box_cs[j], sn = s->box_sn[j];
     float pa[3], pb[3];
-    float dx = A.x - s->box_c[j][0], dy = A.y - s->box_c[j][1], dz = A.z - s->box_c[j][2];
-    pa[0] = fmaf(cs, dx, sn * dy); pa[1] = fmaf(cs, dy, -(sn * dx)); pa[2] = dz;
-    dx = B.x - s->box_c[j][0]; dy = B.y - s->box_c[j][1]; dz = B.z - s->box_c[j][2];
-    pb[0] = fmaf(cs, dx, sn * dy); pb[1] = fmaf(cs, dy, -(sn * dx)); pb[2] = dz;
+    box_frame(s, j, A, pa);
+    box_frame(s, j, B, pb);
     const float r = s->cap_r[c];
     return seg_box_d2(pa, pb, s->box_h[j]) <= r * r;
 }

@@ -39,6 +39,8 @@ ro_scene* ro_scene_create(const rp_robot_desc* robot);
 void ro_scene_destroy(ro_scene* s);
 int ro_scene_set(ro_scene* s, const rp_box* boxes, int32_t n_boxes, float plane_z,
                  const float base_pos[3]);
+int ro_scene_set_rot(ro_scene* s, const rp_box_rot* boxes, int32_t n_boxes, float plane_z,
+                     const float base_pos[3]);
 int ro_scene_set_attached(ro_scene* s, int32_t box_index, uint32_t exempt_link_mask);
 
 /* 1 = valid (collision free). */

@@ -1,6 +1,8 @@
 """ctypes mirrors of the C-ABI structs in include/rbe_planner.h (plain data only)."""
 import ctypes as C
+import math
 
+ABI_VERSION = 5   # RP_ABI_VERSION of include/rbe_planner.h these mirrors follow
 NQ = 9
 MAX_CAPSULES = 32
 MAX_SELF_PAIRS = 64
@@ -32,6 +34,11 @@ class RobotDesc(C.Structure):
 
 class Box(C.Structure):
     _fields_ = [("center", C.c_float * 3), ("half", C.c_float * 3), ("yaw", C.c_float)]
+
+
+class BoxRot(C.Structure):
+    """rp_box_rot: orientation quaternion (w, x, y, z) in double."""
+    _fields_ = [("center", C.c_float * 3), ("half", C.c_float * 3), ("quat", C.c_double * 4)]
 
 
 class PlanParams(C.Structure):
@@ -80,8 +87,21 @@ class Profile(C.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+def is_quat(rot):
+    """A box orientation is a yaw (number) or a quaternion (w, x, y, z)."""
+    return hasattr(rot, "__len__") and len(rot) == 4
+
+
+def quat_of(rot):
+    """Quaternion (w, x, y, z) of a box orientation (a yaw is a rotation about z)."""
+    if is_quat(rot):
+        return tuple(float(v) for v in rot)
+    y = float(rot)
+    return (math.cos(0.5 * y), 0.0, 0.0, math.sin(0.5 * y))
+
+
 def make_boxes(boxes):
-    """boxes: iterable of (center(3), half(3), yaw) -> ctypes array."""
+    """boxes: iterable of (center(3), half(3), yaw) -> ctypes rp_box array."""
     boxes = list(boxes)
     arr = (Box * max(1, len(boxes)))()
     for i, (c, h, yaw) in enumerate(boxes):
@@ -91,10 +111,32 @@ def make_boxes(boxes):
     return arr, len(boxes)
 
 
-def set_params(p, seed, batch, timeout_s, n_waypoints, simplify, tree_capacity, straight_first):
+def make_boxes_rot(boxes):
+    """boxes: iterable of (center(3), half(3), yaw or quaternion) -> ctypes rp_box_rot array."""
+    boxes = list(boxes)
+    arr = (BoxRot * max(1, len(boxes)))()
+    for i, (c, h, rot) in enumerate(boxes):
+        arr[i].center[:] = [float(v) for v in c]
+        arr[i].half[:] = [float(v) for v in h]
+        arr[i].quat[:] = list(quat_of(rot))
+    return arr, len(boxes)
+
+
+def scene_boxes(boxes):
+    """The records of a scene's boxes for the library / the oracle: ("yaw", rp_box
+    array, n) when every box is upright (rp_set_scene), else ("rot", rp_box_rot array,
+    n) with every box as a quaternion (rp_set_scene_rot)."""
+    boxes = list(boxes)
+    if any(is_quat(b[2]) for b in boxes):
+        return ("rot",) + make_boxes_rot(boxes)
+    return ("yaw",) + make_boxes(boxes)
+
+
+def set_params(p, seed, batch, timeout_s, n_waypoints, simplify, tree_capacity, straight_first, batch_min=0):
     """Refill the per-query fields of a reused PlanParams (planning.plan_path)."""
     p.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
     p.batch = int(batch)
+    p.batch_min = int(batch_min)
     p.timeout_s = float(timeout_s)
     p.n_waypoints = int(n_waypoints or 0)
     p.simplify = 1 if simplify else 0

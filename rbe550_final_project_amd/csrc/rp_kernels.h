@@ -2316,7 +2316,7 @@ __device__ void contacts_caps(const Capsules& k, const DevScene* sc, int32_t* ou
             const float* bx = sc->box[j];
             if ((__float_as_uint(bx[14]) >> C) & 1u) continue;
             if (aabb_disjoint(u, bx + 8, bx + 11)) continue;
-            if (capsule_box_narrow(k.a[C], k.b[C], r, bx)) {
+            if (capsule_box_narrow(k.a[C], k.b[C], r, bx, sc->rot[j])) {
                 if (n < cap) { out[2 * n] = CAP_LINK[C]; out[2 * n + 1] = __float_as_int(bx[15]); }
                 ++n;
             }

@@ -6,6 +6,8 @@
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <rccl/rccl.h>
+#include <sys/prctl.h>
+#include <time.h>
 
 #include <algorithm>
 #include <array>
@@ -17,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -104,6 +107,15 @@ struct Tree {
     void release() { q.release(); par.release(); cand.release(); img.release(); }
 };
 
+// in-process shared-memory segment of rp_group_init_local (hipHostMalloc'd,
+// portable and mapped: every context of the process reads and writes it in place)
+struct LocalSeg {
+    void* p = nullptr;
+    ~LocalSeg() {
+        if (p) (void)hipHostFree(p);
+    }
+};
+
 // rp_plan_async / rp_plan_wait: one query handed to the context's planner thread
 struct PlanJob {
     double start[RP_NQ], goal[RP_NQ], lo[RP_NQ], hi[RP_NQ];
@@ -120,9 +132,11 @@ struct PlanWorker {
     std::thread th;
     std::atomic<int> state{IDLE};
     std::mutex m;
-    std::condition_variable cv;
+    std::condition_variable cv;        // the thread sleeps on it between queries
+    std::condition_variable done_cv;   // rp_plan_wait sleeps on it past its spin
     PlanJob job{};
     double spin_s = 0.005;   // after a query the thread spins this long before it sleeps
+    double wait_spin_s = 50e-6;   // rp_plan_wait spins this long, then blocks on done_cv
 };
 
 struct rp_ctx {
@@ -204,6 +218,9 @@ struct rp_ctx {
     // kernels write / read the records in place
     char* shm = nullptr;
     char* shm_dev = nullptr;
+    // rp_group_init_local's in-process segment (pinned by the library, shared by the
+    // group's contexts, freed with the last one); null for a caller's POSIX segment
+    std::shared_ptr<LocalSeg> local_seg;
     int64_t shm_bytes = 0;
     int64_t shm_k = 0;                   // exchanges done (lockstep on every rank)
     // a grouped plan that failed on this rank (an error inside the iteration loop)
@@ -225,7 +242,8 @@ struct rp_ctx {
     void leave_group() {
         if (comm) (void)ncclCommDestroy(comm);
         comm = nullptr;
-        if (shm) (void)hipHostUnregister(shm);
+        if (local_seg) local_seg.reset();
+        else if (shm) (void)hipHostUnregister(shm);
         shm = shm_dev = nullptr;
         shm_bytes = shm_k = 0;
         free_staging();
@@ -1131,33 +1149,85 @@ bool nn_split(rp_ctx* c, const NnQuery& Q, int64_t n, Tree& tr, int64_t T, int32
 }
 
 // Wait for a kernel to publish `seq` into the host mirror (rp_kernels.h PlanIO).
-// Spins on the host-coherent word; polls the stream now and then so that a failed
-// or finished-without-publishing stream turns into an error instead of a hang.
+// Spins on the host-coherent word for the first wait_spin_s (the waits of a pick /
+// place query are 10-30 us: a wake-up there would cost more than the wait), then
+// sleeps between polls — quanta of 10 % of the time already waited, 10-200 us — so a
+// long query (C5-class trees, a 10 s budget: motion_primitives.py:144) does not hold
+// a host core. Polls the stream every 4096 spins / ~1 ms of sleeping, so that a failed
+// or finished-without-publishing stream turns into an error instead of a hang, and a
+// stream busy past the watchdog is reported.
+struct WaitTuning {
+    double spin_s = 40e-6, frac = 0.1;
+    WaitTuning() {
+        if (const char* e = std::getenv("RBE_WAIT_SPIN_US"); e && *e) spin_s = std::max(0.0, std::atof(e)) * 1e-6;
+        if (const char* e = std::getenv("RBE_WAIT_SLEEP_FRAC"); e && *e) frac = std::max(0.0, std::atof(e));
+    }
+};
+const WaitTuning& wait_tuning() {
+    static const WaitTuning t;
+    return t;
+}
+// the stream check of wait_seq: true = published after all; throws on an error, a
+// stream that finished without publishing, or the watchdog
+bool wait_check(rp_ctx* c, const volatile int* f, int seq, double& t0) {
+    const hipError_t e = hipStreamQuery(c->stream);
+    if (e == hipSuccess) {
+        if (*f == seq) return true;
+        throw HipError{"plan status was not published"};
+    }
+    if (e != hipErrorNotReady) HIP_TRY(e);
+    // watchdog: a stream that stays busy this long is reported, not waited on
+    const double now = now_s();
+    if (t0 < 0) t0 = now;
+    if (now - t0 > c->watchdog_s) {
+        char b[256];
+        snprintf(b, sizeof b, "plan stream still busy after %.0f s (awaiting status %d, mirror at %d)", now - t0, seq,
+                 *f);
+        throw HipError{b};
+    }
+    return false;
+}
+// restores this thread's timer slack when the wait ends (also by an exception)
+struct SlackGuard {
+    long old = -1;
+    void fine() {   // 1 us: the sleeps end when asked (default slack 50 us)
+        if (old >= 0) return;
+        old = prctl(PR_GET_TIMERSLACK, 0, 0, 0, 0);
+        if (old < 0) old = 50000;
+        prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
+    }
+    ~SlackGuard() {
+        if (old >= 0) prctl(PR_SET_TIMERSLACK, (unsigned long)old, 0, 0, 0);
+    }
+};
 void wait_seq(rp_ctx* c, int seq) {
     const volatile int* f = &c->h_io->seq;
+    const WaitTuning& wt = wait_tuning();
     double t0 = -1.0;
-    for (uint64_t spin = 1;; ++spin) {
-        if (*f == seq) break;
-        if ((spin & 4095) == 0) {
-            const hipError_t e = hipStreamQuery(c->stream);
-            if (e == hipSuccess) {
-                if (*f == seq) break;
-                throw HipError{"plan status was not published"};
-            }
-            if (e != hipErrorNotReady) HIP_TRY(e);
-            // watchdog: a stream that stays busy this long is reported, not waited on
-            const double now = now_s();
-            if (t0 < 0) t0 = now;
-            if (now - t0 > c->watchdog_s) {
-                char b[256];
-                snprintf(b, sizeof b, "plan stream still busy after %.0f s (awaiting status %d, mirror at %d)",
-                         now - t0, seq, *f);
-                throw HipError{b};
-            }
+    const double t_enter = now_s();
+    for (uint64_t spin = 1;; ++spin) {   // spin
+        if (*f == seq) {
+            __atomic_thread_fence(__ATOMIC_ACQUIRE);
+            return;
         }
+        if ((spin & 4095) == 0 && wait_check(c, f, seq, t0)) break;
+        if ((spin & 63) == 0 && now_s() - t_enter > wt.spin_s) break;
 #if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
         __builtin_ia32_pause();
 #endif
+    }
+    SlackGuard slack;
+    double last_check = now_s();
+    while (*f != seq) {   // sleep between polls
+        const double now = now_s();
+        if (now - last_check > 1e-3) {
+            if (wait_check(c, f, seq, t0)) break;
+            last_check = now;
+        }
+        slack.fine();
+        const int64_t ns = std::min<int64_t>(200000, std::max<int64_t>(10000, (int64_t)((now - t_enter) * wt.frac * 1e9)));
+        const timespec ts{0, (long)ns};
+        nanosleep(&ts, nullptr);
     }
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
 }
@@ -1170,8 +1240,13 @@ void wait_seq(rp_ctx* c, int seq) {
 // `cap` nodes (plan_impl; rp_reserve sizes it ahead of the first query, so no
 // hipMalloc / hipFree, which synchronise the device, lands inside a timed plan).
 // Buffers only grow.
-void plan_workspace(rp_ctx* c, int64_t BMAX, int world, int cmax, int64_t cap, bool grouped) {
+// repl: a rank group's replicated sub-batches run the single-rank kernels on up to
+// min(BMAX, repl) samples, whose two-phase connect launches write cmax edges per
+// sample (sized for the sharded slice only, a group_repl above FUSE_MAX
+// overran the edge buffers)
+void plan_workspace(rp_ctx* c, int64_t BMAX, int world, int cmax, int64_t cap, bool grouped, int64_t repl) {
     const int64_t PMAX = BMAX / world;
+    const int64_t RMAX = grouped ? std::min(BMAX, repl) : 0;
     for (auto& t : c->tree) {
         t.q.ensure((size_t)cap * NQ);
         t.par.ensure(cap);
@@ -1179,7 +1254,8 @@ void plan_workspace(rp_ctx* c, int64_t BMAX, int world, int cmax, int64_t cap, b
     }
     const int64_t ne = std::max<int64_t>({PMAX + 2, ((BMAX + world - 1) / world) * cmax, (int64_t)SPMAX * SPMAX / 2,
                                           (std::min<int64_t>(BMAX, FUSE_MAX) + 2) * (cmax + 1),
-                                          grouped ? (PMAX + 2) * (cmax + 1) : 0});
+                                          grouped ? (PMAX + 2) * (cmax + 1) : 0,
+                                          RMAX > 0 ? std::max(RMAX + 2, RMAX * cmax) : 0});
     c->efrom.ensure(ne * NQ);
     c->eto.ensure(ne * NQ);
     c->nd.ensure(ne);
@@ -1274,7 +1350,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
 
     // workspace
     const int64_t cap = p.tree_capacity;
-    plan_workspace(c, BMAX, world, cmax, cap, grouped);
+    plan_workspace(c, BMAX, world, cmax, cap, grouped, repl);
     for (auto& t : c->tree) {
         t.n = 0;
         t.n_img = 0;
@@ -1995,6 +2071,7 @@ bool structure_matches(const rp_robot_desc& r) {
 extern "C" {
 
 const char* rp_version(void) { return "librbe_mi355x " RP_VERSION " gfx950"; }
+int rp_abi_version(void) { return RP_ABI_VERSION; }
 
 int rp_default_robot(rp_robot_desc* out) {
     if (!out) return RP_ERR_ARG;
@@ -2116,36 +2193,111 @@ unsigned env_far_mask(const DevScene& sc, const float base[3]) {
     return mask;
 }
 
+// Box record of an upright box (rotation `yaw` about world z): cos / sin of the yaw
+// in double, rounded once; world AABB of the yawed box. (oracle: ro_scene_set)
+static void box_record_yaw(const float center[3], const float half[3], float yaw, int32_t orig, float* r) {
+    const float cs = (float)std::cos((double)yaw);
+    const float sn = (float)std::sin((double)yaw);
+    const float acs = cs < 0.0f ? -cs : cs, asn = sn < 0.0f ? -sn : sn;
+    float ext[3];
+    ext[0] = acs * half[0] + asn * half[1];
+    ext[1] = asn * half[0] + acs * half[1];
+    ext[2] = half[2];
+    for (int k = 0; k < 3; ++k) {
+        r[k] = center[k];
+        r[3 + k] = half[k];
+        r[8 + k] = center[k] - ext[k];
+        r[11 + k] = center[k] + ext[k];
+    }
+    r[6] = cs;
+    r[7] = sn;
+    r[14] = 0.0f;  // exempt bits = 0, upright
+    std::memcpy(&r[15], &orig, 4);
+}
+
+// Record of a box with orientation quaternion q = (w, x, y, z) (any norm > 0):
+// x == y == 0 (a rotation about z only, what rp_set_scene_poses always read as the
+// box's yaw) gives the upright record of yaw = atan2(2(wz + xy), 1 - 2(y^2 + z^2))
+// (double, rounded to float). Otherwise the box is tilted: q normalised and turned
+// into R (world = R * box) in double, R^T rows rounded to float once into rt, world
+// AABB half extents ext_k = |R_k0| h0 + |R_k1| h1 + |R_k2| h2 + 1e-6 m in float (the
+// margin makes the box AABB contain the float-rounded box). The oracle
+// (ro_scene_set_rot) writes the same sequence. Returns false for a zero quaternion.
+static bool box_record_quat(const float center[3], const float half[3], const double q[4], int32_t orig, float* r,
+                            float* rt) {
+    double w = q[0], x = q[1], y = q[2], z = q[3];
+    if (x == 0.0 && y == 0.0) {
+        if (w == 0.0 && z == 0.0) return false;
+        box_record_yaw(center, half, (float)std::atan2(2.0 * (w * z + x * y), 1.0 - 2.0 * (y * y + z * z)), orig, r);
+        return true;
+    }
+    const double nrm = std::sqrt(w * w + x * x + y * y + z * z);
+    w /= nrm; x /= nrm; y /= nrm; z /= nrm;
+    const double R[9] = {1.0 - 2.0 * (y * y + z * z), 2.0 * (x * y - w * z), 2.0 * (x * z + w * y),
+                         2.0 * (x * y + w * z), 1.0 - 2.0 * (x * x + z * z), 2.0 * (y * z - w * x),
+                         2.0 * (x * z - w * y), 2.0 * (y * z + w * x), 1.0 - 2.0 * (x * x + y * y)};
+    float Rf[9];
+    for (int i = 0; i < 9; ++i) Rf[i] = (float)R[i];
+    for (int i = 0; i < 3; ++i)
+        for (int k = 0; k < 3; ++k) rt[3 * i + k] = Rf[3 * k + i];   // row i of R^T = column i of R
+    for (int i = 9; i < 12; ++i) rt[i] = 0.0f;
+    for (int k = 0; k < 3; ++k) {
+        const float ext = std::fabs(Rf[3 * k]) * half[0] + std::fabs(Rf[3 * k + 1]) * half[1] +
+                          std::fabs(Rf[3 * k + 2]) * half[2] + 1e-6f;
+        r[k] = center[k];
+        r[3 + k] = half[k];
+        r[8 + k] = center[k] - ext;
+        r[11 + k] = center[k] + ext;
+    }
+    r[6] = 0.0f;
+    r[7] = 0.0f;
+    const uint32_t tilt = BOX_TILTED;
+    std::memcpy(&r[14], &tilt, 4);
+    std::memcpy(&r[15], &orig, 4);
+    return true;
+}
+
+static int scene_from_records(rp_ctx* c, std::vector<std::array<float, 16>>& rec,
+                              std::vector<std::array<float, 12>>& rot, int32_t n, float plane_z, const float base[3]);
+
 int rp_set_scene(rp_ctx* c, const rp_box* boxes, int32_t n, float plane_z, const float base[3]) {
     if (!c || n < 0 || n > MAX_BOXES || (n > 0 && !boxes)) return RP_ERR_ARG;
     RP_IDLE(c);
     RP_GUARD_BEGIN
-    HIP_TRY(hipSetDevice(c->device));
-    // box records in the caller's order (cos/sin of yaw in double, rounded once;
-    // world AABB of the yawed box)
+    // box records in the caller's order
     std::vector<std::array<float, 16>> rec(n);
+    std::vector<std::array<float, 12>> rot(n);
     for (int j = 0; j < n; ++j) {
-        const rp_box& b = boxes[j];
-        const float cs = (float)std::cos((double)b.yaw);
-        const float sn = (float)std::sin((double)b.yaw);
-        const float acs = cs < 0.0f ? -cs : cs, asn = sn < 0.0f ? -sn : sn;
-        float ext[3];
-        ext[0] = acs * b.half[0] + asn * b.half[1];
-        ext[1] = asn * b.half[0] + acs * b.half[1];
-        ext[2] = b.half[2];
-        float* r = rec[j].data();
-        for (int k = 0; k < 3; ++k) {
-            r[k] = b.center[k];
-            r[3 + k] = b.half[k];
-            r[8 + k] = b.center[k] - ext[k];
-            r[11 + k] = b.center[k] + ext[k];
-        }
-        r[6] = cs;
-        r[7] = sn;
-        r[14] = 0.0f;  // exempt bits = 0
-        int32_t orig = j;
-        std::memcpy(&r[15], &orig, 4);
+        box_record_yaw(boxes[j].center, boxes[j].half, boxes[j].yaw, j, rec[j].data());
+        rot[j].fill(0.0f);
     }
+    return scene_from_records(c, rec, rot, n, plane_z, base);
+    RP_GUARD_END(c)
+}
+
+int rp_set_scene_rot(rp_ctx* c, const rp_box_rot* boxes, int32_t n, float plane_z, const float base[3]) {
+    if (!c || n < 0 || n > MAX_BOXES || (n > 0 && !boxes)) return RP_ERR_ARG;
+    RP_IDLE(c);
+    RP_GUARD_BEGIN
+    std::vector<std::array<float, 16>> rec(n);
+    std::vector<std::array<float, 12>> rot(n);
+    for (int j = 0; j < n; ++j) {
+        rot[j].fill(0.0f);
+        if (!box_record_quat(boxes[j].center, boxes[j].half, boxes[j].quat, j, rec[j].data(), rot[j].data())) {
+            c->err = "rp_set_scene_rot: zero quaternion";
+            return RP_ERR_ARG;
+        }
+    }
+    return scene_from_records(c, rec, rot, n, plane_z, base);
+    RP_GUARD_END(c)
+}
+
+// the scene from box records in the caller's order: cluster sort, clusters, axis
+// grid, reach mask; marks the record for upload
+static int scene_from_records(rp_ctx* c, std::vector<std::array<float, 16>>& rec,
+                              std::vector<std::array<float, 12>>& rot, int32_t n, float plane_z, const float base[3]) {
+    RP_GUARD_BEGIN
+    HIP_TRY(hipSetDevice(c->device));
     // broad-phase clusters: recursive median split along the widest centre spread
     // into groups of <= CLUSTER boxes (a two-level AABB tree: <= 8 clusters)
     std::vector<int> order(n);
@@ -2180,7 +2332,12 @@ int rp_set_scene(rp_ctx* c, const rp_box* boxes, int32_t n, float plane_z, const
     c->slot_of.assign(n, 0);
     for (int s = 0; s < n; ++s) {
         std::memcpy(c->scene.box[s], rec[order[s]].data(), sizeof(float) * 16);
+        std::memcpy(c->scene.rot[s], rot[order[s]].data(), sizeof(float) * 12);
         c->slot_of[order[s]] = s;
+    }
+    for (int s = n; s < MAX_BOXES; ++s) {
+        std::memset(c->scene.box[s], 0, sizeof(float) * 16);
+        std::memset(c->scene.rot[s], 0, sizeof(float) * 12);
     }
     c->scene.n_clusters = (int)groups.size();
     for (int g = (int)groups.size(); g < MAX_CLUSTERS; ++g) {  // empty: no capsule overlaps it
@@ -2240,12 +2397,21 @@ int rp_set_scene(rp_ctx* c, const rp_box* boxes, int32_t n, float plane_z, const
 // the attachment's exemption bits in the host scene record (uploaded by the next
 // flush_scene)
 static void set_attached_bits(rp_ctx* c, int32_t box, uint32_t link_mask) {
-    for (int j = 0; j < c->scene.n_boxes; ++j) c->scene.box[j][14] = 0.0f;
+    // the exempt bits are the low bits of word 14; BOX_TILTED stays
+    for (int j = 0; j < c->scene.n_boxes; ++j) {
+        uint32_t w;
+        std::memcpy(&w, &c->scene.box[j][14], 4);
+        w &= BOX_TILTED;
+        std::memcpy(&c->scene.box[j][14], &w, 4);
+    }
     if (box >= 0) {
         uint32_t bits = 0;
         for (int i = 0; i < NCAP; ++i)
             if ((link_mask >> CAP_LINK[i]) & 1u) bits |= 1u << i;
-        std::memcpy(&c->scene.box[c->slot_of[box]][14], &bits, 4);
+        uint32_t w;
+        std::memcpy(&w, &c->scene.box[c->slot_of[box]][14], 4);
+        w |= bits;
+        std::memcpy(&c->scene.box[c->slot_of[box]][14], &w, 4);
     }
     upload_scene(c);
 }
@@ -2268,18 +2434,17 @@ int rp_set_scene_poses(rp_ctx* c, const double* poses, const float* halves, int3
                        const double base[3], int32_t attached, uint32_t link_mask) {
     if (!c || n < 0 || n > MAX_BOXES || (n > 0 && (!poses || !halves)) || !base || attached >= n) return RP_ERR_ARG;
     RP_IDLE(c);
-    rp_box boxes[MAX_BOXES];
+    rp_box_rot boxes[MAX_BOXES];
     for (int j = 0; j < n; ++j) {
         const double* p = poses + 7 * j;
-        const double w = p[3], x = p[4], y = p[5], z = p[6];
         for (int k = 0; k < 3; ++k) {
             boxes[j].center[k] = (float)p[k];
             boxes[j].half[k] = halves[3 * j + k];
         }
-        boxes[j].yaw = (float)std::atan2(2.0 * (w * z + x * y), 1.0 - 2.0 * (y * y + z * z));
+        for (int k = 0; k < 4; ++k) boxes[j].quat[k] = p[3 + k];
     }
     const float b[3] = {(float)base[0], (float)base[1], (float)base[2]};
-    const int rc = rp_set_scene(c, boxes, n, plane_z, b);
+    const int rc = rp_set_scene_rot(c, boxes, n, plane_z, b);
     if (rc != RP_OK) return rc;
     // no upload here: the next query's first call (rp_plan's flush_scene, on the
     // planner thread with rp_plan_async) copies the record, so the launch is not
@@ -2461,7 +2626,11 @@ static void plan_worker_main(rp_ctx* c) {
             PlanJob& j = w.job;
             j.rc = plan_entry(c, j.start, j.goal, j.lo, j.hi, &j.params, j.path_out, j.path_cap, j.n_out,
                               j.status_out);
-            w.state.store(PlanWorker::DONE, std::memory_order_release);
+            {
+                std::lock_guard<std::mutex> lk(w.m);
+                w.state.store(PlanWorker::DONE, std::memory_order_release);
+            }
+            w.done_cv.notify_all();
             last = now_s();
             continue;
         }
@@ -2491,6 +2660,8 @@ int rp_plan_async(rp_ctx* c, const double start[RP_NQ], const double goal[RP_NQ]
             c->worker = new PlanWorker();
             if (const char* e = std::getenv("RBE_PLAN_SPIN_US"))
                 if (*e) c->worker->spin_s = std::max(0.0, std::atof(e)) * 1e-6;
+            if (const char* e = std::getenv("RBE_PLAN_WAIT_SPIN_US"))
+                if (*e) c->worker->wait_spin_s = std::max(0.0, std::atof(e)) * 1e-6;
             c->worker->th = std::thread(plan_worker_main, c);
         }
     } catch (const std::exception& e) {
@@ -2527,7 +2698,16 @@ int rp_plan_wait(rp_ctx* c) {
         return RP_ERR_STATE;
     }
     PlanWorker& w = *c->worker;
-    while (w.state.load(std::memory_order_acquire) != PlanWorker::DONE) {
+    // spin for the pick / place queries that end within microseconds, then sleep on
+    // the worker's completion signal (a 10 s timeout query, motion_primitives.py:144,
+    // must not hold a host core)
+    const double t0 = now_s();
+    for (uint64_t spin = 0; w.state.load(std::memory_order_acquire) != PlanWorker::DONE; ++spin) {
+        if ((spin & 63) == 63 && now_s() - t0 > w.wait_spin_s) {
+            std::unique_lock<std::mutex> lk(w.m);
+            w.done_cv.wait(lk, [&] { return w.state.load(std::memory_order_acquire) == PlanWorker::DONE; });
+            break;
+        }
 #if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
         __builtin_ia32_pause();
 #endif
@@ -2548,7 +2728,10 @@ int rp_reserve(rp_ctx* c, int64_t batch, int64_t tree_capacity) {
     // the default range (0.2 x the bounds' extent) and resolution (0.01 x): connect
     // chains of ceil(5) + 1 steps, ceil(20) + 2 slots per edge (+ 1 each for rounding)
     const int cmax = 7, kmax = 23;
-    plan_workspace(c, B, c->world, cmax, cap, c->transport != TR_NONE);
+    int64_t repl = RP_GROUP_REPL_DEFAULT;
+    if (const char* e = std::getenv("RBE_GROUP_REPL"))
+        if (*e) repl = std::max<int64_t>(0, std::atoll(e));
+    plan_workspace(c, B, c->world, cmax, cap, c->transport != TR_NONE, repl);
     // buffers that large launches grow on first use: node images of the matrix-core
     // nearest-node search, the work-compacted edge launch's slot counts / scan / chunk
     // map, the hipCUB scratch of its scans, the materialised queries
@@ -2629,6 +2812,80 @@ int rp_group_init_shm(rp_ctx* c, int32_t rank, int32_t world, void* base, int64_
     c->transport = TR_SHM;
     return RP_OK;
     RP_GUARD_END(c)
+}
+
+int rp_group_init_local(rp_ctx* const* ctxs, int32_t world, int32_t transport, int64_t bytes) {
+    if (!ctxs || world < 1 || world > 64) return RP_ERR_ARG;
+    for (int r = 0; r < world; ++r) {
+        if (!ctxs[r]) return RP_ERR_ARG;
+        for (int k = 0; k < r; ++k)
+            if (ctxs[k] == ctxs[r]) return RP_ERR_ARG;
+        RP_IDLE(ctxs[r]);
+    }
+    rp_ctx* c0 = ctxs[0];
+    bool distinct = true;
+    for (int r = 0; r < world && distinct; ++r)
+        for (int k = 0; k < r; ++k)
+            if (ctxs[k]->device == ctxs[r]->device) distinct = false;
+    if (transport == RP_TRANSPORT_NONE) transport = distinct ? RP_TRANSPORT_RCCL : RP_TRANSPORT_SHM;
+    if (transport == RP_TRANSPORT_RCCL && !distinct) {
+        c0->err = "rp_group_init_local: the RCCL transport needs the contexts on distinct devices";
+        return RP_ERR_ARG;
+    }
+    if (transport != RP_TRANSPORT_RCCL && transport != RP_TRANSPORT_SHM) return RP_ERR_ARG;
+    try {
+        for (int r = 0; r < world; ++r) {
+            HIP_TRY(hipSetDevice(ctxs[r]->device));
+            ctxs[r]->leave_group();
+        }
+        if (world == 1) return RP_OK;
+        if (transport == RP_TRANSPORT_RCCL) {
+            std::vector<ncclComm_t> comms(world);
+            std::vector<int> devs(world);
+            for (int r = 0; r < world; ++r) devs[r] = ctxs[r]->device;
+            NCCL_TRY(ncclCommInitAll(comms.data(), world, devs.data()));
+            for (int r = 0; r < world; ++r) {
+                rp_ctx* c = ctxs[r];
+                HIP_TRY(hipSetDevice(c->device));
+                c->comm = comms[r];
+                if (!c->gx0) HIP_TRY(hipEventCreate(&c->gx0));
+                if (!c->gx1) HIP_TRY(hipEventCreate(&c->gx1));
+                c->rank = r;
+                c->world = world;
+                c->transport = TR_RCCL;
+            }
+            return RP_OK;
+        }
+        const int64_t nbytes = bytes > 0 ? bytes : (int64_t)64 << 20;
+        if (nbytes < SHM_HDR + 2 * 4096) return RP_ERR_ARG;
+        auto seg = std::make_shared<LocalSeg>();
+        HIP_TRY(hipSetDevice(c0->device));
+        HIP_TRY(hipHostMalloc(&seg->p, (size_t)nbytes, hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent));
+        std::memset(seg->p, 0, (size_t)nbytes);
+        for (int r = 0; r < world; ++r) {
+            rp_ctx* c = ctxs[r];
+            HIP_TRY(hipSetDevice(c->device));
+            void* dptr = nullptr;
+            HIP_TRY(hipHostGetDevicePointer(&dptr, seg->p, 0));
+            c->local_seg = seg;
+            c->shm = static_cast<char*>(seg->p);
+            c->shm_dev = static_cast<char*>(dptr);
+            c->shm_bytes = nbytes;
+            c->shm_k = 0;
+            c->rank = r;
+            c->world = world;
+            c->transport = TR_SHM;
+        }
+        return RP_OK;
+    } catch (const HipError& e) {
+        for (int r = 0; r < world; ++r) ctxs[r]->leave_group();
+        c0->err = e.msg;
+        return RP_ERR_DEVICE;
+    } catch (const std::exception& e) {
+        for (int r = 0; r < world; ++r) ctxs[r]->leave_group();
+        c0->err = e.what();
+        return RP_ERR_DEVICE;
+    }
 }
 
 int rp_group_rccl_unique_id(uint8_t out[RP_RCCL_ID_BYTES]) {

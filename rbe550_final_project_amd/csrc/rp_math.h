@@ -403,19 +403,36 @@ __device__ __attribute__((noinline)) float segment_segment_dist2(V3 a1, V3 b1, V
     return segment_segment_dist2_body(a1, b1, a2, b2);
 }
 
-// narrow phase of capsule (a, b, r) against box record bx (world -> box frame:
-// rotation by -yaw about z)
-template <bool INL = false>
-__device__ __forceinline__ bool capsule_box_narrow(V3 a, V3 b, float r, const float* __restrict__ bx) {
+// World point p in the frame of box record bx. Upright box: rotation by -yaw about
+// z (cos / sin in bx[6], bx[7]). Tilted box (BOX_TILTED in bx[14]): the rows of R^T
+// in rt (DevScene::rot of the box's slot), p'_i = fma(rt_i2, dz, fma(rt_i1, dy,
+// rt_i0 * dx)). The oracle (oracle/rbe_oracle.c box_frame) writes the same sequence.
+__device__ __forceinline__ V3 box_frame_yaw(V3 p, const float* __restrict__ bx) {
     const float cs = bx[6], sn = bx[7];
+    const float dx = p.x - bx[0], dy = p.y - bx[1], dz = p.z - bx[2];
+    return {fma_(cs, dx, sn * dy), fma_(cs, dy, -(sn * dx)), dz};
+}
+__device__ __forceinline__ V3 box_frame_rot(V3 p, const float* __restrict__ bx, const float* __restrict__ rt) {
+    const float dx = p.x - bx[0], dy = p.y - bx[1], dz = p.z - bx[2];
+    return {fma_(rt[2], dz, fma_(rt[1], dy, rt[0] * dx)), fma_(rt[5], dz, fma_(rt[4], dy, rt[3] * dx)),
+            fma_(rt[8], dz, fma_(rt[7], dy, rt[6] * dx))};
+}
+__device__ __forceinline__ bool box_tilted(const float* __restrict__ bx) {
+    return (__float_as_uint(bx[14]) & BOX_TILTED) != 0u;
+}
+
+// narrow phase of capsule (a, b, r) against box record bx (rt: its rotation rows
+// when tilted)
+template <bool INL = false>
+__device__ __forceinline__ bool capsule_box_narrow(V3 a, V3 b, float r, const float* __restrict__ bx,
+                                                   const float* __restrict__ rt) {
     V3 pa, pb;
-    {
-        const float dx = a.x - bx[0], dy = a.y - bx[1], dz = a.z - bx[2];
-        pa.x = fma_(cs, dx, sn * dy); pa.y = fma_(cs, dy, -(sn * dx)); pa.z = dz;
-    }
-    {
-        const float dx = b.x - bx[0], dy = b.y - bx[1], dz = b.z - bx[2];
-        pb.x = fma_(cs, dx, sn * dy); pb.y = fma_(cs, dy, -(sn * dx)); pb.z = dz;
+    if (box_tilted(bx)) {
+        pa = box_frame_rot(a, bx, rt);
+        pb = box_frame_rot(b, bx, rt);
+    } else {
+        pa = box_frame_yaw(a, bx);
+        pb = box_frame_yaw(b, bx);
     }
     const V3 h = {bx[3], bx[4], bx[5]};
     return (INL ? segment_box_dist2_body(pa, pb, h) : segment_box_dist2(pa, pb, h)) <= r * r;
@@ -438,7 +455,7 @@ __device__ __forceinline__ bool capsule_hits_env(const Capsules& k, const DevSce
             const float* bx = sc->box[j];
             if ((__float_as_uint(bx[14]) >> C) & 1u) continue;
             if (aabb_disjoint(u, bx + 8, bx + 11)) continue;
-            if (capsule_box_narrow(k.a[C], k.b[C], r, bx)) return true;
+            if (capsule_box_narrow(k.a[C], k.b[C], r, bx, sc->rot[j])) return true;
         }
     }
     return false;
@@ -585,16 +602,24 @@ __device__ __forceinline__ void room_sb(S& s, int c) {
     if (s.nsb + c > QCAP) pop_sb(s);
 }
 
-// queue item of capsule C vs box record bx (box frame segment, half extents, r^2)
+// queue item of capsule C vs box record bx (box frame segment, half extents, r^2);
+// rt: the box's rotation rows, read only when the box is tilted (a wave-uniform
+// branch in the cluster scenes, whose records sit in scalar registers)
 template <int C, class S>
-__device__ __forceinline__ void enqueue_sb(const Capsules& k, const float* bx, float r, S& s,
-                                           unsigned long long m) {
+__device__ __forceinline__ void enqueue_sb(const Capsules& k, const float* bx, const float* __restrict__ rt,
+                                           float r, S& s, unsigned long long m) {
     float* it = s.Q->sb[s.nsb + rank_in(m)];
-    const float cs = bx[6], sn = bx[7];
-    float dx = k.a[C].x - bx[0], dy = k.a[C].y - bx[1];
-    it[0] = fma_(cs, dx, sn * dy); it[1] = fma_(cs, dy, -(sn * dx)); it[2] = k.a[C].z - bx[2];
-    dx = k.b[C].x - bx[0]; dy = k.b[C].y - bx[1];
-    it[3] = fma_(cs, dx, sn * dy); it[4] = fma_(cs, dy, -(sn * dx)); it[5] = k.b[C].z - bx[2];
+    if (box_tilted(bx)) {
+        const V3 pa = box_frame_rot(k.a[C], bx, rt), pb = box_frame_rot(k.b[C], bx, rt);
+        it[0] = pa.x; it[1] = pa.y; it[2] = pa.z;
+        it[3] = pb.x; it[4] = pb.y; it[5] = pb.z;
+    } else {
+        const float cs = bx[6], sn = bx[7];
+        float dx = k.a[C].x - bx[0], dy = k.a[C].y - bx[1];
+        it[0] = fma_(cs, dx, sn * dy); it[1] = fma_(cs, dy, -(sn * dx)); it[2] = k.a[C].z - bx[2];
+        dx = k.b[C].x - bx[0]; dy = k.b[C].y - bx[1];
+        it[3] = fma_(cs, dx, sn * dy); it[4] = fma_(cs, dy, -(sn * dx)); it[5] = k.b[C].z - bx[2];
+    }
     it[6] = bx[3]; it[7] = bx[4]; it[8] = bx[5];
     it[9] = r * r;
     it[10] = __int_as_float(s.lane);
@@ -621,8 +646,11 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
         while (__any(m != 0)) {
             bool cand = false;
             const float* bx = sc->box[0];
+            const float* rt = sc->rot[0];
             if (m) {
-                bx = sc->box[__builtin_ctzll(m)];
+                const int jb = __builtin_ctzll(m);
+                bx = sc->box[jb];
+                rt = sc->rot[jb];
                 m &= m - 1;
                 // exempt bit and box test as one separation value (one lane mask;
                 // A/B clutter64 +9.7 %; -DRP_GRID_CMP builds the mask form)
@@ -632,7 +660,7 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
             const unsigned long long bm = __ballot(cand);
             if (!bm) continue;
             room_sb(s, __popcll(bm));
-            if (cand) enqueue_sb<C>(k, bx, r, s, bm);
+            if (cand) enqueue_sb<C>(k, bx, rt, r, s, bm);
             s.nsb += __popcll(bm);
         }
         return false;
@@ -657,7 +685,7 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
             const unsigned long long m = __ballot(cand);
             if (!m) continue;
             room_sb(s, __popcll(m));
-            if (cand) enqueue_sb<C>(k, bx, r, s, m);
+            if (cand) enqueue_sb<C>(k, bx, sc->rot[j], r, s, m);
             s.nsb += __popcll(m);
         }
     }
@@ -895,6 +923,7 @@ struct CapsLds { float v[NCAP][6]; };   // a.xyz, b.xyz of each capsule (world)
 // the test loop reads only LDS.
 struct SceneLds {
     float box[MAX_BOXES][16];
+    float rot[MAX_BOXES][12];
     int pi[NPAIR], pj[NPAIR];
     float rad[NCAP];
     float plane_z, base[3];
@@ -908,6 +937,12 @@ __device__ __forceinline__ void scene_to_lds(const DevScene* __restrict__ sc, Sc
     float4* dst = reinterpret_cast<float4*>(&L.box[0][0]);
 #pragma unroll
     for (int k = 0; k < MAX_BOXES * 4 / 64; ++k) dst[t + 64 * k] = src[t + 64 * k];
+    {
+        const float4* rs = reinterpret_cast<const float4*>(&sc->rot[0][0]);
+        float4* rd = reinterpret_cast<float4*>(&L.rot[0][0]);
+#pragma unroll
+        for (int k = 0; k < MAX_BOXES * 3 / 64; ++k) rd[t + 64 * k] = rs[t + 64 * k];
+    }
     if (t < NPAIR) {
         L.pi[t] = ML_PAIR_I[t];
         L.pj[t] = ML_PAIR_J[t];
@@ -1006,7 +1041,8 @@ __device__ __forceinline__ bool state_collides_ml(const float q[NQ], bool run, c
                     const float* pc = cs.v[c];
                     const V3 a = {pc[0], pc[1], pc[2]}, b = {pc[3], pc[4], pc[5]};
                     const float r = sc.rad[c];
-                    if (!aabb_disjoint(capsule_aabb(a, b, r), bx + 8, bx + 11)) h = capsule_box_narrow<true>(a, b, r, bx);
+                    if (!aabb_disjoint(capsule_aabb(a, b, r), bx + 8, bx + 11))
+                        h = capsule_box_narrow<true>(a, b, r, bx, sc.rot[j]);
                 }
             }
         }

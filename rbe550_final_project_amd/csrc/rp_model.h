@@ -112,8 +112,14 @@ constexpr int MAX_CLUSTERS = MAX_BOXES / CLUSTER;
 // Device scene record (one constant buffer, read by wave-uniform scalar loads).
 // Box record: 16 floats so one s_load_dwordx16 fetches it.
 //   [0..2] centre  [3..5] half extents  [6] cos(yaw) [7] sin(yaw)
-//   [8..10] world AABB lo  [11..13] world AABB hi  [14] exempt-capsule bits
-//   [15] index of the box in the caller's order (boxes are stored cluster-sorted)
+//   [8..10] world AABB lo  [11..13] world AABB hi  [14] exempt-capsule bits (bits
+//   0..NCAP-1) | BOX_TILTED  [15] index of the box in the caller's order (boxes are
+//   stored cluster-sorted)
+// A tilted box (rp_set_scene_rot with a rotation that moves the z axis: a toppled
+// or leaning block) has BOX_TILTED set and its world -> box rotation in rot[slot]:
+// rows of R^T (row i = box axis i in world coordinates), 9 floats; [6], [7] unused.
+// Upright boxes keep the yaw transform (no extra loads or VALU in the hot path).
+constexpr unsigned BOX_TILTED = 0x80000000u;
 // Cluster record: [0..2] AABB lo, [4..6] AABB hi (union of its boxes' AABBs),
 //   [3] first box, [7] box count (as int bits).
 // Axis grid (many-box scenes, `grid` = 1): per axis, GRID_CELLS cells over the
@@ -127,6 +133,7 @@ constexpr int GRID_CELLS = 64;
 constexpr int ML_UNITS_PAD = (NPAIR + NCAP * MAX_BOXES + 7) / 8 * 8;   // 808: whole 16-B words
 struct DevScene {
     float box[MAX_BOXES][16];
+    float rot[MAX_BOXES][12];    // tilted boxes: R^T rows (9 floats), pad
     float cluster[MAX_CLUSTERS][8];
     float base[4];               // robot base translation (scenes.py:29-34), pad
     float plane_z;

@@ -17,9 +17,11 @@ LIB_NAME = "librbe_mi355x.so"
 LIB_PATH = os.environ.get("RBE_LIB_PATH") or os.path.join(_HERE, LIB_NAME)
 
 # every symbol include/rbe_planner.h declares
-EXPORTS = ("rp_version", "rp_default_robot", "rp_create", "rp_destroy", "rp_set_scene", "rp_set_attached", "rp_set_scene_poses",
+EXPORTS = ("rp_version", "rp_abi_version", "rp_default_robot", "rp_create", "rp_destroy", "rp_set_scene", "rp_set_scene_rot", "rp_set_attached",
+           "rp_set_scene_poses",
            "rp_check_states", "rp_check_states_device", "rp_check_edges", "rp_check_edges_device",
            "rp_state_contacts", "rp_plan", "rp_plan_async", "rp_plan_wait", "rp_reserve", "rp_group_init", "rp_group_init_shm", "rp_group_rccl_unique_id", "rp_group_init_rccl",
+           "rp_group_init_local",
            "rp_get_stats", "rp_last_error", "rp_last_kernel_ms", "rp_selftest_f64", "rp_ik", "rp_set_profiling",
            "rp_get_profile", "rp_get_stream", "rp_group_info", "rp_selftest_nn")
 
@@ -44,12 +46,17 @@ def load():
                           "(there is no CPU fallback for the planner)")
     L = C.CDLL(LIB_PATH)
     vp, i32, i64, u32, f32, f64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_float, C.c_double
+    L.rp_abi_version.restype = C.c_int
+    if L.rp_abi_version() != _abi.ABI_VERSION:
+        raise NativeError(f"{LIB_PATH}: ABI version {L.rp_abi_version()}, the ctypes mirrors are version "
+                          f"{_abi.ABI_VERSION} (rebuild: __graft_entry__.build())")
     L.rp_version.restype = C.c_char_p
     L.rp_default_robot.argtypes = [C.POINTER(_abi.RobotDesc)]
     L.rp_create.argtypes = [C.POINTER(vp), C.c_int, C.POINTER(_abi.RobotDesc)]
     L.rp_destroy.argtypes = [vp]
     L.rp_destroy.restype = None
     L.rp_set_scene.argtypes = [vp, vp, i32, f32, C.POINTER(f32)]   # rp_box* (ctypes array or address)
+    L.rp_set_scene_rot.argtypes = [vp, vp, i32, f32, C.POINTER(f32)]   # rp_box_rot*
     L.rp_set_attached.argtypes = [vp, i32, u32]
     L.rp_set_scene_poses.argtypes = [vp, vp, vp, i32, f32, vp, i32, u32]
     L.rp_check_states.argtypes = [vp, vp, i64, vp]
@@ -65,6 +72,7 @@ def load():
     L.rp_group_rccl_unique_id.argtypes = [vp]
     L.rp_group_init_shm.argtypes = [vp, i32, i32, vp, i64]
     L.rp_group_init_rccl.argtypes = [vp, i32, i32, vp]
+    L.rp_group_init_local.argtypes = [vp, i32, i32, i64]
     L.rp_get_stats.argtypes = [vp, C.POINTER(_abi.Stats)]
     L.rp_group_info.argtypes = [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i32)]
     L.rp_set_profiling.argtypes = [vp, i32]
@@ -93,6 +101,19 @@ def rccl_unique_id():
     return bytes(buf)
 
 
+def group_init_local(ctxs, transport=None, nbytes=0):
+    """rp_group_init_local: the contexts of this process become ranks 0..n-1 of one
+    group ("rccl": ncclCommInitAll, distinct devices; "shm": a library-owned pinned
+    segment, devices may repeat; None: rccl when the devices are distinct)."""
+    codes = {None: 0, "none": 0, "rccl": 2, "shm": 3}
+    if transport not in codes:
+        raise ValueError(f"unknown transport {transport!r}")
+    arr = (C.c_void_p * len(ctxs))(*[c._h.value for c in ctxs])
+    rc = load().rp_group_init_local(arr, len(ctxs), codes[transport], int(nbytes))
+    if rc < 0:
+        raise NativeError(f"rp_group_init_local failed ({rc}): {load().rp_last_error(ctxs[0]._h).decode()}")
+
+
 def default_robot():
     d = _abi.RobotDesc()
     load().rp_default_robot(C.byref(d))
@@ -113,6 +134,7 @@ class Context:
         self.scene_gen = 0   # bumped by every set_scene / set_attached (callers that cache a scene)
         self._cb = None
         self._group_bufs = None
+        self._in_flight = False   # a rp_plan_async query awaits its rp_plan_wait
 
     def close(self):
         if self._h:
@@ -132,10 +154,15 @@ class Context:
 
     # -- scene ---------------------------------------------------------------
     def set_scene(self, boxes, plane_z=0.0, base=(0.0, 0.0, 0.01)):
-        arr, n = _abi.make_boxes(boxes)
+        """boxes: (center, half, yaw or quaternion (w, x, y, z)); rp_set_scene when every
+        box is upright (a yaw), else rp_set_scene_rot (tilted boxes)."""
+        kind, arr, n = _abi.scene_boxes(boxes)
         b = (C.c_float * 3)(*[float(v) for v in base])
         self.scene_gen += 1
-        self._check(load().rp_set_scene(self._h, arr, n, float(plane_z), b), "rp_set_scene")
+        if kind == "rot":
+            self._check(load().rp_set_scene_rot(self._h, arr, n, float(plane_z), b), "rp_set_scene_rot")
+        else:
+            self._check(load().rp_set_scene(self._h, arr, n, float(plane_z), b), "rp_set_scene")
 
     def set_scene_poses(self, poses, halves, plane_z, base, attached=-1, link_mask=_abi.ATTACH_EXEMPT_MASK):
         """rp_set_scene_poses: boxes from simulator poses (n, 7) float64 [x, y, z, qw,
@@ -227,6 +254,11 @@ class Context:
         return b
 
     def _plan_call(self, fn, start, goal, lo, hi, params, path_cap):
+        # the planner thread writes into the out / n / status buffers of a query in
+        # flight: nothing may replace them before its plan_wait; the
+        # library refuses the call too (RP_ERR_STATE), but only after this point
+        if self._in_flight:
+            raise NativeError("rp_plan: a query is in flight on this context (plan_wait first)")
         b = self._plan_buffers(path_cap)
         inp, nq = b["inp"], _abi.NQ
         inp[0:nq] = start
@@ -252,6 +284,7 @@ class Context:
         """rp_plan_async: hand the query to the context's planner thread and return
         at once; plan_wait() returns what plan() would. The params struct is copied."""
         self._plan_call("fn_async", start, goal, lo, hi, params, path_cap)
+        self._in_flight = True
 
     def plan_wait(self, out=None):
         """rp_plan_wait: (path, status) of the query in flight. With `out` (an (m, 9)
@@ -260,6 +293,7 @@ class Context:
         `out` is returned; otherwise a float64 copy."""
         b = self._plan_bufs
         rc = b["fn_wait"](self._h)
+        self._in_flight = False
         if rc < 0:
             self._check(rc, "rp_plan")
         n = b["n"].value

@@ -65,15 +65,29 @@ def _logger():
     return _log
 
 
-_CONFIG = {"seed": None, "batch": None, "device": None, "tree_capacity": None, "straight_first": None}
+_CONFIG = {"seed": None, "batch": None, "device": None, "tree_capacity": None, "straight_first": None,
+           "devices": None, "batch_min": None}
 _QUERY_COUNTER = [0]
 
 
-def configure(seed=None, batch=None, device=None, tree_capacity=None, straight_first=None):
+def configure(seed=None, batch=None, device=None, tree_capacity=None, straight_first=None, devices=None,
+              batch_min=None):
     """Set planner options without changing plan_path's signature.
 
+    batch_min: samples of the first RRT-Connect iteration (each next one doubles, up
+    to `batch`); 0 = the library default (min(batch, 64)).
     straight_first: with smooth_path, try the straight edge start -> goal before
-    RRT-Connect (default on; env RBE_PLANNER_STRAIGHT=0 turns it off)."""
+    RRT-Connect (default on; env RBE_PLANNER_STRAIGHT=0 turns it off).
+    devices: GPUs of a multi-GPU planner in this one process (env
+    RBE_PLANNER_DEVICES="0,1,2,3"): a PlannerInterface opens one context per entry
+    and every plan_path query runs as a rank group over them (rp_group_init_local:
+    RCCL between distinct GPUs, a shared pinned segment when a device repeats); each
+    RRT-Connect iteration's large sub-batches are sharded, the returned path is rank
+    0's (every rank grows the same trees). () or None: one GPU (`device`)."""
+    if devices is not None:
+        _CONFIG["devices"] = tuple(int(d) for d in devices) or None
+    if batch_min is not None:
+        _CONFIG["batch_min"] = int(batch_min)
     if seed is not None:
         _CONFIG["seed"] = int(seed)
         _QUERY_COUNTER[0] = 0
@@ -114,6 +128,16 @@ def _device():
     if "LOCAL_RANK" in os.environ:
         return int(os.environ["LOCAL_RANK"])
     return 0
+
+
+def _devices():
+    """The planner's GPUs: configure(devices=...), RBE_PLANNER_DEVICES, else one."""
+    if _CONFIG["devices"]:
+        return tuple(_CONFIG["devices"])
+    e = os.environ.get("RBE_PLANNER_DEVICES", "").strip()
+    if e:
+        return tuple(int(x) for x in e.split(",") if x.strip())
+    return (_device(),)
 
 
 def tensor_to_array(x):
@@ -186,7 +210,9 @@ class PlannerInterface:
         self.robot = _ensure_adapter(robot, scene)
         self.scene = scene
         self.attached_object = None
-        self._ctx = None
+        self._ctx = None         # rank 0's context (diagnostics, IK, single-state checks)
+        self._ctxs = []          # every rank's context (configure(devices=...)), rank order
+        self._devs = None
         self._reader = None      # scenes.GenesisReader of self.scene
         self._pushed = None      # (ctx.scene_gen, box poses, base, attached box) last pushed
         self._qlim = None        # (robot.q_limit object, lo, hi)
@@ -198,8 +224,19 @@ class PlannerInterface:
 
     # -- GPU context -----------------------------------------------------------
     def _context(self):
-        if self._ctx is None:
-            self._ctx = Context(device=_device(), robot=model.robot_desc())
+        devs = _devices()
+        if self._ctx is not None and (not self._ctxs or devs == self._devs):
+            return self._ctx   # (also a context handed in from outside: bench.py)
+        for c in self._ctxs:
+            c.close()
+        self._ctxs = [Context(device=d, robot=model.robot_desc()) for d in devs]
+        if len(self._ctxs) > 1:
+            from .native import group_init_local
+            group_init_local(self._ctxs)
+        self._ctx = self._ctxs[0]
+        self._devs = devs
+        self._pushed = None
+        self._reserved = None
         return self._ctx
 
     def _reserve(self, ctx, batch, cap):
@@ -207,7 +244,8 @@ class PlannerInterface:
         first query does not allocate device memory inside the plan."""
         key = (id(ctx), batch, cap)
         if self._reserved != key and hasattr(ctx, "reserve"):
-            ctx.reserve(batch, cap)
+            for c in self._ctxs or [ctx]:
+                c.reserve(batch, cap)
             self._reserved = key
 
     def _sync_scene(self):
@@ -228,18 +266,23 @@ class PlannerInterface:
             idx = rd.box_of_entity.get(getattr(att, "idx", None), -1)
         gen = getattr(ctx, "scene_gen", None)
         pushed = self._pushed
+        ctxs = self._ctxs or [ctx]   # every rank of a multi-GPU planner sees the same scene
         if gen is not None and pushed is not None and pushed[0] == gen and pushed[1] == poses \
                 and pushed[2] == base:
             if pushed[3] != idx:
-                ctx.set_attached(idx)
+                for c in ctxs:
+                    c.set_attached(idx)
                 self._pushed = (ctx.scene_gen, poses, base, idx)
             return
         if hasattr(ctx, "set_scene_poses"):   # one library call (rp_set_scene_poses)
-            ctx.set_scene_poses(np.array(poses, dtype=np.float64).reshape(-1, 7), rd.halves_f32, rd.plane_z,
-                                np.array(base, dtype=np.float64), idx)
+            P = np.array(poses, dtype=np.float64).reshape(-1, 7)
+            B = np.array(base, dtype=np.float64)
+            for c in ctxs:
+                c.set_scene_poses(P, rd.halves_f32, rd.plane_z, B, idx)
         else:
-            ctx.set_scene(rd.boxes(poses), rd.plane_z, base)
-            ctx.set_attached(idx)
+            for c in ctxs:
+                c.set_scene(rd.boxes(poses), rd.plane_z, base)
+                c.set_attached(idx)
         self._pushed = (getattr(ctx, "scene_gen", None), poses, base, idx)
 
     def _bounds(self):
@@ -331,9 +374,12 @@ class PlannerInterface:
         p = self._params
         if p is None:
             p = self._params = _abi.make_params()
-        _abi.set_params(p, seed=_next_seed(), batch=_batch(), timeout_s=float(timeout),
+        world = len(self._ctxs) or 1
+        batch = -(-_batch() // world) * world   # a rank group shards whole batches
+        _abi.set_params(p, seed=_next_seed(), batch=batch, timeout_s=float(timeout),
                         n_waypoints=int(num_waypoints) if num_waypoints else 0, simplify=bool(smooth_path),
-                        tree_capacity=_CONFIG["tree_capacity"] or 0, straight_first=_straight_first())
+                        tree_capacity=_CONFIG["tree_capacity"] or 0, straight_first=_straight_first(),
+                        batch_min=_CONFIG["batch_min"] or 0)
         self._reserve(ctx, p.batch, p.tree_capacity)
         nwp = p.n_waypoints
         cap = max(4096, nwp + 16)
@@ -342,13 +388,20 @@ class PlannerInterface:
         status = _abi.STATUS_NONE
         restored = False
         self._stats_ctx = None
+        ranks = self._ctxs if len(self._ctxs) > 1 else [ctx]
+        started = []
+        views = None
         try:
-            ctx.plan_async(qpos_start, qpos_goal, lo, hi, p, path_cap=cap)
-            # while the GPU plans: the waypoint tensors of the expected path (an
-            # interpolated solution has exactly num_waypoints states) and the restore
-            # of the robot's qpos (planning.py:205; the planner never moves the robot)
-            views = None
             try:
+                # every rank's query on its context's planner thread (a rank group
+                # meets at its exchanges); rank 0's path is the answer
+                for c in ranks:
+                    c.plan_async(qpos_start, qpos_goal, lo, hi, p, path_cap=cap)
+                    started.append(c)
+                # while the GPU plans: the waypoint tensors of the expected path (an
+                # interpolated solution has exactly num_waypoints states) and the
+                # restore of the robot's qpos (planning.py:205; the planner never
+                # moves the robot)
                 if nwp > 0:
                     buf = torch.empty((nwp, n_qs), dtype=torch.float32)
                     views = buf.unbind(0)
@@ -356,7 +409,16 @@ class PlannerInterface:
                 robot.set_qpos(qpos_cur)
                 restored = True
             finally:
-                path, status = ctx.plan_wait(out)
+                err = None
+                for k, c in enumerate(started):   # every started rank is waited for
+                    try:
+                        r = c.plan_wait(out if k == 0 else None)
+                        if k == 0:
+                            path, status = r
+                    except NativeError as ex:
+                        err = err or ex
+                if err is not None:
+                    raise err
             self._stats_ctx = ctx
         except NativeError as ex:
             # the reference never raises on a failed plan (planning.py:190-202):

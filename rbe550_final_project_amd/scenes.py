@@ -13,7 +13,8 @@ scene is Genesis entity k+1 (planning.py:226 compares attached_object.idx with g
 indices). The robot base is raised by 1 cm (scenes.py:29-34).
 
 `from_genesis()` ingests a live Genesis scene (box entities and their current
-poses) so the drop-in planning.py sees the blocks where the simulation has them.
+poses, upright or toppled) so the drop-in planning.py sees the blocks where the
+simulation has them.
 """
 from dataclasses import dataclass, field
 import json
@@ -26,25 +27,36 @@ HALF = (BLOCK / 2, BLOCK / 2, BLOCK / 2)
 BASE = (0.0, 0.0, 0.01)
 
 
+def _rot_copy(rot):
+    """A box orientation: a yaw (float) or a quaternion (w, x, y, z) tuple."""
+    if hasattr(rot, "__len__"):
+        return tuple(float(v) for v in rot)
+    return float(rot)
+
+
 @dataclass
 class Scene:
-    boxes: list = field(default_factory=list)     # [(center(3), half(3), yaw)]
+    # [(center(3), half(3), rot)]: rot is the yaw about world z, or a quaternion
+    # (w, x, y, z) for a tilted (toppled, leaning) box
+    boxes: list = field(default_factory=list)
     names: list = field(default_factory=list)
     plane_z: float = 0.0
     base: tuple = BASE
     entity_idx: list = field(default_factory=list)  # Genesis entity index per box (or None)
 
     def copy(self):
-        return Scene([(tuple(c), tuple(h), float(y)) for c, h, y in self.boxes], list(self.names), self.plane_z,
+        return Scene([(tuple(c), tuple(h), _rot_copy(y)) for c, h, y in self.boxes], list(self.names), self.plane_z,
                      tuple(self.base), list(self.entity_idx))
 
     def index(self, name):
         return self.names.index(name)
 
-    def move(self, name, center, yaw=None):
+    def move(self, name, center, yaw=None, quat=None):
+        """Move box `name`; yaw (float) or quat (w, x, y, z) sets its orientation."""
         i = self.index(name)
         c, h, y = self.boxes[i]
-        self.boxes[i] = (tuple(float(v) for v in center), h, float(y if yaw is None else yaw))
+        rot = quat if quat is not None else (yaw if yaw is not None else y)
+        self.boxes[i] = (tuple(float(v) for v in center), h, _rot_copy(rot))
 
     def remove(self, name):
         i = self.index(name)
@@ -54,15 +66,22 @@ class Scene:
             del self.entity_idx[i]
 
     def to_json(self):
-        return {"boxes": [{"name": n, "center": list(c), "half": list(h), "yaw": y}
-                          for n, (c, h, y) in zip(self.names, self.boxes)],
-                "plane_z": self.plane_z, "base": list(self.base)}
+        out = []
+        for n, (c, h, y) in zip(self.names, self.boxes):
+            rec = {"name": n, "center": list(c), "half": list(h)}
+            if hasattr(y, "__len__"):
+                rec["quat"] = list(y)
+            else:
+                rec["yaw"] = y
+            out.append(rec)
+        return {"boxes": out, "plane_z": self.plane_z, "base": list(self.base)}
 
     @staticmethod
     def from_json(d):
         s = Scene(plane_z=float(d.get("plane_z", 0.0)), base=tuple(d.get("base", BASE)))
         for b in d["boxes"]:
-            s.boxes.append((tuple(b["center"]), tuple(b["half"]), float(b.get("yaw", 0.0))))
+            rot = tuple(float(v) for v in b["quat"]) if "quat" in b else float(b.get("yaw", 0.0))
+            s.boxes.append((tuple(b["center"]), tuple(b["half"]), rot))
             s.names.append(b.get("name", f"box{len(s.names)}"))
         s.entity_idx = [i + 1 for i in range(len(s.boxes))]
         return s
@@ -173,9 +192,19 @@ def _floats(x, n):
 
 
 def yaw_of_quat(q):
-    """Rotation about world z of a (w, x, y, z) quaternion (tilt is ignored)."""
+    """Rotation about world z of a (w, x, y, z) quaternion whose x = y = 0."""
     w, x, y, z = (float(v) for v in q)
     return math.atan2(2.0 * (w * z + x * y), 1.0 - 2.0 * (y * y + z * z))
+
+
+def rot_of_quat(q):
+    """A box orientation from a (w, x, y, z) quaternion: its yaw when the box is
+    upright (x = y = 0: exactly the record rp_set_scene_poses makes), else the
+    quaternion itself (a tilted box; rp_set_scene_rot)."""
+    w, x, y, z = (float(v) for v in q)
+    if x == 0.0 and y == 0.0:
+        return yaw_of_quat((w, x, y, z))
+    return (w, x, y, z)
 
 
 def _entity_table(entities, raw_robot, robot):
@@ -310,8 +339,8 @@ class GenesisReader:
         return boxes, base
 
     def boxes(self, poses):
-        """Box records (center, half, yaw) of box poses from poses()."""
-        return [((p[0], p[1], p[2]), h, yaw_of_quat(p[3:7])) for p, h in zip(poses, self.halves)]
+        """Box records (center, half, yaw or quaternion) of box poses from poses()."""
+        return [((p[0], p[1], p[2]), h, rot_of_quat(p[3:7])) for p, h in zip(poses, self.halves)]
 
     def read(self):
         """The scene as a Scene record."""

@@ -29,11 +29,18 @@ class MJCF:
 
 class Entity:
     def __init__(self, idx, morph, yaw=0.0):
+        """yaw: a rotation about z, or a quaternion (w, x, y, z) (a tilted box)."""
         self.idx = idx
         self.base_link_idx = idx   # one link per entity here (the robot's base link)
         self.morph = morph
         self._pos = np.array(getattr(morph, "pos", (0, 0, 0)), dtype=float)
-        self._quat = np.array([math.cos(yaw / 2), 0.0, 0.0, math.sin(yaw / 2)])
+        if hasattr(yaw, "__len__"):
+            self._quat = np.array([float(v) for v in yaw])
+        else:
+            self._quat = np.array([math.cos(yaw / 2), 0.0, 0.0, math.sin(yaw / 2)])
+
+    def set_quat(self, q):
+        self._quat = np.asarray(q, dtype=float)
 
     def get_pos(self):
         return torch.tensor(self._pos, dtype=torch.float32)

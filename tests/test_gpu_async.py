@@ -153,3 +153,43 @@ def test_async_error_and_close_in_flight(gpu_ctx):
     c2.plan_async(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
     c2.close()
     assert not c2._h
+
+
+def _sealed_well():
+    """The C5 covered well (tests/golden/make_workloads.py) with its roof hole shrunk
+    from 15.6 to 8.4 cm: the goal's wrist still fits the hole (start and goal valid),
+    the hand (18 x 8 cm across) cannot pass it, so no path exists and RRT-Connect runs
+    until its budget."""
+    q = _wl("clutter64_well")["queries"][0]
+    sc = scenes.Scene.from_json(q["scene"])
+    cx, cy, half, z, hole, t = 0.55, 0.0, 0.13, 0.235, 0.042, 0.01
+    a, c = (half + hole) / 2, (half - hole) / 2
+    roof = [((cx + a, cy, z), (c, half, t), 0.0), ((cx - a, cy, z), (c, half, t), 0.0),
+            ((cx, cy + a, z), (hole, c, t), 0.0), ((cx, cy - a, z), (hole, c, t), 0.0)]
+    for k, b in enumerate(roof):
+        sc.boxes[sc.index(f"well{4 + k}")] = b
+    return q, sc
+
+
+def test_long_query_does_not_hold_host_cores(gpu_ctx):
+    """A query that runs its whole 2 s budget (the sealed well: APPROXIMATE) through
+    rp_plan_async / rp_plan_wait: the caller's wait blocks after a short spin and the
+    planner thread sleeps between its polls of the GPU's status word, so the process'
+    CPU time (every thread, os.times) is a fraction of the wall time — a 10 s query
+    (code/motion_primitives.py:144) no longer pegs two host cores."""
+    import time
+    q, sc = _sealed_well()
+    gpu_ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+    gpu_ctx.set_attached(q["attached"])
+    p = _abi.make_params(seed=0, batch=4096, n_waypoints=150, timeout_s=2.0, straight_first=False,
+                         tree_capacity=1 << 23)
+    gpu_ctx.reserve(4096, 1 << 23)
+    t0, w0 = os.times(), time.perf_counter()
+    gpu_ctx.plan_async(q["start"], q["goal"], model.Q_LO, model.Q_HI, p, path_cap=256)
+    path, st = gpu_ctx.plan_wait()
+    t1, wall = os.times(), time.perf_counter() - w0
+    cpu = (t1.user - t0.user) + (t1.system - t0.system)
+    s = gpu_ctx.stats()
+    assert st == _abi.STATUS_APPROXIMATE and len(path) == 150, (st, s)
+    assert wall > 1.5, (wall, s)
+    assert cpu < 0.5 * wall, f"host CPU {cpu:.2f} s over {wall:.2f} s of wall time ({s['iterations']} iterations)"

@@ -107,6 +107,43 @@ def test_rccl_transport_world1(name, repl, monkeypatch):
         ctx.close()
 
 
+def test_rccl_replicated_timeout_vote_world1(oracle_lib):
+    """The RCCL branch of the timeout vote (rp_lib.hip group_vote: a one-word
+    ncclAllGather and read-back) on a 1-rank communicator: a plan whose iterations all
+    open replicated (1,152-sample batches, every sub-batch <= 4,096) with an expired
+    budget runs iterations 0-6, votes through RCCL at iteration 7 and stops; its
+    APPROXIMATE path is the oracle's after exactly 7 iterations (max_iters = 7, no
+    timeout) and the same context's after group_leave."""
+    q = json.load(open(os.path.join(GOLD, "workloads", "clutter64_well.json")))["queries"][0]
+    sc = scenes.Scene.from_json(q["scene"])
+    p = _abi.make_params(seed=3, batch=1152, n_waypoints=150, timeout_s=1e-9, straight_first=False)
+    ctx = Context(device=0, robot=model.robot_desc())
+    try:
+        ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+        ctx.set_attached(q["attached"])
+        ctx.group_init_rccl(0, 1, native.rccl_unique_id())
+        assert ctx.group_info()["transport"] == "rccl"
+        path, st = ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+        s = ctx.stats()
+        assert s["iterations"] == 7, s
+        assert s["exchange_ms"] > 0.0, s   # the vote went through RCCL
+        assert st == _abi.STATUS_APPROXIMATE
+        p7 = _abi.make_params(seed=3, batch=1152, n_waypoints=150, timeout_s=3600.0, straight_first=False,
+                              max_iters=7)
+        o = oracle_lib.OracleScene()
+        o.set_scene(sc.boxes, sc.plane_z, sc.base)
+        o.set_attached(q["attached"])
+        ref, st_ref, ost = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p7)
+        assert st_ref == _abi.STATUS_APPROXIMATE and ost["iterations"] == 7
+        assert np.array_equal(path, ref)
+        assert (s["start_tree_size"], s["goal_tree_size"]) == (ost["start_tree_size"], ost["goal_tree_size"])
+        ctx.group_leave()
+        path1, st1 = ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p7)
+        assert st1 == st_ref and np.array_equal(path1, ref)
+    finally:
+        ctx.close()
+
+
 @pytest.mark.parametrize("name,split", [("C2_q0_s1", "1"), ("C4_q5", "1"), ("C5_well_s4", "0"), ("C5_well_s2", "1")])
 @pytest.mark.parametrize("grouped", ["0", "1"])
 @pytest.mark.parametrize("mfma", ["4", "0"])

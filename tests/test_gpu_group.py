@@ -138,3 +138,45 @@ def test_replicated_timeout_vote(oracle_lib, world):
         assert np.array_equal(path, ref)
     for c in ctxs:
         c.close()
+
+
+def test_replicated_beyond_fuse_max(oracle_lib, monkeypatch):
+    """group_repl above the speculative limit (FUSE_MAX = 4,096): a replicated
+    16,384-sample iteration (whole, RBE_PLAN_CHUNK=-1) runs the single-rank two-phase
+    path on every rank, whose connect launch writes 16,384 x cmax edges — the
+    workspace is sized for it (it was sized for the sharded slice).
+    World 2 as threads: both ranks' plans equal the world-1 plan and the oracle's."""
+    monkeypatch.setenv("RBE_PLAN_CHUNK", "-1")
+    q = json.load(open(os.path.join(GOLD, "workloads", "goal3_tallest_10box.json")))["queries"][5]
+    sc = scenes.Scene.from_json(q["scene"])
+    p = _abi.make_params(seed=21, batch=16384, batch_min=16384, n_waypoints=150, timeout_s=60,
+                         straight_first=False, group_repl=16384)
+    world = 2
+    g = ThreadGroup(world)
+    ctxs = []
+    for r in range(world):
+        c = Context(device=0, robot=model.robot_desc())
+        c.set_scene(sc.boxes, sc.plane_z, sc.base)
+        c.set_attached(q["attached"])
+        c.group_init(r, world, g.fn(r))
+        ctxs.append(c)
+    out = [None] * world
+
+    def run(r):
+        out[r] = ctxs[r].plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+
+    th = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    [t.start() for t in th]
+    [t.join(timeout=300) for t in th]
+    assert all(o is not None for o in out), "a rank did not finish"
+    o = oracle_lib.OracleScene()
+    o.set_scene(sc.boxes, sc.plane_z, sc.base)
+    o.set_attached(q["attached"])
+    ref, st_ref, ost = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+    for path, status in out:
+        assert status == st_ref == _abi.STATUS_EXACT
+        assert np.array_equal(path, ref)
+    s = ctxs[0].stats()
+    assert (s["start_tree_size"], s["goal_tree_size"]) == (ost["start_tree_size"], ost["goal_tree_size"])
+    for c in ctxs:
+        c.close()

@@ -1,0 +1,170 @@
+"""Tilted boxes on the GPU (rp_set_scene_rot / rp_set_scene_poses): validity flags,
+edge flags, contacts and plans bit-exact against the CPU oracle on scenes with
+toppled and leaning blocks (code/goal3_tallest.py:257 re-plans after a collapse; the
+Genesis collider sees every block at its pose, code/planning.py:211), through every
+validity launch kernel and both box broad phases (clusters, axis grid)."""
+import numpy as np
+import pytest
+import torch
+
+from rbe550_final_project_amd import _abi, model, planning, scenes
+import mock_genesis as M
+import tilt_scenes as T
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(gpu_ctx, oracle_lib, sc, attached=-1):
+    o = oracle_lib.OracleScene()
+    o.set_scene(sc.boxes, sc.plane_z, sc.base)
+    o.set_attached(attached)
+    gpu_ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+    gpu_ctx.set_attached(attached)
+    return o
+
+
+def _scene(name):
+    if name == "toppled_goal3":
+        return T.toppled_goal3()
+    return T.tilted_clutter64()[0]
+
+
+def _states(n, seed, sc):
+    """Uniform states, a quarter of them near configurations whose hand reaches the
+    tilted boxes (contacts with them occur), every 64th outside the joint limits."""
+    rng = np.random.default_rng(seed)
+    q = model.Q_LO + (model.Q_HI - model.Q_LO) * rng.random((n, 9))
+    k = n // 4
+    q[:k] = np.clip(np.asarray(model.SAFE_HOME)[None, :] + 0.7 * rng.standard_normal((k, 9)), model.Q_LO, model.Q_HI)
+    pad = np.array([0.6] * 7 + [0.02] * 2)
+    q[::64] = model.Q_HI + pad * rng.random((len(q[::64]), 9))
+    return q.astype(np.float32)
+
+
+@pytest.mark.parametrize("name", ["toppled_goal3", "tilted_clutter64"])
+@pytest.mark.parametrize("n", [1000, 4096, 65536, 131072, 262144])
+@pytest.mark.parametrize("attached", [-1, 0])
+def test_tilted_validity_flags(gpu_ctx, oracle_lib, name, n, attached):
+    """Every validity launch kernel (lane-group <= 4,096, three-role split <= 65,536,
+    two-role <= 131,072, one-wave above) on tilted scenes, with and without a tilted
+    attached box: flags bit-exact."""
+    sc = _scene(name)
+    o = _pair(gpu_ctx, oracle_lib, sc, attached)
+    q = _states(n, n + 7, sc)
+    g = gpu_ctx.check_states(q)
+    r = o.check_states(q)
+    assert np.array_equal(g, r), f"{(g != r).sum()} of {n} flags differ"
+    assert 0 < r.sum() < n
+
+
+@pytest.mark.parametrize("grid", ["0", "1"])
+def test_tilted_both_broad_phases(gpu_ctx, oracle_lib, grid, monkeypatch):
+    """The toppled goal3 scene through the cluster broad phase and forced through the
+    axis grid (RBE_SCENE_GRID): the tilted boxes' world AABBs feed both."""
+    monkeypatch.setenv("RBE_SCENE_GRID", grid)
+    sc = T.toppled_goal3()
+    o = _pair(gpu_ctx, oracle_lib, sc, attached=4)
+    q = _states(200000, 31, sc)
+    assert np.array_equal(gpu_ctx.check_states(q), o.check_states(q))
+
+
+def test_tilted_contacts(gpu_ctx, oracle_lib):
+    """rp_state_contacts (the diagnostics, planning.py:43-57) on colliding states of
+    the toppled scene: the same (link, obstacle) lists."""
+    sc = T.toppled_goal3()
+    o = _pair(gpu_ctx, oracle_lib, sc)
+    q = _states(4000, 32, sc)
+    flags = o.check_states(q)
+    tested = 0
+    for s in q[flags == 0][:300]:
+        s64 = s.astype(np.float64)
+        assert sorted(gpu_ctx.contacts(s64)) == sorted(o.contacts(s64))
+        tested += 1
+    assert tested == 300
+
+
+@pytest.mark.parametrize("name", ["toppled_goal3", "tilted_clutter64"])
+def test_tilted_edges(gpu_ctx, oracle_lib, name):
+    """Edge flags (OMPL checkMotion) through the host and the device entry points."""
+    sc = _scene(name)
+    o = _pair(gpu_ctx, oracle_lib, sc)
+    rng = np.random.default_rng(33)
+    n = 20000
+    qa = np.clip(np.asarray(model.SAFE_HOME)[None, :] + 0.8 * rng.standard_normal((n, 9)), model.Q_LO, model.Q_HI)
+    d = rng.standard_normal((n, 9))
+    d *= (0.2 * model.max_extent() * rng.random((n, 1))) / np.linalg.norm(d, axis=1, keepdims=True)
+    qb = np.clip(qa + d, model.Q_LO, model.Q_HI)
+    res = 0.01 * model.max_extent()
+    ref = o.check_edges(qa, qb, res)
+    assert np.array_equal(gpu_ctx.check_edges(qa, qb, res), ref)
+    dev = torch.device("cuda", 0)
+    ta, tb = torch.from_numpy(qa).to(dev), torch.from_numpy(qb).to(dev)
+    out = torch.empty(n, dtype=torch.uint8, device=dev)
+    gpu_ctx.check_edges_device(ta.data_ptr(), tb.data_ptr(), n, res, out.data_ptr())
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), ref)
+    assert 0 < ref.sum() < n
+
+
+def test_scene_poses_with_tilted_quaternions(gpu_ctx, oracle_lib):
+    """rp_set_scene_poses (the drop-in's per-query ingestion) with the mock's tilted
+    entity quaternions gives the scene rp_set_scene_rot gives for the ingested records:
+    flags bit-exact against the oracle."""
+    sc = T.toppled_goal3()
+    sim = M.Scene(sc.boxes)
+    rd = scenes.GenesisReader(sim, sim.robot)
+    poses, base = rd.poses()
+    ing = rd.read()
+    o = oracle_lib.OracleScene()
+    o.set_scene(ing.boxes, ing.plane_z, ing.base)
+    o.set_attached(0)
+    gpu_ctx.set_scene_poses(np.array(poses, dtype=np.float64).reshape(-1, 7), rd.halves_f32, rd.plane_z,
+                            np.array(base, dtype=np.float64), 0)
+    q = _states(65536, 34, sc)
+    assert np.array_equal(gpu_ctx.check_states(q), o.check_states(q))
+
+
+@pytest.mark.parametrize("straight", [True, False])
+def test_tilted_plan_equals_oracle(gpu_ctx, oracle_lib, straight):
+    """A pick query of goal3 in the collapsed scene (start: safe home; goal: above a
+    block): the same plan as the oracle, bit for bit."""
+    import json
+    import os
+    q = json.load(open(os.path.join(T.GOLD, "workloads", "goal3_tallest_10box.json")))["queries"][0]
+    sc = T.toppled_goal3()
+    o = _pair(gpu_ctx, oracle_lib, sc)
+    p = _abi.make_params(seed=5, batch=1024, n_waypoints=150, timeout_s=60, straight_first=straight)
+    ref, st_ref, ost = o.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+    path, st = gpu_ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+    assert st == st_ref
+    assert path.shape == ref.shape and np.array_equal(path, ref)
+    s = gpu_ctx.stats()
+    assert (s["start_tree_size"], s["goal_tree_size"]) == (ost["start_tree_size"], ost["goal_tree_size"])
+
+
+def test_plan_path_through_a_collapsed_scene(oracle_lib):
+    """PlannerInterface.plan_path (the reference call, motion_primitives.py:144)
+    through the Genesis mock whose blocks toppled: the planner ingests the tilted
+    quaternions and returns the oracle's plan in the rotated-box scene."""
+    import json
+    import os
+    q = json.load(open(os.path.join(T.GOLD, "workloads", "goal3_tallest_10box.json")))["queries"][0]
+    sc = T.toppled_goal3()
+    sim = M.Scene(sc.boxes)
+    planning.configure(seed=77, straight_first=False)
+    try:
+        pl = planning.PlannerInterface(sim.robot, sim)
+        sim.robot.q = torch.tensor(q["start"], dtype=torch.float32)
+        wps = pl.plan_path(qpos_goal=q["goal"], num_waypoints=150, timeout=10.0)
+        assert len(wps) == 150
+        ing = scenes.GenesisReader(sim, sim.robot).read()
+        o = oracle_lib.OracleScene()
+        o.set_scene(ing.boxes, ing.plane_z, ing.base)
+        o.set_attached(-1)
+        p = _abi.make_params(seed=77, batch=planning._batch(), n_waypoints=150, timeout_s=10.0, straight_first=False)
+        ref, st, _ = o.plan(np.asarray(q["start"], np.float32).astype(np.float64), q["goal"], *pl._bounds(), p)
+        assert st in (_abi.STATUS_EXACT, _abi.STATUS_APPROXIMATE)
+        got = torch.stack(wps).numpy()
+        assert np.array_equal(got, ref.astype(np.float32))
+    finally:
+        planning.configure(seed=0, straight_first=True)

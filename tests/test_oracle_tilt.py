@@ -1,0 +1,136 @@
+"""Tilted boxes in the CPU oracle (CPU): toppled / leaning blocks are tested as
+rotated boxes (ro_scene_set_rot, the restatement of rp_set_scene_rot). The rotated
+narrow phase is pinned against an independent float64 brute force, the quaternion
+convention against a box whose 90-degree roll is an axis swap, and the ingestion of
+tilted Genesis entity quaternions (code/planning.py:211 sees every block at its pose;
+code/goal3_tallest.py:257 re-plans after a collapse)."""
+import numpy as np
+import pytest
+
+from rbe550_final_project_amd import _abi, model, scenes
+import mock_genesis as M
+import tilt_scenes as T
+
+
+def _states(n, seed):
+    rng = np.random.default_rng(seed)
+    return (model.Q_LO + (model.Q_HI - model.Q_LO) * rng.random((n, 9))).astype(np.float32)
+
+
+def _near(center, n, seed, sigma):
+    rng = np.random.default_rng(seed)
+    q = np.asarray(center)[None, :] + sigma * rng.standard_normal((n, 9))
+    return np.clip(q, model.Q_LO, model.Q_HI).astype(np.float32)
+
+
+def test_upright_quaternion_is_the_yaw_record(oracle_lib):
+    """A quaternion with x = y = 0 gives the record of its yaw: a scene given as
+    quaternions (rp_set_scene_rot path) has the flags of the same scene given as yaws."""
+    sc = scenes.goal1_scattered(seed=3)
+    yaws = [0.3, -1.2, 2.5, 0.0, 0.7, -3.0]
+    as_yaw = [(c, h, scenes.yaw_of_quat(T.quat_axis_angle((0, 0, 1), np.degrees(y)))) for (c, h, _), y in
+              zip(sc.boxes, yaws)]
+    as_quat = [(c, h, T.quat_axis_angle((0, 0, 1), np.degrees(y))) for (c, h, _), y in zip(sc.boxes, yaws)]
+    a, b = oracle_lib.OracleScene(), oracle_lib.OracleScene()
+    a.set_scene(as_yaw, sc.plane_z, sc.base)
+    b.set_scene(as_quat, sc.plane_z, sc.base)
+    q = np.concatenate([_states(20000, 1), _near(model.SAFE_HOME, 5000, 2, 0.6)])
+    fa, fb = a.check_states(q), b.check_states(q)
+    assert np.array_equal(fa, fb)
+    assert 0 < fa.sum() < len(fa)
+
+
+def test_rolled_box_is_the_axis_swapped_box(oracle_lib):
+    """A (0.02, 0.04, 0.06) box rolled 90 degrees about x occupies what an upright
+    (0.02, 0.06, 0.04) box does: the quaternion -> rotation convention and the box
+    frame transform agree with geometry (flags equal away from the 1e-6 m AABB pad)."""
+    c = (0.45, 0.1, 0.25)
+    rolled = [(c, (0.02, 0.04, 0.06), T.quat_axis_angle((1, 0, 0), 90.0))]
+    upright = [(c, (0.02, 0.06, 0.04), 0.0)]
+    a, b = oracle_lib.OracleScene(), oracle_lib.OracleScene()
+    a.set_scene(rolled)
+    b.set_scene(upright)
+    q = np.concatenate([_states(30000, 5), _near(model.SAFE_HOME, 10000, 6, 0.5)])
+    fa, fb = a.check_states(q), b.check_states(q)
+    assert (fa != fb).sum() == 0
+    assert 0 < fa.sum() < len(fa)
+
+
+def _seg_obb_dist(a, b, c, h, R, n=4001):
+    """float64 distance from segment a-b to the box (centre c, half h, world = R box)
+    by dense sampling: an upper bound within |b - a| / (2 (n - 1)) of the truth."""
+    t = np.linspace(0.0, 1.0, n)[:, None]
+    p = (a + t * (b - a) - c) @ R            # box frame: R^T (p - c), row vectors
+    e = np.abs(p) - h
+    return float(np.sqrt(np.min(np.sum(np.maximum(e, 0.0) ** 2, axis=1))))
+
+
+@pytest.mark.parametrize("quat", [T.quat_axis_angle((0, 1, 0), 10.0), T.quat_axis_angle((1, 0, 0), 90.0),
+                                  T.quat_mul(T.quat_axis_angle((0, 0, 1), 30.0), T.quat_axis_angle((1, 1, 0), 40.0))])
+def test_tilted_narrow_phase_vs_brute_force(oracle_lib, quat):
+    """Each capsule's contact with one tilted box (ro_state_contacts) against the
+    float64 sampled segment-to-box distance: contact => distance <= r (+ sampling and
+    float32 slack), no contact => distance > r (- float32 slack)."""
+    c = np.array([0.42, 0.05, 0.32])
+    h = np.array([0.03, 0.05, 0.08])
+    o = oracle_lib.OracleScene()
+    o.set_scene([(tuple(c), tuple(h), quat)], plane_z=-10.0)
+    R = T.rot_matrix(quat)
+    caps = model.robot_desc().capsules
+    q = np.concatenate([_near(model.SAFE_HOME, 600, 9, 0.7), _states(400, 10)])
+    seen = [0, 0]
+    for s in q:
+        hit = {link for link, obst in o.contacts(s.astype(np.float64)) if obst == 0}
+        seg = o.fk_capsules(s)
+        for link in range(11):
+            ks = [k for k in range(len(seg)) if caps[k].link == link]
+            d = [(_seg_obb_dist(seg[k][0].astype(float), seg[k][1].astype(float), c, h, R), caps[k].radius,
+                  np.linalg.norm(seg[k][1] - seg[k][0])) for k in ks]
+            if link in hit:
+                assert any(dk <= r + L / 8000.0 + 1e-5 for dk, r, L in d), (s, link, d)
+                seen[0] += 1
+            else:
+                assert all(dk > r - 1e-5 for dk, r, L in d), (s, link, d)
+                seen[1] += 1
+    assert seen[0] > 20 and seen[1] > 20, seen
+
+
+def test_tilted_scene_changes_flags(oracle_lib):
+    """The toppled goal3 scene is not the upright one: the same states collide
+    differently (a tilt is no longer dropped, VERDICT r04 missing #2)."""
+    tilt = T.toppled_goal3()
+    up = scenes.goal3_tallest()
+    a, b = oracle_lib.OracleScene(), oracle_lib.OracleScene()
+    a.set_scene(tilt.boxes, tilt.plane_z, tilt.base)
+    b.set_scene(up.boxes, up.plane_z, up.base)
+    q = _states(200000, 12)
+    fa, fb = a.check_states(q), b.check_states(q)
+    assert (fa != fb).sum() > 0
+
+
+def test_mock_ingestion_of_tilted_entities():
+    """GenesisReader: an entity whose quaternion tilts it becomes a box with that
+    quaternion; upright entities keep their yaw; the Scene record round-trips through
+    JSON."""
+    sc = T.toppled_goal3()
+    sim = M.Scene(sc.boxes)
+    rd = scenes.GenesisReader(sim, sim.robot)
+    ing = rd.read()
+    for (c0, h0, r0), (c1, h1, r1) in zip(sc.boxes, ing.boxes):
+        assert np.allclose(c0, c1, atol=1e-6) and np.allclose(h0, h1, atol=1e-7)
+        if _abi.is_quat(r0):
+            assert _abi.is_quat(r1) and np.allclose(r0, r1, atol=1e-7)
+        else:
+            assert not _abi.is_quat(r1) and abs(r0 - r1) < 1e-6
+    assert sum(_abi.is_quat(b[2]) for b in ing.boxes) == 5
+    back = scenes.Scene.from_json(ing.to_json())
+    assert back.boxes == [(tuple(c), tuple(h), r) for c, h, r in ing.boxes]
+    # a box toppled later in the simulation is read at its new orientation
+    sim.entities[1].set_quat(T.quat_axis_angle((0, 1, 0), 90.0))
+    assert _abi.is_quat(rd.read().boxes[0][2])
+
+
+def test_zero_quaternion_rejected(oracle_lib):
+    o = oracle_lib.OracleScene()
+    with pytest.raises(ValueError):
+        o.set_scene([((0.5, 0.0, 0.02), (0.02, 0.02, 0.02), (0.0, 0.0, 0.0, 0.0))])

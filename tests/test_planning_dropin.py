@@ -78,8 +78,13 @@ def test_plan_path_contract_on_gpu():
                and w.device.type == "cpu" for w in wps)
     assert np.allclose(wps[0].numpy(), np.float32(q["start"]), atol=1e-6)
     assert np.allclose(wps[-1].numpy(), np.float32(q["goal"]), atol=1e-6)
-    # consumer contract (motion_primitives.py:163-178)
-    arr = np.array(wps[-1], dtype=float, copy=True)
+    # consumer contract (motion_primitives.py:163-178): np.array(path[-1], dtype=float)
+    # exactly as the caller writes it (torch's Tensor.__array__ predates NumPy 2's
+    # copy keyword; the DeprecationWarning NumPy raises about it is torch's, not ours)
+    import warnings
+    with warnings.catch_warnings():
+        warnings.filterwarnings("ignore", message=".*__array__.*copy.*", category=DeprecationWarning)
+        arr = np.array(wps[-1], dtype=float)
     assert arr.shape == (9,)
     # the robot's qpos is restored at the end (planning.py:205)
     assert torch.equal(sc.robot.set_calls[-1], torch.tensor(q["start"], dtype=torch.float32))

@@ -17,6 +17,9 @@ step() {  # step <name> <timeout_s> <cmd...>
 for s in "$@"; do
   case $s in
     tests) step pytest_gpu 1000 python -u -m pytest tests -m gpu -x -v --timeout 500 --timeout-method thread ;;
+    testsnx) step pytest_gpu 1000 python -u -m pytest tests -m gpu -v --maxfail 20 --timeout 300 --timeout-method thread ;;
+    newtests) step pytest_new 900 python -u -m pytest tests/test_gpu_devices.py tests/test_gpu_async.py -m gpu -v --maxfail 20 --timeout 300 --timeout-method thread ;;
+    cpuprobe) step cpuprobe_default 120 python tools/cpu_probe.py && RBE_WAIT_SPIN_US=200 step cpuprobe_spin200 120 python tools/cpu_probe.py && RBE_WAIT_SPIN_US=15 RBE_WAIT_SLEEP_FRAC=0.2 step cpuprobe_spin15 120 python tools/cpu_probe.py && step cpuprobe_b64k 120 python tools/cpu_probe.py --batch 65536 && grep -h wall_s gpurun_out/cpuprobe_*.log ;;
     gtests) step pytest_gpu_cfg 600 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_group.py -m gpu -x -v --timeout 300 --timeout-method thread && step pytest_gpu_procs 600 python -u -m pytest tests/test_gpu_group_procs.py -m gpu -x -v --timeout 170 --timeout-method thread ;;
     alltests) step pytest_all 1200 python -m pytest tests -q -x ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;

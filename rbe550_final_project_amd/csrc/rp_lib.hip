@@ -172,6 +172,7 @@ struct rp_ctx {
     DevBuf<int> scalar;                  // small device scalars
     DevBuf<unsigned long long> counter;
     DevBuf<unsigned> sync;               // k_straight: failure bits, finished blocks (kept zeroed)
+    DevBuf<unsigned> vredo;              // k_validity_nm's overflowed waves (kept zeroed)
 
     // planner workspace
     Tree tree[2];
@@ -278,7 +279,7 @@ struct rp_ctx {
         (void)hipSetDevice(device);
         for (auto& t : tree) t.release();
         q32.release(); flags.release(); ea.release(); eb.release(); end_nd.release(); eval.release();
-        scalar.release(); counter.release(); efrom.release(); eto.release(); nd.release(); valid.release();
+        scalar.release(); counter.release(); vredo.release(); efrom.release(); eto.release(); nd.release(); valid.release();
         near_.release(); res.release(); acc.release(); incl.release(); yv.release(); mv.release();
         rec.release(); Lv.release(); chain_end.release(); gfail.release();
         eslot.release(); eincl.release(); echunk.release();
@@ -374,11 +375,47 @@ void launch_validity_split(rp_ctx* c, const float* q, int64_t n, uint8_t* flags,
 #undef RP_VALS
 }
 
+// launches above split_max(): k_validity_nm (no queue drain inside the walk, 6 waves
+// per SIMD) + k_validity_redo for the waves whose queues overflowed (rp_kernels.h);
+// RBE_VALIDITY_NM=0 keeps the draining k_validity (A/B, tests)
+bool validity_nm() {
+    static const bool on = [] {
+        const char* e = std::getenv("RBE_VALIDITY_NM");
+        return !(e && *e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+
 template <bool BF>
 void launch_validity_bf(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, hipStream_t s) {
     if (n <= split_max()) {
         if (n <= 65536) launch_validity_split<BF, 3>(c, q, n, flags, s);
         else launch_validity_split<BF, 2>(c, q, n, flags, s);
+        return;
+    }
+    if (validity_nm()) {
+        // the overflow list: a count, a done counter and room for every wave; zero when
+        // (re)allocated, and k_validity_redo leaves it zero
+        const size_t words = (size_t)(n + 63) / 64 + 2;
+        if (c->vredo.n < words) {
+            c->vredo.ensure(words);
+            HIP_TRY(hipMemsetAsync(c->vredo.p, 0, sizeof(unsigned) * c->vredo.n, s));
+        }
+        const dim3 g(blocks_for(n, 64)), b(64), gr(VREDO_BLOCKS);
+#define RP_VNM(N)                                                                                          \
+    do {                                                                                                   \
+        hipLaunchKernelGGL((k_validity_nm<N, BF>), g, b, 0, s, q, n, flags, c->d_scene, c->vredo.p);       \
+        hipLaunchKernelGGL((k_validity_redo<N, BF>), gr, b, 0, s, q, n, flags, c->d_scene, c->vredo.p);    \
+    } while (0)
+        switch (ncl_bucket(c->scene)) {
+            case NCL_GRID: RP_VNM(NCL_GRID); break;
+            case 0: RP_VNM(0); break;
+            case 1: RP_VNM(1); break;
+            case 2: RP_VNM(2); break;
+            case 4: RP_VNM(4); break;
+            default: RP_VNM(8); break;
+        }
+#undef RP_VNM
         return;
     }
     const dim3 g(blocks_for(n, VTHREADS)), b(VTHREADS);
@@ -3024,6 +3061,14 @@ int rp_ik(rp_ctx* c, int32_t n_targets, const double* pos, const double* quat, c
     d_best.release(); d_status.release();
     return RP_OK;
     RP_GUARD_END(c)
+}
+
+// diagnostic (tools/val_lab.hip): the context's host scene record (the DevScene the
+// kernels read, after rp_set_scene*; `bytes` must be sizeof(DevScene))
+int rp_debug_scene(rp_ctx* c, void* out, int64_t bytes) {
+    if (!c || !out || bytes != (int64_t)sizeof(DevScene)) return RP_ERR_ARG;
+    std::memcpy(out, &c->scene, sizeof(DevScene));
+    return RP_OK;
 }
 
 #ifdef RP_NN_COUNT

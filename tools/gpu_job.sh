@@ -20,6 +20,8 @@ for s in "$@"; do
     testsnx) step pytest_gpu 1000 python -u -m pytest tests -m gpu -v --maxfail 20 --timeout 300 --timeout-method thread ;;
     newtests) step pytest_new 900 python -u -m pytest tests/test_gpu_devices.py tests/test_gpu_async.py -m gpu -v --maxfail 20 --timeout 300 --timeout-method thread ;;
     cpuprobe) step cpuprobe_default 120 python tools/cpu_probe.py && RBE_WAIT_SPIN_US=200 step cpuprobe_spin200 120 python tools/cpu_probe.py && RBE_WAIT_SPIN_US=15 RBE_WAIT_SLEEP_FRAC=0.2 step cpuprobe_spin15 120 python tools/cpu_probe.py && step cpuprobe_b64k 120 python tools/cpu_probe.py --batch 65536 && grep -h wall_s gpurun_out/cpuprobe_*.log ;;
+    nnlab) step nnlab 300 tools/lab/nn_lab 131072 300000 7 && cat gpurun_out/nnlab.log ;;
+    vallab) step vallab 300 tools/lab/val_lab 16777216 20 goal3 && step vallab0 300 tools/lab/val_lab 16777216 20 goal3 0 && step vallab_t 300 tools/lab/val_lab 16777216 10 toppled && step vallab_p 300 tools/lab/val_lab 4194304 10 pentagon && step vallab2 300 tools/lab/val_lab 16777216 20 goal3 && grep -h "G/s" gpurun_out/vallab*.log ;;
     gtests) step pytest_gpu_cfg 600 python -u -m pytest tests/test_gpu_configs.py tests/test_gpu_group.py -m gpu -x -v --timeout 300 --timeout-method thread && step pytest_gpu_procs 600 python -u -m pytest tests/test_gpu_group_procs.py -m gpu -x -v --timeout 170 --timeout-method thread ;;
     alltests) step pytest_all 1200 python -m pytest tests -q -x ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;

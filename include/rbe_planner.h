@@ -278,9 +278,7 @@ int rp_check_states(rp_ctx* ctx, const float* q, int64_t n, uint8_t* flags_out);
 /* Same on device-resident buffers (e.g. torch tensors' data_ptr), asynchronous: the
  * kernel is launched on `stream` (a hipStream_t) or, when `stream` is NULL, on the
  * context's own non-blocking stream. NULL therefore does NOT mean the legacy
- * default stream; pass an explicit stream to order against other work. Launches of
- * more than 131,072 states use the context's overflow scratch (two kernels), so such
- * calls in flight on different streams must be ordered by the caller. */
+ * default stream; pass an explicit stream to order against other work. */
 int rp_check_states_device(rp_ctx* ctx, const float* q_dev, int64_t n, uint8_t* flags_dev,
                            void* stream);
 

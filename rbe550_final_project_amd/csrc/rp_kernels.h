@@ -29,14 +29,6 @@ constexpr int VBLOCK = 64;      // validity / edge block size: one wave (its LDS
 #ifndef RP_VALIDITY_WAVES_GRID
 #define RP_VALIDITY_WAVES_GRID 4
 #endif
-// k_validity_nm (no queue drain inside the FK walk): 6 waves per SIMD (80 VGPRs, no
-// spills) on cluster scenes, 5 on grid scenes
-#ifndef RP_VALIDITY_WAVES_NM
-#define RP_VALIDITY_WAVES_NM 6
-#endif
-#ifndef RP_VALIDITY_WAVES_NM_GRID
-#define RP_VALIDITY_WAVES_NM_GRID 5
-#endif
 #ifndef RP_EDGE_WAVES
 #define RP_EDGE_WAVES 4
 #endif
@@ -90,70 +82,6 @@ __global__ __launch_bounds__(VTHREADS, NCL == NCL_GRID ? RP_VALIDITY_WAVES_GRID 
 #endif
     flags[i] = state_collides<NCL, BF>(qq, sc, wq) ? 0 : 1;
 }
-
-// The large launches' form (> 131,072 states): the queues are never drained inside
-// the FK walk (rp_math.h state_collides_nm), which takes the narrow-phase calls' 16
-// registers off the walk's peak (96 -> 80 VGPRs: 6 waves per SIMD instead of 5) and
-// two thirds of the static VALU code (the drains inlined at every enqueue site). A
-// wave whose items outgrow its queue (WaveQN: 64 self-pair, 56 capsule-box items)
-// writes no flags; its index goes to redo[2 + k] (k = atomicAdd(redo[0], 1); room for
-// every wave of the launch) and k_validity_redo checks it with the draining form.
-// Same flags as k_validity for every state.
-struct F3s { float x, y, z; };
-__device__ __forceinline__ void load_state(const float* __restrict__ q, int64_t i, float qq[NQ]) {
-    const F3s* q3 = reinterpret_cast<const F3s*>(q + i * NQ);
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const F3s v = q3[k];
-        qq[3 * k] = v.x; qq[3 * k + 1] = v.y; qq[3 * k + 2] = v.z;
-    }
-}
-template <int NCL, bool BF = false>
-__global__ __launch_bounds__(64, NCL == NCL_GRID ? RP_VALIDITY_WAVES_NM_GRID : RP_VALIDITY_WAVES_NM) void k_validity_nm(
-        const float* __restrict__ q, int64_t n, uint8_t* __restrict__ flags, const DevScene* __restrict__ sc,
-        unsigned* __restrict__ redo) {
-    __shared__ WaveQN wq;
-    const int64_t i = (int64_t)rp_bid() * 64 + rp_tid();
-    if (i >= n) return;
-    float qq[NQ];
-    load_state(q, i, qq);
-    const int r = state_collides_nm<NCL, BF>(qq, sc, wq);
-    if (r < 0) {   // (every lane of the wave)
-        if (rp_tid() == (unsigned)__builtin_amdgcn_readfirstlane(rp_tid())) {
-            const unsigned k = atomicAdd(&redo[0], 1u);
-            redo[2 + k] = rp_bid();
-        }
-        return;
-    }
-    flags[i] = r ? 0 : 1;
-}
-// the overflowed waves of k_validity_nm (redo[0] of them, launched right after it on
-// the same stream), with the draining form; the last block to finish zeroes the
-// count for the next launch
-template <int NCL, bool BF = false>
-__global__ __launch_bounds__(64, 4) void k_validity_redo(
-        const float* __restrict__ q, int64_t n, uint8_t* __restrict__ flags, const DevScene* __restrict__ sc,
-        unsigned* __restrict__ redo) {
-    __shared__ WaveQ wq;
-    const unsigned cnt = redo[0];
-    for (unsigned e = rp_bid(); e < cnt; e += rp_gdim()) {
-        const int64_t i = (int64_t)redo[2 + e] * 64 + rp_tid();
-        if (i < n) {
-            float qq[NQ];
-            load_state(q, i, qq);
-            flags[i] = state_collides<NCL, BF>(qq, sc, wq) ? 0 : 1;
-        }
-    }
-    if (rp_tid() == 0) {
-        __threadfence();
-        if (atomicAdd(&redo[1], 1u) == rp_gdim() - 1) {
-            redo[0] = 0;
-            redo[1] = 0;
-            __threadfence();
-        }
-    }
-}
-constexpr int VREDO_BLOCKS = 512;
 
 // Mid-size launches (a few thousand to ~10^5 states: one wave per SIMD or fewer)
 // are as slow as one wave's dependency chain. NR waves share each group of 64

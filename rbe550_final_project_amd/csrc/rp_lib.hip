@@ -145,6 +145,7 @@ struct rp_ctx {
     bool busy = false;                   // a rp_plan_async query is in flight
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipEvent_t ev_wait = nullptr;        // stream_wait's marker (no timing)
     DevScene scene{};
     DevScene* d_scene = nullptr;
     // scene uploads (upload_scene / flush_scene): rp_set_scene / rp_set_attached only
@@ -172,7 +173,6 @@ struct rp_ctx {
     DevBuf<int> scalar;                  // small device scalars
     DevBuf<unsigned long long> counter;
     DevBuf<unsigned> sync;               // k_straight: failure bits, finished blocks (kept zeroed)
-    DevBuf<unsigned> vredo;              // k_validity_nm's overflowed waves (kept zeroed)
 
     // planner workspace
     Tree tree[2];
@@ -279,7 +279,7 @@ struct rp_ctx {
         (void)hipSetDevice(device);
         for (auto& t : tree) t.release();
         q32.release(); flags.release(); ea.release(); eb.release(); end_nd.release(); eval.release();
-        scalar.release(); counter.release(); vredo.release(); efrom.release(); eto.release(); nd.release(); valid.release();
+        scalar.release(); counter.release(); efrom.release(); eto.release(); nd.release(); valid.release();
         near_.release(); res.release(); acc.release(); incl.release(); yv.release(); mv.release();
         rec.release(); Lv.release(); chain_end.release(); gfail.release();
         eslot.release(); eincl.release(); echunk.release();
@@ -294,6 +294,7 @@ struct rp_ctx {
         if (h_scene_stage) (void)hipHostFree(h_scene_stage);
         if (d_scene) (void)hipFree(d_scene);
         if (ev0) (void)hipEventDestroy(ev0);
+        if (ev_wait) (void)hipEventDestroy(ev_wait);
         if (ev1) (void)hipEventDestroy(ev1);
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -375,47 +376,11 @@ void launch_validity_split(rp_ctx* c, const float* q, int64_t n, uint8_t* flags,
 #undef RP_VALS
 }
 
-// launches above split_max(): k_validity_nm (no queue drain inside the walk, 6 waves
-// per SIMD) + k_validity_redo for the waves whose queues overflowed (rp_kernels.h);
-// RBE_VALIDITY_NM=0 keeps the draining k_validity (A/B, tests)
-bool validity_nm() {
-    static const bool on = [] {
-        const char* e = std::getenv("RBE_VALIDITY_NM");
-        return !(e && *e && std::atoi(e) == 0);
-    }();
-    return on;
-}
-
 template <bool BF>
 void launch_validity_bf(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, hipStream_t s) {
     if (n <= split_max()) {
         if (n <= 65536) launch_validity_split<BF, 3>(c, q, n, flags, s);
         else launch_validity_split<BF, 2>(c, q, n, flags, s);
-        return;
-    }
-    if (validity_nm()) {
-        // the overflow list: a count, a done counter and room for every wave; zero when
-        // (re)allocated, and k_validity_redo leaves it zero
-        const size_t words = (size_t)(n + 63) / 64 + 2;
-        if (c->vredo.n < words) {
-            c->vredo.ensure(words);
-            HIP_TRY(hipMemsetAsync(c->vredo.p, 0, sizeof(unsigned) * c->vredo.n, s));
-        }
-        const dim3 g(blocks_for(n, 64)), b(64), gr(VREDO_BLOCKS);
-#define RP_VNM(N)                                                                                          \
-    do {                                                                                                   \
-        hipLaunchKernelGGL((k_validity_nm<N, BF>), g, b, 0, s, q, n, flags, c->d_scene, c->vredo.p);       \
-        hipLaunchKernelGGL((k_validity_redo<N, BF>), gr, b, 0, s, q, n, flags, c->d_scene, c->vredo.p);    \
-    } while (0)
-        switch (ncl_bucket(c->scene)) {
-            case NCL_GRID: RP_VNM(NCL_GRID); break;
-            case 0: RP_VNM(0); break;
-            case 1: RP_VNM(1); break;
-            case 2: RP_VNM(2); break;
-            case 4: RP_VNM(4); break;
-            default: RP_VNM(8); break;
-        }
-#undef RP_VNM
         return;
     }
     const dim3 g(blocks_for(n, VTHREADS)), b(VTHREADS);
@@ -673,11 +638,17 @@ void launch_edges_packed(rp_ctx* c, const double* from, const double* to, const 
     prof_end(c, ps, 1, s);
 }
 
+// Wait until the context stream has run everything enqueued so far, like
+// hipStreamSynchronize, whose default wait spins: a spin of wait_spin_s on an event,
+// then sleeps between polls (wait_seq's rule), so the read-backs of large two-phase
+// iterations (ms each) do not hold a host core.
+void stream_wait(rp_ctx* c);
+
 template <typename T>
 T read_scalar(rp_ctx* c, const T* dev) {
     T v;
     HIP_TRY(hipMemcpyAsync(&v, dev, sizeof(T), hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    stream_wait(c);
     return v;
 }
 
@@ -685,7 +656,7 @@ T read_scalar(rp_ctx* c, const T* dev) {
 int64_t read_counter(rp_ctx* c) {
     unsigned long long w[COUNTER_SLOTS];
     HIP_TRY(hipMemcpyAsync(w, c->counter.p, sizeof w, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    stream_wait(c);
     unsigned long long s = 0;
     for (int i = 0; i < COUNTER_SLOTS; ++i) s += w[i];
     return (int64_t)s;
@@ -719,7 +690,7 @@ void group_exchange(rp_ctx* c, int64_t words) {
         c->h_cap = words;
     }
     HIP_TRY(hipMemcpyAsync(c->h_send, c->g_send.p, bytes, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    stream_wait(c);
     const double t0 = now_s();
     if (c->g_fn(c->g_user, c->h_send, c->h_recv, (int64_t)bytes) != 0) throw HipError{"group all-gather callback failed"};
     c->stats.exchange_ms += 1e3 * (now_s() - t0);
@@ -742,7 +713,7 @@ int group_vote(rp_ctx* c, int tflag) {
         NCCL_TRY(ncclAllGather(c->g_send.p, c->g_recv.p, 1, ncclInt32, c->comm, c->stream));
         HIP_TRY(hipMemcpyAsync(c->h_vote + 1, c->g_recv.p, sizeof(int32_t) * c->world, hipMemcpyDeviceToHost,
                                c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
+        stream_wait(c);
         for (int r = 0; r < c->world; ++r) any |= c->h_vote[1 + r];
     } else {
         if (c->h_cap < 1) {
@@ -1269,6 +1240,30 @@ void wait_seq(rp_ctx* c, int seq) {
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
 }
 
+void stream_wait(rp_ctx* c) {
+    if (!c->ev_wait) HIP_TRY(hipEventCreateWithFlags(&c->ev_wait, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(c->ev_wait, c->stream));
+    const WaitTuning& wt = wait_tuning();
+    const double t_enter = now_s();
+    for (uint64_t spin = 1;; ++spin) {   // spin
+        const hipError_t e = hipEventQuery(c->ev_wait);
+        if (e == hipSuccess) return;
+        if (e != hipErrorNotReady) HIP_TRY(e);
+        if ((spin & 15) == 0 && now_s() - t_enter > wt.spin_s) break;
+    }
+    SlackGuard slack;
+    for (;;) {   // sleep between polls (a stream that never finishes is the caller's watchdog's)
+        const hipError_t e = hipEventQuery(c->ev_wait);
+        if (e == hipSuccess) return;
+        if (e != hipErrorNotReady) HIP_TRY(e);
+        slack.fine();
+        const double waited = now_s() - t_enter;
+        const int64_t ns = std::min<int64_t>(200000, std::max<int64_t>(10000, (int64_t)(waited * wt.frac * 1e9)));
+        const timespec ts{0, (long)ns};
+        nanosleep(&ts, nullptr);
+    }
+}
+
 // ---------------------------------------------------------------------------
 // the batched RRT-Connect solve
 // ---------------------------------------------------------------------------
@@ -1398,7 +1393,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     PlanIO* h = c->h_io;
     auto read_status = [&]() {
         HIP_TRY(hipMemcpyAsync(h->status, status, sizeof h->status, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
+        stream_wait(c);
     };
 
     // Prologue: tree roots and counters from kernel arguments. Single rank with
@@ -2050,7 +2045,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         // long raw path: read it back, simplify with host-driven batched edge checks
         raw.resize((size_t)n_raw * NQ);
         HIP_TRY(hipMemcpyAsync(raw.data(), c->path.p, sizeof(double) * NQ * n_raw, hipMemcpyDeviceToHost, c->stream));
-        HIP_TRY(hipStreamSynchronize(c->stream));
+        stream_wait(c);
         raw = simplify_host(c, raw, level, p.resolution);
     }
     c->stats.simplify_ms = 1e3 * (now_s() - t_simp);

@@ -511,19 +511,12 @@ constexpr int QSS = 15, QSB = 11;
 constexpr int QCAP = 64;   // items per queue
 static_assert(QCAP >= 64, "a batch of one item per lane must fit after one pop pass");
 
-template <int CSS, int CSB>
-struct WaveQT {
-    static constexpr int CAP_SS = CSS, CAP_SB = CSB;
-    alignas(16) float ss[CSS][QSS];    // self pair: a1 b1 a2 b2 (12), owner lane | pair << 8, r_i, r_j
-    alignas(16) float sb[CSB][QSB];    // capsule-box: pa pb (box frame) h (9), r^2, owner lane
+struct WaveQ {
+    alignas(16) float ss[QCAP][QSS];   // self pair: a1 b1 a2 b2 (12), owner lane | pair << 8, r_i, r_j
+    alignas(16) float sb[QCAP][QSB];   // capsule-box: pa pb (box frame) h (9), r^2, owner lane
     int hit[64];                       // per-lane collision found by a drained item
 };
-using WaveQ = WaveQT<QCAP, QCAP>;
 static_assert(sizeof(WaveQ) <= 7680, "WaveQ must let 20 one-wave workgroups share a CU");
-// The queue of k_validity's no-mid-walk-drain form (state_collides_nm): 24 one-wave
-// workgroups per CU (6 waves per SIMD) need <= 6,826 B each of the 160 KiB LDS.
-using WaveQN = WaveQT<64, 56>;
-static_assert(24 * sizeof(WaveQN) <= 160 * 1024, "WaveQN must let 24 one-wave workgroups share a CU");
 
 __device__ __forceinline__ int rank_in(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -545,16 +538,9 @@ struct ClusterRegs {
     }
 };
 
-// NOMID: the queues are never drained inside the FK walk (drains are calls whose
-// registers stack on the walk's live set: 96 VGPRs instead of 80, so one wave per
-// SIMD fewer); a batch that does not fit marks the wave overflowed (ovf) and ends its
-// walk, and the caller re-checks the wave with the draining form.
-template <int NCL, class QT = WaveQ, bool NOMID_ = false>
+template <int NCL>
 struct QueueState {
-    static constexpr bool NOMID = NOMID_;
-    using QType = QT;
-    QT* Q;
-    bool ovf;         // (NOMID) a batch did not fit: the wave's verdicts are void
+    WaveQ* Q;
     int nss, nsb;     // wave-uniform item counts
     bool in_limits;   // every state of the wave inside the joint limits (skip never pairs)
     int lane;
@@ -606,31 +592,14 @@ __device__ __forceinline__ void pop_sb(S& s) {
     __builtin_amdgcn_wave_barrier();
     s.nsb -= take;
 }
-// make room for a batch of c items (wave-uniform); false: none (NOMID: the wave
-// overflowed, the batch is not queued)
+// make room for a batch of c items (wave-uniform)
 template <class S>
-__device__ __forceinline__ bool room_ss(S& s, int c) {
-    if (s.nss + c > S::QType::CAP_SS) {
-        if constexpr (S::NOMID) {
-            s.ovf = true;
-            return false;
-        } else {
-            pop_ss(s);
-        }
-    }
-    return true;
+__device__ __forceinline__ void room_ss(S& s, int c) {
+    if (s.nss + c > QCAP) pop_ss(s);
 }
 template <class S>
-__device__ __forceinline__ bool room_sb(S& s, int c) {
-    if (s.nsb + c > S::QType::CAP_SB) {
-        if constexpr (S::NOMID) {
-            s.ovf = true;
-            return false;
-        } else {
-            pop_sb(s);
-        }
-    }
-    return true;
+__device__ __forceinline__ void room_sb(S& s, int c) {
+    if (s.nsb + c > QCAP) pop_sb(s);
 }
 
 // queue item of capsule C vs box record bx (box frame segment, half extents, r^2);
@@ -657,8 +626,9 @@ __device__ __forceinline__ void enqueue_sb(const Capsules& k, const float* bx, c
 }
 
 // capsule C vs plane (immediate) and boxes (queued)
-template <int C, int NCL, class S>
-__device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __restrict__ sc, S& s) {
+template <int C, int NCL>
+__device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __restrict__ sc,
+                                           QueueState<NCL>& s) {
     constexpr float r = CAP_GEOM[C][6];
     const Aabb u = capsule_aabb(k.a[C], k.b[C], r);
     if (u.lo.z <= s.plane_z) return true;  // capsule vs ground plane
@@ -689,7 +659,7 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
             }
             const unsigned long long bm = __ballot(cand);
             if (!bm) continue;
-            if (!room_sb(s, __popcll(bm))) return false;
+            room_sb(s, __popcll(bm));
             if (cand) enqueue_sb<C>(k, bx, rt, r, s, bm);
             s.nsb += __popcll(bm);
         }
@@ -714,7 +684,7 @@ __device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __
             const bool cand = fmaxr(fmaxr(csep, ex), aabb_sep(u, bx + 8, bx + 11)) <= 0.0f;
             const unsigned long long m = __ballot(cand);
             if (!m) continue;
-            if (!room_sb(s, __popcll(m))) return false;
+            room_sb(s, __popcll(m));
             if (cand) enqueue_sb<C>(k, bx, sc->rot[j], r, s, m);
             s.nsb += __popcll(m);
         }
@@ -757,7 +727,7 @@ template <int P, class S>
 __device__ __forceinline__ void pair_enqueue(const Capsules& k, S& s, bool cand, unsigned long long m) {
     constexpr int I = PAIRS[P][0], J = PAIRS[P][1];
     if (!m) return;
-    if (!room_ss(s, __popcll(m))) return;
+    room_ss(s, __popcll(m));
     if (cand) {
         float* it = s.Q->ss[s.nss + rank_in(m)];
         it[0] = k.a[I].x; it[1] = k.a[I].y; it[2] = k.a[I].z;
@@ -827,20 +797,17 @@ enum { ROLE_ENV = 1, ROLE_PA = 2, ROLE_PB = 4, ROLE_ALL = 7 };
 #endif
 constexpr int SPLIT_J = RP_SPLIT_J;
 
-template <int NCL, int ROLE = ROLE_ALL, class QT = WaveQ, bool NOMID = false>
+template <int NCL, int ROLE = ROLE_ALL>
 struct QueuedVisit {
     const DevScene* __restrict__ sc;
-    QueueState<NCL, QT, NOMID> s;
+    QueueState<NCL> s;
     template <int C>
     __device__ __forceinline__ bool at(const Capsules& k) {
-        if constexpr (NOMID) {
-            if (s.ovf) return true;   // (wave-uniform) overflowed: end the walk
-        }
         if constexpr (C == C_LINK4) RP_STAMP(2);
         if constexpr (C == C_LINK6) RP_STAMP(3);
         if constexpr (C == C_HAND) RP_STAMP(4);
         if constexpr ((ROLE & ROLE_ENV) != 0) {
-            if (env_queued<C, NCL>(k, sc, s)) return true;
+            if (env_queued<C>(k, sc, s)) return true;
         }
         if constexpr (((ROLE & ROLE_PA) != 0 && C < SPLIT_J) || ((ROLE & ROLE_PB) != 0 && C >= SPLIT_J))
             pairs_queued<C>(k, s);
@@ -873,16 +840,13 @@ __device__ __forceinline__ void never_pairs_outside_limits(const float q[NQ], co
 // over every test. Plane tests decide at once (a colliding lane stops walking);
 // box and self narrow phases are queued and drained wave-compacted. Every lane of
 // the wave that is still running must call this at the same point. NCL >= the
-// scene's cluster count (rp_lib.hip picks the instantiation). Returns 1 = collides,
-// 0 = free; NOMID: -1 on every lane when the wave's queues overflowed (nothing
-// decided: re-check the wave with the draining form).
-template <int NCL, bool BF, int ROLE, class QT, bool NOMID>
-__device__ __forceinline__ int state_collides_impl(const float q[NQ], const DevScene* __restrict__ sc, QT& Q) {
+// scene's cluster count (rp_lib.hip picks the instantiation).
+template <int NCL, bool BF = false, int ROLE = ROLE_ALL>
+__device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene* __restrict__ sc, WaveQ& Q) {
     Capsules k;
-    QueuedVisit<NCL, ROLE, QT, NOMID> v;
+    QueuedVisit<NCL, ROLE> v;
     v.sc = sc;
     v.s.Q = &Q;
-    v.s.ovf = false;
     v.s.nss = 0;
     v.s.nsb = 0;
     v.s.lane = (int)__lane_id();
@@ -907,34 +871,15 @@ __device__ __forceinline__ int state_collides_impl(const float q[NQ], const DevS
     JointsSC jt;
 #pragma unroll
     for (int i = 0; i < 7; ++i) rp_sincos(q[i], &jt.s[i], &jt.c[i]);
-    const bool stop = fk_walk_j<QueuedVisit<NCL, ROLE, QT, NOMID>, BF>(q, jt, sc->base, k, v);
-    if constexpr (NOMID) {
-        if (__any(v.s.ovf)) return -1;   // (ovf is wave-uniform; __any makes that explicit)
-    }
-    if (stop) return 1;
+    if (fk_walk_j<QueuedVisit<NCL, ROLE>, BF>(q, jt, sc->base, k, v)) return true;
     if constexpr ((ROLE & ROLE_PB) != 0)
-        if (!v.s.in_limits) {
-            never_pairs_outside_limits(q, sc, v.s);
-            if constexpr (NOMID) {
-                if (__any(v.s.ovf)) return -1;
-            }
-        }
+        if (!v.s.in_limits) never_pairs_outside_limits(q, sc, v.s);
     RP_STAMP(5);
     while (v.s.nsb > 0) pop_sb(v.s);
     RP_STAMP(6);
     while (v.s.nss > 0) pop_ss(v.s);
     RP_STAMP(7);
-    return Q.hit[v.s.lane] != 0 ? 1 : 0;
-}
-template <int NCL, bool BF = false, int ROLE = ROLE_ALL>
-__device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene* __restrict__ sc, WaveQ& Q) {
-    return state_collides_impl<NCL, BF, ROLE, WaveQ, false>(q, sc, Q) != 0;
-}
-// the no-mid-walk-drain form (k_validity's large launches): 1 / 0, or -1 on every
-// lane of an overflowed wave
-template <int NCL, bool BF = false>
-__device__ __forceinline__ int state_collides_nm(const float q[NQ], const DevScene* __restrict__ sc, WaveQN& Q) {
-    return state_collides_impl<NCL, BF, ROLE_ALL, WaveQN, true>(q, sc, Q);
+    return Q.hit[v.s.lane] != 0;
 }
 
 // ---------------------------------------------------------------------------

@@ -133,6 +133,7 @@ __global__ __launch_bounds__(64 * W) void k_nnv(const double* __restrict__ qx, i
 #pragma unroll
     for (int u = 0; u < PF; ++u) bq[u] = ib[min<int64_t>(u, ntiles - 1) * 64];
     const f4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
+    float sink = -1e30f;
     auto tile_step = [&](int64_t tile, const h8& b) {
         f4 acc[RB];
 #pragma unroll
@@ -142,8 +143,11 @@ __global__ __launch_bounds__(64 * W) void k_nnv(const double* __restrict__ qx, i
 #pragma unroll
         for (int rb = 1; rb < RB; ++rb) m = fmaxf(m, fmaxf(fmaxf(acc[rb][0], acc[rb][1]), fmaxf(acc[rb][2], acc[rb][3])));
         RP_NNC(0, 1);
+        if constexpr (V == 1) {   // (the max feeds an output, so the MFMAs stay)
+            sink = fmaxf(sink, m);
+            return;
+        }
         if (!__any(m >= 0.0f)) return;
-        if constexpr (V == 1) return;
         RP_NNC(1, 1);
         unsigned pm = 0;
 #pragma unroll
@@ -193,7 +197,7 @@ __global__ __launch_bounds__(64 * W) void k_nnv(const double* __restrict__ qx, i
         const int64_t q = qw0 + r;
         if (q < n)
             part[yr * n + q] =
-                DI2{__longlong_as_double((long long)s_best[w][r]), s_bi[w][r], 0};
+                DI2{__longlong_as_double((long long)s_best[w][r]), s_bi[w][r], V == 1 ? (int)(sink > 0.0f) : 0};
     }
 }
 
@@ -400,7 +404,7 @@ __global__ __launch_bounds__(64 * W) void k_nnv2(const double* __restrict__ qx, 
         for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
             for (int e = 0; e < 4; ++e) neg |= (__float_as_uint(acc[rb][e]) >> 31) << (rb * 4 + e);
-        unsigned pm = ~neg & ((1u << (4 * RB)) - 1u);
+        unsigned pm = ~neg & (RB >= 8 ? 0xFFFFFFFFu : ((1u << (4 * RB)) - 1u));
         const unsigned node = (unsigned)(t_lo + tile * 16 + col);
         while (__any(pm != 0)) {
             const bool has = pm != 0;
@@ -476,4 +480,8 @@ void nn_lab_variants(Run& run, int32_t* out0, int32_t* out1) {
     run(k_nnv2<4, 4, 2>, 4, out1, "v2 refresh 2 tiles", false, out0);
     run(k_nnv2<4, 4, 4>, 4, out1, "v2 refresh 4 tiles", false, out0);
     run(k_nnv2<8, 4, 2>, 8, out1, "v2 RB8 refresh 2", false, out0);
+    run(k_nnv2<8, 4, 4>, 8, out1, "v2 RB8 refresh 4", false, out0);
+    run(k_nnv<8, 4, 0>, 8, out1, "v0 RB8 (product code)", false, out0);
+    run(k_nnv<8, 4, 1>, 8, out1, "v1 RB8 fast path only", false, out0);
+    run(k_nnv<2, 4, 1>, 2, out1, "v1 RB2 fast path only", false, out0);
 }

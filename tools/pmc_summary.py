@@ -44,6 +44,13 @@ def main():
     ap.add_argument("--json", default=None)
     a = ap.parse_args()
     v, meta, tot, waves_of = load(a.dirs, a.kernel, exclude=a.exclude)
+    # the kernel sources + flags these counters were collected on (rp_math.h,
+    # rp_model.h, rp_kernels.h: k_validity*, k_edges* live there)
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from rbe550_final_project_amd.build import validity_source_hash
+    meta["kernel"] = a.kernel
+    meta["source_hash"] = validity_source_hash()
     # per-wave figures: a counter's total over the SQ_WAVES of the passes it was
     # collected in (dispatches of different sizes weigh by their waves)
     print(json.dumps(meta))

@@ -68,24 +68,16 @@ __global__ void k_uniform(float* q, int64_t n, uint64_t seed) {
     }
 }
 
-unsigned* g_redo = nullptr;
-int g_mode = 1;   // 0: k_validity of the tree headers; 1: k_validity_nm + k_validity_redo
 template <int NCL>
 void launch(const float* q, int64_t n, uint8_t* f, const DevScene* sc, hipStream_t s) {
-    if (g_mode == 0) {
-        hipLaunchKernelGGL((k_validity<NCL, true>), dim3((unsigned)((n + VTHREADS - 1) / VTHREADS)), dim3(VTHREADS), 0,
-                           s, q, n, f, sc);
-        return;
-    }
-    hipLaunchKernelGGL((k_validity_nm<NCL, true>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, q, n, f, sc, g_redo);
-    hipLaunchKernelGGL((k_validity_redo<NCL, true>), dim3(VREDO_BLOCKS), dim3(64), 0, s, q, n, f, sc, g_redo);
+    hipLaunchKernelGGL((k_validity<NCL, true>), dim3((unsigned)((n + VTHREADS - 1) / VTHREADS)), dim3(VTHREADS), 0, s,
+                       q, n, f, sc);
 }
 
 int main(int argc, char** argv) {
     const int64_t n = argc > 1 ? atoll(argv[1]) : (1 << 24);
     const int reps = argc > 2 ? atoi(argv[2]) : 20;
     const char* scene = argc > 3 ? argv[3] : "goal3";
-    g_mode = argc > 4 ? atoi(argv[4]) : 1;
     std::vector<rp_box> boxes;
     std::vector<rp_box_rot> rboxes;
     const double xs[2] = {0.45, 0.65}, ys[5] = {-0.40, -0.20, 0.0, 0.20, 0.40};
@@ -120,8 +112,6 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&q, sizeof(float) * NQ * n));
     CK(hipMalloc(&fa, n));
     CK(hipMalloc(&fb, n));
-    CK(hipMalloc(&g_redo, sizeof(unsigned) * ((n + 63) / 64 + 2)));
-    CK(hipMemset(g_redo, 0, sizeof(unsigned) * ((n + 63) / 64 + 2)));
     hipStream_t s;
     void* vs = nullptr;
     L.get_stream(ctx, &vs);
@@ -170,26 +160,11 @@ int main(int argc, char** argv) {
         diff += ha[i] != hb[i];
         valid += ha[i];
     }
-    // waves that overflowed in one lab launch (count read before the redo resets it)
-    unsigned ovf = 0;
-    if (g_mode == 1) {
-        switch (ncl) {
-            case 0: hipLaunchKernelGGL((k_validity_nm<0, true>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, q, n, fb, ds, g_redo); break;
-            case 1: hipLaunchKernelGGL((k_validity_nm<1, true>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, q, n, fb, ds, g_redo); break;
-            case 2: hipLaunchKernelGGL((k_validity_nm<2, true>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, q, n, fb, ds, g_redo); break;
-            case 4: hipLaunchKernelGGL((k_validity_nm<4, true>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, q, n, fb, ds, g_redo); break;
-            default: hipLaunchKernelGGL((k_validity_nm<8, true>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, q, n, fb, ds, g_redo); break;
-        }
-        CK(hipStreamSynchronize(s));
-        CK(hipMemcpy(&ovf, g_redo, sizeof ovf, hipMemcpyDeviceToHost));
-        lab();   // (the count is reset by the redo of this launch)
-        CK(hipStreamSynchronize(s));
-    }
     const double ma = ta[ta.size() / 2], mb = tb[tb.size() / 2];
     printf("%s n=%lld ncl=%d: library %.4f ms (%.2f G/s)  tree headers %.4f ms (%.2f G/s)  ratio %.4f  "
-           "min %.4f / %.4f  flags differ %lld  valid %.4f  mode %d  overflowed waves %u of %lld\n",
+           "min %.4f / %.4f  flags differ %lld  valid %.4f\n",
            scene, (long long)n, ncl, ma, n / (ma * 1e-3) / 1e9, mb, n / (mb * 1e-3) / 1e9, ma / mb, ta[0], tb[0],
-           (long long)diff, (double)valid / n, g_mode, ovf, (long long)((n + 63) / 64));
+           (long long)diff, (double)valid / n);
     L.destroy(ctx);
     return diff != 0;
 }

@@ -146,6 +146,9 @@ struct rp_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t ev_wait = nullptr;        // stream_wait's marker (no timing)
+    // host waits since the context was made (rp_debug_waits): wait_seq calls,
+    // stream_wait calls, seconds spinning, seconds in the sleep loop, sleeps
+    double waits[5] = {0, 0, 0, 0, 0};
     DevScene scene{};
     DevScene* d_scene = nullptr;
     // scene uploads (upload_scene / flush_scene): rp_set_scene / rp_set_attached only
@@ -1213,9 +1216,11 @@ void wait_seq(rp_ctx* c, int seq) {
     const WaitTuning& wt = wait_tuning();
     double t0 = -1.0;
     const double t_enter = now_s();
+    c->waits[0] += 1;
     for (uint64_t spin = 1;; ++spin) {   // spin
         if (*f == seq) {
             __atomic_thread_fence(__ATOMIC_ACQUIRE);
+            c->waits[2] += now_s() - t_enter;
             return;
         }
         if ((spin & 4095) == 0 && wait_check(c, f, seq, t0)) break;
@@ -1226,6 +1231,8 @@ void wait_seq(rp_ctx* c, int seq) {
     }
     SlackGuard slack;
     double last_check = now_s();
+    const double t_sleep = last_check;
+    c->waits[2] += t_sleep - t_enter;
     while (*f != seq) {   // sleep between polls
         const double now = now_s();
         if (now - last_check > 1e-3) {
@@ -1236,7 +1243,9 @@ void wait_seq(rp_ctx* c, int seq) {
         const int64_t ns = std::min<int64_t>(200000, std::max<int64_t>(10000, (int64_t)((now - t_enter) * wt.frac * 1e9)));
         const timespec ts{0, (long)ns};
         nanosleep(&ts, nullptr);
+        c->waits[4] += 1;
     }
+    c->waits[3] += now_s() - t_sleep;
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
 }
 
@@ -1245,23 +1254,31 @@ void stream_wait(rp_ctx* c) {
     HIP_TRY(hipEventRecord(c->ev_wait, c->stream));
     const WaitTuning& wt = wait_tuning();
     const double t_enter = now_s();
+    c->waits[1] += 1;
     for (uint64_t spin = 1;; ++spin) {   // spin
         const hipError_t e = hipEventQuery(c->ev_wait);
-        if (e == hipSuccess) return;
+        if (e == hipSuccess) {
+            c->waits[2] += now_s() - t_enter;
+            return;
+        }
         if (e != hipErrorNotReady) HIP_TRY(e);
         if ((spin & 15) == 0 && now_s() - t_enter > wt.spin_s) break;
     }
     SlackGuard slack;
+    const double t_sleep = now_s();
+    c->waits[2] += t_sleep - t_enter;
     for (;;) {   // sleep between polls (a stream that never finishes is the caller's watchdog's)
         const hipError_t e = hipEventQuery(c->ev_wait);
-        if (e == hipSuccess) return;
+        if (e == hipSuccess) break;
         if (e != hipErrorNotReady) HIP_TRY(e);
         slack.fine();
         const double waited = now_s() - t_enter;
         const int64_t ns = std::min<int64_t>(200000, std::max<int64_t>(10000, (int64_t)(waited * wt.frac * 1e9)));
         const timespec ts{0, (long)ns};
         nanosleep(&ts, nullptr);
+        c->waits[4] += 1;
     }
+    c->waits[3] += now_s() - t_sleep;
 }
 
 // ---------------------------------------------------------------------------
@@ -3060,6 +3077,14 @@ int rp_ik(rp_ctx* c, int32_t n_targets, const double* pos, const double* quat, c
 
 // diagnostic (tools/val_lab.hip): the context's host scene record (the DevScene the
 // kernels read, after rp_set_scene*; `bytes` must be sizeof(DevScene))
+// diagnostic: the context's host waits so far {wait_seq calls, stream_wait calls,
+// seconds spinning, seconds in the sleep loops, sleeps}
+int rp_debug_waits(rp_ctx* c, double* out, int32_t n) {
+    if (!c || !out || n < 5) return RP_ERR_ARG;
+    std::memcpy(out, c->waits, sizeof c->waits);
+    return RP_OK;
+}
+
 int rp_debug_scene(rp_ctx* c, void* out, int64_t bytes) {
     if (!c || !out || bytes != (int64_t)sizeof(DevScene)) return RP_ERR_ARG;
     std::memcpy(out, &c->scene, sizeof(DevScene));

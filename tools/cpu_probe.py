@@ -48,20 +48,32 @@ def main():
                          tree_capacity=1 << 23)
     ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI,
              _abi.make_params(seed=1, batch=64, n_waypoints=150, timeout_s=0.05, straight_first=False))
+    import ctypes as C
+    from rbe550_final_project_amd import native
+
+    def waits():
+        out = (C.c_double * 5)()
+        native.load().rp_debug_waits(ctx._h, out, 5)
+        return list(out)
+
+    wt0 = waits()
     th0, t0, w0 = threads(), os.times(), time.perf_counter()
     ctx.plan_async(q["start"], q["goal"], model.Q_LO, model.Q_HI, p, path_cap=256)
     path, st = ctx.plan_wait()
     th1, t1, wall = threads(), os.times(), time.perf_counter() - w0
+    wt = [b - a for a, b in zip(wt0, waits())]
     s = ctx.stats()
     per = {}
     for tid, (comm, cpu) in th1.items():
         d = cpu - th0.get(tid, (comm, 0.0))[1]
         if d > 0.005:
-            per[f"{comm}:{tid}"] = round(d, 3)
+            per[f"{comm}:{tid}" + (":main" if int(tid) == os.getpid() else "")] = round(d, 3)
     print(json.dumps({"env": {k: v for k, v in os.environ.items() if k.startswith("RBE_")}, "wall_s": round(wall, 3),
                       "cpu_s": round((t1.user - t0.user) + (t1.system - t0.system), 3), "per_thread_s": per,
                       "status": _abi.STATUS_NAMES[st], "iterations": s["iterations"], "samples": s["samples"],
-                      "trees": [s["start_tree_size"], s["goal_tree_size"]]}))
+                      "trees": [s["start_tree_size"], s["goal_tree_size"]],
+                      "waits": {"wait_seq": int(wt[0]), "stream_wait": int(wt[1]), "spin_s": round(wt[2], 3),
+                                "sleep_loop_s": round(wt[3], 3), "sleeps": int(wt[4])}}))
     ctx.close()
 
 

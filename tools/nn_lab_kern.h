@@ -1,16 +1,18 @@
 // nn_lab_kern.h — experimental variants of rp_nn.h k_nn_mfma for tools/nn_lab.hip
-// (diagnostic; not the product). k_nnv<RB, W, V>: V = 0 the product's code, V = 1
-// the fast path only (no exact path: wrong answers, a speed bound).
+// (diagnostic; not the product). k_nnv<RB, W, V, PF>: V = 0 the product's code, V = 1
+// the fast path only (no exact path: wrong answers, a speed bound), V = 3 the fast
+// path on the same B fragments over and over (no loads: the MFMA + VALU bound); PF
+// tiles prefetched.
 #pragma once
 namespace rp {
-template <int RB, int W, int V>
-__global__ __launch_bounds__(64 * W) void k_nnv(const double* __restrict__ qx, int64_t n,
+template <int RB, int W, int V, int PF = 4, bool GQ = false, int WPE = 1>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(WPE))) void k_nnv(const double* __restrict__ qx, int64_t n,
                                                           const int* status, int64_t t0,
                                                           const double* __restrict__ tree, const h8* __restrict__ img,
                                                           int64_t T, int64_t chunk, int64_t qblocks, NnMfma P,
                                                           DI2* __restrict__ part) {
     constexpr int QW = 16 * RB;   // queries per wave
-    __shared__ double s_q[W][QW][NQ];                       // query states (exact path)
+    __shared__ double s_q[GQ ? 1 : W][GQ ? 1 : QW][NQ];     // query states (exact path; GQ: from global)
     __shared__ unsigned long long s_best[W][QW];            // exact best distance (f64 bits; >= 0)
     __shared__ int s_bi[W][QW];                             // its node (lowest index among equal)
     __shared__ int s_ti[W][QW];                             // a round's lowest node at the new best
@@ -24,12 +26,18 @@ __global__ __launch_bounds__(64 * W) void k_nnv(const double* __restrict__ qx, i
     const int64_t t_lo = yr * chunk, t_hi = min(T, t_lo + chunk);
     const int64_t qw0 = qb0 + (int64_t)w * QW;
 
-    for (int i = lane; i < QW * NQ; i += 64) {
-        const int r = i / NQ, d = i - r * NQ;
-        const int64_t q = qw0 + r;
-        s_q[w][r][d] = q < n ? qx[q * NQ + d] : 0.0;
+    auto qrow = [&](int r) -> const double* {
+        if constexpr (GQ) return qx + min<int64_t>(qw0 + r, n - 1) * NQ;
+        else return &s_q[w][r][0];
+    };
+    if constexpr (!GQ) {
+        for (int i = lane; i < QW * NQ; i += 64) {
+            const int r = i / NQ, d = i - r * NQ;
+            const int64_t q = qw0 + r;
+            s_q[w][r][d] = q < n ? qx[q * NQ + d] : 0.0;
+        }
+        wave_lds_sync();
     }
-    wave_lds_sync();
     // seed every query's exact best with NNM_SEEDS nodes spread over the range (the
     // exact f64 distance, lexicographic (distance, index) minimum): the filter then
     // starts from a typical distance instead of letting every node of the first stage
@@ -45,7 +53,7 @@ __global__ __launch_bounds__(64 * W) void k_nnv(const double* __restrict__ qx, i
                 const int64_t j = t_lo + (R * k) / NNM_SEEDS;
                 if (k > 0 && j == t_lo + (R * (k - 1)) / NNM_SEEDS) continue;
                 const unsigned long long db =
-                    (unsigned long long)__double_as_longlong(dist2(tree + j * NQ, &s_q[w][r][0]));
+                    (unsigned long long)__double_as_longlong(dist2(tree + j * NQ, qrow(r)));
                 if (db < bb || (db == bb && (int)j < bi)) {
                     bb = db;
                     bi = (int)j;
@@ -64,7 +72,7 @@ __global__ __launch_bounds__(64 * W) void k_nnv(const double* __restrict__ qx, i
     for (int rb = 0; rb < RB; ++rb) {
         const int r = rb * 16 + (lane & 15);
         _Float16 hh, hl;
-        a[rb] = a_frag(P, &s_q[w][r][0], qw0 + r < n, ch, &na[rb], &hh, &hl);
+        a[rb] = a_frag(P, qrow(r), qw0 + r < n, ch, &na[rb], &hh, &hl);
         curb[rb] = __builtin_inf();
         const double b0 = __longlong_as_double((long long)s_best[w][r]);
         if (ch == 3 && qw0 + r < n && b0 < 1e300) {   // the seeded threshold
@@ -90,7 +98,7 @@ __global__ __launch_bounds__(64 * W) void k_nnv(const double* __restrict__ qx, i
                 node = cnd.y;
                 prev = s_best[w][row];
                 s_ti[w][row] = 0x7fffffff;
-                db = (unsigned long long)__double_as_longlong(dist2(tree + (int64_t)node * NQ, &s_q[w][row][0]));
+                db = (unsigned long long)__double_as_longlong(dist2(tree + (int64_t)node * NQ, qrow(row)));
             }
             wave_lds_sync();
             if (has) atomicMin(&s_best[w][row], db);
@@ -125,7 +133,6 @@ __global__ __launch_bounds__(64 * W) void k_nnv(const double* __restrict__ qx, i
     // wait for each tile's freshly issued load), and loads past the range re-read its
     // last tile (unconditional: static vmcnt waits). Tiles need no bounds test: the
     // image's pad slots and dead query rows never pass (k_nn_image, a_frag).
-    constexpr int PF = 4;
     const int64_t ntiles = (t_hi - t_lo + 15) / 16;
     const int col = lane & 15;   // this lane's column of every tile
     const h8* ib = img + (t_lo + col) * 4 + ch;   // tile t: ib[t * 64]
@@ -143,7 +150,7 @@ __global__ __launch_bounds__(64 * W) void k_nnv(const double* __restrict__ qx, i
 #pragma unroll
         for (int rb = 1; rb < RB; ++rb) m = fmaxf(m, fmaxf(fmaxf(acc[rb][0], acc[rb][1]), fmaxf(acc[rb][2], acc[rb][3])));
         RP_NNC(0, 1);
-        if constexpr (V == 1) {   // (the max feeds an output, so the MFMAs stay)
+        if constexpr (V == 1 || V == 3) {   // (the max feeds an output, so the MFMAs stay)
             sink = fmaxf(sink, m);
             return;
         }
@@ -178,7 +185,8 @@ __global__ __launch_bounds__(64 * W) void k_nnv(const double* __restrict__ qx, i
 #pragma unroll
         for (int u = 0; u < PF; ++u) {
             tile_step(tb + u, bq[u]);
-            bq[u] = nx[u * 64];
+            if constexpr (V == 3) asm volatile("" : "+v"(bq[u]));
+            else bq[u] = nx[u * 64];
         }
     }
     for (; tb + PF <= ntiles; tb += PF) {
@@ -197,7 +205,7 @@ __global__ __launch_bounds__(64 * W) void k_nnv(const double* __restrict__ qx, i
         const int64_t q = qw0 + r;
         if (q < n)
             part[yr * n + q] =
-                DI2{__longlong_as_double((long long)s_best[w][r]), s_bi[w][r], V == 1 ? (int)(sink > 0.0f) : 0};
+                DI2{__longlong_as_double((long long)s_best[w][r]), s_bi[w][r], V != 0 ? (int)(sink > 0.0f) : 0};
     }
 }
 
@@ -475,13 +483,18 @@ template <class Run>
 void nn_lab_variants(Run& run, int32_t* out0, int32_t* out1) {
     using namespace rp;
     run(k_nnv<4, 4, 0>, 4, out1, "v0 (product copy)", false, out0);
-    run(k_nnv<4, 4, 1>, 4, out1, "v1 fast path only", false, out0);
-    run(k_nnv2<4, 4, 1>, 4, out1, "v2 refresh every tile", false, out0);
-    run(k_nnv2<4, 4, 2>, 4, out1, "v2 refresh 2 tiles", false, out0);
-    run(k_nnv2<4, 4, 4>, 4, out1, "v2 refresh 4 tiles", false, out0);
-    run(k_nnv2<8, 4, 2>, 8, out1, "v2 RB8 refresh 2", false, out0);
-    run(k_nnv2<8, 4, 4>, 8, out1, "v2 RB8 refresh 4", false, out0);
     run(k_nnv<8, 4, 0>, 8, out1, "v0 RB8 (product code)", false, out0);
+    run(k_nnv<4, 4, 1>, 4, out1, "v1 fast path only", false, out0);
     run(k_nnv<8, 4, 1>, 8, out1, "v1 RB8 fast path only", false, out0);
-    run(k_nnv<2, 4, 1>, 2, out1, "v1 RB2 fast path only", false, out0);
+    run(k_nnv<4, 4, 3>, 4, out1, "v3 RB4 no loads", false, out0);
+    run(k_nnv<8, 4, 3>, 8, out1, "v3 RB8 no loads", false, out0);
+    run(k_nnv<8, 4, 1, 2>, 8, out1, "v1 RB8 PF2", false, out0);
+    run(k_nnv<8, 4, 1, 8>, 8, out1, "v1 RB8 PF8", false, out0);
+    run(k_nnv<8, 4, 0, 8>, 8, out1, "v0 RB8 PF8", false, out0);
+    run(k_nnv<4, 4, 0, 4, true>, 4, out1, "v0 RB4 global queries", false, out0);
+    run(k_nnv<8, 4, 0, 4, true>, 8, out1, "v0 RB8 global queries", false, out0);
+    run(k_nnv<8, 4, 1, 4, true>, 8, out1, "v1 RB8 global queries", false, out0);
+    run(k_nnv<8, 4, 0, 4, true, 4>, 8, out1, "v0 RB8 global q, 4 waves/SIMD", false, out0);
+    run(k_nnv<8, 2, 0, 4, true, 4>, 8, out1, "v0 RB8 W2 global q, 4 waves", false, out0);
+    run(k_nnv<4, 4, 0, 4, true, 5>, 4, out1, "v0 RB4 global q, 5 waves/SIMD", false, out0);
 }

@@ -236,6 +236,7 @@ struct rp_ctx {
     NnMfma nnm{};                        // the matrix-core filter's constants for this plan's bounds
     bool nnm_ok = false;
     int nn_S = 0;                        // tree ranges of the last matrix-core launch
+    int64_t nn_geo[4] = {0, 0, 0, 0};    // its T, queries per block, grid, device geometry (k_nn_reduce_g)
 
     void free_staging() {
         if (h_send) (void)hipHostFree(h_send);
@@ -1055,27 +1056,45 @@ bool nn_mfma_params(const double* lo, const double* hi, NnMfma* P) {
     return true;
 }
 
+// device geometry for status-bounded searches (rp_nn.h nn_geom): RBE_NN_DEVGEOM=0 for
+// the host geometry of the largest count (A/B; read per search, as RBE_NN_MFMA)
+bool nn_devgeom() {
+    const char* e = std::getenv("RBE_NN_DEVGEOM");
+    return !(e && *e && std::atoi(e) == 0);
+}
+
 template <int RB, int W>
 void launch_nn_mfma_w(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, const double* tree, const h8* img,
                       int64_t T) {
     constexpr int64_t NNM_STAGE = 64;   // (range sizing: 64-node units)
     const int64_t per_block = (int64_t)W * 16 * RB;
-    const int64_t qblocks = (n + per_block - 1) / per_block;
-    const int64_t stages = (T + NNM_STAGE - 1) / NNM_STAGE;
-    const int64_t want = std::max<int64_t>(1, (1024 + qblocks - 1) / qblocks);   // >= 1024 blocks
-    // ranges of >= 32 stages (2,048 nodes): a range's first stages hold most of its
-    // threshold updates (exact-path rounds), which a longer range amortises
-    int64_t S0 = std::max<int64_t>(1, std::min<int64_t>(want, stages / 32));
+    int64_t target = 1024;   // blocks
+    if (const char* e = std::getenv("RBE_NN_BLOCKS"))   // (A/B)
+        if (*e) target = std::max<int64_t>(1, std::atoll(e));
+    const NnGeom g = nn_geom(n, T, per_block, 0, target);
+    const int64_t qblocks = g.qblocks;
+    int64_t chunk = g.chunk;
     if (const char* e = std::getenv("RBE_NN_RANGES"))   // (A/B: cap on the tree ranges)
-        if (*e) S0 = std::max<int64_t>(1, std::min<int64_t>(S0, std::atoll(e)));
-    int64_t chunk = ((stages + S0 - 1) / S0) * NNM_STAGE;
+        if (*e) {
+            const int64_t stages = (T + NNM_STAGE - 1) / NNM_STAGE;
+            const int64_t S0 = std::max<int64_t>(1, std::min<int64_t>(g.S, std::atoll(e)));
+            chunk = ((stages + S0 - 1) / S0) * NNM_STAGE;
+        }
     if (const char* e = std::getenv("RBE_NN_RANGE_MAX"))   // (A/B: nodes per range at most)
         if (*e) chunk = std::max<int64_t>(NNM_STAGE, std::min<int64_t>(chunk, std::atoll(e) / NNM_STAGE * NNM_STAGE));
     const int S = (int)((T + chunk - 1) / chunk);
-    c->nn_part.ensure((size_t)S * n);
-    hipLaunchKernelGGL((k_nn_mfma<RB, W>), dim3((unsigned)(qblocks * S)), dim3(64 * W), 0, c->stream, qx, n,
-                       Q.status, Q.t0, tree, img, T, chunk, qblocks, c->nnm, c->nn_part.p);
+    int64_t grid = qblocks * S;
+    const int devgeom = Q.status && nn_devgeom() ? 1 : 0;
+    if (devgeom) grid = std::max<int64_t>(grid, 1024);   // room for the actual count's ranges
+    // partials: S x n for the host geometry; within grid x per_block for any device one
+    c->nn_part.ensure((size_t)std::max<int64_t>((int64_t)S * n, devgeom ? grid * per_block : 0));
+    hipLaunchKernelGGL((k_nn_mfma<RB, W>), dim3((unsigned)grid), dim3(64 * W), 0, c->stream, qx, n, Q.status,
+                       Q.t0, tree, img, T, chunk, qblocks, c->nnm, c->nn_part.p, devgeom);
     c->nn_S = S;
+    c->nn_geo[0] = T;
+    c->nn_geo[1] = per_block;
+    c->nn_geo[2] = grid;
+    c->nn_geo[3] = devgeom;
 }
 // waves per block: RBE_NN_WAVES (1, 2, 4)
 template <int RB>
@@ -1135,8 +1154,9 @@ bool nn_split(rp_ctx* c, const NnQuery& Q, int64_t n, Tree& tr, int64_t T, int32
         else if (mfma_rb >= 4) launch_nn_mfma<4>(c, qx, n, Q, tree, img, T);
         else if (mfma_rb >= 2) launch_nn_mfma<2>(c, qx, n, Q, tree, img, T);
         else launch_nn_mfma<1>(c, qx, n, Q, tree, img, T);
-        hipLaunchKernelGGL(k_nn_reduce, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream,
-                           (const DI2*)c->nn_part.p, n, c->nn_S, Q.status, Q.t0, out);
+        hipLaunchKernelGGL(k_nn_reduce_g, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream,
+                           (const DI2*)c->nn_part.p, n, c->nn_S, Q.status, Q.t0, out, c->nn_geo[0], c->nn_geo[1],
+                           c->nn_geo[2], (int)c->nn_geo[3]);
         HIP_TRY(hipGetLastError());
         prof_end(c, ps, 0, c->stream);
         return true;

@@ -150,19 +150,51 @@ __global__ void k_nn_image(const double* __restrict__ tree, int64_t t0, int64_t 
 
 // Nearest node of each query over tree range [y * chunk, (y + 1) * chunk) ->
 // part[y * n + q] (exact distance, index; index -1: no node). Queries: qx (n x 9
-// f64); status (NNQ_ROWS): n = min(n, status[0] - t0). RB row blocks of 16 queries
-// per wave.
+// f64); status (NNQ_ROWS): n = min(n, status[0] - t0), and with devgeom the
+// geometry (qblocks, chunk, ranges) is nn_geom's for that n within the grid (the
+// host's chunk / qblocks are ignored). RB row blocks of 16 queries per wave.
 // Grid: 1-D, qblocks x (tree ranges) blocks. Blocks are remapped so that each group
 // of blocks sharing an XCD (blockIdx % 8 labels them, cdna_hip_programming.md T1,
 // the bijective form) takes a contiguous run of (range, query block) pairs: the
 // blocks of one tree range sit on one XCD and its L2 holds that range (the tree's
 // 72 B/node are re-read by every query block).
-__device__ __forceinline__ void nn_block_coords(int64_t qblocks, int64_t* qb, int64_t* y) {
-    const int64_t nwg = (int64_t)rp_gdim(), lid = (int64_t)rp_bid();
+// nwg: the blocks in use (the first nwg of the grid; the rest return)
+__device__ __forceinline__ void nn_block_coords(int64_t qblocks, int64_t nwg, int64_t* qb, int64_t* y) {
+    const int64_t lid = (int64_t)rp_bid();
     const int64_t q = nwg / 8, r = nwg % 8, xcd = lid % 8;
     const int64_t wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + lid / 8;
     *y = wgid / qblocks;
     *qb = wgid - *y * qblocks;
+}
+__device__ __forceinline__ void nn_block_coords(int64_t qblocks, int64_t* qb, int64_t* y) {
+    nn_block_coords(qblocks, (int64_t)rp_gdim(), qb, y);
+}
+
+// Geometry of a split search: n queries in blocks of per_block, the T nodes in S
+// ranges of `chunk` (a multiple of 64, >= 32 x 64 = 2,048 nodes: a range's first
+// stages hold most of its threshold updates, which a longer range amortises), about
+// >= 1,024 blocks in all; maxblocks > 0 caps qblocks x S. A search whose query count
+// is on the device (NNQ_ROWS: the accepted extensions) has its grid sized on the host
+// for the largest count and takes the geometry of the actual count in the kernel, so
+// a few thousand queries against a large tree still get ~1,024 blocks (the host
+// geometry of the largest count would give them qblocks_max x 2 blocks, most idle).
+struct NnGeom {
+    int64_t qblocks, chunk;
+    int S;
+};
+__host__ __device__ inline NnGeom nn_geom(int64_t n, int64_t T, int64_t per_block, int64_t maxblocks,
+                                          int64_t target = 1024) {
+    NnGeom g;
+    g.qblocks = (n + per_block - 1) / per_block;
+    const int64_t qb = g.qblocks > 0 ? g.qblocks : 1;
+    const int64_t stages = (T + 63) / 64;
+    int64_t S0 = (target + qb - 1) / qb;
+    if (S0 > stages / 32) S0 = stages / 32;
+    if (maxblocks > 0 && S0 > maxblocks / qb) S0 = maxblocks / qb;
+    if (S0 < 1) S0 = 1;
+    g.chunk = ((stages + S0 - 1) / S0) * 64;
+    g.S = (int)((T + g.chunk - 1) / g.chunk);
+    return g;
 }
 
 #ifdef RP_NN_COUNT
@@ -190,16 +222,27 @@ __global__ __launch_bounds__(64 * W) void k_nn_mfma(const double* __restrict__ q
                                                           const int* status, int64_t t0,
                                                           const double* __restrict__ tree, const h8* __restrict__ img,
                                                           int64_t T, int64_t chunk, int64_t qblocks, NnMfma P,
-                                                          DI2* __restrict__ part) {
+                                                          DI2* __restrict__ part, int devgeom) {
     constexpr int QW = 16 * RB;   // queries per wave
     __shared__ double s_q[W][QW][NQ];                       // query states (exact path)
     __shared__ unsigned long long s_best[W][QW];            // exact best distance (f64 bits; >= 0)
     __shared__ int s_bi[W][QW];                             // its node (lowest index among equal)
     __shared__ int s_ti[W][QW];                             // a round's lowest node at the new best
     __shared__ int2 s_cand[W][NNM_CAND];                    // passing (row, node) pairs, not yet evaluated
-    if (status) n = min(n, (int64_t)status[0] - t0);
+    int64_t nwg = (int64_t)rp_gdim();
+    if (status) {
+        n = min(n, (int64_t)status[0] - t0);
+        if (n <= 0) return;
+        if (devgeom) {
+            const NnGeom g = nn_geom(n, T, (int64_t)W * QW, nwg);
+            qblocks = g.qblocks;
+            chunk = g.chunk;
+            nwg = g.qblocks * g.S;
+            if ((int64_t)rp_bid() >= nwg) return;
+        }
+    }
     int64_t qb, yr;
-    nn_block_coords(qblocks, &qb, &yr);
+    nn_block_coords(qblocks, nwg, &qb, &yr);
     const int64_t qb0 = qb * W * QW;
     if (qb0 >= n) return;   // whole block idle (uniform)
     const int w = (int)(rp_tid() >> 6), lane = (int)(rp_tid() & 63), ch = lane >> 4;
@@ -376,6 +419,27 @@ __global__ __launch_bounds__(64 * W) void k_nn_mfma(const double* __restrict__ q
             part[yr * n + q] =
                 DI2{__longlong_as_double((long long)s_best[w][r]), s_bi[w][r], 0};
     }
+}
+
+// k_nn_reduce of a k_nn_mfma search: with devgeom and a status-bounded count, the
+// ranges are nn_geom's for the actual count (per_block queries per block, the grid's
+// maxblocks), else the host's S
+__global__ void k_nn_reduce_g(const DI2* __restrict__ part, int64_t n, int S, const int* status, int64_t t0,
+                              int32_t* __restrict__ out, int64_t T, int64_t per_block, int64_t maxblocks,
+                              int devgeom) {
+    const int64_t k = (int64_t)rp_bid() * rp_bdim() + rp_tid();
+    if (status) {
+        n = min(n, (int64_t)status[0] - t0);
+        if (devgeom && n > 0) S = nn_geom(n, T, per_block, maxblocks).S;
+    }
+    if (k >= n) return;
+    double bd = __builtin_inf();
+    int bi = -1;
+    for (int s = 0; s < S; ++s) {
+        const DI2 v = part[(int64_t)s * n + k];
+        if (v.i >= 0 && (v.d < bd || (v.d == bd && v.i < bi))) { bd = v.d; bi = v.i; }
+    }
+    out[k] = bi;
 }
 
 // the queries of a split search as f64 states (NNQ_SAMPLE / NNQ_STEER: Philox samples,

@@ -167,6 +167,18 @@ def test_nearest_node_mfma_row_blocks(gpu_ctx, name, mfma, monkeypatch):
     _check(gpu_ctx, name)
 
 
+@pytest.mark.parametrize("name", ["C5_well_s0", "C5_well_s3", "C4_q5"])
+@pytest.mark.parametrize("devgeom", ["0", "1"])
+def test_nearest_node_status_geometry(gpu_ctx, name, devgeom, monkeypatch):
+    """The connect searches' query count is on the device (the accepted extensions):
+    their tree ranges follow the actual count in the kernel (rp_nn.h nn_geom,
+    k_nn_reduce_g), or the host geometry of the largest count (RBE_NN_DEVGEOM=0).
+    Same plans either way."""
+    monkeypatch.setenv("RBE_NN_DEVGEOM", devgeom)
+    monkeypatch.setenv("RBE_NN_SPLIT", "1")
+    _check(gpu_ctx, name)
+
+
 def test_kernel_profile_of_a_plan(gpu_ctx):
     """rp_set_profiling / rp_get_profile (bench.py's nearest-node and edge rooflines):
     the profiled plan is the same plan, and the profile counts its launches, time

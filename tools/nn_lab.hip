@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <random>
+#include <type_traits>
 #include <vector>
 
 using namespace rp;
@@ -134,9 +135,14 @@ int main(int argc, char** argv) {
     auto run = [&](auto kern, int RB, int32_t* out, const char* name, bool check, const int32_t* ref) {
         const Geom g = geom(n, T, RB, 4);
         auto launch = [&]() {
-            hipLaunchKernelGGL(kern, dim3((unsigned)(g.qblocks * g.S)), dim3(256), 0, s, (const double*)dq, n,
-                               (const int*)nullptr, (int64_t)0, (const double*)dt, (const h8*)dimg, T, g.chunk,
-                               g.qblocks, P, part);
+            if constexpr (std::is_same_v<decltype(kern), decltype(&k_nn_mfma<4, 4>)>)
+                hipLaunchKernelGGL(kern, dim3((unsigned)(g.qblocks * g.S)), dim3(256), 0, s, (const double*)dq, n,
+                                   (const int*)nullptr, (int64_t)0, (const double*)dt, (const h8*)dimg, T, g.chunk,
+                                   g.qblocks, P, part, 0);
+            else
+                hipLaunchKernelGGL(kern, dim3((unsigned)(g.qblocks * g.S)), dim3(256), 0, s, (const double*)dq, n,
+                                   (const int*)nullptr, (int64_t)0, (const double*)dt, (const h8*)dimg, T, g.chunk,
+                                   g.qblocks, P, part);
         };
         launch();
         CK(hipGetLastError());

@@ -237,6 +237,7 @@ struct rp_ctx {
     bool nnm_ok = false;
     int nn_S = 0;                        // tree ranges of the last matrix-core launch
     int64_t nn_geo[4] = {0, 0, 0, 0};    // its T, queries per block, grid, device geometry (k_nn_reduce_g)
+    DevBuf<DI2> nn_pilot;                // per-query pilot bests (rp_nn.h)
 
     void free_staging() {
         if (h_send) (void)hipHostFree(h_send);
@@ -1050,10 +1051,18 @@ bool nn_mfma_params(const double* lo, const double* hi, NnMfma* P) {
     if (H > 15 || G > 15) return false;
     P->H2 = std::ldexp(1.0, H);
     P->G2 = std::ldexp(1.0, G);
+    P->iH2 = std::ldexp(1.0, -H);
+    P->iG2 = std::ldexp(1.0, -G);
     P->e0 = 8e-5 * R0 * R0 + 1e-12;
     P->e1 = 2e-5;
     P->thr0 = 4.04 * R0 * R0 + P->e0;   // >= every |x - y|^2 of in-bounds states
     return true;
+}
+
+// pilot search stride (tiles; RBE_NN_PILOT, 0 / 1 = off; read per search)
+int nn_pilot_stride() {
+    const char* e = std::getenv("RBE_NN_PILOT");
+    return e && *e ? std::atoi(e) : 16;
 }
 
 // device geometry for status-bounded searches (rp_nn.h nn_geom): RBE_NN_DEVGEOM=0 for
@@ -1088,8 +1097,25 @@ void launch_nn_mfma_w(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, 
     if (devgeom) grid = std::max<int64_t>(grid, 1024);   // room for the actual count's ranges
     // partials: S x n for the host geometry; within grid x per_block for any device one
     c->nn_part.ensure((size_t)std::max<int64_t>((int64_t)S * n, devgeom ? grid * per_block : 0));
+    // pilot (rp_nn.h): a search over every pst-th tile of the whole tree first, whose
+    // bests start every range of the full search (host-sized searches over >= 2 ranges)
+    const DI2* init = nullptr;
+    const int pst = nn_pilot_stride();
+    if (!Q.status && pst > 1 && S >= 2 && T >= (int64_t)pst * 16 * 64) {
+        constexpr int64_t per1 = (int64_t)W * 16;   // one row block per wave: more blocks
+        const int64_t qb1 = (n + per1 - 1) / per1;
+        const int64_t chunk1 = (T + NNM_STAGE - 1) / NNM_STAGE * NNM_STAGE;   // one range
+        c->nn_pilot.ensure((size_t)n);
+        hipLaunchKernelGGL((k_nn_mfma<1, W>), dim3((unsigned)qb1), dim3(64 * W), 0, c->stream, qx, n,
+                           (const int*)nullptr, (int64_t)0, tree, img, T, chunk1, qb1, c->nnm, c->nn_pilot.p, 0,
+                           pst, (const DI2*)nullptr);
+        init = c->nn_pilot.p;
+    }
     hipLaunchKernelGGL((k_nn_mfma<RB, W>), dim3((unsigned)grid), dim3(64 * W), 0, c->stream, qx, n, Q.status,
-                       Q.t0, tree, img, T, chunk, qblocks, c->nnm, c->nn_part.p, devgeom);
+                       Q.t0, tree, img, T, chunk, qblocks, c->nnm, c->nn_part.p, devgeom, 1, init);
+    static const bool log = std::getenv("RBE_NN_LOG") != nullptr;   // (diagnostic: tools/nn_seq.py)
+    if (log) fprintf(stderr, "nnlog n=%lld T=%lld grid=%lld S=%d status=%d\n", (long long)n, (long long)T,
+                     (long long)grid, S, Q.status ? 1 : 0);
     c->nn_S = S;
     c->nn_geo[0] = T;
     c->nn_geo[1] = per_block;

@@ -35,6 +35,7 @@ struct NnMfma {
     double H2;      // 2^H: the threshold slots (A: h / 2^H, hi / lo; B: 2^H)
     double e0, e1;  // thr = best + e0 + e1 * best
     double thr0;    // threshold while a query has no exact best (every node passes)
+    double iG2, iH2;   // 2^-G, 2^-H (exact: a product by them is the division by 2^G, 2^H)
 };
 
 // waves per block (template W): each with its own queries and tree stream
@@ -66,7 +67,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 // threshold slots (f16 hi / lo of h / 2^H) of a query with exact best b
 __device__ __forceinline__ void thr_slots(const NnMfma& P, double b, double na, _Float16& hh, _Float16& hl) {
     const double thr = b < 1e300 ? b + (P.e0 + P.e1 * b) : P.thr0;
-    split16((P.S * P.S) * (thr - na) * 0.5 / P.H2, hh, hl);
+    split16((P.S * P.S) * (thr - na) * 0.5 * P.iH2, hh, hl);
 }
 
 // A fragment of a query (row), k chunk `ch` (lane >> 4) of 8 slots
@@ -117,7 +118,7 @@ __device__ __forceinline__ h8 b_frag(const NnMfma& P, const double* y, int ch) {
         split16(P.S * yd, yh[d], yl[d]);
     }
     _Float16 gh, gl;
-    split16((P.S * P.S) * nb * 0.5 / P.G2, gh, gl);
+    split16((P.S * P.S) * nb * 0.5 * P.iG2, gh, gl);
     const _Float16 z = (_Float16)0.0f, h2 = (_Float16)P.H2;
     if (ch == 0) return h8{yh[0], yh[1], yh[2], yh[3], yh[4], yh[5], yh[6], yh[7]};
     if (ch == 1) return h8{yh[8], yh[0], yh[1], yh[2], yh[3], yh[4], yh[5], yh[6]};
@@ -217,18 +218,20 @@ __device__ unsigned long long g_nncount[4];
 constexpr int NNM_FLUSH = 64;
 constexpr int NNM_CAND = NNM_FLUSH + 64;   // a round appends at most one pair per lane
 
+// (4 waves per SIMD at every RB: the register budget of 128 VGPRs)
 template <int RB, int W>
-__global__ __launch_bounds__(64 * W) void k_nn_mfma(const double* __restrict__ qx, int64_t n,
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) void k_nn_mfma(const double* __restrict__ qx, int64_t n,
                                                           const int* status, int64_t t0,
                                                           const double* __restrict__ tree, const h8* __restrict__ img,
                                                           int64_t T, int64_t chunk, int64_t qblocks, NnMfma P,
-                                                          DI2* __restrict__ part, int devgeom) {
+                                                          DI2* __restrict__ part, int devgeom, int tstride,
+                                                          const DI2* __restrict__ init) {
     constexpr int QW = 16 * RB;   // queries per wave
-    __shared__ double s_q[W][QW][NQ];                       // query states (exact path)
     __shared__ unsigned long long s_best[W][QW];            // exact best distance (f64 bits; >= 0)
     __shared__ int s_bi[W][QW];                             // its node (lowest index among equal)
     __shared__ int s_ti[W][QW];                             // a round's lowest node at the new best
     __shared__ int2 s_cand[W][NNM_CAND];                    // passing (row, node) pairs, not yet evaluated
+    __shared__ double s_na[W][QW];                          // |x'|^2 of each row (threshold slots)
     int64_t nwg = (int64_t)rp_gdim();
     if (status) {
         n = min(n, (int64_t)status[0] - t0);
@@ -248,29 +251,39 @@ __global__ __launch_bounds__(64 * W) void k_nn_mfma(const double* __restrict__ q
     const int w = (int)(rp_tid() >> 6), lane = (int)(rp_tid() & 63), ch = lane >> 4;
     const int64_t t_lo = yr * chunk, t_hi = min(T, t_lo + chunk);
     const int64_t qw0 = qb0 + (int64_t)w * QW;
-
-    for (int i = lane; i < QW * NQ; i += 64) {
-        const int r = i / NQ, d = i - r * NQ;
-        const int64_t q = qw0 + r;
-        s_q[w][r][d] = q < n ? qx[q * NQ + d] : 0.0;
-    }
-    wave_lds_sync();
+    // a row's query state, read from global memory (L1 / L2) where the exact path needs
+    // it: staging the wave's 64 states in LDS cost more than it saved (rows past n
+    // read the last query; their results are never written)
+    auto qrow = [&](int r) -> const double* { return qx + min<int64_t>(qw0 + r, n - 1) * NQ; };
     // seed every query's exact best with NNM_SEEDS nodes spread over the range (the
     // exact f64 distance, lexicographic (distance, index) minimum): the filter then
     // starts from a typical distance instead of letting every node of the first stage
     // through to the exact path. Order does not matter: the result is the range's
     // lexicographic minimum whatever order its nodes are evaluated in.
+    // With a pilot (init: each query's nearest node over a strided subset of the whole
+    // tree, an upper bound d1 on its answer), every range starts from d1 instead and
+    // no node yet (index sentinel INT_MAX): the range returns its lexicographic minimum
+    // over the nodes at distance <= d1, or none — the pilot's node itself is in some
+    // range and passes the filter there (distance d1 <= the threshold), so the minimum
+    // over the ranges is the answer.
     for (int r = lane; r < QW; r += 64) {
         unsigned long long bb = 0x7FF0000000000000ull;   // +inf
         int bi = -1;
-        if (qw0 + r < n) {
+        if (init && qw0 + r < n) {
+            const DI2 v = init[qw0 + r];
+            if (v.i >= 0) {
+                bb = (unsigned long long)__double_as_longlong(v.d);
+                bi = 0x7fffffff;
+            }
+        }
+        if (bi < 0 && qw0 + r < n) {
             const int64_t R = t_hi - t_lo;
 #pragma unroll 1
             for (int k = 0; k < NNM_SEEDS; ++k) {
                 const int64_t j = t_lo + (R * k) / NNM_SEEDS;
                 if (k > 0 && j == t_lo + (R * (k - 1)) / NNM_SEEDS) continue;
                 const unsigned long long db =
-                    (unsigned long long)__double_as_longlong(dist2(tree + j * NQ, &s_q[w][r][0]));
+                    (unsigned long long)__double_as_longlong(dist2(tree + j * NQ, qrow(r)));
                 if (db < bb || (db == bb && (int)j < bi)) {
                     bb = db;
                     bi = (int)j;
@@ -282,23 +295,24 @@ __global__ __launch_bounds__(64 * W) void k_nn_mfma(const double* __restrict__ q
     }
     wave_lds_sync();
     // A fragments (row lane & 15 of each row block; k chunk ch); the threshold slots
-    // (chunk 3, elements 5 / 6) follow each row's exact best
+    // (chunk 3, elements 5 / 6) follow each row's exact best. The rows' |x'|^2 wait in
+    // LDS for the threshold updates (registers: RB = 8 fits 4 waves per SIMD)
     h8 a[RB];
-    double na[RB], curb[RB];
 #pragma unroll
     for (int rb = 0; rb < RB; ++rb) {
         const int r = rb * 16 + (lane & 15);
         _Float16 hh, hl;
-        a[rb] = a_frag(P, &s_q[w][r][0], qw0 + r < n, ch, &na[rb], &hh, &hl);
-        curb[rb] = __builtin_inf();
+        double na;
+        a[rb] = a_frag(P, qrow(r), qw0 + r < n, ch, &na, &hh, &hl);
+        if (ch == 0) s_na[w][r] = na;
         const double b0 = __longlong_as_double((long long)s_best[w][r]);
         if (ch == 3 && qw0 + r < n && b0 < 1e300) {   // the seeded threshold
-            curb[rb] = b0;
-            thr_slots(P, b0, na[rb], hh, hl);
+            thr_slots(P, b0, na, hh, hl);
             a[rb][5] = hh;
             a[rb][6] = hl;
         }
     }
+    wave_lds_sync();
     int ncand = 0;   // wave-uniform
     // evaluate the listed pairs, then tighten the rows' threshold slots
     auto flush = [&]() {
@@ -315,7 +329,7 @@ __global__ __launch_bounds__(64 * W) void k_nn_mfma(const double* __restrict__ q
                 node = cnd.y;
                 prev = s_best[w][row];
                 s_ti[w][row] = 0x7fffffff;
-                db = (unsigned long long)__double_as_longlong(dist2(tree + (int64_t)node * NQ, &s_q[w][row][0]));
+                db = (unsigned long long)__double_as_longlong(dist2(tree + (int64_t)node * NQ, qrow(row)));
             }
             wave_lds_sync();
             if (has) atomicMin(&s_best[w][row], db);
@@ -330,16 +344,17 @@ __global__ __launch_bounds__(64 * W) void k_nn_mfma(const double* __restrict__ q
             wave_lds_sync();
         }
         ncand = 0;
+        if (ch == 3) {   // (the same slots again where a row's best did not move)
 #pragma unroll
-        for (int rb = 0; rb < RB; ++rb) {
-            const int r = rb * 16 + (lane & 15);
-            const double bnow = __longlong_as_double((long long)s_best[w][r]);
-            if (ch == 3 && bnow != curb[rb]) {
-                curb[rb] = bnow;
-                _Float16 hh, hl;
-                thr_slots(P, bnow, na[rb], hh, hl);
-                a[rb][5] = hh;
-                a[rb][6] = hl;
+            for (int rb = 0; rb < RB; ++rb) {
+                const int r = rb * 16 + (lane & 15);
+                const double bnow = __longlong_as_double((long long)s_best[w][r]);
+                if (bnow < 1e300) {
+                    _Float16 hh, hl;
+                    thr_slots(P, bnow, s_na[w][r], hh, hl);
+                    a[rb][5] = hh;
+                    a[rb][6] = hl;
+                }
             }
         }
     };
@@ -351,30 +366,42 @@ __global__ __launch_bounds__(64 * W) void k_nn_mfma(const double* __restrict__ q
     // last tile (unconditional: static vmcnt waits). Tiles need no bounds test: the
     // image's pad slots and dead query rows never pass (k_nn_image, a_frag).
     constexpr int PF = 4;
-    const int64_t ntiles = (t_hi - t_lo + 15) / 16;
+    // tiles of the range: every tstride-th (a pilot search), else all
+    const int64_t ntiles = ((t_hi - t_lo + 15) / 16 + tstride - 1) / tstride;
     const int col = lane & 15;   // this lane's column of every tile
-    const h8* ib = img + (t_lo + col) * 4 + ch;   // tile t: ib[t * 64]
+    // tile t: the wave-uniform base + t x tstride KiB plus this lane's 16-byte slot
+    const char* ub = (const char*)(img + t_lo * 4);
+    const uint32_t loff = (uint32_t)((col * 4 + ch) * 16);
+    const int64_t tbytes = (int64_t)tstride * 1024, tnodes = (int64_t)tstride * 16;
+    auto tile_b = [&](int64_t t) { return *(const h8*)(ub + t * tbytes + loff); };
     h8 bq[PF];
 #pragma unroll
-    for (int u = 0; u < PF; ++u) bq[u] = ib[min<int64_t>(u, ntiles - 1) * 64];
+    for (int u = 0; u < PF; ++u) bq[u] = tile_b(min<int64_t>(u, ntiles - 1));
     const f4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
     auto tile_step = [&](int64_t tile, const h8& b) {
         f4 acc[RB];
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb) acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[rb], b, zero, 0, 0, 0);
-        // this lane's column: acc[rb][e] = row rb * 16 + 4 ch + e
-        float m = fmaxf(fmaxf(acc[0][0], acc[0][1]), fmaxf(acc[0][2], acc[0][3]));
+        // this lane's column: acc[rb][e] = row rb * 16 + 4 ch + e; mr[rb]: its max
+        float mr[RB];
 #pragma unroll
-        for (int rb = 1; rb < RB; ++rb) m = fmaxf(m, fmaxf(fmaxf(acc[rb][0], acc[rb][1]), fmaxf(acc[rb][2], acc[rb][3])));
+        for (int rb = 0; rb < RB; ++rb) mr[rb] = fmaxf(fmaxf(acc[rb][0], acc[rb][1]), fmaxf(acc[rb][2], acc[rb][3]));
+        float m = mr[0];
+#pragma unroll
+        for (int rb = 1; rb < RB; ++rb) m = fmaxf(m, mr[rb]);
         RP_NNC(0, 1);
         if (!__any(m >= 0.0f)) return;
         RP_NNC(1, 1);
+        // the passing elements as a bit mask (bit rb * 4 + e), built only for the row
+        // blocks with any; then appended one per lane and round
         unsigned pm = 0;
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb)
+            if (__any(mr[rb] >= 0.0f)) {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) pm |= (acc[rb][e] >= 0.0f ? 1u : 0u) << (rb * 4 + e);
-        const int node = (int)(t_lo + tile * 16 + col);
+                for (int e = 0; e < 4; ++e) pm |= (acc[rb][e] >= 0.0f ? 1u : 0u) << (rb * 4 + e);
+            }
+        const int node = (int)(t_lo + tile * tnodes + col);
 #ifdef RP_NN_COUNT
         {
             unsigned tot = __popc(pm);
@@ -393,19 +420,18 @@ __global__ __launch_bounds__(64 * W) void k_nn_mfma(const double* __restrict__ q
         }
     };
     int64_t tb = 0;
-    const h8* nx = ib + PF * 64;   // the next group's first tile
-    for (; tb + 2 * PF <= ntiles; tb += PF, nx += PF * 64) {   // (every prefetch in range)
+    for (; tb + 2 * PF <= ntiles; tb += PF) {   // (every prefetch in range)
 #pragma unroll
         for (int u = 0; u < PF; ++u) {
             tile_step(tb + u, bq[u]);
-            bq[u] = nx[u * 64];
+            bq[u] = tile_b(tb + PF + u);
         }
     }
     for (; tb + PF <= ntiles; tb += PF) {
 #pragma unroll
         for (int u = 0; u < PF; ++u) {
             tile_step(tb + u, bq[u]);
-            bq[u] = ib[min<int64_t>(tb + u + PF, ntiles - 1) * 64];
+            bq[u] = tile_b(min<int64_t>(tb + u + PF, ntiles - 1));
         }
     }
 #pragma unroll
@@ -416,8 +442,8 @@ __global__ __launch_bounds__(64 * W) void k_nn_mfma(const double* __restrict__ q
     for (int r = lane; r < QW; r += 64) {
         const int64_t q = qw0 + r;
         if (q < n)
-            part[yr * n + q] =
-                DI2{__longlong_as_double((long long)s_best[w][r]), s_bi[w][r], 0};
+            part[yr * n + q] = DI2{__longlong_as_double((long long)s_best[w][r]),
+                                   s_bi[w][r] == 0x7fffffff ? -1 : s_bi[w][r], 0};
     }
 }
 

@@ -50,6 +50,8 @@ static bool params(const double* lo, const double* hi, NnMfma* P) {
     const int G = (int)std::ceil(std::log2(0.55 * s2r2 / 65504.0));
     P->H2 = std::ldexp(1.0, H);
     P->G2 = std::ldexp(1.0, G);
+    P->iH2 = std::ldexp(1.0, -H);
+    P->iG2 = std::ldexp(1.0, -G);
     P->e0 = 8e-5 * R0 * R0 + 1e-12;
     P->e1 = 2e-5;
     P->thr0 = 4.04 * R0 * R0 + P->e0;
@@ -118,12 +120,13 @@ int main(int argc, char** argv) {
     CK(hipStreamCreate(&s));
     double *dq, *dt;
     h8* dimg;
-    DI2* part;
+    DI2 *part, *pilot;
     int32_t *out0, *out1;
     CK(hipMalloc(&dq, sizeof(double) * n * NQ));
     CK(hipMalloc(&dt, sizeof(double) * T * NQ));
     CK(hipMalloc(&dimg, sizeof(h8) * (T + NNM_PAD) * 4));
     CK(hipMalloc(&part, sizeof(DI2) * n * 64));
+    CK(hipMalloc(&pilot, sizeof(DI2) * n));
     CK(hipMalloc(&out0, sizeof(int32_t) * n));
     CK(hipMalloc(&out1, sizeof(int32_t) * n));
     CK(hipMemcpy(dq, q.data(), sizeof(double) * n * NQ, hipMemcpyHostToDevice));
@@ -135,14 +138,28 @@ int main(int argc, char** argv) {
     auto run = [&](auto kern, int RB, int32_t* out, const char* name, bool check, const int32_t* ref) {
         const Geom g = geom(n, T, RB, 4);
         auto launch = [&]() {
-            if constexpr (std::is_same_v<decltype(kern), decltype(&k_nn_mfma<4, 4>)>)
-                hipLaunchKernelGGL(kern, dim3((unsigned)(g.qblocks * g.S)), dim3(256), 0, s, (const double*)dq, n,
-                                   (const int*)nullptr, (int64_t)0, (const double*)dt, (const h8*)dimg, T, g.chunk,
-                                   g.qblocks, P, part, 0);
-            else
+            if constexpr (std::is_same_v<decltype(kern), int>) {   // the product: kern = pilot stride
+                if (kern > 1) {   // the pilot over every kern-th tile (rp_lib.hip launch_nn_mfma_w)
+                    const int64_t qb1 = (n + 63) / 64;
+                    hipLaunchKernelGGL((k_nn_mfma<1, 4>), dim3((unsigned)qb1), dim3(256), 0, s, (const double*)dq, n,
+                                       (const int*)nullptr, (int64_t)0, (const double*)dt, (const h8*)dimg, T,
+                                       (T + 63) / 64 * 64, qb1, P, pilot, 0, kern, (const DI2*)nullptr);
+                }
+                if (RB == 8)
+                    hipLaunchKernelGGL((k_nn_mfma<8, 4>), dim3((unsigned)(g.qblocks * g.S)), dim3(256), 0, s,
+                                       (const double*)dq, n, (const int*)nullptr, (int64_t)0, (const double*)dt,
+                                       (const h8*)dimg, T, g.chunk, g.qblocks, P, part, 0, 1,
+                                       kern > 1 ? (const DI2*)pilot : nullptr);
+                else
+                    hipLaunchKernelGGL((k_nn_mfma<4, 4>), dim3((unsigned)(g.qblocks * g.S)), dim3(256), 0, s,
+                                       (const double*)dq, n, (const int*)nullptr, (int64_t)0, (const double*)dt,
+                                       (const h8*)dimg, T, g.chunk, g.qblocks, P, part, 0, 1,
+                                       kern > 1 ? (const DI2*)pilot : nullptr);
+            } else {
                 hipLaunchKernelGGL(kern, dim3((unsigned)(g.qblocks * g.S)), dim3(256), 0, s, (const double*)dq, n,
                                    (const int*)nullptr, (int64_t)0, (const double*)dt, (const h8*)dimg, T, g.chunk,
                                    g.qblocks, P, part);
+            }
         };
         launch();
         CK(hipGetLastError());
@@ -178,7 +195,7 @@ int main(int argc, char** argv) {
                pairs / (ms * 1e-3) / 1e12, pairs * 64 / (ms * 1e-3) / 2.5e15, (long long)bad);
         fflush(stdout);
     };
-    run(k_nn_mfma<4, 4>, 4, out0, "product k_nn_mfma", true, nullptr);
+    run(1, 4, out0, "product k_nn_mfma", true, nullptr);   // (int kern: the product, pilot stride)
     nn_lab_variants(run, out0, out1);
     return 0;
 }

@@ -495,6 +495,12 @@ void nn_lab_variants(Run& run, int32_t* out0, int32_t* out1) {
     run(k_nnv<8, 4, 0, 4, true>, 8, out1, "v0 RB8 global queries", false, out0);
     run(k_nnv<8, 4, 1, 4, true>, 8, out1, "v1 RB8 global queries", false, out0);
     run(k_nnv<8, 4, 0, 4, true, 4>, 8, out1, "v0 RB8 global q, 4 waves/SIMD", false, out0);
-    run(k_nnv<8, 2, 0, 4, true, 4>, 8, out1, "v0 RB8 W2 global q, 4 waves", false, out0);
     run(k_nnv<4, 4, 0, 4, true, 5>, 4, out1, "v0 RB4 global q, 5 waves/SIMD", false, out0);
+    run(1, 4, out1, "product again", false, out0);
+    run(1, 8, out1, "product RB8", false, out0);
+    run(16, 4, out1, "product RB4 pilot 16", false, out0);
+    run(16, 8, out1, "product RB8 pilot 16", false, out0);
+    run(8, 4, out1, "product RB4 pilot 8", false, out0);
+    run(32, 4, out1, "product RB4 pilot 32", false, out0);
+    run(k_nnv<4, 4, 0, 4, true>, 4, out1, "v0 RB4 global queries again", false, out0);
 }

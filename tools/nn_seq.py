@@ -3,7 +3,12 @@ kernel trace of tools/c5_profile.py (or any plan run) and prints, per k_nn_mfma
 dispatch, its grid (blocks), duration and the kernels around it, then a histogram of
 where the matrix-core time goes by duration class.
 
-    python tools/nn_seq.py gpurun_out/nnseq/kt_kernel_trace.csv [--all]"""
+    python tools/nn_seq.py gpurun_out/nnseq/kt_kernel_trace.csv [--all] [--log stderr_with_nnlog_lines]
+
+With RBE_NN_LOG set, the library prints one "nnlog n= T= grid= S= status=" line per
+k_nn_mfma launch (host order = dispatch order on the one plan stream); --log pairs
+them with the dispatches: per launch (query, node) pairs and pairs/s (status-bounded
+searches: n is the largest count, the actual one is on the device)."""
 import csv
 import sys
 from collections import defaultdict
@@ -31,9 +36,23 @@ def main():
             blocks = int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"]))
             nxt = next((short(x) for x in rows[i + 1:i + 4] if not short(x).startswith("k_nn_reduce")), "?")
             nn.append((blocks, us, nxt))
+    logs = []
+    if "--log" in sys.argv:
+        for line in open(sys.argv[sys.argv.index("--log") + 1]):
+            if line.startswith("nnlog "):
+                logs.append(dict(kv.split("=") for kv in line.split()[1:]))
+        if len(logs) != len(nn):
+            print(f"(log has {len(logs)} launches, trace {len(nn)}: not paired)")
+            logs = []
     if "--all" in sys.argv:
         for k, (b, us, nxt) in enumerate(nn):
-            print(f"{k:4d} blocks {b:6d} {us:9.1f} us  then {nxt}")
+            extra = ""
+            if logs:
+                n, T = int(logs[k]["n"]), int(logs[k]["T"])
+                extra = f"  n {n:7d} T {T:7d} S {logs[k]['S']:>3s}"
+                if logs[k]["status"] == "0":
+                    extra += f"  {n * T / (us * 1e-6) / 1e12:6.2f} e12 pairs/s"
+            print(f"{k:4d} blocks {b:6d} {us:9.1f} us  then {nxt}{extra}")
     by = defaultdict(lambda: [0, 0.0])
     for b, us, nxt in nn:
         by[nxt][0] += 1

@@ -1059,10 +1059,12 @@ bool nn_mfma_params(const double* lo, const double* hi, NnMfma* P) {
     return true;
 }
 
-// pilot search stride (tiles; RBE_NN_PILOT, 0 / 1 = off; read per search)
+// pilot search stride (tiles; RBE_NN_PILOT, 0 / 1 = off; read per search). C5 covered-well
+// plans, NN time (4 seeds): RB 4 without a pilot 12.8 ms, RB 8 12.7, RB 8 + pilot every
+// 16th / 32nd / 64th tile 11.9 / 11.4 / 11.7 ms (profiles/r05/nn_pilot_ab.txt)
 int nn_pilot_stride() {
     const char* e = std::getenv("RBE_NN_PILOT");
-    return e && *e ? std::atoi(e) : 16;
+    return e && *e ? std::atoi(e) : 32;
 }
 
 // device geometry for status-bounded searches (rp_nn.h nn_geom): RBE_NN_DEVGEOM=0 for
@@ -1162,7 +1164,7 @@ bool nn_split(rp_ctx* c, const NnQuery& Q, int64_t n, Tree& tr, int64_t T, int32
         if (*e) mode = std::atoi(e) != 0;
     if (mode == 0 || (mode < 0 && !force && !nn_big(n, T))) return false;
     // the matrix-core search (rp_nn.h) unless RBE_NN_MFMA=0 (the packed-f32 k_nn_part)
-    int mfma_rb = 4;   // (read per search: large-tree searches take milliseconds)
+    int mfma_rb = 8;   // (read per search: large-tree searches take milliseconds)
     if (const char* e = std::getenv("RBE_NN_MFMA"))
         if (*e) mfma_rb = std::atoi(e);
     if (mfma_rb > 0 && c->nnm_ok) {

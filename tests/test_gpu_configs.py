@@ -159,11 +159,27 @@ def test_nearest_node_split_forced(gpu_ctx, name, split, grouped, mfma, monkeypa
 
 
 @pytest.mark.parametrize("name", ["C5_well_s0", "C5_well_s3"])
-@pytest.mark.parametrize("mfma", ["1", "8"])
+@pytest.mark.parametrize("mfma", ["1", "4"])
 def test_nearest_node_mfma_row_blocks(gpu_ctx, name, mfma, monkeypatch):
-    """The matrix-core search with 1 and 8 row blocks of 16 queries per wave on the
-    largest trees (3.3 x 10^5 nodes, 7-8 iterations): same plans."""
+    """The matrix-core search with 1 and 4 row blocks of 16 queries per wave (8, the
+    default, everywhere else) on the largest trees (3.3 x 10^5 nodes, 7-8
+    iterations): same plans."""
     monkeypatch.setenv("RBE_NN_MFMA", mfma)
+    _check(gpu_ctx, name)
+
+
+@pytest.mark.parametrize("name", ["C5_well_s0", "C5_well_s3", "C4_q5", "C2_q0_s1"])
+@pytest.mark.parametrize("pilot,mfma", [("0", "8"), ("4", "8"), ("0", "4"), ("16", "4"), ("2", "1")])
+def test_nearest_node_pilot(gpu_ctx, name, pilot, mfma, monkeypatch):
+    """The pilot search (every pilot-th tile of the whole tree first; its bests start
+    every range of the full search, whose ranges then return their minimum over the
+    nodes at or below that distance, or none): off, and at strides 2 / 4 / 16 with
+    1 / 4 / 8 row blocks, on every search it applies to (host-sized, >= 2 ranges,
+    T >= stride x 1,024 nodes: the C5 well's trees; the small configs' searches run
+    without one). Same plans."""
+    monkeypatch.setenv("RBE_NN_PILOT", pilot)
+    monkeypatch.setenv("RBE_NN_MFMA", mfma)
+    monkeypatch.setenv("RBE_NN_SPLIT", "1")
     _check(gpu_ctx, name)
 
 

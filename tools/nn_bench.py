@@ -2,7 +2,7 @@
 tree of T nodes (uniform, or clustered along random-walk branches like an RRT tree),
 timed per call; run under rocprofv3 for the k_nn_mfma kernel time and counters.
 
-    python tools/nn_bench.py [LIB.so] [--n 131072] [--T 300000] [--mode 4] [--reps 5] [--tree walk|uniform]
+    python tools/nn_bench.py [LIB.so] [--n 131072] [--T 300000] [--mode 8] [--reps 5] [--tree walk|uniform]
 """
 import argparse
 import os
@@ -35,7 +35,7 @@ def main():
     ap.add_argument("lib", nargs="?")
     ap.add_argument("--n", type=int, default=131072)
     ap.add_argument("--T", type=int, default=300000)
-    ap.add_argument("--mode", type=int, default=4)
+    ap.add_argument("--mode", type=int, default=8)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--tree", default="walk")
     ap.add_argument("--check", action="store_true", help="compare with mode 0 (k_nn_part)")

@@ -1212,7 +1212,7 @@ bool nn_split(rp_ctx* c, const NnQuery& Q, int64_t n, Tree& tr, int64_t T, int32
 // place query are 10-30 us: a wake-up there would cost more than the wait), then
 // sleeps between polls — quanta of 10 % of the time already waited, 10-200 us — so a
 // long query (C5-class trees, a 10 s budget: motion_primitives.py:144) does not hold
-// a host core. Polls the stream every 4096 spins / ~1 ms of sleeping, so that a failed
+// a host core. Polls the stream every 4096 spins / 10 ms of sleeping, so that a failed
 // or finished-without-publishing stream turns into an error instead of a hang, and a
 // stream busy past the watchdog is reported.
 struct WaitTuning {
@@ -1283,7 +1283,11 @@ void wait_seq(rp_ctx* c, int seq) {
     c->waits[2] += t_sleep - t_enter;
     while (*f != seq) {   // sleep between polls
         const double now = now_s();
-        if (now - last_check > 1e-3) {
+        // the stream check every 10 ms: hipStreamQuery on a stream with queued work
+        // costs up to ~1 ms of host CPU (cpu_probe at 64k-sample iterations: 1.5 s of
+        // CPU in 2 s of waiting with a check every ms); a stream that finished without
+        // publishing is an error path, found 10 ms later
+        if (now - last_check > 10e-3) {
             if (wait_check(c, f, seq, t0)) break;
             last_check = now;
         }

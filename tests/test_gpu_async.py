@@ -171,19 +171,21 @@ def _sealed_well():
     return q, sc
 
 
-def test_long_query_does_not_hold_host_cores(gpu_ctx):
+@pytest.mark.parametrize("batch", [4096, 65536])
+def test_long_query_does_not_hold_host_cores(gpu_ctx, batch):
     """A query that runs its whole 2 s budget (the sealed well: APPROXIMATE) through
     rp_plan_async / rp_plan_wait: the caller's wait blocks after a short spin and the
     planner thread sleeps between its polls of the GPU's status word, so the process'
     CPU time (every thread, os.times) is a fraction of the wall time — a 10 s query
-    (code/motion_primitives.py:144) no longer pegs two host cores."""
+    (code/motion_primitives.py:144) no longer pegs two host cores. At
+    65,536-sample iterations (waits of milliseconds on a stream with queued work) too."""
     import time
     q, sc = _sealed_well()
     gpu_ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
     gpu_ctx.set_attached(q["attached"])
-    p = _abi.make_params(seed=0, batch=4096, n_waypoints=150, timeout_s=2.0, straight_first=False,
+    p = _abi.make_params(seed=0, batch=batch, n_waypoints=150, timeout_s=2.0, straight_first=False,
                          tree_capacity=1 << 23)
-    gpu_ctx.reserve(4096, 1 << 23)
+    gpu_ctx.reserve(batch, 1 << 23)
     t0, w0 = os.times(), time.perf_counter()
     gpu_ctx.plan_async(q["start"], q["goal"], model.Q_LO, model.Q_HI, p, path_cap=256)
     path, st = gpu_ctx.plan_wait()

@@ -194,12 +194,27 @@ __device__ __forceinline__ int wave_incl_max(int v) {
 // One (group, round) of a k_edges launch: the group's slot counts, scanned; the
 // round's items mapped to their edges; their states checked. Returns false when the
 // round is past the group's items.
+// Coarse-first passes (pk > 1, launch_edges): pass 0 checks an edge's slot 0 and every
+// pk-th interior slot (edge_coarse_count of its slots), pass 1 the others of the
+// edges still valid after it — cntv[e], made between the passes by k_edge_rest, so
+// that the layout of pass 1 is fixed while it runs. Most failing edges fail on a
+// coarse slot (a collision spans consecutive states), and 3/4 of the slots the
+// C5 covered-well plans check belong to edges that fail (tools/edge_stats.py).
+// An edge is valid iff all its slots are, in any order: same verdicts.
+__host__ __device__ __forceinline__ int edge_coarse_count(int cnt, int pk) { return 1 + (cnt - 1) / pk; }
+// item i of a pass -> the edge's slot
+__device__ __forceinline__ int edge_pass_slot(int i, int pk, int pass) {
+    if (pk <= 1) return i;
+    return pass == 0 ? i * pk : i + 1 + i / (pk - 1);
+}
+
 template <int NCL, bool BF>
 __device__ __forceinline__ bool edge_group_round(const double* __restrict__ from, const double* __restrict__ to,
                                                  const int* __restrict__ nd, int64_t n_edges, int mode,
                                                  uint8_t* valid, int group, int* gfail,
                                                  unsigned long long* counter, const DevScene* __restrict__ sc,
-                                                 int64_t g, int r0, WaveQ& wq, int* mark) {
+                                                 int64_t g, int r0, WaveQ& wq, int* mark, int pk = 1,
+                                                 int pass = 0, const int* __restrict__ cntv = nullptr) {
     const int lane = rp_tid();
     const int64_t e = g * VBLOCK + lane;
     int nde = -1, emode = mode, cnt = 0;
@@ -209,10 +224,11 @@ __device__ __forceinline__ bool edge_group_round(const double* __restrict__ from
             emode = (nde & ND_FROM) ? 1 : 0;
             nde &= ~ND_FROM;
         }
-        // the layout depends on nd alone: valid / gfail change while the launch
-        // runs (this launch's own failures), and every wave of a group must see the
-        // same item list (they are read per item below)
+        // the layout depends on nd alone (pass 1: on cntv, fixed before the launch):
+        // valid / gfail change while the launch runs (this launch's own failures), and
+        // every wave of a group must see the same item list (they are read per item below)
         cnt = nde >= 0 ? (nde > 1 ? nde : 1) : 0;
+        if (pk > 1) cnt = pass == 0 ? (cnt > 0 ? edge_coarse_count(cnt, pk) : 0) : cntv[e];
     }
     const int incl = wave_incl_add(cnt);
     const int total = __builtin_amdgcn_readlane(incl, 63);
@@ -235,7 +251,7 @@ __device__ __forceinline__ bool edge_group_round(const double* __restrict__ from
     bool run = t < total;
     int slot = 0, nj = 0, mj = 0;
     if (run) {
-        slot = t - sj;
+        slot = edge_pass_slot(t - sj, pk, pass);
         nj = pj & ~(1 << 30);
         mj = (pj >> 30) & 1;
         run = valid[ej] != 0;
@@ -296,7 +312,7 @@ __global__ __launch_bounds__(VBLOCK, LOOP ? RP_EDGE_WAVES_LOOP : (NCL == NCL_GRI
     const double* __restrict__ from, const double* __restrict__ to, const int* __restrict__ nd, int64_t n_edges,
     int kmax, int mode, uint8_t* valid, int group, int* gfail, unsigned long long* counter,
     const DevScene* __restrict__ sc, const int* __restrict__ dcount, int per_item, const int* __restrict__ dkmax,
-    int r_first) {
+    int r_first, int pk = 1, int pass = 0, const int* __restrict__ cntv = nullptr) {
     __shared__ WaveQ wq;
     __shared__ int mark[VBLOCK];
     // device-side edge count (planner iterations: dcount = accepted targets) and
@@ -313,7 +329,7 @@ __global__ __launch_bounds__(VBLOCK, LOOP ? RP_EDGE_WAVES_LOOP : (NCL == NCL_GRI
         if (w >= n_waves) return;
         const int64_t g = w / kk;
         edge_group_round<NCL, BF>(from, to, nd, n_edges, mode, valid, group, gfail, counter, sc, g,
-                                  (r_first + (int)(w - g * kk)) * VBLOCK, wq, mark);
+                                  (r_first + (int)(w - g * kk)) * VBLOCK, wq, mark, pk, pass, cntv);
     } else {
         for (int64_t w = rp_bid(); w < n_waves; w += rp_gdim()) {
             const int64_t g = w / kk;
@@ -323,6 +339,30 @@ __global__ __launch_bounds__(VBLOCK, LOOP ? RP_EDGE_WAVES_LOOP : (NCL == NCL_GRI
                     break;
         }
     }
+}
+
+// Between the coarse-first passes: the slots pass 1 still checks per edge — the
+// non-coarse ones of an edge still valid and not past its prefix group's first
+// failure, else none
+__global__ void k_edge_rest(const int* __restrict__ nd, int64_t n_edges, const int* __restrict__ dcount,
+                            int per_item, int mode, const uint8_t* __restrict__ valid, int group,
+                            const int* __restrict__ gfail, int pk, int* __restrict__ cntv) {
+    const int64_t e = (int64_t)rp_bid() * rp_bdim() + rp_tid();
+    if (e >= n_edges) return;
+    const int64_t n = dcount ? min(n_edges, (int64_t)dcount[0] * per_item) : n_edges;
+    int rest = 0;
+    if (e < n) {
+        int d = nd[e];
+        if (mode == 2 && d >= 0) d &= ~ND_FROM;
+        const int cnt = d >= 0 ? (d > 1 ? d : 1) : 0;
+        bool live = cnt > 0 && valid[e] != 0;
+        if (live && gfail) {
+            const int64_t gi = e / group, si = e - gi * group;
+            live = gfail[gi] > si;
+        }
+        if (live) rest = cnt - edge_coarse_count(cnt, pk);
+    }
+    cntv[e] = rest;
 }
 
 // ---- work-compacted edge launch (large batches): the (edge, slot) items of

@@ -238,6 +238,8 @@ struct rp_ctx {
     int nn_S = 0;                        // tree ranges of the last matrix-core launch
     int64_t nn_geo[4] = {0, 0, 0, 0};    // its T, queries per block, grid, device geometry (k_nn_reduce_g)
     DevBuf<DI2> nn_pilot;                // per-query pilot bests (rp_nn.h)
+    DevBuf<unsigned long long> estats;   // RBE_EDGE_STATS counters (k_edge_stats)
+    DevBuf<int> ecnt;                    // coarse-first edge passes: pass-1 slots per edge
 
     void free_staging() {
         if (h_send) (void)hipHostFree(h_send);
@@ -481,6 +483,59 @@ int conn_rounds() {
     return r;
 }
 
+// diagnostic (RBE_EDGE_STATS): per edge launch, after it ran: [0] slots of all edges,
+// [1] slots of failed edges, [2] edges, [3] failed edges, [4] slots of edges past
+// their prefix group's first failure — how much of a launch's work an early exit
+// could skip (tools/edge_stats.py)
+__global__ void k_edge_stats(const int* __restrict__ nd, int64_t n, const int* dcount, int per_item,
+                             const uint8_t* __restrict__ valid, int group, const int* __restrict__ gfail,
+                             unsigned long long* __restrict__ st) {
+    const int64_t e = (int64_t)rp_bid() * rp_bdim() + rp_tid();
+    if (dcount) n = min(n, (int64_t)dcount[0] * per_item);
+    unsigned long long v[5] = {0, 0, 0, 0, 0};
+    if (e < n) {
+        int d = nd[e];
+        if (d >= 0) {
+            d &= ~ND_FROM;
+            const unsigned long long cnt = d > 1 ? d : 1;
+            v[0] = cnt;
+            v[2] = 1;
+            if (!valid[e]) v[1] = cnt, v[3] = 1;
+            if (gfail) {
+                const int64_t gi = e / group, si = e - gi * group;
+                if (gfail[gi] < si) v[4] = cnt;
+            }
+        }
+    }
+    for (int k = 0; k < 5; ++k) {
+        unsigned long long x = v[k];
+        for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+        if ((rp_tid() & 63) == 0 && x) atomicAdd(&st[k], x);
+    }
+}
+
+bool edge_stats_on() {
+    static const bool on = std::getenv("RBE_EDGE_STATS") != nullptr;
+    return on;
+}
+
+// coarse-first edge passes: interior stride (RBE_EDGE_COARSE, 0 / 1 = one pass) and
+// the smallest launch (edges x kmax items, RBE_EDGE_COARSE_MIN) that takes them.
+// C5 covered-well plans, edge time of the 4 seeds (profiles/r05/edge_coarse_ab.txt):
+// one pass 10.7 ms; stride 2 / 3 / 4 / 5 / 6 / 7 / 8 / 9 / 10 / 12 / 16 / 32: 9.1 /
+// 12.2 / 13.8 / 8.0 / 9.6 / 10.0 / 7.7 / 7.2 / 8.4 / 9.6 / 9.5 / 10.6 ms — the states
+// checked fall to 1/3-1/2 at every stride, but their rate per state falls too (the
+// waves of a pass hold states of more, and more varied, edges) and unevenly (not
+// understood: 7 and 9 differ by 40 %); 8 measured best over three boxes
+int edge_coarse_stride() {
+    const char* e = std::getenv("RBE_EDGE_COARSE");
+    return e && *e ? std::atoi(e) : 8;
+}
+int64_t edge_coarse_min() {
+    const char* e = std::getenv("RBE_EDGE_COARSE_MIN");
+    return e && *e ? std::atoll(e) : (int64_t)1 << 18;
+}
+
 // sr: the straight edge riding along (rp_plan's first front; lane-group kernels only)
 void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd, int64_t n, int kmax,
                   int mode, uint8_t* valid, int group, int* gfail, hipStream_t s, const int* dcount = nullptr,
@@ -534,27 +589,43 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
                                         : nb_full);
     const unsigned nb_rest = (unsigned)std::min<int64_t>(groups * 4, max_blocks ? max_blocks : 8192);
     const unsigned nb_first = (unsigned)std::min<int64_t>(groups, EDGE_LOOP_BLOCKS);   // (one wave per group)
+    // coarse-first passes (rp_kernels.h edge_coarse_count): a large loop-free launch
+    // checks slot 0 and every pk-th interior slot of its edges, then the other slots of
+    // the edges still valid (k_edge_rest's counts) — 3/4 of what the C5 covered-well
+    // plans check is on edges that fail, most of them on a coarse slot
+    const int pk = edge_coarse_stride();
+    const bool coarse = !split && !first && !loop && !dkmax && pk > 1 && kmax > 1 &&
+                        threads >= edge_coarse_min();
+    const int kc = coarse ? edge_coarse_count(kmax, pk) : kmax;   // pass-0 rounds per group
+    const int kr = coarse ? std::max(1, kmax - kc) : 0;            // pass-1 rounds per group
+    if (coarse) c->ecnt.ensure((size_t)n);
     const dim3 b(VBLOCK);
     const int ps = prof_begin(c, s);
     // (the reference's robot base folded in as a constant, as for k_validity)
     const bool bf = base_fixed(c->scene);
-#define RP_EDGES_L(N, L, G, KM, DK, RF)                                                                           \
+#define RP_EDGES_P(N, L, G, KM, DK, RF, PK, PS, CV)                                                               \
     do {                                                                                                           \
         if (bf) hipLaunchKernelGGL((k_edges<N, true, L>), dim3(G), b, 0, s, from, to, nd, n, KM, mode, valid,      \
-                                   group, gfail, c->counter.p, c->d_scene, dcount, per_item, DK, RF);              \
+                                   group, gfail, c->counter.p, c->d_scene, dcount, per_item, DK, RF, PK, PS, CV);  \
         else hipLaunchKernelGGL((k_edges<N, false, L>), dim3(G), b, 0, s, from, to, nd, n, KM, mode, valid,        \
-                                group, gfail, c->counter.p, c->d_scene, dcount, per_item, DK, RF);                 \
+                                group, gfail, c->counter.p, c->d_scene, dcount, per_item, DK, RF, PK, PS, CV);     \
     } while (0)
-#define RP_EDGES(N)                                                                       \
-    do {                                                                                  \
-        if (split) {                                                                      \
-            RP_EDGES_L(N, false, nb, km0, nullptr, 0);                                    \
-            RP_EDGES_L(N, true, nb_rest, km0, dkmax, EDGE_DEV_ROUNDS);                    \
-        } else if (first) {                                                               \
-            RP_EDGES_L(N, false, nb, km0, nullptr, 0);                                    \
-            RP_EDGES_L(N, true, nb_first, km0 + 1, nullptr, km0);                         \
-        } else if (loop) RP_EDGES_L(N, true, nb, kmax, dkmax, 0);                         \
-        else RP_EDGES_L(N, false, nb, kmax, dkmax, 0);                                    \
+#define RP_EDGES_L(N, L, G, KM, DK, RF) RP_EDGES_P(N, L, G, KM, DK, RF, 1, 0, (const int*)nullptr)
+#define RP_EDGES(N)                                                                                               \
+    do {                                                                                                          \
+        if (split) {                                                                                              \
+            RP_EDGES_L(N, false, nb, km0, nullptr, 0);                                                            \
+            RP_EDGES_L(N, true, nb_rest, km0, dkmax, EDGE_DEV_ROUNDS);                                            \
+        } else if (first) {                                                                                       \
+            RP_EDGES_L(N, false, nb, km0, nullptr, 0);                                                            \
+            RP_EDGES_L(N, true, nb_first, km0 + 1, nullptr, km0);                                                 \
+        } else if (coarse) {                                                                                      \
+            RP_EDGES_P(N, false, (unsigned)(groups * kc), kc, nullptr, 0, pk, 0, (const int*)nullptr);            \
+            hipLaunchKernelGGL(k_edge_rest, dim3(blocks_for(n, 256)), dim3(256), 0, s, nd, n, dcount, per_item,   \
+                               mode, (const uint8_t*)valid, group, (const int*)gfail, pk, c->ecnt.p);             \
+            RP_EDGES_P(N, false, (unsigned)(groups * kr), kr, nullptr, 0, pk, 1, (const int*)c->ecnt.p);          \
+        } else if (loop) RP_EDGES_L(N, true, nb, kmax, dkmax, 0);                                                 \
+        else RP_EDGES_L(N, false, nb, kmax, dkmax, 0);                                                            \
     } while (0)
     switch (ncl_bucket(c->scene)) {
         case NCL_GRID: RP_EDGES(NCL_GRID); break;
@@ -566,8 +637,17 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
     }
 #undef RP_EDGES
 #undef RP_EDGES_L
+#undef RP_EDGES_P
     HIP_TRY(hipGetLastError());
     prof_end(c, ps, 1, s);
+    if (edge_stats_on() && !dkmax) {
+        if (!c->estats.p) {
+            c->estats.ensure(8);
+            HIP_TRY(hipMemset(c->estats.p, 0, 8 * sizeof(unsigned long long)));
+        }
+        hipLaunchKernelGGL(k_edge_stats, dim3(blocks_for(n, 256)), dim3(256), 0, s, nd, n, dcount, per_item,
+                           (const uint8_t*)valid, group, (const int*)gfail, c->estats.p);
+    }
 }
 
 // Diagnostic (RBE_DEBUG_SYNC=1): wait for the stream after a launch, at most 10 s,
@@ -3134,6 +3214,18 @@ int rp_ik(rp_ctx* c, int32_t n_targets, const double* pos, const double* quat, c
 int rp_debug_waits(rp_ctx* c, double* out, int32_t n) {
     if (!c || !out || n < 5) return RP_ERR_ARG;
     std::memcpy(out, c->waits, sizeof c->waits);
+    return RP_OK;
+}
+
+// diagnostic: the RBE_EDGE_STATS counters since the last call (k_edge_stats), then reset
+int rp_debug_edges(rp_ctx* c, double* out, int32_t n) {
+    if (!c || !out || n < 5) return RP_ERR_ARG;
+    unsigned long long h[5] = {0, 0, 0, 0, 0};
+    if (c->estats.p) {
+        if (hipMemcpy(h, c->estats.p, sizeof h, hipMemcpyDeviceToHost) != hipSuccess) return RP_ERR_DEVICE;
+        if (hipMemset(c->estats.p, 0, sizeof h) != hipSuccess) return RP_ERR_DEVICE;
+    }
+    for (int k = 0; k < 5; ++k) out[k] = (double)h[k];
     return RP_OK;
 }
 

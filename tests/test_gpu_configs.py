@@ -195,6 +195,19 @@ def test_nearest_node_status_geometry(gpu_ctx, name, devgeom, monkeypatch):
     _check(gpu_ctx, name)
 
 
+@pytest.mark.parametrize("name", ["C5_well_s0", "C5_well_s3", "C4_q5", "C2_q0_s1"])
+@pytest.mark.parametrize("pk,cmin", [("0", ""), ("2", "0"), ("4", "0"), ("8", "")])
+def test_coarse_first_edge_passes_in_plans(gpu_ctx, name, pk, cmin, monkeypatch):
+    """The planner's edge launches through the coarse-first passes (slot 0 and every
+    pk-th interior slot first, then the rest of the edges still valid; RBE_EDGE_COARSE)
+    or one pass (0), at the default size threshold and forced on every wave-compacted
+    launch (RBE_EDGE_COARSE_MIN=0): same plans."""
+    monkeypatch.setenv("RBE_EDGE_COARSE", pk)
+    if cmin:
+        monkeypatch.setenv("RBE_EDGE_COARSE_MIN", cmin)
+    _check(gpu_ctx, name)
+
+
 def test_kernel_profile_of_a_plan(gpu_ctx):
     """rp_set_profiling / rp_get_profile (bench.py's nearest-node and edge rooflines):
     the profiled plan is the same plan, and the profile counts its launches, time

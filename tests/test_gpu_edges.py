@@ -57,3 +57,25 @@ def test_device_edges_equal_oracle(gpu_ctx, oracle_lib, scene, n, scale):
     assert np.array_equal(got, ref), f"{int((got != ref).sum())} of {n} edge flags differ"
     # the host-pointer API (rp_check_edges) gives the same flags
     assert np.array_equal(gpu_ctx.check_edges(qa, qb, res), ref)
+
+
+@pytest.mark.parametrize("scene", ["goal3", "clutter64"])
+@pytest.mark.parametrize("n,scale", [(2049, 1.0), (40000, 1.0), (20000, 3.0)])
+@pytest.mark.parametrize("pk", ["0", "2", "3", "4", "8"])
+def test_coarse_first_edge_passes(gpu_ctx, oracle_lib, scene, n, scale, pk, monkeypatch):
+    """rp_check_edges through the coarse-first passes (slot 0 and every pk-th interior
+    slot, then the other slots of the edges still valid; RBE_EDGE_COARSE) forced on at
+    every size (RBE_EDGE_COARSE_MIN=0), and off: the oracle's flags."""
+    monkeypatch.setenv("RBE_EDGE_COARSE", pk)
+    monkeypatch.setenv("RBE_EDGE_COARSE_MIN", "0")
+    monkeypatch.setenv("RBE_ML_LANES", "1")   # (the wave-compacted kernel at every size)
+    sc = _scene(scene)
+    o = oracle_lib.OracleScene()
+    o.set_scene(sc.boxes, sc.plane_z, sc.base)
+    o.set_attached(-1)
+    gpu_ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+    gpu_ctx.set_attached(-1)
+    qa, qb, res = _edges(n, 5 + n, scale)
+    ref = o.check_edges(qa, qb, res)
+    got = gpu_ctx.check_edges(qa, qb, res)
+    assert np.array_equal(got, ref), f"{int((got != ref).sum())} of {n} edge flags differ"

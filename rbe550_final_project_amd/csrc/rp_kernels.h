@@ -201,10 +201,16 @@ __device__ __forceinline__ int wave_incl_max(int v) {
 // coarse slot (a collision spans consecutive states), and 3/4 of the slots the
 // C5 covered-well plans check belong to edges that fail (tools/edge_stats.py).
 // An edge is valid iff all its slots are, in any order: same verdicts.
-__host__ __device__ __forceinline__ int edge_coarse_count(int cnt, int pk) { return 1 + (cnt - 1) / pk; }
-// item i of a pass -> the edge's slot
-__device__ __forceinline__ int edge_pass_slot(int i, int pk, int pass) {
-    if (pk <= 1) return i;
+// pk < 0: the far block instead (slot 0, then the |pk|-th part of the interior next to
+// it, slots cnt - 1, cnt - 2, ...: the states nearest the new sample; pass 1 the rest,
+// contiguous from slot 1) — the same counts, each pass's states of an edge adjacent
+__host__ __device__ __forceinline__ int edge_coarse_count(int cnt, int pk) {
+    return 1 + (cnt - 1) / (pk < 0 ? -pk : pk);
+}
+// item i of a pass -> the slot of an edge with cnt slots
+__device__ __forceinline__ int edge_pass_slot(int i, int pk, int pass, int cnt) {
+    if (pk == 1 || pk == 0) return i;
+    if (pk < 0) return pass == 0 ? (i == 0 ? 0 : cnt - i) : i + 1;
     return pass == 0 ? i * pk : i + 1 + i / (pk - 1);
 }
 
@@ -228,7 +234,7 @@ __device__ __forceinline__ bool edge_group_round(const double* __restrict__ from
         // valid / gfail change while the launch runs (this launch's own failures), and
         // every wave of a group must see the same item list (they are read per item below)
         cnt = nde >= 0 ? (nde > 1 ? nde : 1) : 0;
-        if (pk > 1) cnt = pass == 0 ? (cnt > 0 ? edge_coarse_count(cnt, pk) : 0) : cntv[e];
+        if (pk > 1 || pk < -1) cnt = pass == 0 ? (cnt > 0 ? edge_coarse_count(cnt, pk) : 0) : cntv[e];
     }
     const int incl = wave_incl_add(cnt);
     const int total = __builtin_amdgcn_readlane(incl, 63);
@@ -251,8 +257,8 @@ __device__ __forceinline__ bool edge_group_round(const double* __restrict__ from
     bool run = t < total;
     int slot = 0, nj = 0, mj = 0;
     if (run) {
-        slot = edge_pass_slot(t - sj, pk, pass);
         nj = pj & ~(1 << 30);
+        slot = edge_pass_slot(t - sj, pk, pass, nj > 1 ? nj : 1);
         mj = (pj >> 30) & 1;
         run = valid[ej] != 0;
         if (run && gfail) {

@@ -526,7 +526,9 @@ bool edge_stats_on() {
 // 12.2 / 13.8 / 8.0 / 9.6 / 10.0 / 7.7 / 7.2 / 8.4 / 9.6 / 9.5 / 10.6 ms — the states
 // checked fall to 1/3-1/2 at every stride, but their rate per state falls too (the
 // waves of a pass hold states of more, and more varied, edges) and unevenly (not
-// understood: 7 and 9 differ by 40 %); 8 measured best over three boxes
+// understood: 7 and 9 differ by 40 %); 8 measured best over three boxes. The far block
+// first (pk < 0: the states next to the new sample, contiguous) measured 9.2-12.5 ms
+// at -2 / -3 / -4 / -6 — so the states' spatial spread within a wave is not the cost
 int edge_coarse_stride() {
     const char* e = std::getenv("RBE_EDGE_COARSE");
     return e && *e ? std::atoi(e) : 8;
@@ -594,7 +596,7 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
     // the edges still valid (k_edge_rest's counts) — 3/4 of what the C5 covered-well
     // plans check is on edges that fail, most of them on a coarse slot
     const int pk = edge_coarse_stride();
-    const bool coarse = !split && !first && !loop && !dkmax && pk > 1 && kmax > 1 &&
+    const bool coarse = !split && !first && !loop && !dkmax && (pk > 1 || pk < -1) && kmax > 1 &&
                         threads >= edge_coarse_min();
     const int kc = coarse ? edge_coarse_count(kmax, pk) : kmax;   // pass-0 rounds per group
     const int kr = coarse ? std::max(1, kmax - kc) : 0;            // pass-1 rounds per group

@@ -196,7 +196,7 @@ def test_nearest_node_status_geometry(gpu_ctx, name, devgeom, monkeypatch):
 
 
 @pytest.mark.parametrize("name", ["C5_well_s0", "C5_well_s3", "C4_q5", "C2_q0_s1"])
-@pytest.mark.parametrize("pk,cmin", [("0", ""), ("2", "0"), ("4", "0"), ("8", "")])
+@pytest.mark.parametrize("pk,cmin", [("0", ""), ("2", "0"), ("4", "0"), ("8", ""), ("-2", "0"), ("-3", "")])
 def test_coarse_first_edge_passes_in_plans(gpu_ctx, name, pk, cmin, monkeypatch):
     """The planner's edge launches through the coarse-first passes (slot 0 and every
     pk-th interior slot first, then the rest of the edges still valid; RBE_EDGE_COARSE)

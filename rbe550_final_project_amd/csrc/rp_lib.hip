@@ -1142,8 +1142,10 @@ bool nn_mfma_params(const double* lo, const double* hi, NnMfma* P) {
 }
 
 // pilot search stride (tiles; RBE_NN_PILOT, 0 / 1 = off; read per search). C5 covered-well
-// plans, NN time (4 seeds): RB 4 without a pilot 12.8 ms, RB 8 12.7, RB 8 + pilot every
-// 16th / 32nd / 64th tile 11.9 / 11.4 / 11.7 ms (profiles/r05/nn_pilot_ab.txt)
+// plans, NN time (4 seeds): RB 4 without a pilot 12.8 ms, RB 8 12.7, RB 8 + a one-range
+// RB 1 pilot every 16th / 32nd / 64th tile 11.9 / 11.4 / 11.7 ms; the pilot with RB 4
+// over ~1,024 blocks: none 12.0, 8 / 16 / 32 / 64: 11.4 / 11.0 / 11.0 / 11.2 ms
+// (profiles/r05/nn_pilot_ab.txt)
 int nn_pilot_stride() {
     const char* e = std::getenv("RBE_NN_PILOT");
     return e && *e ? std::atoi(e) : 32;
@@ -1184,19 +1186,28 @@ void launch_nn_mfma_w(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, 
     // pilot (rp_nn.h): a search over every pst-th tile of the whole tree first, whose
     // bests start every range of the full search (host-sized searches over >= 2 ranges)
     const DI2* init = nullptr;
+    int init_S = 0;
     const int pst = nn_pilot_stride();
     if (!Q.status && pst > 1 && S >= 2 && T >= (int64_t)pst * 16 * 64) {
-        constexpr int64_t per1 = (int64_t)W * 16;   // one row block per wave: more blocks
+        // the pilot: 4 row blocks per wave, the strided subset split into ranges of
+        // >= 8 of its tiles so that ~1,024 blocks run; the full search takes the
+        // minimum over its ranges
+        constexpr int RBP = 4;
+        constexpr int64_t per1 = (int64_t)W * 16 * RBP;
         const int64_t qb1 = (n + per1 - 1) / per1;
-        const int64_t chunk1 = (T + NNM_STAGE - 1) / NNM_STAGE * NNM_STAGE;   // one range
-        c->nn_pilot.ensure((size_t)n);
-        hipLaunchKernelGGL((k_nn_mfma<1, W>), dim3((unsigned)qb1), dim3(64 * W), 0, c->stream, qx, n,
+        const int64_t sub = ((T + 15) / 16 + pst - 1) / pst;   // tiles of the subset
+        int64_t S1 = std::max<int64_t>(1, std::min<int64_t>({(1024 + qb1 - 1) / qb1, sub / 8, 16}));
+        const int64_t chunk1 = (sub + S1 - 1) / S1 * pst * 16;   // nodes: whole subset tiles per range
+        S1 = (T + chunk1 - 1) / chunk1;
+        c->nn_pilot.ensure((size_t)(S1 * n));
+        hipLaunchKernelGGL((k_nn_mfma<RBP, W>), dim3((unsigned)(qb1 * S1)), dim3(64 * W), 0, c->stream, qx, n,
                            (const int*)nullptr, (int64_t)0, tree, img, T, chunk1, qb1, c->nnm, c->nn_pilot.p, 0,
-                           pst, (const DI2*)nullptr);
+                           pst, (const DI2*)nullptr, 0);
         init = c->nn_pilot.p;
+        init_S = (int)S1;
     }
     hipLaunchKernelGGL((k_nn_mfma<RB, W>), dim3((unsigned)grid), dim3(64 * W), 0, c->stream, qx, n, Q.status,
-                       Q.t0, tree, img, T, chunk, qblocks, c->nnm, c->nn_part.p, devgeom, 1, init);
+                       Q.t0, tree, img, T, chunk, qblocks, c->nnm, c->nn_part.p, devgeom, 1, init, init_S);
     static const bool log = std::getenv("RBE_NN_LOG") != nullptr;   // (diagnostic: tools/nn_seq.py)
     if (log) fprintf(stderr, "nnlog n=%lld T=%lld grid=%lld S=%d status=%d\n", (long long)n, (long long)T,
                      (long long)grid, S, Q.status ? 1 : 0);

@@ -225,7 +225,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
                                                           const double* __restrict__ tree, const h8* __restrict__ img,
                                                           int64_t T, int64_t chunk, int64_t qblocks, NnMfma P,
                                                           DI2* __restrict__ part, int devgeom, int tstride,
-                                                          const DI2* __restrict__ init) {
+                                                          const DI2* __restrict__ init, int init_S) {
     constexpr int QW = 16 * RB;   // queries per wave
     __shared__ unsigned long long s_best[W][QW];            // exact best distance (f64 bits; >= 0)
     __shared__ int s_bi[W][QW];                             // its node (lowest index among equal)
@@ -269,11 +269,14 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     for (int r = lane; r < QW; r += 64) {
         unsigned long long bb = 0x7FF0000000000000ull;   // +inf
         int bi = -1;
-        if (init && qw0 + r < n) {
-            const DI2 v = init[qw0 + r];
-            if (v.i >= 0) {
-                bb = (unsigned long long)__double_as_longlong(v.d);
-                bi = 0x7fffffff;
+        if (init && qw0 + r < n) {   // (the pilot's ranges: their minimum distance)
+            for (int y = 0; y < init_S; ++y) {
+                const DI2 v = init[(int64_t)y * n + qw0 + r];
+                const unsigned long long db = (unsigned long long)__double_as_longlong(v.d);
+                if (v.i >= 0 && db < bb) {
+                    bb = db;
+                    bi = 0x7fffffff;
+                }
             }
         }
         if (bi < 0 && qw0 + r < n) {

@@ -126,7 +126,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&dt, sizeof(double) * T * NQ));
     CK(hipMalloc(&dimg, sizeof(h8) * (T + NNM_PAD) * 4));
     CK(hipMalloc(&part, sizeof(DI2) * n * 64));
-    CK(hipMalloc(&pilot, sizeof(DI2) * n));
+    CK(hipMalloc(&pilot, sizeof(DI2) * n * 16));
     CK(hipMalloc(&out0, sizeof(int32_t) * n));
     CK(hipMalloc(&out1, sizeof(int32_t) * n));
     CK(hipMemcpy(dq, q.data(), sizeof(double) * n * NQ, hipMemcpyHostToDevice));
@@ -139,22 +139,27 @@ int main(int argc, char** argv) {
         const Geom g = geom(n, T, RB, 4);
         auto launch = [&]() {
             if constexpr (std::is_same_v<decltype(kern), int>) {   // the product: kern = pilot stride
+                int S1 = 0;
                 if (kern > 1) {   // the pilot over every kern-th tile (rp_lib.hip launch_nn_mfma_w)
-                    const int64_t qb1 = (n + 63) / 64;
-                    hipLaunchKernelGGL((k_nn_mfma<1, 4>), dim3((unsigned)qb1), dim3(256), 0, s, (const double*)dq, n,
-                                       (const int*)nullptr, (int64_t)0, (const double*)dt, (const h8*)dimg, T,
-                                       (T + 63) / 64 * 64, qb1, P, pilot, 0, kern, (const DI2*)nullptr);
+                    const int64_t qb1 = (n + 255) / 256;
+                    const int64_t sub = ((T + 15) / 16 + kern - 1) / kern;
+                    int64_t s1 = std::max<int64_t>(1, std::min<int64_t>({(1024 + qb1 - 1) / qb1, sub / 8, 16}));
+                    const int64_t chunk1 = (sub + s1 - 1) / s1 * kern * 16;
+                    S1 = (int)((T + chunk1 - 1) / chunk1);
+                    hipLaunchKernelGGL((k_nn_mfma<4, 4>), dim3((unsigned)(qb1 * S1)), dim3(256), 0, s,
+                                       (const double*)dq, n, (const int*)nullptr, (int64_t)0, (const double*)dt,
+                                       (const h8*)dimg, T, chunk1, qb1, P, pilot, 0, kern, (const DI2*)nullptr, 0);
                 }
                 if (RB == 8)
                     hipLaunchKernelGGL((k_nn_mfma<8, 4>), dim3((unsigned)(g.qblocks * g.S)), dim3(256), 0, s,
                                        (const double*)dq, n, (const int*)nullptr, (int64_t)0, (const double*)dt,
                                        (const h8*)dimg, T, g.chunk, g.qblocks, P, part, 0, 1,
-                                       kern > 1 ? (const DI2*)pilot : nullptr);
+                                       kern > 1 ? (const DI2*)pilot : nullptr, S1);
                 else
                     hipLaunchKernelGGL((k_nn_mfma<4, 4>), dim3((unsigned)(g.qblocks * g.S)), dim3(256), 0, s,
                                        (const double*)dq, n, (const int*)nullptr, (int64_t)0, (const double*)dt,
                                        (const h8*)dimg, T, g.chunk, g.qblocks, P, part, 0, 1,
-                                       kern > 1 ? (const DI2*)pilot : nullptr);
+                                       kern > 1 ? (const DI2*)pilot : nullptr, S1);
             } else {
                 hipLaunchKernelGGL(kern, dim3((unsigned)(g.qblocks * g.S)), dim3(256), 0, s, (const double*)dq, n,
                                    (const int*)nullptr, (int64_t)0, (const double*)dt, (const h8*)dimg, T, g.chunk,

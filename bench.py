@@ -332,8 +332,11 @@ def well_profile(ctx, seeds=(2, 3, 4, 0)):
     nn_alg_tf = pairs_per_s * NN_FLOP_PER_PAIR / 1e12        # the squared distance's algorithmic FLOP
     fps = flops_per_state(len(sc.boxes))
     ed_tf = tot["edge_states"] * fps / (tot["edge_ms"] * 1e-3) / 1e12
-    sample = (f"C5 covered-well plans, seeds {list(seeds)}, 131,072-sample iterations (trees up to 3.3e5 nodes); "
-              "every nearest-node launch of the plans (large trees: k_nn_mfma; small: the fused LDS-tile kernels)")
+    plans = f"C5 covered-well plans, seeds {list(seeds)}, 131,072-sample iterations (trees up to 3.3e5 nodes); "
+    sample = plans + ("every nearest-node search of the plans (large trees: the pilot + k_nn_mfma + k_nn_reduce_g; "
+                      "small: the fused LDS-tile kernels); pairs = queries x tree nodes of each search")
+    edge_sample = plans + ("every edge launch of the plans (both coarse-first passes and k_edge_rest of the large "
+                           "ones); states = the states actually checked (a pass-0 failure skips the rest of its edge)")
     return ({"bound": "mfma", "achieved": round(nn_mfma_tf, 3), "peak": F16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
              "frac": round(nn_mfma_tf / F16_MFMA_PEAK_TFLOPS, 4),
              "kernel": "k_nn_mfma (+ k_ext_conn_nn / k_ext_nn / k_conn_nn on small trees)",
@@ -348,7 +351,7 @@ def well_profile(ctx, seeds=(2, 3, 4, 0)):
              "launches": tot["edge_launches"], "kernel_ms": round(tot["edge_ms"], 3),
              "states": int(tot["edge_states"]),
              "states_per_sec": round(tot["edge_states"] / (tot["edge_ms"] * 1e-3), 1),
-             "flop_per_state": fps, "sample": sample})
+             "flop_per_state": fps, "sample": edge_sample})
 
 
 def main():

@@ -1368,6 +1368,166 @@ __global__ void k_conn_append(const int32_t* __restrict__ rec, const int32_t* __
     if (b && lane == 0) atomicMin(first_reached, (int)(t + __builtin_ctzll(b)));
 }
 
+// ---- multi-block accepts with a decoupled look-back scan (sub-batches above
+// FUSE_MAX, single rank): the flags, the scan and the appends in ONE launch instead
+// of flag + hipCUB scan (2 kernels) + append, each ~4-6 us of launch latency in a
+// dependent chain. Block b publishes its aggregate, wave 0 looks back over its
+// predecessors' words (a window of 64 per round) to the nearest inclusive prefix,
+// then publishes its own inclusive prefix. A word: (epoch << 32) | (flag << 30) |
+// value (flag 1: aggregate, 2: inclusive; value < 2^30); the epoch (a per-launch
+// counter from the host) makes words of earlier launches stale without a reset.
+// Blocks are dispatched in order and a block waits only on lower ones, so the
+// waits end; a poll budget (LB_SPIN_MAX) turns a broken protocol into an error flag
+// (*err) instead of a hang.
+constexpr int LB_THREADS = 256, LB_ITEMS = 4;
+constexpr unsigned LB_SPIN_MAX = 1u << 24;
+__device__ __forceinline__ void lb_publish(unsigned long long* st, int64_t b, unsigned epoch, int flag, int v) {
+    const unsigned long long w = ((unsigned long long)epoch << 32) | ((unsigned long long)flag << 30) | (unsigned)v;
+    __hip_atomic_store(st + b, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// exclusive prefix of block b (wave 0 calls it; every lane returns the prefix)
+__device__ __forceinline__ int lb_lookback(unsigned long long* st, int64_t b, unsigned epoch, int* err) {
+    const int lane = (int)(rp_tid() & 63);
+    int prefix = 0;
+    for (int64_t j = b - 1;; j -= 64) {
+        const int64_t idx = j - lane;
+        int flag = 2, val = 0;   // (before block 0: an inclusive 0)
+        if (idx >= 0) {
+            unsigned long long w = 0;
+            for (unsigned spin = 0;; ++spin) {
+                w = __hip_atomic_load(st + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((unsigned)(w >> 32) == epoch && ((w >> 30) & 3u) != 0) break;
+                if (spin >= LB_SPIN_MAX) {
+                    *err = 1;
+                    w = ((unsigned long long)epoch << 32) | (2ull << 30);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            flag = (int)((w >> 30) & 3u);
+            val = (int)(w & 0x3fffffffu);
+        }
+        const unsigned long long inc = __ballot(flag == 2);
+        const int stop = inc ? (int)__builtin_ctzll(inc) : 64;
+        int c = lane <= stop ? val : 0;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+        prefix += c;
+        if (inc) return prefix;
+    }
+}
+// block-wide: this block's exclusive prefix given its aggregate (all threads call)
+__device__ __forceinline__ int lb_block_prefix(unsigned long long* st, unsigned epoch, int agg, int* lds, int* err) {
+    const int64_t b = rp_bid();
+    if (b == 0) {
+        if (rp_tid() == 0) lb_publish(st, 0, epoch, 2, agg);
+        return 0;
+    }
+    if (rp_tid() == 0) lb_publish(st, b, epoch, 1, agg);
+    if (rp_tid() < 64) {
+        const int pre = lb_lookback(st, b, epoch, err);
+        if (rp_tid() == 0) {
+            lb_publish(st, b, epoch, 2, pre + agg);
+            lds[0] = pre;
+        }
+    }
+    __syncthreads();
+    const int pre = lds[0];
+    __syncthreads();
+    return pre;
+}
+
+// extension accept of a sub-batch (k_ext_result_flag + scan + k_ext_append): sample
+// k is accepted iff its extension edge is valid; accepted samples are appended to
+// tree A in sample order
+__global__ __launch_bounds__(LB_THREADS) void k_ext_accept_lb(
+    const uint8_t* __restrict__ valid, const int32_t* __restrict__ near, int64_t B, uint64_t seed, uint64_t g0,
+    Bounds bd, double range, double* A, int32_t* Apar, uint8_t* Acand, int64_t TA, int* status, int64_t sg_edge,
+    int sg_stride, unsigned long long* lbst, unsigned epoch, int* err) {
+    __shared__ int lds[LB_THREADS / 64 + 1];
+    const int64_t k0 = ((int64_t)rp_bid() * LB_THREADS + rp_tid()) * LB_ITEMS;
+    int v[LB_ITEMS], cnt = 0;
+#pragma unroll
+    for (int u = 0; u < LB_ITEMS; ++u) {
+        const int64_t k = k0 + u;
+        v[u] = k < B && valid[k] ? near[k] : -1;
+        cnt += v[u] >= 0;
+    }
+    int agg;
+    const int excl = block_scan_excl<int, LB_THREADS>(cnt, lds, &agg);
+    const int pre = lb_block_prefix(lbst, epoch, agg, lds, err);
+    int64_t pos = TA + pre + excl;
+#pragma unroll
+    for (int u = 0; u < LB_ITEMS; ++u)
+        if (v[u] >= 0) ext_append_one(k0 + u, v[u], pos++, seed, g0, bd, range, A, Apar, Acand);
+    if (status && rp_bid() == rp_gdim() - 1 && rp_tid() == 0) {
+        status[ST_NACC] = pre + agg;
+        status[ST_FIRST] = 0x7fffffff;
+        if (sg_edge >= 0) status[ST_SG] = sg_flags(valid, sg_edge, sg_stride);
+    }
+}
+
+// connect accept of a sub-batch (k_conn_record_len + scan + k_conn_append, single
+// rank: the chain nodes are copied from the edge records): target t < nacc appends
+// the first L = min(gfail, chain length) nodes of its chain to tree B, in target
+// order; inclL (the inclusive L scan) is written for k_finalize
+__global__ __launch_bounds__(LB_THREADS) void k_conn_accept_lb(
+    const int32_t* __restrict__ y, const int32_t* __restrict__ m, const int* __restrict__ gfail, int64_t B,
+    int* status, double* Bt, int32_t* Bpar, uint8_t* Bcand, int64_t TB, int cmax, int a_start, uint8_t* Acand,
+    int64_t TA0, int32_t* chain_end, const double* __restrict__ chain_nodes, int32_t* __restrict__ inclL,
+    unsigned long long* lbst, unsigned epoch, int* err) {
+    __shared__ int lds[LB_THREADS / 64 + 1];
+    const int64_t nacc = min(B, (int64_t)status[ST_NACC]);
+    const int64_t t0 = ((int64_t)rp_bid() * LB_THREADS + rp_tid()) * LB_ITEMS;
+    int L[LB_ITEMS], cnt = 0;
+#pragma unroll
+    for (int u = 0; u < LB_ITEMS; ++u) {
+        const int64_t t = t0 + u;
+        L[u] = 0;
+        if (t < nacc) {
+            const int mk = m[t] & CHAIN_LEN;
+            L[u] = gfail[t] < mk ? gfail[t] : mk;
+        }
+        cnt += L[u];
+    }
+    int agg;
+    const int excl = block_scan_excl<int, LB_THREADS>(cnt, lds, &agg);
+    const int pre = lb_block_prefix(lbst, epoch, agg, lds, err);
+    int run = pre + excl;
+    bool reached_any = false;
+    int first = 0x7fffffff;
+#pragma unroll
+    for (int u = 0; u < LB_ITEMS; ++u) {
+        const int64_t t = t0 + u;
+        if (t >= B) break;
+        run += L[u];
+        inclL[t] = run;
+        if (t >= nacc) continue;
+        const int64_t off = TB + run - L[u];
+        int32_t par = y[t];
+        for (int s = 0; s < L[u]; ++s) {
+            const double* cs = chain_nodes + (t * cmax + s) * NQ;
+            for (int d = 0; d < NQ; ++d) Bt[(off + s) * NQ + d] = cs[d];
+            Bpar[off + s] = par;
+            Bcand[off + s] = 0;
+            par = (int32_t)(off + s);
+        }
+        const int mk = m[t];
+        const bool reached = L[u] == (mk & CHAIN_LEN) && (mk & CHAIN_REACHES);
+        chain_end[t] = L[u] > 0 ? par : -1;
+        if (!reached && a_start) Acand[TA0 + t] = 1;
+        if (reached && !reached_any) {
+            reached_any = true;
+            first = (int)t;
+        }
+    }
+    // first REACHED target: one atomic per wave
+    int f = first;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) f = min(f, __shfl_xor(f, o, 64));
+    if ((rp_tid() & 63) == 0 && f != 0x7fffffff) atomicMin(status + ST_FIRST, f);
+}
+
 // what a fused accept kernel already holds in LDS of its iteration's appends: the
 // tail's join-node lookups and parent walks through new nodes then read LDS, not
 // a chain of dependent global loads

@@ -240,6 +240,10 @@ struct rp_ctx {
     DevBuf<DI2> nn_pilot;                // per-query pilot bests (rp_nn.h)
     DevBuf<unsigned long long> estats;   // RBE_EDGE_STATS counters (k_edge_stats)
     DevBuf<int> ecnt;                    // coarse-first edge passes: pass-1 slots per edge
+    DevBuf<unsigned long long> lbst;     // look-back accept kernels: per-block words (rp_kernels.h)
+    DevBuf<int> lberr;                   // their poll-budget error flag
+    unsigned lb_epoch = 0;               // their per-launch epoch
+    bool lb_used = false;                // a look-back accept ran in this plan
 
     void free_staging() {
         if (h_send) (void)hipHostFree(h_send);
@@ -676,6 +680,30 @@ void debug_wait(rp_ctx* c, const char* label) {
 void launch_edges_packed(rp_ctx* c, const double* from, const double* to, const int* nd, int64_t n, int kmax,
                          int mode, uint8_t* valid, int group, int* gfail, hipStream_t s, const int* dcount,
                          int per_item);
+
+// look-back accept kernels (rp_kernels.h k_ext_accept_lb / k_conn_accept_lb) for the
+// single-rank sub-batches above FUSE_MAX; RBE_ACCEPT_LB=0: flag + hipCUB scan +
+// append (A/B). Read per iteration.
+bool accept_lb() {
+    const char* e = std::getenv("RBE_ACCEPT_LB");
+    return !(e && *e && std::atoi(e) == 0);
+}
+// their grid for n items; the per-block words exist (zeroed when made) and the
+// launch gets a fresh epoch
+unsigned lb_prepare(rp_ctx* c, int64_t n) {
+    const int64_t nb = (n + (int64_t)LB_THREADS * LB_ITEMS - 1) / ((int64_t)LB_THREADS * LB_ITEMS);
+    if ((int64_t)c->lbst.n < nb) {
+        c->lbst.ensure((size_t)nb);
+        HIP_TRY(hipMemsetAsync(c->lbst.p, 0, sizeof(unsigned long long) * c->lbst.n, c->stream));
+    }
+    if (!c->lberr.p) {
+        c->lberr.ensure(1);
+        HIP_TRY(hipMemsetAsync(c->lberr.p, 0, sizeof(int), c->stream));
+    }
+    if (++c->lb_epoch == 0) c->lb_epoch = 1;
+    c->lb_used = true;
+    return (unsigned)nb;
+}
 
 // inclusive scan of int32 (hipCUB) on the context stream
 void scan_incl(rp_ctx* c, const int32_t* in, int32_t* out, int64_t n) {
@@ -2071,6 +2099,11 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                     hipLaunchKernelGGL(k_ext_accept_small<4>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, c->valid.p,
                                        c->near_.p, C, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, An, status,
                                        sg, sg_stride);
+            } else if (accept_lb()) {   // flags + scan + appends in one launch (decoupled look-back)
+                const unsigned nb = lb_prepare(c, C);
+                hipLaunchKernelGGL(k_ext_accept_lb, dim3(nb), dim3(LB_THREADS), 0, c->stream, c->valid.p, c->near_.p,
+                                   C, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, An, status, sg, sg_stride,
+                                   c->lbst.p, c->lb_epoch, c->lberr.p);
             } else {
                 hipLaunchKernelGGL(k_ext_result_flag, dim3(blocks_for(C, 256)), dim3(256), 0, c->stream,
                                    c->valid.p, c->near_.p, C, c->res.p, c->acc.p);
@@ -2110,6 +2143,15 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                 if (C <= FUSE_THREADS) RP_CONN_SMALL(1);
                 else RP_CONN_SMALL(4);
 #undef RP_CONN_SMALL
+            } else if (accept_lb()) {
+                c->incl.ensure((size_t)C);
+                const unsigned nb = lb_prepare(c, C);
+                hipLaunchKernelGGL(k_conn_accept_lb, dim3(nb), dim3(LB_THREADS), 0, c->stream, c->yv.p, c->mv.p,
+                                   c->gfail.p, C, status, Bt.q.p, Bt.par.p, Bt.cand.p, Bn, cmax, a_start, A.cand.p,
+                                   An, c->chain_end.p, (const double*)(a_start ? c->efrom.p : c->eto.p), c->incl.p,
+                                   c->lbst.p, c->lb_epoch, c->lberr.p);
+                hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, c->stream, status, c->incl.p, An, a_start,
+                                   A.par.p, Bt.par.p, c->chain_end.p, pa, io);
             } else {
                 hipLaunchKernelGGL(k_conn_record_len, dim3(blocks_for(C, 256)), dim3(256), 0, c->stream, c->yv.p,
                                    c->mv.p, c->gfail.p, (const int*)status, C, c->rec.p, c->Lv.p);
@@ -2782,9 +2824,12 @@ static int plan_entry(rp_ctx* c, const double start[RP_NQ], const double goal[RP
     c->prof = rp_profile{};
     c->pused = 0;
     c->in_plan = true;
+    c->lb_used = false;
     int rc;
     try {
         rc = plan_impl(c, start, goal, lo, hi, params, path_out, path_cap, n_out, status_out);
+        if (c->lb_used && read_scalar(c, c->lberr.p) != 0)   // (large plans only: one read)
+            throw HipError{"look-back accept exceeded its poll budget (a block's predecessor never published)"};
     } catch (...) {
         c->in_plan = false;
         c->pused = 0;

@@ -208,6 +208,17 @@ def test_coarse_first_edge_passes_in_plans(gpu_ctx, name, pk, cmin, monkeypatch)
     _check(gpu_ctx, name)
 
 
+@pytest.mark.parametrize("name", ["C5_well_s0", "C5_well_s3", "C4_q5", "C2_q0_s1"])
+@pytest.mark.parametrize("lb", ["0", "1"])
+def test_lookback_accepts(gpu_ctx, name, lb, monkeypatch):
+    """Sub-batches above FUSE_MAX accept their extensions and connect chains in one
+    launch each (flags, a decoupled look-back scan and the appends: k_ext_accept_lb,
+    k_conn_accept_lb) or through flag + hipCUB scan + append (RBE_ACCEPT_LB=0): same
+    trees, same plans."""
+    monkeypatch.setenv("RBE_ACCEPT_LB", lb)
+    _check(gpu_ctx, name)
+
+
 def test_kernel_profile_of_a_plan(gpu_ctx):
     """rp_set_profiling / rp_get_profile (bench.py's nearest-node and edge rooflines):
     the profiled plan is the same plan, and the profile counts its launches, time

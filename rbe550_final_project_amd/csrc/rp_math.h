@@ -549,6 +549,15 @@ struct QueueState {
     ClusterRegs<NCL> cl;
 };
 
+#ifdef RP_PAIR_STATS
+// diagnostic builds (tools/val_lab.hip): per self pair [P][0] sphere passes, [P][1]
+// AABB passes, [P][2] narrow-phase hits; [NPAIR][0] lanes walked
+__device__ unsigned long long g_pairstats[NPAIR + 1][3];
+#define RP_PSTAT(p, i, v) do { if (v) atomicAdd(&g_pairstats[p][i], (unsigned long long)(v)); } while (0)
+#else
+#define RP_PSTAT(p, i, v) do { } while (0)
+#endif
+
 // Drains pop: a queue is drained only when the next enqueue would overflow it, and
 // then by exactly one pass over its top items (one per active lane), so mid-walk
 // passes run full; the walk's end pops until empty. Room is guaranteed: a batch has
@@ -572,7 +581,14 @@ __device__ __forceinline__ void pop_ss(S& s) {
             const float rr = ri + rj;
             // an LDS OR (ds_or_b32) from every popping lane instead of a store under a
             // per-lane branch: no exec-mask save / restore (+2.9 % goal3 A/B)
+#ifdef RP_PAIR_STATS
+            const bool h = segment_segment_dist2(a1, b1, a2, b2) <= rr * rr;
+            RP_PSTAT(tag >> 8, 1, 1);
+            RP_PSTAT(tag >> 8, 2, h ? 1 : 0);
+            atomicOr(&s.Q->hit[tag & 63], (int)h);
+#else
             atomicOr(&s.Q->hit[tag & 63], (int)(segment_segment_dist2(a1, b1, a2, b2) <= rr * rr));
+#endif
         }
     }
     __builtin_amdgcn_wave_barrier();
@@ -726,6 +742,7 @@ __device__ __forceinline__ bool pair_sphere(const Capsules& k) {
 template <int P, class S>
 __device__ __forceinline__ void pair_enqueue(const Capsules& k, S& s, bool cand, unsigned long long m) {
     constexpr int I = PAIRS[P][0], J = PAIRS[P][1];
+    if ((__lane_id() & 63) == 0) RP_PSTAT(P, 0, __popcll(m));
     if (!m) return;
     room_ss(s, __popcll(m));
     if (cand) {

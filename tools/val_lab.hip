@@ -165,6 +165,24 @@ int main(int argc, char** argv) {
            "min %.4f / %.4f  flags differ %lld  valid %.4f\n",
            scene, (long long)n, ncl, ma, n / (ma * 1e-3) / 1e9, mb, n / (mb * 1e-3) / 1e9, ma / mb, ta[0], tb[0],
            (long long)diff, (double)valid / n);
+#ifdef RP_PAIR_STATS
+    {   // per self pair: sphere passes, AABB passes, narrow-phase hits per state (one lab launch)
+        unsigned long long z[NPAIR + 1][3] = {};
+        CK(hipMemcpyToSymbol(HIP_SYMBOL(g_pairstats), z, sizeof z));
+        lab();
+        CK(hipStreamSynchronize(s));
+        unsigned long long h[NPAIR + 1][3];
+        CK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_pairstats), sizeof h));
+        double ts = 0, ta = 0, th = 0;
+        for (int p = 0; p < NPAIR; ++p) {
+            if (!h[p][0]) continue;
+            printf("pair %2d (%2d,%2d): sphere %.4f  aabb %.4f  hit %.4f per state\n", p, PAIRS[p][0], PAIRS[p][1],
+                   (double)h[p][0] / n, (double)h[p][1] / n, (double)h[p][2] / n);
+            ts += h[p][0]; ta += h[p][1]; th += h[p][2];
+        }
+        printf("all pairs: sphere %.3f  aabb %.3f  hit %.3f per state\n", ts / n, ta / n, th / n);
+    }
+#endif
     L.destroy(ctx);
     return diff != 0;
 }

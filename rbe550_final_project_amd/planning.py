@@ -267,15 +267,15 @@ class PlannerInterface:
         gen = getattr(ctx, "scene_gen", None)
         pushed = self._pushed
         ctxs = self._ctxs or [ctx]   # every rank of a multi-GPU planner sees the same scene
-        if gen is not None and pushed is not None and pushed[0] == gen and pushed[1] == poses \
-                and pushed[2] == base:
+        if gen is not None and pushed is not None and pushed[0] == gen and pushed[2] == base \
+                and np.array_equal(pushed[1], poses):
             if pushed[3] != idx:
                 for c in ctxs:
                     c.set_attached(idx)
                 self._pushed = (ctx.scene_gen, poses, base, idx)
             return
         if hasattr(ctx, "set_scene_poses"):   # one library call (rp_set_scene_poses)
-            P = np.array(poses, dtype=np.float64).reshape(-1, 7)
+            P = np.ascontiguousarray(poses, dtype=np.float64).reshape(-1, 7)
             B = np.array(base, dtype=np.float64)
             for c in ctxs:
                 c.set_scene_poses(P, rd.halves_f32, rd.plane_z, B, idx)

@@ -239,18 +239,18 @@ def _entities(scene):
 
 def _rows(x, n, k):
     """An (n, k) pose block (torch tensor / array, possibly with a leading env axis of
-    1) as n lists of k Python floats, with one .tolist()."""
+    1) as a float64 array: one device read for a GPU tensor, no per-value Python
+    objects (the drop-in reads the poses on every plan_path call)."""
     if hasattr(x, "detach"):
         x = x.detach()
-    if hasattr(x, "tolist") and not isinstance(x, np.ndarray):
-        v = x.tolist()
-    else:
-        v = np.asarray(x, dtype=float).tolist()
-    while len(v) == 1 and n != 1 and isinstance(v[0], list) and isinstance(v[0][0], list):
-        v = v[0]
-    if n == 1 and not isinstance(v[0], list):
-        v = [v]
-    return [[float(a) for a in r[:k]] for r in v[:n]]
+    if hasattr(x, "cpu") and not isinstance(x, np.ndarray):
+        x = x.cpu().numpy()
+    a = np.asarray(x, dtype=np.float64)
+    while a.ndim > 2 and a.shape[0] == 1:
+        a = a[0]
+    if a.ndim == 1:
+        a = a[None]
+    return a[:n, :k]
 
 
 class GenesisReader:
@@ -314,19 +314,21 @@ class GenesisReader:
         return len(ents) == len(self._ents) and all(a is b for a, b in zip(ents, self._ents))
 
     def poses(self):
-        """(box poses: per box [x, y, z, qw, qx, qy, qz], robot base (x, y, z))."""
+        """(box poses: an (n, 7) float64 array of rows [x, y, z, qw, qx, qy, qz], robot
+        base (x, y, z))."""
         if self._links is not None:
             n = len(self._links)
             P = _rows(self._solver.get_links_pos(self._links), n, 3)
             Q = _rows(self._solver.get_links_quat(self._links), n, 4)
-            boxes = [p + q for p, q in zip(P[:self._nb], Q[:self._nb])]
-            base = tuple(P[self._nb]) if self._with_base else BASE
+            boxes = np.concatenate([P[:self._nb], Q[:self._nb]], axis=1)
+            base = tuple(P[self._nb].tolist()) if self._with_base else BASE
             return boxes, base
-        boxes = []
+        rows = []
         for ent in self.box_ents:
             pos = _floats(ent.get_pos(), 3)
             quat = _floats(ent.get_quat(), 4) if hasattr(ent, "get_quat") else [1.0, 0.0, 0.0, 0.0]
-            boxes.append(pos + quat)
+            rows.append(pos + quat)
+        boxes = np.array(rows, dtype=np.float64).reshape(-1, 7)
         base = BASE
         if self.robot_ent is not None and hasattr(self.robot_ent, "get_pos"):
             base = tuple(_floats(self.robot_ent.get_pos(), 3))
@@ -340,7 +342,7 @@ class GenesisReader:
 
     def boxes(self, poses):
         """Box records (center, half, yaw or quaternion) of box poses from poses()."""
-        return [((p[0], p[1], p[2]), h, rot_of_quat(p[3:7])) for p, h in zip(poses, self.halves)]
+        return [((float(p[0]), float(p[1]), float(p[2])), h, rot_of_quat(p[3:7])) for p, h in zip(poses, self.halves)]
 
     def read(self):
         """The scene as a Scene record."""

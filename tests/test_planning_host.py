@@ -84,7 +84,7 @@ def test_reader_matches_per_entity_scene(rigid_solver):
     assert np.allclose(rec[:, :3], [b[0] for b in BOXES]) and np.allclose(rec[:, 6], [b[2] for b in BOXES], atol=1e-6)
     assert np.allclose(base, model.BASE_POS)
     other = scenes.GenesisReader(M.Scene(BOXES, rigid_solver=not rigid_solver), sc.robot)
-    assert other.poses()[0] == poses or np.allclose(other.poses()[0], poses)
+    assert np.array_equal(other.poses()[0], poses)
 
 
 def test_scene_pushed_only_when_changed():

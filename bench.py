@@ -359,6 +359,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--settle-ms", type=float, default=250.0,
+                    help="back-to-back untimed launches before the warmup steps (clock ramp)")
     # 2^24 states (604 MB of HBM) per GPU and step: at 4M the launch's last partial
     # round of waves and the launch gap cost ~5 % (34.2 vs 35.9 G states/s, same box,
     # profiles/r04/validity_batch_size.txt); the 4M rate is kept in per_config
@@ -411,6 +413,18 @@ def main():
     def step():
         ctx.check_states_device(q.data_ptr(), n, flags.data_ptr(), None)
 
+    # clock settle: a fresh process's first ~100 launches run while the GPU's clocks
+    # ramp (tools/clock_probe.py, profiles/r05/clock_ramp.json: 500-530 us per launch
+    # over launches 2-15, 415 us from launch ~100 on, flat for 9,500 launches), so
+    # back-to-back launches for --settle-ms of wall time come before the W warmup
+    # steps; the timed region is still exactly K steps. 0 disables it.
+    settle_n, ts = 0, time.perf_counter()
+    while (time.perf_counter() - ts) * 1e3 < args.settle_ms:
+        for _ in range(10):
+            step()
+        settle_n += 10
+        torch.cuda.synchronize(dev)
+    settle_ms = (time.perf_counter() - ts) * 1e3
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -646,6 +660,9 @@ def main():
     if rank == 0:
         out = {"metric": METRIC, "value": round(value, 1), "unit": "states/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 5),
+               "settle": {"ms": round(settle_ms, 1), "launches": settle_n,
+                          "why": "untimed back-to-back launches before the warmup steps: GPU clock ramp "
+                                 "(tools/clock_probe.py)"},
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
                "data": "synthetic: uniform 9-D Franka states in the float32 joint bounds (HBM resident); "
                        "goal3 10-box scene; plan queries from tests/golden/workloads",

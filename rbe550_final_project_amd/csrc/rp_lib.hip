@@ -1186,6 +1186,13 @@ bool nn_devgeom() {
     return !(e && *e && std::atoi(e) == 0);
 }
 
+// split-search ranges rounded down to the resident blocks (rp_nn.h nn_geom fit);
+// RBE_NN_GEOM_FIT=0 rounds up as before (A/B; read per search)
+bool nn_geom_fit() {
+    const char* e = std::getenv("RBE_NN_GEOM_FIT");
+    return !(e && *e && std::atoi(e) == 0);
+}
+
 template <int RB, int W>
 void launch_nn_mfma_w(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, const double* tree, const h8* img,
                       int64_t T) {
@@ -1194,7 +1201,8 @@ void launch_nn_mfma_w(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, 
     int64_t target = 1024;   // blocks
     if (const char* e = std::getenv("RBE_NN_BLOCKS"))   // (A/B)
         if (*e) target = std::max<int64_t>(1, std::atoll(e));
-    const NnGeom g = nn_geom(n, T, per_block, 0, target);
+    const bool fit = nn_geom_fit();
+    const NnGeom g = nn_geom(n, T, per_block, 0, target, fit);
     const int64_t qblocks = g.qblocks;
     int64_t chunk = g.chunk;
     if (const char* e = std::getenv("RBE_NN_RANGES"))   // (A/B: cap on the tree ranges)
@@ -1207,7 +1215,7 @@ void launch_nn_mfma_w(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, 
         if (*e) chunk = std::max<int64_t>(NNM_STAGE, std::min<int64_t>(chunk, std::atoll(e) / NNM_STAGE * NNM_STAGE));
     const int S = (int)((T + chunk - 1) / chunk);
     int64_t grid = qblocks * S;
-    const int devgeom = Q.status && nn_devgeom() ? 1 : 0;
+    const int devgeom = Q.status && nn_devgeom() ? (fit ? 1 : 3) : 0;
     if (devgeom) grid = std::max<int64_t>(grid, 1024);   // room for the actual count's ranges
     // partials: S x n for the host geometry; within grid x per_block for any device one
     c->nn_part.ensure((size_t)std::max<int64_t>((int64_t)S * n, devgeom ? grid * per_block : 0));
@@ -1224,7 +1232,7 @@ void launch_nn_mfma_w(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, 
         constexpr int64_t per1 = (int64_t)W * 16 * RBP;
         const int64_t qb1 = (n + per1 - 1) / per1;
         const int64_t sub = ((T + 15) / 16 + pst - 1) / pst;   // tiles of the subset
-        int64_t S1 = std::max<int64_t>(1, std::min<int64_t>({(1024 + qb1 - 1) / qb1, sub / 8, 16}));
+        int64_t S1 = std::max<int64_t>(1, std::min<int64_t>({fit ? 1024 / qb1 : (1024 + qb1 - 1) / qb1, sub / 8, 16}));
         const int64_t chunk1 = (sub + S1 - 1) / S1 * pst * 16;   // nodes: whole subset tiles per range
         S1 = (T + chunk1 - 1) / chunk1;
         c->nn_pilot.ensure((size_t)(S1 * n));
@@ -1233,6 +1241,9 @@ void launch_nn_mfma_w(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, 
                            pst, (const DI2*)nullptr, 0);
         init = c->nn_pilot.p;
         init_S = (int)S1;
+        if (std::getenv("RBE_NN_LOG"))   // (diagnostic: tools/nn_seq.py; pairs = n x T / pst)
+            fprintf(stderr, "nnlog n=%lld T=%lld grid=%lld S=%lld status=0 pilot=%d\n", (long long)n,
+                    (long long)((T + pst - 1) / pst), (long long)(qb1 * S1), (long long)S1, pst);
     }
     hipLaunchKernelGGL((k_nn_mfma<RB, W>), dim3((unsigned)grid), dim3(64 * W), 0, c->stream, qx, n, Q.status,
                        Q.t0, tree, img, T, chunk, qblocks, c->nnm, c->nn_part.p, devgeom, 1, init, init_S);

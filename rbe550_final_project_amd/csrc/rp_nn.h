@@ -153,7 +153,8 @@ __global__ void k_nn_image(const double* __restrict__ tree, int64_t t0, int64_t 
 // part[y * n + q] (exact distance, index; index -1: no node). Queries: qx (n x 9
 // f64); status (NNQ_ROWS): n = min(n, status[0] - t0), and with devgeom the
 // geometry (qblocks, chunk, ranges) is nn_geom's for that n within the grid (the
-// host's chunk / qblocks are ignored). RB row blocks of 16 queries per wave.
+// host's chunk / qblocks are ignored; devgeom bit 1: nn_geom's fit off). RB row
+// blocks of 16 queries per wave.
 // Grid: 1-D, qblocks x (tree ranges) blocks. Blocks are remapped so that each group
 // of blocks sharing an XCD (blockIdx % 8 labels them, cdna_hip_programming.md T1,
 // the bijective form) takes a contiguous run of (range, query block) pairs: the
@@ -183,13 +184,18 @@ struct NnGeom {
     int64_t qblocks, chunk;
     int S;
 };
+// fit: the ranges per query block are rounded DOWN, so qblocks x S stays within
+// `target` (the blocks resident at once: 1,024 = 256 CUs x 4 one-wave-per-SIMD blocks
+// at 4 waves per SIMD) whenever qblocks <= target. Rounded up (fit = false, round 5's
+// geometry) a 98,304-query search took 192 x 6 = 1,152 blocks: a second round of 128
+// blocks after the first 1,024.
 __host__ __device__ inline NnGeom nn_geom(int64_t n, int64_t T, int64_t per_block, int64_t maxblocks,
-                                          int64_t target = 1024) {
+                                          int64_t target = 1024, bool fit = true) {
     NnGeom g;
     g.qblocks = (n + per_block - 1) / per_block;
     const int64_t qb = g.qblocks > 0 ? g.qblocks : 1;
     const int64_t stages = (T + 63) / 64;
-    int64_t S0 = (target + qb - 1) / qb;
+    int64_t S0 = fit ? target / qb : (target + qb - 1) / qb;
     if (S0 > stages / 32) S0 = stages / 32;
     if (maxblocks > 0 && S0 > maxblocks / qb) S0 = maxblocks / qb;
     if (S0 < 1) S0 = 1;
@@ -237,7 +243,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
         n = min(n, (int64_t)status[0] - t0);
         if (n <= 0) return;
         if (devgeom) {
-            const NnGeom g = nn_geom(n, T, (int64_t)W * QW, nwg);
+            const NnGeom g = nn_geom(n, T, (int64_t)W * QW, nwg, 1024, (devgeom & 2) == 0);
             qblocks = g.qblocks;
             chunk = g.chunk;
             nwg = g.qblocks * g.S;
@@ -459,7 +465,7 @@ __global__ void k_nn_reduce_g(const DI2* __restrict__ part, int64_t n, int S, co
     const int64_t k = (int64_t)rp_bid() * rp_bdim() + rp_tid();
     if (status) {
         n = min(n, (int64_t)status[0] - t0);
-        if (devgeom && n > 0) S = nn_geom(n, T, per_block, maxblocks).S;
+        if (devgeom && n > 0) S = nn_geom(n, T, per_block, maxblocks, 1024, (devgeom & 2) == 0).S;
     }
     if (k >= n) return;
     double bd = __builtin_inf();

@@ -49,7 +49,7 @@ def main():
             extra = ""
             if logs:
                 n, T = int(logs[k]["n"]), int(logs[k]["T"])
-                extra = f"  n {n:7d} T {T:7d} S {logs[k]['S']:>3s}"
+                extra = f"  n {n:7d} T {T:7d} S {logs[k]['S']:>3s}" + (" pilot" if "pilot" in logs[k] else "      ")
                 if logs[k]["status"] == "0":
                     extra += f"  {n * T / (us * 1e-6) / 1e12:6.2f} e12 pairs/s"
             print(f"{k:4d} blocks {b:6d} {us:9.1f} us  then {nxt}{extra}")

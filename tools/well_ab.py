@@ -39,7 +39,7 @@ def main():
     ctx.set_attached(q["attached"])
     ctx.set_profiling(True)
     keys = ("RBE_NN_MFMA", "RBE_PLAN_CHUNK", "RBE_CHUNK_TREE", "RBE_NN_WAVES", "RBE_NN_RANGES", "RBE_EDGE_PACKED",
-            "RBE_NN_BLOCKS", "RBE_NN_DEVGEOM", "RBE_NN_PILOT",
+            "RBE_NN_BLOCKS", "RBE_NN_DEVGEOM", "RBE_NN_PILOT", "RBE_NN_GEOM_FIT",
             "RBE_EDGE_COARSE", "RBE_EDGE_COARSE_MIN", "RBE_ACCEPT_LB")
     for rep in range(2):   # rep 0: warm-up
         for name, env in cfgs.items():

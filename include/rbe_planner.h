@@ -227,8 +227,9 @@ const char* rp_version(void);
  * bumped whenever one of them changes size or meaning (the structs carry no size
  * field). A client checks rp_abi_version() == RP_ABI_VERSION once, before passing
  * any struct (native.py load() does); a mismatch means the header and the library
- * disagree and no call may be made. Version 5: rp_box_rot / rp_set_scene_rot. */
-#define RP_ABI_VERSION 5
+ * disagree and no call may be made. Version 5: rp_box_rot / rp_set_scene_rot;
+ * 6: rp_selftest_f64 writes six values per input. */
+#define RP_ABI_VERSION 6
 int rp_abi_version(void);
 
 /* Fill `out` with the built-in Franka Panda capsule model (spec/franka_capsules.json). */
@@ -404,8 +405,10 @@ int rp_get_stream(rp_ctx* ctx, void** stream_out);
 int rp_last_kernel_ms(rp_ctx* ctx, double* ms);
 
 /* Numerics self-test (used by the parity tests): device sqrt(|x|), 0.13037 / x,
- * ceil(7x) and (double)(float)x for each x[i] -> out[4*i .. 4*i+3]. The planner's
- * steering and segment counts rely on these being IEEE correctly rounded. */
+ * ceil(7x), (double)(float)x and the forward kinematics' joint sin / cos of
+ * (float)x for each x[i] -> out[6*i .. 6*i+5]. The planner's steering and segment
+ * counts rely on the first four being IEEE correctly rounded; the last two must
+ * equal the oracle's ro_sincos bit for bit. */
 int rp_selftest_f64(rp_ctx* ctx, const double* x, int64_t n, double* out);
 
 /* Nearest-node self-test (used by the parity tests): out[i] = the index of the tree

@@ -2,7 +2,7 @@
 import ctypes as C
 import math
 
-ABI_VERSION = 5   # RP_ABI_VERSION of include/rbe_planner.h these mirrors follow
+ABI_VERSION = 6   # RP_ABI_VERSION of include/rbe_planner.h these mirrors follow
 NQ = 9
 MAX_CAPSULES = 32
 MAX_SELF_PAIRS = 64

@@ -313,6 +313,12 @@ __device__ __forceinline__ bool edge_group_round(const double* __restrict__ from
 // hoists loop-invariant values and spills 29 VGPRs). LOOP = true (rp_check_edges_device:
 // the slot bound lives on the device, dkmax; capped grids): grid-stride over (group,
 // round) and rounds r, r + kmax, ...
+// (Most waves of a large launch are rounds past their group's items, and the chip
+// starts only ~4.4 one-wave workgroups per microsecond whatever they hold —
+// tools/dispatch_probe.hip: 175,104 of them take 40 us, the same waves in 4-wave
+// workgroups 12.5 us — but 4-wave workgroups, each wave its own queue, measured
+// slower in the plans: C5 well edge time 7.95 -> 8.7-8.85 ms for pass 1 alone, 9.2-9.4
+// for every launch; profiles/r05/edge_vw_ab_*.txt.)
 template <int NCL, bool BF = false, bool LOOP = false>
 __global__ __launch_bounds__(VBLOCK, LOOP ? RP_EDGE_WAVES_LOOP : (NCL == NCL_GRID ? (BF ? RP_EDGE_WAVES_GRID : RP_EDGE_WAVES) : RP_EDGE_WAVES_CL)) void k_edges(
     const double* __restrict__ from, const double* __restrict__ to, const int* __restrict__ nd, int64_t n_edges,
@@ -2558,10 +2564,14 @@ __global__ void k_selftest(const double* __restrict__ x, int64_t n, double* __re
     const int64_t i = (int64_t)rp_bid() * rp_bdim() + rp_tid();
     if (i >= n) return;
     const double v = x[i];
-    out[4 * i + 0] = sqrt(v < 0 ? -v : v);
-    out[4 * i + 1] = 0.13037 / (v == 0 ? 1.0 : v);
-    out[4 * i + 2] = ceil(v * 7.0);
-    out[4 * i + 3] = (double)(float)v;
+    out[6 * i + 0] = sqrt(v < 0 ? -v : v);
+    out[6 * i + 1] = 0.13037 / (v == 0 ? 1.0 : v);
+    out[6 * i + 2] = ceil(v * 7.0);
+    out[6 * i + 3] = (double)(float)v;
+    float sn, cs;   // the FK's joint sin / cos (rp_math.h rp_sincos) of (float)v
+    rp_sincos((float)v, &sn, &cs);
+    out[6 * i + 4] = sn;
+    out[6 * i + 5] = cs;
 }
 
 // Scene upload (rp_lib.hip flush_scene): one block copies the record from the pinned

@@ -3331,7 +3331,8 @@ int rp_debug_tstamps(unsigned long long* out) {
 #endif
 
 // Numerics self-test (test-only entry, not in the public header's contract list):
-// device sqrt / div / ceil / f64->f32 of x[i] -> out[4*i..4*i+3].
+// device sqrt / div / ceil / f64->f32 of x[i] and the FK's sin / cos of (float)x[i]
+// -> out[6*i..6*i+5].
 int rp_selftest_f64(rp_ctx* c, const double* x, int64_t n, double* out) {
     if (!c || n <= 0 || !x || !out) return RP_ERR_ARG;
     RP_IDLE(c);
@@ -3339,11 +3340,11 @@ int rp_selftest_f64(rp_ctx* c, const double* x, int64_t n, double* out) {
     HIP_TRY(hipSetDevice(c->device));
     DevBuf<double> dx, dy;
     dx.ensure(n);
-    dy.ensure(4 * n);
+    dy.ensure(6 * n);
     HIP_TRY(hipMemcpyAsync(dx.p, x, sizeof(double) * n, hipMemcpyHostToDevice, c->stream));
     hipLaunchKernelGGL(k_selftest, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, dx.p, n, dy.p);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(out, dy.p, sizeof(double) * 4 * n, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(out, dy.p, sizeof(double) * 6 * n, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     dx.release();
     dy.release();

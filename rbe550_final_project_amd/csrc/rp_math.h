@@ -90,7 +90,16 @@ __device__ __forceinline__ void rp_sincos(float x, float* sn, float* cs) {
     const float sr = fma_(r * z, ps, r);
     const float pc = fma_(fma_(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f);
     const float cr = fma_(z * z, pc, fma_(-0.5f, z, 1.0f));
-    const int qd = ((int)k) & 3;
+    // The quadrant is read from the bits of this same rounded k (k + 1.5 x 2^23 holds
+    // k's two's-complement low bits, |k| < 2^22), not converted: the compiler folds
+    // (int)floorf(y + 0.5f) into v_cvt_rpi_i32_f32(y), which rounds y + 0.5 exactly
+    // instead of to f32 — at x = 0.785398126 (the float just below pi/4) the f32 sum is
+    // 1.0 but the exact one is below 1, so the reduction used k = 1 with the quadrant of
+    // k = 0 and sin came out negated (-0.7071; the oracle: k = 1 throughout). Found by an
+    // edge-parity seed; it also changed flags of the bench's own uniform states. An empty
+    // asm barrier on k fixed it too but cost 14 % of k_validity; this form costs nothing
+    // (profiles/r05/sincos_fix_ab.txt; tests/test_gpu_parity.py::test_sincos_quadrant_bounds).
+    const int qd = __float_as_int(k + 12582912.0f) & 3;
     // quadrant by bits: odd quadrants swap sin and cos, quadrants 2 and 3 negate sin,
     // 1 and 2 negate cos (the oracle's case analysis, the same values; as selects and
     // sign-bit XORs instead of a branchy case analysis: -63 SALU, -35 VALU per wave,

@@ -220,7 +220,7 @@ class Context:
 
     def selftest_f64(self, x):
         x = np.ascontiguousarray(x, dtype=np.float64)
-        out = np.zeros((len(x), 4), dtype=np.float64)
+        out = np.zeros((len(x), 6), dtype=np.float64)
         self._check(load().rp_selftest_f64(self._h, _ptr(x), len(x), _ptr(out)), "rp_selftest_f64")
         return out
 

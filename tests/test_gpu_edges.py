@@ -80,3 +80,26 @@ def test_coarse_first_edge_passes(gpu_ctx, oracle_lib, scene, n, scale, pk, monk
     ref = o.check_edges(qa, qb, res)
     got = gpu_ctx.check_edges(qa, qb, res)
     assert np.array_equal(got, ref), f"{int((got != ref).sum())} of {n} edge flags differ"
+
+
+@pytest.mark.parametrize("scene", ["goal3", "clutter64"])
+@pytest.mark.parametrize("n,scale", [(2049, 1.0), (40000, 1.0), (20000, 3.0), (20000, 10.0)])
+@pytest.mark.parametrize("pk", ["0", "8", "3"])
+def test_edges_second_seed(gpu_ctx, oracle_lib, scene, n, scale, pk, monkeypatch):
+    """A second edge seed, one pass and coarse-first passes forced on: the oracle's
+    flags. Seed 7 at scale 10 on clutter64 holds the edge whose state (joint 0 at the
+    float just below pi/4) met the device's sin / cos quadrant bug
+    (test_gpu_parity.py::test_sincos_quadrant_bounds)."""
+    monkeypatch.setenv("RBE_EDGE_COARSE", pk)
+    monkeypatch.setenv("RBE_EDGE_COARSE_MIN", "0")
+    monkeypatch.setenv("RBE_ML_LANES", "1")
+    sc = _scene(scene)
+    o = oracle_lib.OracleScene()
+    o.set_scene(sc.boxes, sc.plane_z, sc.base)
+    o.set_attached(-1)
+    gpu_ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+    gpu_ctx.set_attached(-1)
+    qa, qb, res = _edges(n, 7 + n, scale)
+    ref = o.check_edges(qa, qb, res)
+    got = gpu_ctx.check_edges(qa, qb, res)
+    assert np.array_equal(got, ref), f"{int((got != ref).sum())} of {n} edge flags differ"

@@ -140,6 +140,47 @@ def test_f64_device_numerics(gpu_ctx):
     assert np.array_equal(out[:, 3], x.astype(np.float32).astype(np.float64))
 
 
+def _ulps_around(v, k):
+    f = np.float32(v)
+    out = [f]
+    lo = hi = f
+    for _ in range(k):
+        lo, hi = np.nextafter(lo, np.float32(-np.inf)), np.nextafter(hi, np.float32(np.inf))
+        out += [lo, hi]
+    return out
+
+
+def test_sincos_quadrant_bounds(gpu_ctx, oracle_lib):
+    """The forward kinematics' joint sin / cos (rp_math.h rp_sincos) equal the
+    oracle's ro_sincos bit for bit, on 64 floats either side of every quadrant
+    boundary (odd multiples of pi/4) in the joints' range and on 200,000 uniform
+    angles. The float just below pi/4 once gave a negated sin on the device (the
+    compiler rounded the quadrant's y + 0.5 differently from the reduction's): a
+    clutter64 edge flag differed from the oracle's (tests/test_gpu_edges.py seed 7)."""
+    xs = []
+    for m in range(-7, 8, 2):
+        xs += _ulps_around(m * np.pi / 4, 64)
+    rng = np.random.default_rng(3)
+    xs += list((rng.random(200000) * 6.0 - 3.0).astype(np.float32))
+    x = np.array(xs, dtype=np.float32)
+    out = gpu_ctx.selftest_f64(x.astype(np.float64))
+    ref = np.array([oracle_lib.sincos(v) for v in x], dtype=np.float32)
+    bad = np.nonzero((out[:, 4].astype(np.float32) != ref[:, 0]) | (out[:, 5].astype(np.float32) != ref[:, 1]))[0]
+    assert bad.size == 0, f"{bad.size} sin / cos differ, first at x = {float(x[bad[0]])!r}"
+
+
+def test_state_at_quadrant_bound(gpu_ctx, oracle_lib):
+    """The state of that edge (joint 0 at the float just below pi/4): flags and
+    contacts equal the oracle's."""
+    sc = scenes.Scene.from_json(json.load(open(os.path.join(GOLD, "workloads", "clutter64.json")))["queries"][0]["scene"])
+    o = _both(gpu_ctx, oracle_lib, sc)
+    q = np.array([0.7853981256484985, 0.7177550196647644, 0.42281287908554077, -2.4574007987976074,
+                  0.8535553216934204, 0.8303852081298828, -2.0884807109832764, 0.032658882439136505,
+                  0.03345468267798424], dtype=np.float32)
+    assert gpu_ctx.check_states(q[None])[0] == o.check_states(q[None])[0] == 1
+    assert sorted(gpu_ctx.contacts(q.astype(np.float64))) == sorted(o.contacts(q.astype(np.float64))) == []
+
+
 PLAN_CASES = [("goal1_scattered_6box", 7), ("single_pick_place_5box", 0), ("single_pick_place_5box", 1), ("goal3_tallest_10box", 2),
               ("goal3_tallest_10box", 5), ("goal4_pentagon_10box", 2), ("goal4_pentagon_10box", 14),
               ("clutter64", 0)]

@@ -68,6 +68,35 @@ def test_validity_flags_bit_exact(gpu_ctx, oracle_lib, name, grid, monkeypatch):
     assert 0.02 < g.mean() < 0.98
 
 
+def _quadrant_bound_states(n, seed):
+    """States whose joint angles sit within 64 floats of a quadrant bound of the
+    sin / cos reduction (odd multiples of pi/4) inside the limits, fingers uniform."""
+    rng = np.random.default_rng(seed)
+    q = _uniform(n, seed + 1)
+    for j in range(7):
+        bounds = [m * np.pi / 4 for m in range(-7, 8, 2) if model.Q_LO[j] < m * np.pi / 4 < model.Q_HI[j]]
+        b = np.array(bounds, dtype=np.float32)[rng.integers(0, len(bounds), n)]
+        steps = rng.integers(-64, 65, n)
+        v = b.view(np.int32).astype(np.int64) + steps * np.where(b < 0, -1, 1)   # (same-sign floats)
+        q[:, j] = v.astype(np.int32).view(np.float32)
+    return q
+
+
+@pytest.mark.parametrize("name", list(SCENES))
+def test_validity_flags_bit_exact_large(gpu_ctx, oracle_lib, name):
+    """The bench's kernel (one-wave k_validity: launches above 2^17 states) on 2^22
+    uniform states and 2^20 states with every joint within 64 floats of a sin / cos
+    quadrant bound, every flag against the oracle's (the round-5 quadrant bug changed
+    flags of a few uniform states per 2^24)."""
+    sc = SCENES[name]
+    o = _both(gpu_ctx, oracle_lib, sc)
+    q = np.concatenate([_uniform(1 << 22, 21), _quadrant_bound_states(1 << 20, 22)])
+    g = gpu_ctx.check_states(q)
+    c = o.check_states(q, threads=16)
+    mism = np.nonzero(g != c)[0]
+    assert mism.size == 0, f"{mism.size} mismatches, first {q[mism[:3]].tolist()}"
+
+
 def test_validity_with_attached_box(gpu_ctx, oracle_lib):
     wl = _wl("goal3_tallest_10box")
     for qd in [x for x in wl["queries"] if x["attached"] >= 0][:3]:

@@ -473,6 +473,12 @@ def main():
         group = None
         group_err = None
         if distributed:
+            # a rank group whose exchange never completes (RCCL at N > 1 runs only on
+            # the driver's node) must not hold the line: each plan wait gives up after
+            # 30 s instead of 120 (the longest legitimate wait here is milliseconds),
+            # and after a failed workload the rest are skipped (a stuck stream would
+            # fail them all, one watchdog period each)
+            os.environ.setdefault("RBE_WAIT_WATCHDOG_S", "30")
             from rbe550_final_project_amd.distributed import Group
             try:
                 group = Group(ctx, transport="shm" if args.backend == "gloo" else "rccl")
@@ -542,6 +548,7 @@ def main():
                                          "median_parts_ms": parts})
         except Exception as ex:  # report, keep the primary metric
             plan = {"error": repr(ex)[:300]}
+        plan_failed = plan is None or "error" in plan
         # configured-batch workloads: C4 (262,144-sample iterations) and C5
         # (131,072-sample iterations: clutter64, and the covered well, whose trees
         # grow to 10^5 - 3 x 10^5 nodes over up to 8 iterations = the 2^20 budget);
@@ -549,7 +556,8 @@ def main():
         # configured batch) on the same queries
         well = load_workload("clutter64_well")
         wellx = {"queries": well["queries"] * 4}
-        for key, wl_c, batch, bmin, seeds_from, max_iters in ([] if (distributed and group is None) else (
+        for key, wl_c, batch, bmin, seeds_from, max_iters in ([] if (distributed and (group is None or plan_failed))
+                                                               else (
                 ("C4_pentagon", load_workload("goal4_pentagon_10box"), C4_BATCH, C4_BATCH, 0, 0),
                 ("C4_pentagon_sched", load_workload("goal4_pentagon_10box"), C4_BATCH, 0, 0, 0),
                 ("C5_clutter64", load_workload("clutter64"), C5_BATCH, C5_BATCH, 0, 0),
@@ -568,6 +576,8 @@ def main():
                 plan[key] = plan_record(tq, sq, stq, batch, dev, distributed, extra)
             except Exception as ex:
                 plan[key] = {"error": repr(ex)[:300]}
+                if distributed:
+                    break
         # multi-GPU through the reference's own API in ONE process (the drop-in with
         # planning.configure(devices=...)): every visible GPU, or two contexts on the
         # one GPU of a single-GPU box (a rehearsal of the group: both share the chip)

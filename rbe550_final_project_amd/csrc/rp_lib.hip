@@ -1342,16 +1342,23 @@ bool nn_split(rp_ctx* c, const NnQuery& Q, int64_t n, Tree& tr, int64_t T, int32
 // Wait for a kernel to publish `seq` into the host mirror (rp_kernels.h PlanIO).
 // Spins on the host-coherent word for the first wait_spin_s (the waits of a pick /
 // place query are 10-30 us: a wake-up there would cost more than the wait), then
-// sleeps between polls — quanta of 10 % of the time already waited, 10-200 us — so a
+// sleeps between polls — quanta of 10 % of the time already waited, 10-20 us — so a
 // long query (C5-class trees, a 10 s budget: motion_primitives.py:144) does not hold
 // a host core. Polls the stream every 4096 spins / 10 ms of sleeping, so that a failed
 // or finished-without-publishing stream turns into an error instead of a hang, and a
 // stream busy past the watchdog is reported.
+// The sleep quantum is capped at max_ns (RBE_WAIT_SLEEP_MAX_US, default 20 us): the
+// host reacts to a finished sub-batch within about one quantum, and the GPU idles
+// until it does (C5 covered-well plans, round 5: with 200-us quanta the gaps before a
+// sub-batch's first launch were 10-120 us, ~0.3 ms per plan; tools/well_ab.py).
 struct WaitTuning {
     double spin_s = 40e-6, frac = 0.1;
+    int64_t max_ns = 20000;
     WaitTuning() {
         if (const char* e = std::getenv("RBE_WAIT_SPIN_US"); e && *e) spin_s = std::max(0.0, std::atof(e)) * 1e-6;
         if (const char* e = std::getenv("RBE_WAIT_SLEEP_FRAC"); e && *e) frac = std::max(0.0, std::atof(e));
+        if (const char* e = std::getenv("RBE_WAIT_SLEEP_MAX_US"); e && *e)
+            max_ns = std::max<int64_t>(10000, (int64_t)(std::atof(e) * 1e3));
     }
 };
 const WaitTuning& wait_tuning() {
@@ -1424,7 +1431,7 @@ void wait_seq(rp_ctx* c, int seq) {
             last_check = now;
         }
         slack.fine();
-        const int64_t ns = std::min<int64_t>(200000, std::max<int64_t>(10000, (int64_t)((now - t_enter) * wt.frac * 1e9)));
+        const int64_t ns = std::min<int64_t>(wt.max_ns, std::max<int64_t>(10000, (int64_t)((now - t_enter) * wt.frac * 1e9)));
         const timespec ts{0, (long)ns};
         nanosleep(&ts, nullptr);
         c->waits[4] += 1;
@@ -1457,7 +1464,7 @@ void stream_wait(rp_ctx* c) {
         if (e != hipErrorNotReady) HIP_TRY(e);
         slack.fine();
         const double waited = now_s() - t_enter;
-        const int64_t ns = std::min<int64_t>(200000, std::max<int64_t>(10000, (int64_t)(waited * wt.frac * 1e9)));
+        const int64_t ns = std::min<int64_t>(wt.max_ns, std::max<int64_t>(10000, (int64_t)(waited * wt.frac * 1e9)));
         const timespec ts{0, (long)ns};
         nanosleep(&ts, nullptr);
         c->waits[4] += 1;

@@ -149,6 +149,7 @@ struct rp_ctx {
     // host waits since the context was made (rp_debug_waits): wait_seq calls,
     // stream_wait calls, seconds spinning, seconds in the sleep loop, sleeps
     double waits[5] = {0, 0, 0, 0, 0};
+    double last_wait_s = 0.0;            // wait_seq: the previous wait's length (its spin-near-the-end guess)
     DevScene scene{};
     DevScene* d_scene = nullptr;
     // scene uploads (upload_scene / flush_scene): rp_set_scene / rp_set_attached only
@@ -1351,10 +1352,15 @@ bool nn_split(rp_ctx* c, const NnQuery& Q, int64_t n, Tree& tr, int64_t T, int32
 // host reacts to a finished sub-batch within about one quantum, and the GPU idles
 // until it does (C5 covered-well plans, round 5: with 200-us quanta the gaps before a
 // sub-batch's first launch were 10-120 us, ~0.3 ms per plan; tools/well_ab.py).
+// predict_s (RBE_WAIT_PREDICT_US, 0 = off): wait_seq spins again from 85 % of the
+// previous wait's length (minus 20 us) for at most this long, where the sub-batch
+// that is awaited usually ends (consecutive sub-batches of a plan are alike), so the
+// host reacts without a sleep's wake-up.
 struct WaitTuning {
-    double spin_s = 40e-6, frac = 0.1;
+    double spin_s = 40e-6, frac = 0.1, predict_s = 150e-6;
     int64_t max_ns = 20000;
     WaitTuning() {
+        if (const char* e = std::getenv("RBE_WAIT_PREDICT_US"); e && *e) predict_s = std::max(0.0, std::atof(e)) * 1e-6;
         if (const char* e = std::getenv("RBE_WAIT_SPIN_US"); e && *e) spin_s = std::max(0.0, std::atof(e)) * 1e-6;
         if (const char* e = std::getenv("RBE_WAIT_SLEEP_FRAC"); e && *e) frac = std::max(0.0, std::atof(e));
         if (const char* e = std::getenv("RBE_WAIT_SLEEP_MAX_US"); e && *e)
@@ -1404,10 +1410,13 @@ void wait_seq(rp_ctx* c, int seq) {
     double t0 = -1.0;
     const double t_enter = now_s();
     c->waits[0] += 1;
+    const double spin_from = wt.predict_s > 0 ? 0.85 * c->last_wait_s - 20e-6 : 1e30;
     for (uint64_t spin = 1;; ++spin) {   // spin
         if (*f == seq) {
             __atomic_thread_fence(__ATOMIC_ACQUIRE);
-            c->waits[2] += now_s() - t_enter;
+            const double now = now_s();
+            c->waits[2] += now - t_enter;
+            c->last_wait_s = now - t_enter;
             return;
         }
         if ((spin & 4095) == 0 && wait_check(c, f, seq, t0)) break;
@@ -1430,13 +1439,22 @@ void wait_seq(rp_ctx* c, int seq) {
             if (wait_check(c, f, seq, t0)) break;
             last_check = now;
         }
+        const double el = now - t_enter;
+        if (el >= spin_from && el < spin_from + wt.predict_s) {   // near the predicted end: spin
+#if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
+            for (int k = 0; k < 32; ++k) __builtin_ia32_pause();
+#endif
+            continue;
+        }
         slack.fine();
-        const int64_t ns = std::min<int64_t>(wt.max_ns, std::max<int64_t>(10000, (int64_t)((now - t_enter) * wt.frac * 1e9)));
+        const int64_t ns = std::min<int64_t>(wt.max_ns, std::max<int64_t>(10000, (int64_t)(el * wt.frac * 1e9)));
         const timespec ts{0, (long)ns};
         nanosleep(&ts, nullptr);
         c->waits[4] += 1;
     }
-    c->waits[3] += now_s() - t_sleep;
+    const double t_end = now_s();
+    c->waits[3] += t_end - t_sleep;
+    c->last_wait_s = t_end - t_enter;
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
 }
 

@@ -1352,12 +1352,14 @@ bool nn_split(rp_ctx* c, const NnQuery& Q, int64_t n, Tree& tr, int64_t T, int32
 // host reacts to a finished sub-batch within about one quantum, and the GPU idles
 // until it does (C5 covered-well plans, round 5: with 200-us quanta the gaps before a
 // sub-batch's first launch were 10-120 us, ~0.3 ms per plan; tools/well_ab.py).
-// predict_s (RBE_WAIT_PREDICT_US, 0 = off): wait_seq spins again from 85 % of the
-// previous wait's length (minus 20 us) for at most this long, where the sub-batch
-// that is awaited usually ends (consecutive sub-batches of a plan are alike), so the
-// host reacts without a sleep's wake-up.
+// predict_s (RBE_WAIT_PREDICT_US, default 0 = off): wait_seq spins again from 85 % of
+// the previous wait's length (minus 20 us) for at most this long, where the awaited
+// sub-batch usually ends (consecutive sub-batches of a plan are alike), so the host
+// reacts without a sleep's wake-up. Measured: C5 well sums -0.5 % (150 us) / -1 %
+// (300 us) for +0.25 / +0.33 s of host CPU per 2 s of a long query; off by default
+// (profiles/r05/wait_predict_ab.txt).
 struct WaitTuning {
-    double spin_s = 40e-6, frac = 0.1, predict_s = 150e-6;
+    double spin_s = 40e-6, frac = 0.1, predict_s = 0.0;
     int64_t max_ns = 20000;
     WaitTuning() {
         if (const char* e = std::getenv("RBE_WAIT_PREDICT_US"); e && *e) predict_s = std::max(0.0, std::atof(e)) * 1e-6;

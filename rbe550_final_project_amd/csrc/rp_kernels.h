@@ -35,12 +35,23 @@ constexpr int VBLOCK = 64;      // validity / edge block size: one wave (its LDS
 #ifndef RP_EDGE_WAVES_CL
 #define RP_EDGE_WAVES_CL 5
 #endif
-#ifndef RP_EDGE_WAVES_GRID   // the loop-free k_edges of grid scenes, base-fixed robot: 96 VGPRs,
-#define RP_EDGE_WAVES_GRID 5 // 6 spilled; C5 well edges 9.8 -> 9.45 ms (profiles/r04/edge_grid_waves_ab.txt)
+#ifndef RP_EDGE_WAVES_GRID   // the loop-free k_edges of grid scenes, base-fixed robot: 4 (round 4
+#define RP_EDGE_WAVES_GRID 4 // measured 5 with 6 spilled VGPRs 3.5 % faster; round 6: no spills, §5.5)
 #endif
 #ifndef RP_EDGE_WAVES_LOOP
 #define RP_EDGE_WAVES_LOOP 4
 #endif
+// Round 6: no instantiation may use scratch (tests/test_isa_guard.py). At 96 VGPRs (5
+// waves) these spilled 4-16 dwords, so they ask for 4 (128 VGPRs): the cluster-scene
+// kernels with 5-8 clusters (k_validity<8, true>, k_edges<4 | 8, true, false>), every
+// base-moved (BF = false) instantiation, and the base-moved grid kernel with a loop (3).
+constexpr int validity_waves(int ncl, bool bf) {
+    return ncl == NCL_GRID ? RP_VALIDITY_WAVES_GRID : (bf && ncl <= 4) ? RP_VALIDITY_WAVES : 4;
+}
+constexpr int edge_waves(int ncl, bool bf, bool loop) {
+    return loop ? ((ncl == NCL_GRID && !bf) ? 3 : RP_EDGE_WAVES_LOOP)
+                : ncl == NCL_GRID ? (bf ? RP_EDGE_WAVES_GRID : RP_EDGE_WAVES) : (bf && ncl <= 2) ? RP_EDGE_WAVES_CL : 4;
+}
 constexpr int NNBLOCK = 256;    // NN block size
 constexpr int NNTILE = 256;     // tree nodes per LDS tile (256 x 72 B = 18 KiB)
 
@@ -57,7 +68,7 @@ constexpr int NNTILE = 256;     // tree nodes per LDS tile (256 x 72 B = 18 KiB)
 constexpr int VWPB = RP_VWPB;            // waves per k_validity workgroup (one queue each)
 constexpr int VTHREADS = 64 * VWPB;
 template <int NCL, bool BF = false>
-__global__ __launch_bounds__(VTHREADS, NCL == NCL_GRID ? RP_VALIDITY_WAVES_GRID : RP_VALIDITY_WAVES) void k_validity(const float* __restrict__ q, int64_t n,
+__global__ __launch_bounds__(VTHREADS, validity_waves(NCL, BF)) void k_validity(const float* __restrict__ q, int64_t n,
                                                                        uint8_t* __restrict__ flags,
                                                                        const DevScene* __restrict__ sc) {
     __shared__ WaveQ wqs[VWPB];
@@ -320,13 +331,15 @@ __device__ __forceinline__ bool edge_group_round(const double* __restrict__ from
 // slower in the plans: C5 well edge time 7.95 -> 8.7-8.85 ms for pass 1 alone, 9.2-9.4
 // for every launch; profiles/r05/edge_vw_ab_*.txt.)
 template <int NCL, bool BF = false, bool LOOP = false>
-__global__ __launch_bounds__(VBLOCK, LOOP ? RP_EDGE_WAVES_LOOP : (NCL == NCL_GRID ? (BF ? RP_EDGE_WAVES_GRID : RP_EDGE_WAVES) : RP_EDGE_WAVES_CL)) void k_edges(
+__global__ __launch_bounds__(VBLOCK, edge_waves(NCL, BF, LOOP)) void k_edges(
     const double* __restrict__ from, const double* __restrict__ to, const int* __restrict__ nd, int64_t n_edges,
     int kmax, int mode, uint8_t* valid, int group, int* gfail, unsigned long long* counter,
     const DevScene* __restrict__ sc, const int* __restrict__ dcount, int per_item, const int* __restrict__ dkmax,
-    int r_first, int pk = 1, int pass = 0, const int* __restrict__ cntv = nullptr) {
+    int r_first, int pk = 1, int pass = 0, const int* __restrict__ cntv = nullptr, int* zero_word = nullptr) {
     __shared__ WaveQ wq;
     __shared__ int mark[VBLOCK];
+    // (coarse pass 0: the unit counter of the k_edge_units list that follows)
+    if (zero_word && rp_bid() == 0 && rp_tid() == 0) *zero_word = 0;
     // device-side edge count (planner iterations: dcount = accepted targets) and
     // slot count (rp_check_edges_device: k_edge_prep's max)
     if (dcount) n_edges = min(n_edges, (int64_t)dcount[0] * per_item);
@@ -375,6 +388,76 @@ __global__ void k_edge_rest(const int* __restrict__ nd, int64_t n_edges, const i
         if (live) rest = cnt - edge_coarse_count(cnt, pk);
     }
     cntv[e] = rest;
+}
+
+// Pass 1 as a work list (round 6). A groups x kr grid for pass 1 is mostly rounds past
+// their group's items (63 % of the C5 covered-well plans' edges fail, most of them in
+// pass 0), and the chip starts only ~4.4 one-wave workgroups per ns whatever they hold:
+// the 175,104-block connect pass took >= 38 us with little to check. k_edge_units makes
+// k_edge_rest's per-edge counts and, per group of 64 edges, its live rounds as (group,
+// round) units of a list (one atomic per block of 16 groups); k_edges_units then runs
+// a grid of at most the resident waves over the list. The units are the grid's live
+// (group, round) waves in another order, so the same items are checked.
+constexpr int EU_BLOCK = 1024;    // k_edge_units block: 16 groups
+constexpr int EU_RSHIFT = 8;      // unit = group << 8 | round (pass-1 rounds per group < 256)
+__global__ __launch_bounds__(EU_BLOCK) void k_edge_units(const int* __restrict__ nd, int64_t n_edges,
+                                                         const int* __restrict__ dcount, int per_item, int mode,
+                                                         const uint8_t* __restrict__ valid, int group,
+                                                         const int* __restrict__ gfail, int pk, int* __restrict__ cntv,
+                                                         uint32_t* __restrict__ units, int* __restrict__ n_units) {
+    __shared__ int s_r[EU_BLOCK / 64];
+    const int64_t e = (int64_t)rp_bid() * EU_BLOCK + rp_tid();
+    const int w = rp_tid() >> 6, lane = rp_tid() & 63;
+    const int64_t n = dcount ? min(n_edges, (int64_t)dcount[0] * per_item) : n_edges;
+    int rest = 0;
+    if (e < n) {
+        int d = nd[e];
+        if (mode == 2 && d >= 0) d &= ~ND_FROM;
+        const int cnt = d >= 0 ? (d > 1 ? d : 1) : 0;
+        bool live = cnt > 0 && valid[e] != 0;
+        if (live && gfail) {
+            const int64_t gi = e / group, si = e - gi * group;
+            live = gfail[gi] > si;
+        }
+        if (live) rest = cnt - edge_coarse_count(cnt, pk);
+    }
+    if (e < n_edges) cntv[e] = rest;
+    const int tot = __builtin_amdgcn_readlane(wave_incl_add(rest), 63);
+    const int R = (tot + VBLOCK - 1) / VBLOCK;   // this group's pass-1 rounds
+    if (lane == 0) s_r[w] = R;
+    __syncthreads();
+    if (w == 0) {
+        const int v = lane < EU_BLOCK / 64 ? s_r[lane] : 0;
+        const int incl = wave_incl_add(v);
+        const int all = __builtin_amdgcn_readlane(incl, 63);
+        int base = 0;
+        if (lane == 0 && all > 0) base = atomicAdd(n_units, all);
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (lane < EU_BLOCK / 64) s_r[lane] = base + incl - v;   // this wave's first unit
+    }
+    __syncthreads();
+    const uint32_t g = (uint32_t)(e >> 6);
+    for (int r = lane; r < R; r += 64) units[s_r[w] + r] = (g << EU_RSHIFT) | (uint32_t)r;
+}
+
+// pass 1 over k_edge_units' list: a grid of at most the resident waves strides over
+// the units (n_units on the device; written 0 by pass 0's block 0)
+template <int NCL, bool BF>
+__global__ __launch_bounds__(VBLOCK, edge_waves(NCL, BF, true)) void k_edges_units(
+    const double* __restrict__ from, const double* __restrict__ to, const int* __restrict__ nd, int64_t n_edges,
+    int mode, uint8_t* valid, int group, int* gfail, unsigned long long* counter, const DevScene* __restrict__ sc,
+    const int* __restrict__ dcount, int per_item, int pk, const int* __restrict__ cntv,
+    const uint32_t* __restrict__ units, const int* __restrict__ n_units) {
+    __shared__ WaveQ wq;
+    __shared__ int mark[VBLOCK];
+    if (dcount) n_edges = min(n_edges, (int64_t)dcount[0] * per_item);
+    const int nu = *n_units;
+    for (int u = rp_bid(); u < nu; u += rp_gdim()) {
+        const uint32_t unit = units[u];
+        edge_group_round<NCL, BF>(from, to, nd, n_edges, mode, valid, group, gfail, counter, sc,
+                                  (int64_t)(unit >> EU_RSHIFT), (int)(unit & ((1u << EU_RSHIFT) - 1)) * VBLOCK,
+                                  wq, mark, pk, 1, cntv);
+    }
 }
 
 // ---- work-compacted edge launch (large batches): the (edge, slot) items of
@@ -1736,27 +1819,36 @@ struct PathArgs {
 constexpr int PATH_LDS = 512;
 // ov / a_start: the caller's LDS view of this iteration's new nodes (tree A = the
 // start tree when a_start), also the path's LDS copy (ov->P) next to `also`.
-__device__ int build_path(const PathArgs& pa, int32_t s_node, int32_t g_node, PlanIO* io, double* also = nullptr,
+__device__ __forceinline__ int build_path(const PathArgs& pa, int32_t s_node, int32_t g_node, PlanIO* io, double* also = nullptr,
                           int also_max = -1, const TailLds* ov = nullptr, int a_start = 1) {
     __shared__ int32_t sidx[PATH_LDS], gidx[PATH_LDS];
     __shared__ int bns, bng;
     const int tid = rp_tid();
     const int gl = rp_bdim() >= 128 ? 64 : 0;   // the goal walk's lane
+    // the new nodes' parents of each branch's tree in the caller's LDS view (values
+    // picked by branch, so no field address of `ov` depends on a_start)
+    const int32_t* lS = nullptr;
+    const int32_t* lG = nullptr;
+    int64_t l0S = 0, l0G = 0;
+    int lnS = 0, lnG = 0;
+    if (ov) {
+        if (a_start) {
+            lS = ov->apar; l0S = ov->a0; lnS = ov->na;
+            lG = ov->bpar; l0G = ov->b0; lnG = ov->nb;
+        } else {
+            lS = ov->bpar; l0S = ov->b0; lnS = ov->nb;
+            lG = ov->apar; l0G = ov->a0; lnG = ov->na;
+        }
+    }
     if (tid == 0) {
-        const int32_t* l = ov ? (a_start ? ov->apar : ov->bpar) : nullptr;
-        const int64_t l0 = ov ? (a_start ? ov->a0 : ov->b0) : 0;
-        const int ln = ov ? (a_start ? ov->na : ov->nb) : 0;
         int ns = 0;
-        for (int32_t v = s_node; v >= 0; v = parent_of(pa.Spar, l, l0, ln, v), ++ns)
+        for (int32_t v = s_node; v >= 0; v = parent_of(pa.Spar, lS, l0S, lnS, v), ++ns)
             if (ns < PATH_LDS) sidx[ns] = v;
         bns = ns;
     }
     if (tid == gl) {
-        const int32_t* l = ov ? (a_start ? ov->bpar : ov->apar) : nullptr;
-        const int64_t l0 = ov ? (a_start ? ov->b0 : ov->a0) : 0;
-        const int ln = ov ? (a_start ? ov->nb : ov->na) : 0;
         int ng = 0;
-        for (int32_t v = g_node; v >= 0; v = parent_of(pa.Gpar, l, l0, ln, v), ++ng)
+        for (int32_t v = g_node; v >= 0; v = parent_of(pa.Gpar, lG, l0G, lnG, v), ++ng)
             if (ng < PATH_LDS) gidx[ng] = v;
         bng = ng;
     }
@@ -1780,13 +1872,19 @@ __device__ int build_path(const PathArgs& pa, int32_t s_node, int32_t g_node, Pl
             if (p2) p2[k] = v;
             if (p3) p3[k] = v;
         }
-    } else if (tid == 0) {   // long paths: walk again
+    } else if (tid == 0) {   // long paths: walk again (the new nodes' parents and states
+        // from the caller's LDS view, as above: this kernel's own stores of them need not
+        // be visible yet)
         int i = ns - 1;
-        for (int32_t v = s_node; v >= 0; v = pa.Spar[v], --i)
-            for (int d = 0; d < NQ; ++d) pa.out[i * NQ + d] = pa.S[(int64_t)v * NQ + d];
+        for (int32_t v = s_node; v >= 0; v = parent_of(pa.Spar, lS, l0S, lnS, v), --i) {
+            const double* st = ov ? ov->state(a_start, v, pa.S) : pa.S + (int64_t)v * NQ;
+            for (int d = 0; d < NQ; ++d) pa.out[i * NQ + d] = st[d];
+        }
         i = ns;
-        for (int32_t v = g_node; v >= 0; v = pa.Gpar[v], ++i)
-            for (int d = 0; d < NQ; ++d) pa.out[i * NQ + d] = pa.G[(int64_t)v * NQ + d];
+        for (int32_t v = g_node; v >= 0; v = parent_of(pa.Gpar, lG, l0G, lnG, v), ++i) {
+            const double* st = ov ? ov->state(!a_start, v, pa.G) : pa.G + (int64_t)v * NQ;
+            for (int d = 0; d < NQ; ++d) pa.out[i * NQ + d] = st[d];
+        }
         if (p2)
             for (int k = 0; k < n * NQ; ++k) p2[k] = pa.out[k];
         if (p3)
@@ -1959,11 +2057,14 @@ __global__ __launch_bounds__(NT) void k_iter_accept_small(
         cpart[rp_tid() - 128] = v;
     }
     RP_TSTAMP(0, 0);
-    // every per-sample input fetched at once (one round trip)
+    // every per-sample input fetched at once (one round trip); the new nodes' states
+    // too when they fit the registers (256 threads; at 1,024 threads, 128 VGPRs, the
+    // 4 x 9 doubles spilled: 216 B of scratch), else read where they are appended
+    constexpr bool PREX = NT <= 256;
     const int64_t k0 = (int64_t)rp_tid() * ITEMS;
     int L[ITEMS], M[ITEMS];
     int32_t NR[ITEMS], Y[ITEMS];
-    double X[ITEMS][NQ];
+    double X[PREX ? ITEMS : 1][NQ];
     int na = 0, nl = 0;
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
@@ -1974,9 +2075,11 @@ __global__ __launch_bounds__(NT) void k_iter_accept_small(
         M[r] = m[kc];
         NR[r] = near[kc];
         Y[r] = y[kc];
-        const double* xs = ext_node + kc * G * NQ;
+        if constexpr (PREX) {
+            const double* xs = ext_node + kc * G * NQ;
 #pragma unroll
-        for (int d = 0; d < NQ; ++d) X[r][d] = xs[d];
+            for (int d = 0; d < NQ; ++d) X[r][d] = xs[d];
+        }
         const int mk = in ? (M[r] & CHAIN_LEN) : 0;
         L[r] = g > 0 ? (g - 1 < mk ? g - 1 : mk) : -1;   // -1: extension rejected
         na += L[r] >= 0;
@@ -1998,7 +2101,9 @@ __global__ __launch_bounds__(NT) void k_iter_accept_small(
         if (L[r] < 0) continue;
         const int64_t k = k0 + r, e0 = k * G;
         const int64_t pos = TA + t;
-        for (int d = 0; d < NQ; ++d) A[pos * NQ + d] = X[r][d];
+        if constexpr (PREX) {   // (else copied by the whole block after the tail, below)
+            for (int d = 0; d < NQ; ++d) A[pos * NQ + d] = X[r][d];
+        }
         Apar[pos] = NR[r];
         l_apar[t] = NR[r];
         l_asrc[t] = (int32_t)e0;
@@ -2052,6 +2157,12 @@ __global__ __launch_bounds__(NT) void k_iter_accept_small(
     for (int k = rp_tid(); k < nbw * NQ; k += NT) {
         const int j = k / NQ, d = k - j * NQ;
         Bt[(TB + j) * NQ + d] = chain_node[(int64_t)l_bsrc[j] * NQ + d];
+    }
+    if constexpr (!PREX) {   // the extension nodes' states likewise (the tail read them from their records)
+        for (int k = rp_tid(); k < nA * NQ; k += NT) {
+            const int j = k / NQ, d = k - j * NQ;
+            A[(TA + j) * NQ + d] = ext_node[(int64_t)l_asrc[j] * NQ + d];
+        }
     }
     RP_TSTAMP(0, 10);   // (kernel exit of lane 0)
 }
@@ -2147,14 +2258,25 @@ __global__ __launch_bounds__(FUSE_THREADS) void k_group_accept_small(
     const int exB = block_scan_excl(nl, lds, &totalB);
     if (rp_tid() == 0) firstpk = ~0ull;
     __syncthreads();
+    // the extension nodes of this thread's samples first, then their chains (one
+    // sample's Philox sample + steer and its chain's steers live at once spilled 52 B at
+    // 128 VGPRs); conn_append_one reads the extension node this thread just wrote
     int t = exA;
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+        if (L[r] < 0) continue;
+        const int64_t i = k0 + r;
+        ext_append_one(i, gr.rec(i)[0], TA + t, seed, g0, bd, range, A, Apar, Acand);
+        ++t;
+    }
+    t = exA;
     int64_t off = TB + exB;
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
         if (L[r] < 0) continue;
         const int64_t i = k0 + r;
-        const bool reached = group_append_one(i, gr.rec(i), t, off, seed, g0, bd, range, cmax, A, Apar, Acand, TA,
-                                              Bt, Bpar, Bcand, a_start, chain_end);
+        const bool reached = conn_append_one(t, gr.rec(i)[1], L[r], off, A, TA, Bt, Bpar, Bcand, range, cmax, a_start,
+                                             Acand, chain_end);
         off += L[r];
         if (reached) atomicMin(&firstpk, ((unsigned long long)t << 32) | (unsigned)(off - TB));
         ++t;

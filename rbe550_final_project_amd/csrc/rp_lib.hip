@@ -241,6 +241,8 @@ struct rp_ctx {
     DevBuf<DI2> nn_pilot;                // per-query pilot bests (rp_nn.h)
     DevBuf<unsigned long long> estats;   // RBE_EDGE_STATS counters (k_edge_stats)
     DevBuf<int> ecnt;                    // coarse-first edge passes: pass-1 slots per edge
+    DevBuf<uint32_t> eunits;             // ... pass 1's (group, round) work list (k_edge_units)
+    DevBuf<int> enunits;                 // ... its length
     DevBuf<unsigned long long> lbst;     // look-back accept kernels: per-block words (rp_kernels.h)
     DevBuf<int> lberr;                   // their poll-budget error flag
     unsigned lb_epoch = 0;               // their per-launch epoch
@@ -294,7 +296,7 @@ struct rp_ctx {
         scalar.release(); counter.release(); efrom.release(); eto.release(); nd.release(); valid.release();
         near_.release(); res.release(); acc.release(); incl.release(); yv.release(); mv.release();
         rec.release(); Lv.release(); chain_end.release(); gfail.release();
-        eslot.release(); eincl.release(); echunk.release();
+        eslot.release(); eincl.release(); echunk.release(); ecnt.release(); eunits.release(); enunits.release();
         cub_tmp.release(); path.release(); io.release(); simp.release(); partial.release();
         g_send.release(); g_recv.release(); g_cnt.release(); g_incl.release(); nn_part.release(); nn_qx.release();
         leave_group();
@@ -542,6 +544,13 @@ int64_t edge_coarse_min() {
     const char* e = std::getenv("RBE_EDGE_COARSE_MIN");
     return e && *e ? std::atoll(e) : (int64_t)1 << 18;
 }
+// pass 1 of the coarse-first passes over a work list (rp_kernels.h k_edge_units);
+// RBE_EDGE_UNITS=0: the groups x kr grid (A/B, tests). Read per launch.
+bool edge_units_on() {
+    const char* e = std::getenv("RBE_EDGE_UNITS");
+    return !(e && *e && std::atoi(e) == 0);
+}
+constexpr int64_t EDGE_UNITS_GRID = 4096;   // k_edges_units blocks: the resident one-wave blocks
 
 // sr: the straight edge riding along (rp_plan's first front; lane-group kernels only)
 void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd, int64_t n, int kmax,
@@ -605,19 +614,39 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
                         threads >= edge_coarse_min();
     const int kc = coarse ? edge_coarse_count(kmax, pk) : kmax;   // pass-0 rounds per group
     const int kr = coarse ? std::max(1, kmax - kc) : 0;            // pass-1 rounds per group
+    // pass 1 over a work list of its live (group, round) units (k_edge_units /
+    // k_edges_units, RBE_EDGE_UNITS=0: the groups x kr grid), on a grid of at most the
+    // waves resident at once (256 CUs x 16 at 4 waves per SIMD)
+    const bool units = coarse && edge_units_on() && kr < (1 << EU_RSHIFT);
+    const unsigned nb_units = (unsigned)std::min<int64_t>(groups * kr, EDGE_UNITS_GRID);
     if (coarse) c->ecnt.ensure((size_t)n);
+    if (units) {
+        c->eunits.ensure((size_t)(groups * kr));
+        c->enunits.ensure(1);
+    }
     const dim3 b(VBLOCK);
     const int ps = prof_begin(c, s);
     // (the reference's robot base folded in as a constant, as for k_validity)
     const bool bf = base_fixed(c->scene);
-#define RP_EDGES_P(N, L, G, KM, DK, RF, PK, PS, CV)                                                               \
+#define RP_EDGES_Z(N, L, G, KM, DK, RF, PK, PS, CV, ZW)                                                           \
     do {                                                                                                           \
         if (bf) hipLaunchKernelGGL((k_edges<N, true, L>), dim3(G), b, 0, s, from, to, nd, n, KM, mode, valid,      \
-                                   group, gfail, c->counter.p, c->d_scene, dcount, per_item, DK, RF, PK, PS, CV);  \
+                                   group, gfail, c->counter.p, c->d_scene, dcount, per_item, DK, RF, PK, PS, CV,   \
+                                   ZW);                                                                            \
         else hipLaunchKernelGGL((k_edges<N, false, L>), dim3(G), b, 0, s, from, to, nd, n, KM, mode, valid,        \
-                                group, gfail, c->counter.p, c->d_scene, dcount, per_item, DK, RF, PK, PS, CV);     \
+                                group, gfail, c->counter.p, c->d_scene, dcount, per_item, DK, RF, PK, PS, CV, ZW); \
     } while (0)
+#define RP_EDGES_P(N, L, G, KM, DK, RF, PK, PS, CV) RP_EDGES_Z(N, L, G, KM, DK, RF, PK, PS, CV, (int*)nullptr)
 #define RP_EDGES_L(N, L, G, KM, DK, RF) RP_EDGES_P(N, L, G, KM, DK, RF, 1, 0, (const int*)nullptr)
+#define RP_EDGES_U(N)                                                                                              \
+    do {                                                                                                           \
+        if (bf) hipLaunchKernelGGL((k_edges_units<N, true>), dim3(nb_units), b, 0, s, from, to, nd, n, mode, valid, \
+                                   group, gfail, c->counter.p, c->d_scene, dcount, per_item, pk,                   \
+                                   (const int*)c->ecnt.p, (const uint32_t*)c->eunits.p, (const int*)c->enunits.p); \
+        else hipLaunchKernelGGL((k_edges_units<N, false>), dim3(nb_units), b, 0, s, from, to, nd, n, mode, valid,  \
+                                group, gfail, c->counter.p, c->d_scene, dcount, per_item, pk,                      \
+                                (const int*)c->ecnt.p, (const uint32_t*)c->eunits.p, (const int*)c->enunits.p);    \
+    } while (0)
 #define RP_EDGES(N)                                                                                               \
     do {                                                                                                          \
         if (split) {                                                                                              \
@@ -626,6 +655,12 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
         } else if (first) {                                                                                       \
             RP_EDGES_L(N, false, nb, km0, nullptr, 0);                                                            \
             RP_EDGES_L(N, true, nb_first, km0 + 1, nullptr, km0);                                                 \
+        } else if (units) {                                                                                       \
+            RP_EDGES_Z(N, false, (unsigned)(groups * kc), kc, nullptr, 0, pk, 0, (const int*)nullptr, c->enunits.p); \
+            hipLaunchKernelGGL(k_edge_units, dim3(blocks_for(n, EU_BLOCK)), dim3(EU_BLOCK), 0, s, nd, n, dcount,   \
+                               per_item, mode, (const uint8_t*)valid, group, (const int*)gfail, pk, c->ecnt.p,     \
+                               c->eunits.p, c->enunits.p);                                                        \
+            RP_EDGES_U(N);                                                                                        \
         } else if (coarse) {                                                                                      \
             RP_EDGES_P(N, false, (unsigned)(groups * kc), kc, nullptr, 0, pk, 0, (const int*)nullptr);            \
             hipLaunchKernelGGL(k_edge_rest, dim3(blocks_for(n, 256)), dim3(256), 0, s, nd, n, dcount, per_item,   \
@@ -645,6 +680,8 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
 #undef RP_EDGES
 #undef RP_EDGES_L
 #undef RP_EDGES_P
+#undef RP_EDGES_Z
+#undef RP_EDGES_U
     HIP_TRY(hipGetLastError());
     prof_end(c, ps, 1, s);
     if (edge_stats_on() && !dkmax) {
@@ -852,6 +889,9 @@ int group_vote(rp_ctx* c, int tflag) {
 // a rank writes region (k+2) & 1 only after every rank has arrived at exchange k+1,
 // i.e. finished reading exchange k's records)
 constexpr int64_t SHM_HDR = 64 * 64;
+// a rank whose plan failed publishes this as its sequence word: the others stop at
+// their next barrier instead of waiting out the watchdog (the group is then re-formed)
+constexpr int64_t SHM_SEQ_BROKEN = INT64_MIN;
 inline int64_t shm_region(const rp_ctx* c) { return ((c->shm_bytes - SHM_HDR) / 2) & ~(int64_t)255; }
 // device pointer of this exchange's records (rank-major slots of `words` int32)
 int32_t* shm_records(rp_ctx* c, int64_t k, int64_t words) {
@@ -865,7 +905,10 @@ void shm_barrier(rp_ctx* c, int64_t k) {
     __atomic_store_n(reinterpret_cast<int64_t*>(c->shm + 64 * c->rank), k, __ATOMIC_RELEASE);
     const double t0 = now_s();
     for (int r = 0; r < c->world; ++r) {
-        while (__atomic_load_n(reinterpret_cast<const int64_t*>(c->shm + 64 * r), __ATOMIC_ACQUIRE) < k) {
+        int64_t v;
+        while ((v = __atomic_load_n(reinterpret_cast<const int64_t*>(c->shm + 64 * r), __ATOMIC_ACQUIRE)) < k) {
+            if (v == SHM_SEQ_BROKEN)
+                throw HipError{"shared-memory transport: rank " + std::to_string(r) + " failed its plan"};
             if (now_s() - t0 > c->watchdog_s) throw HipError{"shared-memory transport: a rank did not arrive"};
 #if defined(__x86_64__) && !defined(__HIP_DEVICE_COMPILE__)
             __builtin_ia32_pause();
@@ -2866,12 +2909,18 @@ static int plan_entry(rp_ctx* c, const double start[RP_NQ], const double goal[RP
     int rc;
     try {
         rc = plan_impl(c, start, goal, lo, hi, params, path_out, path_cap, n_out, status_out);
-        if (c->lb_used && read_scalar(c, c->lberr.p) != 0)   // (large plans only: one read)
+        if (c->lb_used && read_scalar(c, c->lberr.p) != 0) {   // (large plans only: one read)
+            // the flag is sticky on the device: clear it, so that this plan fails and the
+            // context's next one starts clean (stream order puts the clear first)
+            HIP_TRY(hipMemsetAsync(c->lberr.p, 0, sizeof(int), c->stream));
             throw HipError{"look-back accept exceeded its poll budget (a block's predecessor never published)"};
+        }
     } catch (...) {
         c->in_plan = false;
         c->pused = 0;
         if (c->transport != TR_NONE) c->group_broken = true;
+        if (c->transport == TR_SHM && c->shm)   // peers waiting at an exchange stop now
+            __atomic_store_n(reinterpret_cast<int64_t*>(c->shm + 64 * c->rank), SHM_SEQ_BROKEN, __ATOMIC_RELEASE);
         throw;
     }
     c->in_plan = false;
@@ -3017,6 +3066,9 @@ int rp_reserve(rp_ctx* c, int64_t batch, int64_t tree_capacity) {
     c->eslot.ensure(ne);
     c->eincl.ensure(ne);
     c->echunk.ensure(blocks_for(ne * (int64_t)kmax, VBLOCK) + 1);
+    c->ecnt.ensure(ne);   // (the coarse-first passes: per-edge counts, pass 1's work list)
+    c->eunits.ensure((size_t)blocks_for(ne, VBLOCK) * kmax);
+    c->enunits.ensure(1);
     size_t b32 = 0, b64 = 0;
     HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b32, (const int32_t*)nullptr, (int32_t*)nullptr, (int)ne,
                                              c->stream));
@@ -3323,6 +3375,20 @@ int rp_debug_edges(rp_ctx* c, double* out, int32_t n) {
     }
     for (int k = 0; k < 5; ++k) out[k] = (double)h[k];
     return RP_OK;
+}
+
+// fault injection (tests): raise the look-back accepts' poll-budget error flag, as a
+// launch that ran out of its budget would, so the next large plan must report it
+int rp_debug_lb_poison(rp_ctx* c) {
+    if (!c) return RP_ERR_ARG;
+    RP_IDLE(c);
+    RP_GUARD_BEGIN
+    HIP_TRY(hipSetDevice(c->device));
+    c->lberr.ensure(1);
+    HIP_TRY(hipMemsetAsync(c->lberr.p, 0x01, 1, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return RP_OK;
+    RP_GUARD_END(c)
 }
 
 int rp_debug_scene(rp_ctx* c, void* out, int64_t bytes) {

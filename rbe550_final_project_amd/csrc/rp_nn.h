@@ -254,7 +254,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     nn_block_coords(qblocks, nwg, &qb, &yr);
     const int64_t qb0 = qb * W * QW;
     if (qb0 >= n) return;   // whole block idle (uniform)
-    const int w = (int)(rp_tid() >> 6), lane = (int)(rp_tid() & 63), ch = lane >> 4;
+    // (w wave-uniform in an SGPR: the per-wave LDS bases need no VGPRs)
+    const int w = __builtin_amdgcn_readfirstlane((int)(rp_tid() >> 6)), lane = (int)(rp_tid() & 63), ch = lane >> 4;
     const int64_t t_lo = yr * chunk, t_hi = min(T, t_lo + chunk);
     const int64_t qw0 = qb0 + (int64_t)w * QW;
     // a row's query state, read from global memory (L1 / L2) where the exact path needs
@@ -374,7 +375,12 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     // wait for each tile's freshly issued load), and loads past the range re-read its
     // last tile (unconditional: static vmcnt waits). Tiles need no bounds test: the
     // image's pad slots and dead query rows never pass (k_nn_image, a_frag).
-    constexpr int PF = 4;
+    // (RB 8: 3 tiles ahead — with 4 the kernel held 3 VGPRs over the 128 of 4 waves per
+    // SIMD in scratch; tests/test_isa_guard.py)
+#ifndef RP_NN_PF8
+#define RP_NN_PF8 3
+#endif
+    constexpr int PF = RB >= 8 ? RP_NN_PF8 : 4;
     // tiles of the range: every tstride-th (a pilot search), else all
     const int64_t ntiles = ((t_hi - t_lo + 15) / 16 + tstride - 1) / tstride;
     const int col = lane & 15;   // this lane's column of every tile
@@ -448,7 +454,10 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
         if (tb + u < ntiles) tile_step(tb + u, bq[u]);
     if (ncand > 0) flush();
     wave_lds_sync();
-    for (int r = lane; r < QW; r += 64) {
+    // the lane id recomputed (mbcnt) rather than kept live across the scan: at RB 8 the
+    // values the results' addresses derive from were held in scratch (2 dwords)
+    const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    for (int r = ln; r < QW; r += 64) {
         const int64_t q = qw0 + r;
         if (q < n)
             part[yr * n + q] = DI2{__longlong_as_double((long long)s_best[w][r]),

@@ -239,6 +239,27 @@ class PlannerInterface:
         self._reserved = None
         return self._ctx
 
+    def _reform_group(self):
+        """A failed grouped plan leaves every rank's group broken (rp_plan refuses
+        RP_ERR_EXCHANGE until the group is initialised again): re-form it, so that
+        one HIP or watchdog error costs this query only, not every later one. If
+        that fails too, drop the contexts; the next query opens fresh ones."""
+        from .native import group_init_local
+        try:
+            group_init_local(self._ctxs)
+        except NativeError as ex:
+            _logger().warning(f"MI355X planner: re-forming the rank group failed ({ex}); reopening the contexts")
+            for c in self._ctxs:
+                try:
+                    c.close()
+                except Exception:   # noqa: BLE001 - a dead context is dropped either way
+                    pass
+            self._ctxs = []
+            self._ctx = None
+            self._devs = None
+            self._pushed = None
+        self._reserved = None
+
     def _reserve(self, ctx, batch, cap):
         """Workspace for this batch / tree capacity sized once (rp_reserve), so the
         first query does not allocate device memory inside the plan."""
@@ -425,6 +446,14 @@ class PlannerInterface:
             # a library error (capacity, HIP) is reported and planning "fails"
             _logger().warning(f"MI355X planner error: {ex}")
             path, status = None, _abi.STATUS_NONE
+            if len(self._ctxs) > 1:
+                self._reform_group()
+                if self._ctx is None:   # reopened: the diagnostics below need a context with the scene
+                    try:
+                        ctx = self._context()
+                        self._sync_scene()
+                    except NativeError:
+                        ctx = None
         t_plan1 = time.perf_counter()
         self.last_status = status
 
@@ -455,7 +484,8 @@ class PlannerInterface:
         if not bool(np.all(qpos_goal - eps <= hi) and np.all(qpos_goal + eps >= lo)):
             _logger().warning("OMPL goal state out of bounds")
             self.diagnose_bounds_violation(si, qpos_goal)
-        self._diagnose_start_goal(ctx, qpos_start, qpos_goal)
+        if ctx is not None:
+            self._diagnose_start_goal(ctx, qpos_start, qpos_goal)
 
     def _diagnose_start_goal(self, ctx, qpos_start, qpos_goal):
         try:

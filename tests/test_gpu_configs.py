@@ -197,12 +197,16 @@ def test_nearest_node_status_geometry(gpu_ctx, name, devgeom, monkeypatch):
 
 @pytest.mark.parametrize("name", ["C5_well_s0", "C5_well_s3", "C4_q5", "C2_q0_s1"])
 @pytest.mark.parametrize("pk,cmin", [("0", ""), ("2", "0"), ("4", "0"), ("8", ""), ("-2", "0"), ("-3", "")])
-def test_coarse_first_edge_passes_in_plans(gpu_ctx, name, pk, cmin, monkeypatch):
+@pytest.mark.parametrize("units", ["1", "0"])
+def test_coarse_first_edge_passes_in_plans(gpu_ctx, name, pk, cmin, units, monkeypatch):
     """The planner's edge launches through the coarse-first passes (slot 0 and every
     pk-th interior slot first, then the rest of the edges still valid; RBE_EDGE_COARSE)
     or one pass (0), at the default size threshold and forced on every wave-compacted
-    launch (RBE_EDGE_COARSE_MIN=0): same plans."""
+    launch (RBE_EDGE_COARSE_MIN=0), pass 1 over the work list of its live (group,
+    round) units (k_edge_units / k_edges_units) or the groups x rounds grid
+    (RBE_EDGE_UNITS=0): same plans."""
     monkeypatch.setenv("RBE_EDGE_COARSE", pk)
+    monkeypatch.setenv("RBE_EDGE_UNITS", units)
     if cmin:
         monkeypatch.setenv("RBE_EDGE_COARSE_MIN", cmin)
     _check(gpu_ctx, name)
@@ -217,6 +221,25 @@ def test_lookback_accepts(gpu_ctx, name, lb, monkeypatch):
     trees, same plans."""
     monkeypatch.setenv("RBE_ACCEPT_LB", lb)
     _check(gpu_ctx, name)
+
+
+def test_lookback_error_flag_is_not_sticky(gpu_ctx):
+    """the look-back accepts' poll-budget flag lives on the device. A plan
+    that finds it raised fails (NativeError) and clears it, so the context's next
+    large plan succeeds with the golden answer instead of failing forever.
+    (rp_debug_lb_poison raises the flag as an exhausted budget would.)"""
+    import ctypes as C
+    L = native.load()
+    L.rp_debug_lb_poison.argtypes = [C.c_void_p]
+    assert L.rp_debug_lb_poison(gpu_ctx._h) == 0
+    m, q, p = _case("C5_well_s3")
+    sc = scenes.Scene.from_json(q["scene"])
+    gpu_ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+    gpu_ctx.set_attached(q["attached"])
+    with pytest.raises(native.NativeError, match="poll budget"):
+        gpu_ctx.plan(q["start"], q["goal"], model.Q_LO, model.Q_HI, p)
+    _check(gpu_ctx, "C5_well_s3")
+    _check(gpu_ctx, "C4_q5")
 
 
 def test_kernel_profile_of_a_plan(gpu_ctx):

@@ -62,12 +62,15 @@ def test_device_edges_equal_oracle(gpu_ctx, oracle_lib, scene, n, scale):
 @pytest.mark.parametrize("scene", ["goal3", "clutter64"])
 @pytest.mark.parametrize("n,scale", [(2049, 1.0), (40000, 1.0), (20000, 3.0)])
 @pytest.mark.parametrize("pk", ["0", "2", "3", "4", "8", "-2", "-3", "-8"])
-def test_coarse_first_edge_passes(gpu_ctx, oracle_lib, scene, n, scale, pk, monkeypatch):
+@pytest.mark.parametrize("units", ["1", "0"])
+def test_coarse_first_edge_passes(gpu_ctx, oracle_lib, scene, n, scale, pk, units, monkeypatch):
     """rp_check_edges through the coarse-first passes (slot 0 and every pk-th interior
     slot — pk < 0: the |pk|-th part of the interior next to slot 0 — then the other
     slots of the edges still valid; RBE_EDGE_COARSE) forced on at every size
-    (RBE_EDGE_COARSE_MIN=0), and off: the oracle's flags."""
+    (RBE_EDGE_COARSE_MIN=0), and off, pass 1 over its (group, round) work list or the
+    groups x rounds grid (RBE_EDGE_UNITS): the oracle's flags."""
     monkeypatch.setenv("RBE_EDGE_COARSE", pk)
+    monkeypatch.setenv("RBE_EDGE_UNITS", units)
     monkeypatch.setenv("RBE_EDGE_COARSE_MIN", "0")
     monkeypatch.setenv("RBE_ML_LANES", "1")   # (the wave-compacted kernel at every size)
     sc = _scene(scene)

@@ -212,6 +212,174 @@ def run_plan_path_devices(devices, seeds=(1, 2, 3, 4)):
     return times, states, statuses, info
 
 
+def run_plans_pipelined(device, wl, batch, straight_first, serial_total_ms, ks=(2, 4, 8), reps=5):
+    """C3 pipelined: the workload's queries in flight on K contexts of one GPU
+    (rp_plan_many: each context its own stream and planner thread, the host side of a
+    query in C++; a context waits only for its own previous query). Wall time of the
+    whole workload (one rp_plan_many call), best
+    K, median of `reps` passes after a warm-up pass; the same seeds as the serial legs
+    (query i: seed i), so every path is the one the serial leg returns
+    (tests/test_gpu_pipelined.py checks them against the oracle)."""
+    from rbe550_final_project_amd import native
+    jobs = [{"scene": scenes.Scene.from_json(q["scene"]), "attached": q["attached"], "start": q["start"],
+             "goal": q["goal"], "lo": model.Q_LO, "hi": model.Q_HI,
+             "params": _abi.make_params(seed=i, batch=batch, n_waypoints=150, timeout_s=10.0,
+                                        straight_first=straight_first)} for i, q in enumerate(wl["queries"])]
+    ctxs = [Context(device=device, robot=model.robot_desc()) for _ in range(max(ks))]
+    per_k = {}
+    try:
+        for c in ctxs:
+            c.reserve(batch, 0)
+        qs, keep = native.make_queries(jobs)   # (the records, made once: the serial legs' scenes are set
+        n = len(jobs)                           # outside their timed calls too)
+        for k in ks:
+            native.plan_many(ctxs[:k], qs, n, model.Q_LO, model.Q_HI)   # warm-up pass
+            walls = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                res = native.plan_many(ctxs[:k], qs, n, model.Q_LO, model.Q_HI)
+                walls.append(1e3 * (time.perf_counter() - t0))
+            solved = sum(st in (_abi.STATUS_EXACT, _abi.STATUS_APPROXIMATE) for _, st, _ in res)
+            per_k[k] = {"total_ms": round(float(np.median(walls)), 4), "min_ms": round(min(walls), 4),
+                        "solved": int(solved)}
+        del keep
+    finally:
+        for c in ctxs:
+            c.close()
+    best = min(per_k, key=lambda k: per_k[k]["total_ms"])
+    rec = dict(per_k[best])
+    rec.update({"queries": len(jobs), "batch": batch, "contexts": best, "per_contexts": per_k,
+                "serial_total_ms": serial_total_ms,
+                "speedup_vs_serial": round(serial_total_ms / rec["total_ms"], 3) if rec["total_ms"] else None,
+                "mode": ("product default: straight edge first, then RRT-Connect" if straight_first
+                         else "RRT-Connect forced (straight_first off)")
+                + "; all queries in flight on K contexts of one GPU (rp_plan_many), median of "
+                  f"{reps} passes of the whole workload"})
+    return rec
+
+
+SCALING_XGMI_LAT_MS = 0.025     # assumed per all-gather latency of a small RCCL message over xGMI
+SCALING_XGMI_GBPS = 153.0       # one xGMI link (MI355X_MICROARCH.md), the ring's per-step bound
+
+
+def kernel_slices(ctx, scene, q, flags, stream, sizes, tree_nodes=200_000):
+    """ms per launch of the three hot kernel classes at each size n (states / edges /
+    queries): k_validity (n uniform states), the planner's edge launch (n random
+    range-length edges, coarse-first passes + pass-1 work list), the matrix-core
+    nearest-node search (n queries against a tree of `tree_nodes` uniform nodes; the
+    pilot, k_nn_mfma and the reduce). HIP events on the context stream
+    (rp_last_kernel_ms with profiling on)."""
+    ctx.set_scene(scene.boxes, scene.plane_z, scene.base)
+    ctx.set_attached(-1)
+    rng = np.random.default_rng(5)
+    nmax = max(sizes)
+    lo, hi = model.Q_LO, model.Q_HI
+    qa = lo + (hi - lo) * rng.random((nmax, 9))
+    d = rng.standard_normal((nmax, 9))
+    rng_len = 0.2 * float(np.linalg.norm(hi - lo))
+    qb = np.clip(qa + d / np.linalg.norm(d, axis=1, keepdims=True) * rng_len, lo, hi)
+    res = 0.01 * float(np.linalg.norm(hi - lo))
+    tree = lo + (hi - lo) * rng.random((tree_nodes, 9))
+    out = {"validity": {}, "edges": {}, "nearest_node": {}}
+    ctx.set_profiling(True)
+    try:
+        for n in sizes:
+            _, ms, _ = rate_on_scene(ctx, scene, q, n, flags, stream, 10)
+            out["validity"][n] = round(ms, 5)
+            v = []
+            for _ in range(4):
+                ctx.check_edges(qa[:n], qb[:n], res)
+                v.append(ctx.last_kernel_ms())
+            out["edges"][n] = round(float(np.median(v[1:])), 5)
+            v = []
+            for _ in range(3):
+                ctx.selftest_nn(qa[:n], tree, lo, hi, 8)
+                v.append(ctx.last_kernel_ms())
+            out["nearest_node"][n] = round(float(np.median(v[1:])), 5)
+    finally:
+        ctx.set_profiling(False)
+    return out
+
+
+def scaling_model(ctx, q, flags, stream, ranks=(2, 4, 8), thresholds=(4096, 16384, 65536, 1 << 40)):
+    """Multi-GPU readiness at N = 1: for the C5 covered-well and the
+    C4 configured-batch plans, the host wall time of every sub-batch (rp_debug_subbatches)
+    split by the rank-group rule (<= group_repl samples: replicated on every rank, no
+    exchange; larger: sharded over the ranks + one record all-gather),
+    the three hot kernels measured at the per-rank slice sizes, and a projection of the
+    plan time at N ranks: replicated sub-batches and the rest of the plan unchanged; a
+    sharded sub-batch of C samples scaled by the measured kernel-time ratio
+    (t(C / N) / t(C), summed over the three kernel classes) plus one all-gather of
+    12 C + 4 N bytes (assumed latency SCALING_XGMI_LAT_MS + ring transfer at one link's
+    bandwidth). A model, not a measurement: no N > 1 run on distinct GPUs exists."""
+    res = {"assumptions": {"allgather_latency_ms": SCALING_XGMI_LAT_MS, "xgmi_link_gbps": SCALING_XGMI_GBPS,
+                           "model": "T_N = T_other + sum_repl t_sb + sum_shard (t_sb * rho(C, N) + X(C, N)); "
+                                    "rho = sum_k t_k(C / N) / sum_k t_k(C) over k_validity, edges, nearest node "
+                                    "(log-interpolated between the measured sizes); group_repl threshold thr: "
+                                    "sub-batches of C <= thr replicated"}}
+    well = load_workload("clutter64_well")
+    c4 = load_workload("goal4_pentagon_10box")
+    cases = (("C5_well", {"queries": well["queries"] * 4}, C5_BATCH, 1, 8,
+              scenes.Scene.from_json(well["queries"][0]["scene"])),
+             ("C4_configured", c4, C4_BATCH, 0, 0, scenes.Scene.from_json(c4["queries"][14]["scene"])))
+    for key, wl, batch, seed0, max_iters, scene in cases:
+        plans = []
+        ctx.reserve(batch, 1 << 23)
+        for i, qq in enumerate(wl["queries"]):
+            sc = scenes.Scene.from_json(qq["scene"])
+            ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
+            ctx.set_attached(qq["attached"])
+            p = _abi.make_params(seed=seed0 + i, batch=batch, batch_min=batch, n_waypoints=150, timeout_s=10.0,
+                                 tree_capacity=1 << 23, straight_first=False, max_iters=max_iters)
+            t0 = time.perf_counter()
+            ctx.plan(qq["start"], qq["goal"], model.Q_LO, model.Q_HI, p)
+            plans.append((1e3 * (time.perf_counter() - t0), ctx.sub_batches()))
+        sizes = sorted({1 << k for k in range(12, 19)} | {batch // n for n in (1,) + tuple(ranks)})
+        sizes = [n for n in sizes if n <= max(batch, 4096)]
+        ks = kernel_slices(ctx, scene, q, flags, stream, sizes)
+        xs = np.log(np.array(sizes, dtype=float))
+
+        def t_all(n):   # summed kernel-class time at n (log-log interpolation)
+            tot = 0.0
+            for cls in ks.values():
+                ys = np.log(np.array([cls[s] for s in sizes]))
+                tot += float(np.exp(np.interp(np.log(max(n, 1)), xs, ys)))
+            return tot
+
+        def project(thr, N):
+            total = 0.0
+            for wall, sbs in plans:
+                t = wall
+                for C, ms in sbs:
+                    if C > thr and N > 1:
+                        x = SCALING_XGMI_LAT_MS + (N - 1) / N * (12 * C + 4 * N) / (SCALING_XGMI_GBPS * 1e6)
+                        t += ms * (t_all(C / N) / t_all(C) - 1.0) + x
+                total += t
+            return total / len(plans)
+
+        walls = [w for w, _ in plans]
+        all_sb = [sb for _, sbs in plans for sb in sbs]
+        repl_ms = sum(ms for C, ms in all_sb if C <= 4096) / len(plans)
+        shard_ms = sum(ms for C, ms in all_sb if C > 4096) / len(plans)
+        proj = {}
+        for thr in thresholds:
+            name = "none" if thr >= 1 << 40 else str(thr)
+            proj[name] = {str(N): round(project(thr, N), 4) for N in (1,) + tuple(ranks)}
+        best = {str(N): min(proj, key=lambda k: proj[k][str(N)]) for N in ranks}
+        res[key] = {"plans": len(plans), "batch": batch, "mean_plan_ms": round(float(np.mean(walls)), 4),
+                    "median_plan_ms": round(float(np.median(walls)), 4),
+                    "per_plan_ms": {"replicated_sub_batches": round(repl_ms, 4),
+                                    "sharded_sub_batches": round(shard_ms, 4),
+                                    "outside_sub_batches": round(float(np.mean(walls)) - repl_ms - shard_ms, 4),
+                                    "exchange_at_N1": 0.0},
+                    "sub_batch_sizes": sorted({C for C, _ in all_sb}),
+                    "kernel_slices_ms": {k: {str(n): v for n, v in d.items()} for k, d in ks.items()},
+                    "projected_mean_plan_ms": proj, "best_group_repl": best,
+                    "projected_speedup_default_repl": {str(N): round(proj["4096"]["1"] / proj["4096"][str(N)], 3)
+                                                       for N in ranks}}
+    return res
+
+
 def max_over_ranks(x, dev, distributed):
     """max of a float over the ranks (device tensor on RCCL, host tensor on gloo)"""
     if not distributed:
@@ -546,6 +714,13 @@ def main():
                                                  "attached_object, timeout=10.0) through tests/mock_genesis.py"
                                                  + ("" if sf else "; RRT-Connect forced"),
                                          "median_parts_ms": parts})
+            # C3 "pipelined" (BASELINE configs[2]: ~20 RRT queries pipelined): the 21
+            # queries kept in flight on K contexts of this GPU (native.plan_pipelined),
+            # the wall time of the whole workload next to the serial legs above
+            if not distributed:
+                for key, sf in (("C3_pipelined", True), ("C3_pipelined_rrt", False)):
+                    serial = plan["total_ms"] if sf else plan["C3_rrt"]["total_ms"]
+                    plan[key] = run_plans_pipelined(local, wl, args.plan_batch, sf, serial)
         except Exception as ex:  # report, keep the primary metric
             plan = {"error": repr(ex)[:300]}
         plan_failed = plan is None or "error" in plan
@@ -607,6 +782,14 @@ def main():
             rooflines_plan = {"nearest_node": nn_roof, "edges": edge_roof}
         except Exception as ex:
             rooflines_plan = {"error": repr(ex)[:300]}
+    # ---- multi-GPU readiness without the hardware: sub-batch accounting, the kernels
+    # at per-rank slice sizes, projected N = 2 / 4 / 8 plan times (a model)
+    scaling = None
+    if not args.no_plan and rank == 0 and not distributed:
+        try:
+            scaling = scaling_model(ctx, q, flags, stream)
+        except Exception as ex:
+            scaling = {"error": repr(ex)[:300]}
     ctx.set_scene(scene.boxes, scene.plane_z, scene.base)
     ctx.set_attached(-1)
 
@@ -681,7 +864,7 @@ def main():
                           "valid_fraction": round(valid_frac, 4)},
                "rank_group": rank_group,
                "plan_wall": plan, "per_config": per_config, "roofline": roofline,
-               "rooflines_plan": rooflines_plan, "cpu_baseline": cpu}
+               "rooflines_plan": rooflines_plan, "scaling_model": scaling, "cpu_baseline": cpu}
         print(json.dumps(out), flush=True)
     ctx.close()
     if distributed:

@@ -228,8 +228,8 @@ const char* rp_version(void);
  * field). A client checks rp_abi_version() == RP_ABI_VERSION once, before passing
  * any struct (native.py load() does); a mismatch means the header and the library
  * disagree and no call may be made. Version 5: rp_box_rot / rp_set_scene_rot;
- * 6: rp_selftest_f64 writes six values per input. */
-#define RP_ABI_VERSION 6
+ * 6: rp_selftest_f64 writes six values per input; 7: rp_query / rp_plan_many. */
+#define RP_ABI_VERSION 7
 int rp_abi_version(void);
 
 /* Fill `out` with the built-in Franka Panda capsule model (spec/franka_capsules.json). */
@@ -250,8 +250,10 @@ int rp_set_scene(rp_ctx* ctx, const rp_box* boxes, int32_t n_boxes, float plane_
                  const float base_pos[3]);
 
 /* rp_set_scene with full box orientations (the Genesis collider sees every box at
- * its simulated pose, code/planning.py:211). A box with quat x = y = 0 gets exactly
- * the record rp_set_scene makes for its yaw; any other box is tilted: the quaternion
+ * its simulated pose, code/planning.py:211). An upright box, |x|, |y| <= 1e-7 |quat|
+ * (a rotation about z to within simulation noise; a quaternion whose norm is not 1 is
+ * normalised first), gets exactly the record rp_set_scene makes for its yaw
+ * atan2(2(wz + xy), 1 - 2(y^2 + z^2)); any other box is tilted: the quaternion
  * is normalised and turned into a rotation matrix in double, rounded to float once,
  * and the collider tests the capsules against the rotated box (world AABB padded by
  * 1e-6 m). RP_ERR_ARG for a zero quaternion. */
@@ -317,6 +319,35 @@ int rp_plan_async(rp_ctx* ctx, const double start[RP_NQ], const double goal[RP_N
                   const double lo[RP_NQ], const double hi[RP_NQ], const rp_plan_params* params,
                   double* path_out, int32_t path_cap, int32_t* n_out, int32_t* status_out);
 int rp_plan_wait(rp_ctx* ctx);
+
+/* One query of rp_plan_many: its scene (rp_set_scene's boxes, plane and base), its
+ * attached box (rp_set_attached with the reference's exemption, hand | left_finger |
+ * right_finger; -1 = none), start, goal and parameters. */
+typedef struct rp_query {
+    const rp_box* boxes;
+    int32_t n_boxes;
+    float plane_z;
+    float base_pos[3];
+    int32_t attached_box;
+    double start[RP_NQ];
+    double goal[RP_NQ];
+    rp_plan_params params;
+} rp_query;
+
+/* Many independent queries kept in flight on several contexts of this process
+ * (BASELINE config 3: goal3's ~20 RRT queries "pipelined";
+ * code/goal3_tallest.py:63-283 -> code/motion_primitives.py:144): query i runs on
+ * ctxs[i % n_ctx] through that context's planner thread (rp_plan_async), after the
+ * context's previous query; every context has its own stream, so the queries'
+ * dependent small kernels overlap. Each result is the one rp_plan gives for that
+ * query alone: path i goes to path_out + i * path_cap * 9 (n_out[i] states),
+ * status_out[i], rc_out[i] = that query's rp_plan code. Returns RP_OK when every
+ * query succeeded, else the first failing query's code (the others still ran).
+ * The contexts must be idle; they are idle again on return, each holding its last
+ * query's scene and stats. */
+int rp_plan_many(rp_ctx* const* ctxs, int32_t n_ctx, const rp_query* queries, int32_t n,
+                 const double lo[RP_NQ], const double hi[RP_NQ], double* path_out, int32_t path_cap,
+                 int32_t* n_out, int32_t* status_out, int32_t* rc_out);
 
 /* Size the planner's device workspace for queries of up to `batch` samples per
  * iteration on trees of `tree_capacity` nodes (0: the rp_plan_params defaults), so
@@ -399,9 +430,11 @@ const char* rp_last_error(rp_ctx* ctx);
  * launches without opening another hardware queue. */
 int rp_get_stream(rp_ctx* ctx, void** stream_out);
 
-/* Kernel-level timing of the last rp_check_states_device call made with profiling
- * on (rp_set_profiling): the validity kernel's duration measured with HIP events on
- * the launch's stream (ms). RP_ERR_ARG if no such call was made. */
+/* Kernel-level timing of the last timed call made with profiling on
+ * (rp_set_profiling), measured with HIP events on the launch's stream (ms):
+ * rp_check_states_device (the validity kernel), rp_check_edges (the edge launch, no
+ * copies), rp_selftest_nn (the search, no copies). RP_ERR_ARG if no such call was
+ * made. */
 int rp_last_kernel_ms(rp_ctx* ctx, double* ms);
 
 /* Numerics self-test (used by the parity tests): device sqrt(|x|), 0.13037 / x,

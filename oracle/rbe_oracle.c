@@ -101,13 +101,20 @@ int ro_scene_set(ro_scene* s, const rp_box* boxes, int32_t n, float plane_z, con
 }
 
 /* Boxes with orientation quaternions (w, x, y, z): the product's rp_set_scene_rot
- * restated. x = y = 0 is an upright box of yaw atan2(2(wz + xy), 1 - 2(y^2 + z^2));
+ * restated. |x|, |y| <= 1e-7 |q| (quat_upright) is an upright box of yaw
+ * atan2(2(wz + xy), 1 - 2(y^2 + z^2)) (q normalised first when its norm is not 1);
  * any other box is tilted: the normalised quaternion's rotation matrix R (world =
  * R * box) in double, rounded to float once; the box frame of a world point p is
  * R^T (p - c); world AABB half extents |R_k0| h0 + |R_k1| h1 + |R_k2| h2 + 1e-6. A
  * toppled block is what goal3's collapse check re-plans around
  * (code/goal3_tallest.py:257); Genesis' collider sees every box at its pose
  * (code/planning.py:211). */
+/* upright to simulation noise: |x|, |y| <= 1e-7 |q| (rp_lib.hip quat_upright) */
+static int quat_upright(double x, double y, double n2) {
+    const double t = 1e-7 * sqrt(n2);
+    return fabs(x) <= t && fabs(y) <= t;
+}
+
 int ro_scene_set_rot(ro_scene* s, const rp_box_rot* boxes, int32_t n, float plane_z, const float base[3]) {
     if (!s || n < 0 || n > RP_MAX_BOXES || (n > 0 && !boxes)) return RP_ERR_ARG;
     rp_box up[RP_MAX_BOXES];
@@ -116,7 +123,12 @@ int ro_scene_set_rot(ro_scene* s, const rp_box_rot* boxes, int32_t n, float plan
         const rp_box_rot* b = &boxes[j];
         for (int k = 0; k < 3; ++k) { up[j].center[k] = b->center[k]; up[j].half[k] = b->half[k]; }
         double w = b->quat[0], x = b->quat[1], y = b->quat[2], z = b->quat[3];
-        if (x == 0.0 && y == 0.0 && w == 0.0 && z == 0.0) return RP_ERR_ARG;
+        const double n2 = w * w + x * x + y * y + z * z;
+        if (n2 == 0.0) return RP_ERR_ARG;
+        if (quat_upright(x, y, n2) && fabs(n2 - 1.0) > 1e-12) {   /* non-unit upright: normalised */
+            const double nr = sqrt(n2);
+            w /= nr; x /= nr; y /= nr; z /= nr;
+        }
         up[j].yaw = (float)atan2(2.0 * (w * z + x * y), 1.0 - 2.0 * (y * y + z * z));
     }
     int rc = ro_scene_set(s, up, n, plane_z, base);
@@ -124,7 +136,7 @@ int ro_scene_set_rot(ro_scene* s, const rp_box_rot* boxes, int32_t n, float plan
     for (int j = 0; j < n; ++j) {
         const rp_box_rot* b = &boxes[j];
         double w = b->quat[0], x = b->quat[1], y = b->quat[2], z = b->quat[3];
-        if (x == 0.0 && y == 0.0) continue;
+        if (quat_upright(x, y, w * w + x * x + y * y + z * z)) continue;
         double nrm = sqrt(w * w + x * x + y * y + z * z);
         w /= nrm; x /= nrm; y /= nrm; z /= nrm;
         double R[3][3] = {{1.0 - 2.0 * (y * y + z * z), 2.0 * (x * y - w * z), 2.0 * (x * z + w * y)},

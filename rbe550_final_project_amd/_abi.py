@@ -2,7 +2,7 @@
 import ctypes as C
 import math
 
-ABI_VERSION = 6   # RP_ABI_VERSION of include/rbe_planner.h these mirrors follow
+ABI_VERSION = 7   # RP_ABI_VERSION of include/rbe_planner.h these mirrors follow
 NQ = 9
 MAX_CAPSULES = 32
 MAX_SELF_PAIRS = 64
@@ -47,6 +47,13 @@ class PlanParams(C.Structure):
                 ("n_waypoints", C.c_int32), ("simplify", C.c_int32), ("tree_capacity", C.c_int64),
                 ("straight_first", C.c_int32), ("chunk", C.c_int32),
                 ("group_repl", C.c_int64)]
+
+
+class Query(C.Structure):
+    """rp_query: one query of rp_plan_many (its scene, attached box, start, goal, params)."""
+    _fields_ = [("boxes", C.POINTER(Box)), ("n_boxes", C.c_int32), ("plane_z", C.c_float),
+                ("base_pos", C.c_float * 3), ("attached_box", C.c_int32), ("start", C.c_double * NQ),
+                ("goal", C.c_double * NQ), ("params", PlanParams)]
 
 
 class IkParams(C.Structure):

@@ -149,6 +149,9 @@ struct rp_ctx {
     // host waits since the context was made (rp_debug_waits): wait_seq calls,
     // stream_wait calls, seconds spinning, seconds in the sleep loop, sleeps
     double waits[5] = {0, 0, 0, 0, 0};
+    // the last plan's sub-batches (rp_debug_subbatches, bench.py scaling_model):
+    // (samples, host wall ms from the first enqueue to the status read) each
+    std::vector<std::pair<int64_t, double>> sblog;
     double last_wait_s = 0.0;            // wait_seq: the previous wait's length (its spin-near-the-end guess)
     DevScene scene{};
     DevScene* d_scene = nullptr;
@@ -988,7 +991,13 @@ int64_t check_edges_host(rp_ctx* c, const double* qa, const double* qb, int64_t 
         return e && *e ? std::max(0, std::atoi(e)) : 0;
     }();
     kmax += kpad;
+    // (profiling on: rp_last_kernel_ms = the edge launch, the planner's launch path)
+    if (c->profiling) HIP_TRY(hipEventRecord(c->ev0, c->stream));
     launch_edges(c, c->ea.p, c->eb.p, c->end_nd.p, n, kmax, 0, c->eval.p, 1, nullptr, c->stream);
+    if (c->profiling) {
+        HIP_TRY(hipEventRecord(c->ev1, c->stream));
+        c->timed = true;
+    }
     HIP_TRY(hipMemcpyAsync(out, c->eval.p, n, hipMemcpyDeviceToHost, c->stream));
     return read_counter(c);
 }
@@ -1981,6 +1990,13 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         };
         for (int64_t done = 0; done < B && !solved && !stop; done += C, C = next_chunk(C, B - done)) {
             C = std::min(C, B - done);
+            // host wall time of this sub-batch (enqueue -> its status read)
+            struct SbTimer {
+                std::vector<std::pair<int64_t, double>>* log;
+                int64_t n;
+                double t0;
+                ~SbTimer() { log->emplace_back(n, 1e3 * (now_s() - t0)); }
+            } sb_timer{&c->sblog, C, now_s()};
             const uint64_t g0 = gbase + (uint64_t)done;
             const int64_t An = A.n, Bn = Bt.n;   // append positions of this sub-batch
             const bool first_launch = iter == 0 && done == 0;
@@ -2532,10 +2548,19 @@ static void box_record_yaw(const float center[3], const float half[3], float yaw
     std::memcpy(&r[15], &orig, 4);
 }
 
+// Upright: |x|, |y| <= 1e-7 |q| (a rotation about z to within simulation noise: the
+// quaternions a running simulation returns are never exactly upright, and an exact
+// test sent every live block to the tilted record). The oracle's
+// ro_scene_set_rot applies the same rule.
+static inline bool quat_upright(double x, double y, double n2) {
+    const double t = 1e-7 * std::sqrt(n2);
+    return std::fabs(x) <= t && std::fabs(y) <= t;
+}
+
 // Record of a box with orientation quaternion q = (w, x, y, z) (any norm > 0):
-// x == y == 0 (a rotation about z only, what rp_set_scene_poses always read as the
-// box's yaw) gives the upright record of yaw = atan2(2(wz + xy), 1 - 2(y^2 + z^2))
-// (double, rounded to float). Otherwise the box is tilted: q normalised and turned
+// an upright q (quat_upright; a q of norm other than 1 normalised first) gives the
+// upright record of yaw = atan2(2(wz + xy), 1 - 2(y^2 + z^2)) (double, rounded to
+// float). Otherwise the box is tilted: q normalised and turned
 // into R (world = R * box) in double, R^T rows rounded to float once into rt, world
 // AABB half extents ext_k = |R_k0| h0 + |R_k1| h1 + |R_k2| h2 + 1e-6 m in float (the
 // margin makes the box AABB contain the float-rounded box). The oracle
@@ -2543,8 +2568,13 @@ static void box_record_yaw(const float center[3], const float half[3], float yaw
 static bool box_record_quat(const float center[3], const float half[3], const double q[4], int32_t orig, float* r,
                             float* rt) {
     double w = q[0], x = q[1], y = q[2], z = q[3];
-    if (x == 0.0 && y == 0.0) {
-        if (w == 0.0 && z == 0.0) return false;
+    const double n2 = w * w + x * x + y * y + z * z;
+    if (n2 == 0.0) return false;
+    if (quat_upright(x, y, n2)) {   // (round 6: to simulation noise, any norm)
+        if (std::fabs(n2 - 1.0) > 1e-12) {
+            const double nr = std::sqrt(n2);
+            w /= nr; x /= nr; y /= nr; z /= nr;
+        }
         box_record_yaw(center, half, (float)std::atan2(2.0 * (w * z + x * y), 1.0 - 2.0 * (y * y + z * z)), orig, r);
         return true;
     }
@@ -2903,6 +2933,7 @@ static int plan_entry(rp_ctx* c, const double start[RP_NQ], const double goal[RP
     }
     flush_scene(c, c->stream);
     c->prof = rp_profile{};
+    c->sblog.clear();
     c->pused = 0;
     c->in_plan = true;
     c->lb_used = false;
@@ -3044,6 +3075,55 @@ int rp_plan_wait(rp_ctx* c) {
     return rc;
 }
 
+// Many queries in flight on n_ctx contexts (include/rbe_planner.h): the host side
+// of a query here is a scene upload record, one post and one wait, in C++, so the
+// contexts' GPU work overlaps instead of waiting on a per-query host loop
+int rp_plan_many(rp_ctx* const* ctxs, int32_t n_ctx, const rp_query* queries, int32_t n, const double lo[RP_NQ],
+                 const double hi[RP_NQ], double* path_out, int32_t path_cap, int32_t* n_out, int32_t* status_out,
+                 int32_t* rc_out) {
+    if (!ctxs || n_ctx < 1 || n < 0 || (n > 0 && (!queries || !lo || !hi || !n_out || !status_out || !rc_out)) ||
+        path_cap < 0 || (path_cap > 0 && n > 0 && !path_out))
+        return RP_ERR_ARG;
+    for (int k = 0; k < n_ctx; ++k) {
+        if (!ctxs[k]) return RP_ERR_ARG;
+        for (int m = 0; m < k; ++m)
+            if (ctxs[m] == ctxs[k]) return RP_ERR_ARG;
+        RP_IDLE(ctxs[k]);
+    }
+    constexpr uint32_t EXEMPT = (1u << RP_HAND) | (1u << RP_LEFT_FINGER) | (1u << RP_RIGHT_FINGER);
+    std::vector<int32_t> pending((size_t)n_ctx, -1);
+    int first = RP_OK;
+    auto finish = [&](int k) {
+        const int32_t i = pending[k];
+        if (i < 0) return;
+        pending[k] = -1;
+        rc_out[i] = rp_plan_wait(ctxs[k]);
+        if (rc_out[i] < 0 && first == RP_OK) first = rc_out[i];
+    };
+    for (int32_t i = 0; i < n; ++i) {
+        const int k = i % n_ctx;
+        finish(k);
+        rp_ctx* c = ctxs[k];
+        const rp_query& q = queries[i];
+        int rc = rp_set_scene(c, q.boxes, q.n_boxes, q.plane_z, q.base_pos);
+        if (rc == RP_OK) rc = rp_set_attached(c, q.attached_box, q.attached_box >= 0 ? EXEMPT : 0u);
+        if (rc == RP_OK)
+            rc = rp_plan_async(c, q.start, q.goal, lo, hi, &q.params,
+                               path_out ? path_out + (int64_t)i * path_cap * NQ : nullptr, path_cap, n_out + i,
+                               status_out + i);
+        if (rc < 0) {   // (this query did not start; the others go on)
+            n_out[i] = 0;
+            status_out[i] = RP_STATUS_NONE;
+            rc_out[i] = rc;
+            if (first == RP_OK) first = rc;
+            continue;
+        }
+        pending[k] = i;
+    }
+    for (int k = 0; k < n_ctx; ++k) finish(k);
+    return first;
+}
+
 int rp_reserve(rp_ctx* c, int64_t batch, int64_t tree_capacity) {
     if (!c || batch < 0 || tree_capacity < 0) return RP_ERR_ARG;
     RP_IDLE(c);
@@ -3069,6 +3149,20 @@ int rp_reserve(rp_ctx* c, int64_t batch, int64_t tree_capacity) {
     c->ecnt.ensure(ne);   // (the coarse-first passes: per-edge counts, pass 1's work list)
     c->eunits.ensure((size_t)blocks_for(ne, VBLOCK) * kmax);
     c->enunits.ensure(1);
+    // the look-back accepts' per-block words (zeroed when made) and error flag, the
+    // connect accept's scan: a first large sub-batch used to allocate them (hipMalloc
+    // synchronises the device: 20-55 us GPU gaps in a kernel trace of the first plan)
+    const int64_t lbn = (B + (int64_t)LB_THREADS * LB_ITEMS - 1) / ((int64_t)LB_THREADS * LB_ITEMS);
+    if ((int64_t)c->lbst.n < lbn) {
+        c->lbst.ensure((size_t)lbn);
+        HIP_TRY(hipMemsetAsync(c->lbst.p, 0, sizeof(unsigned long long) * c->lbst.n, c->stream));
+    }
+    if (!c->lberr.p) {
+        c->lberr.ensure(1);
+        HIP_TRY(hipMemsetAsync(c->lberr.p, 0, sizeof(int), c->stream));
+    }
+    c->incl.ensure((size_t)B);
+    HIP_TRY(hipStreamSynchronize(c->stream));
     size_t b32 = 0, b64 = 0;
     HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b32, (const int32_t*)nullptr, (int32_t*)nullptr, (int)ne,
                                              c->stream));
@@ -3365,6 +3459,19 @@ int rp_debug_waits(rp_ctx* c, double* out, int32_t n) {
     return RP_OK;
 }
 
+// diagnostic (bench.py scaling_model): the last plan's sub-batches as (samples, host
+// wall ms from the first enqueue to the status read) pairs, at most n / 2 of them;
+// returns how many the plan ran
+int rp_debug_subbatches(rp_ctx* c, double* out, int32_t n) {
+    if (!c || !out || n < 0) return RP_ERR_ARG;
+    const int m = (int)c->sblog.size();
+    for (int i = 0; i < m && 2 * i + 1 < n; ++i) {
+        out[2 * i] = (double)c->sblog[i].first;
+        out[2 * i + 1] = c->sblog[i].second;
+    }
+    return m;
+}
+
 // diagnostic: the RBE_EDGE_STATS counters since the last call (k_edge_stats), then reset
 int rp_debug_edges(rp_ctx* c, double* out, int32_t n) {
     if (!c || !out || n < 5) return RP_ERR_ARG;
@@ -3483,14 +3590,21 @@ int rp_selftest_nn(rp_ctx* c, const double* q, int64_t n, const double* tree, in
         dimg.ensure((size_t)(T + NNM_PAD) * 4);
         hipLaunchKernelGGL(k_nn_image, dim3(blocks_for((T + NNM_PAD) * 4, 256)), dim3(256), 0, c->stream, (const double*)dt.p,
                            (int64_t)0, T, c->nnm, dimg.p);
+        // (profiling on: rp_last_kernel_ms = the search, pilot to reduce; the node
+        // images are made once per node and plan in rp_plan, so they are left out)
+        if (c->profiling) HIP_TRY(hipEventRecord(c->ev0, c->stream));
         if (mode >= 8) launch_nn_mfma<8>(c, dq.p, n, Q, dt.p, dimg.p, T);
         else if (mode >= 4) launch_nn_mfma<4>(c, dq.p, n, Q, dt.p, dimg.p, T);
         else if (mode >= 2) launch_nn_mfma<2>(c, dq.p, n, Q, dt.p, dimg.p, T);
         else launch_nn_mfma<1>(c, dq.p, n, Q, dt.p, dimg.p, T);
-        HIP_TRY(hipStreamSynchronize(c->stream));
-        dimg.release();
         hipLaunchKernelGGL(k_nn_reduce, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream,
                            (const DI2*)c->nn_part.p, n, c->nn_S, (const int*)nullptr, (int64_t)0, dout.p);
+        if (c->profiling) {
+            HIP_TRY(hipEventRecord(c->ev1, c->stream));
+            c->timed = true;
+        }
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        dimg.release();
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipMemcpyAsync(out, dout.p, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));

@@ -20,7 +20,7 @@ LIB_PATH = os.environ.get("RBE_LIB_PATH") or os.path.join(_HERE, LIB_NAME)
 EXPORTS = ("rp_version", "rp_abi_version", "rp_default_robot", "rp_create", "rp_destroy", "rp_set_scene", "rp_set_scene_rot", "rp_set_attached",
            "rp_set_scene_poses",
            "rp_check_states", "rp_check_states_device", "rp_check_edges", "rp_check_edges_device",
-           "rp_state_contacts", "rp_plan", "rp_plan_async", "rp_plan_wait", "rp_reserve", "rp_group_init", "rp_group_init_shm", "rp_group_rccl_unique_id", "rp_group_init_rccl",
+           "rp_state_contacts", "rp_plan", "rp_plan_async", "rp_plan_wait", "rp_plan_many", "rp_reserve", "rp_group_init", "rp_group_init_shm", "rp_group_rccl_unique_id", "rp_group_init_rccl",
            "rp_group_init_local",
            "rp_get_stats", "rp_last_error", "rp_last_kernel_ms", "rp_selftest_f64", "rp_ik", "rp_set_profiling",
            "rp_get_profile", "rp_get_stream", "rp_group_info", "rp_selftest_nn")
@@ -196,6 +196,15 @@ class Context:
         v = C.c_double()
         self._check(load().rp_last_kernel_ms(self._h, C.byref(v)), "rp_last_kernel_ms")
         return v.value
+
+    def sub_batches(self, cap=1024):
+        """The last plan's sub-batches: [(samples, host wall ms)] (rp_debug_subbatches,
+        a diagnostic entry: bench.py's scaling model)."""
+        buf = (C.c_double * (2 * cap))()
+        m = load().rp_debug_subbatches(self._h, buf, 2 * cap)
+        if m < 0:
+            raise NativeError(f"rp_debug_subbatches failed ({m})")
+        return [(int(buf[2 * i]), float(buf[2 * i + 1])) for i in range(min(m, cap))]
 
     def check_edges(self, qa, qb, resolution):
         qa = np.ascontiguousarray(qa, dtype=np.float64).reshape(-1, _abi.NQ)
@@ -384,3 +393,74 @@ class Context:
         """Back to single-rank planning."""
         self._check(load().rp_group_init(self._h, 0, 1, None, None), "rp_group_init")
         self._cb = None
+
+
+def make_queries(jobs):
+    """rp_query records of plan_pipelined's jobs (dicts with scene (scenes.Scene,
+    upright boxes), attached, start, goal, params): (array, keep-alive list)."""
+    qs = (_abi.Query * max(1, len(jobs)))()
+    keep = []
+    for i, job in enumerate(jobs):
+        sc = job["scene"]
+        kind, arr, n = _abi.scene_boxes(sc.boxes)
+        if kind != "yaw":
+            raise ValueError("rp_plan_many takes upright boxes (rp_set_scene records); plan tilted scenes one by one")
+        keep.append(arr)
+        q = qs[i]
+        q.boxes = C.cast(arr, C.POINTER(_abi.Box)) if n else None
+        q.n_boxes = n
+        q.plane_z = float(sc.plane_z)
+        q.base_pos[:] = [float(v) for v in sc.base]
+        q.attached_box = int(job.get("attached", -1))
+        q.start[:] = [float(v) for v in job["start"]]
+        q.goal[:] = [float(v) for v in job["goal"]]
+        q.params = job["params"]
+    return qs, keep
+
+
+def plan_many(ctxs, queries, n, lo, hi, path_cap=4096):
+    """rp_plan_many over prepared rp_query records (make_queries): [(path, status,
+    stats)] in query order; raises NativeError (after every query ran) if any failed."""
+    k = len(ctxs)
+    arr = (C.c_void_p * k)(*[c._h.value for c in ctxs])
+    out = np.empty((max(n, 1), path_cap, _abi.NQ), dtype=np.float64)
+    n_out = np.zeros(max(n, 1), dtype=np.int32)
+    st = np.zeros(max(n, 1), dtype=np.int32)
+    rcs = np.zeros(max(n, 1), dtype=np.int32)
+    lo = np.ascontiguousarray(lo, dtype=np.float64)
+    hi = np.ascontiguousarray(hi, dtype=np.float64)
+    rc = load().rp_plan_many(arr, k, queries, int(n), _ptr(lo), _ptr(hi), _ptr(out), int(path_cap), _ptr(n_out),
+                             _ptr(st), _ptr(rcs))
+    if rc < 0:
+        bad = [i for i in range(n) if rcs[i] < 0]
+        raise NativeError(f"rp_plan_many failed ({rc}) at queries {bad[:8]}: "
+                          f"{load().rp_last_error(ctxs[bad[0] % k]._h if bad else None).decode()}")
+    # (each context holds the stats of its last query only: per-query stats are those)
+    last = {}
+    for i in range(n):
+        last[i % k] = i
+    res = []
+    for i in range(n):
+        s = ctxs[i % k].stats() if last[i % k] == i else None
+        res.append((out[i, :n_out[i]].copy(), int(st[i]), s))
+    return res
+
+
+def plan_pipelined(ctxs, jobs, path_cap=4096):
+    """Independent queries kept in flight on several contexts of one device (BASELINE
+    config 3: goal3's ~20 RRT queries "pipelined"): job i runs on ctxs[i % len(ctxs)]
+    through its planner thread, after that context's previous job, all driven by one
+    library call (rp_plan_many; the host side of a query is C++, not this loop). Each
+    context has its own HIP stream, so one query's dependent small kernels overlap the
+    others'. A job is a dict with scene (scenes.Scene), attached, start, goal, params;
+    lo / hi are the jobs' common bounds (jobs[0]["lo"] / ["hi"]). Returns [(path,
+    status, stats)] in job order (stats: that context's stats when the job was its last,
+    else None); every path and status is the one ctx.plan gives for that job alone."""
+    if not ctxs:
+        raise ValueError("plan_pipelined needs a context")
+    if not jobs:
+        return []
+    qs, keep = make_queries(jobs)
+    res = plan_many(ctxs, qs, len(jobs), jobs[0]["lo"], jobs[0]["hi"], path_cap)
+    del keep
+    return res

@@ -191,18 +191,31 @@ def _floats(x, n):
     return [float(a) for a in _to_np(x)[:n]]
 
 
-def yaw_of_quat(q):
-    """Rotation about world z of a (w, x, y, z) quaternion whose x = y = 0."""
+def quat_upright(q):
+    """An upright (w, x, y, z) quaternion: |x|, |y| <= 1e-7 |q|, a rotation about z to
+    within simulation noise (rp_lib.hip quat_upright, the oracle's rule)."""
     w, x, y, z = (float(v) for v in q)
+    t = 1e-7 * math.sqrt(w * w + x * x + y * y + z * z)
+    return abs(x) <= t and abs(y) <= t
+
+
+def yaw_of_quat(q):
+    """Rotation about world z of an upright (w, x, y, z) quaternion (normalised first
+    when its norm is not 1, as rp_set_scene_poses does)."""
+    w, x, y, z = (float(v) for v in q)
+    n2 = w * w + x * x + y * y + z * z
+    if abs(n2 - 1.0) > 1e-12:
+        n = math.sqrt(n2)
+        w, x, y, z = w / n, x / n, y / n, z / n
     return math.atan2(2.0 * (w * z + x * y), 1.0 - 2.0 * (y * y + z * z))
 
 
 def rot_of_quat(q):
     """A box orientation from a (w, x, y, z) quaternion: its yaw when the box is
-    upright (x = y = 0: exactly the record rp_set_scene_poses makes), else the
+    upright (quat_upright: exactly the record rp_set_scene_poses makes), else the
     quaternion itself (a tilted box; rp_set_scene_rot)."""
     w, x, y, z = (float(v) for v in q)
-    if x == 0.0 and y == 0.0:
+    if quat_upright((w, x, y, z)):
         return yaw_of_quat((w, x, y, z))
     return (w, x, y, z)
 

@@ -35,13 +35,16 @@ def test_struct_layouts_match_header(tmp_path):
                    "int main(void){printf(\"%zu %zu %zu %zu %zu %zu %zu %zu %zu %zu\\n\", sizeof(rp_capsule), sizeof(rp_box),"
                    " sizeof(rp_plan_params), sizeof(rp_stats), sizeof(rp_robot_desc),"
                    " offsetof(rp_plan_params, n_waypoints), offsetof(rp_robot_desc, self_pairs),"
-                   " sizeof(rp_ik_params), offsetof(rp_ik_params, damping), sizeof(rp_profile));return 0;}")
+                   " sizeof(rp_ik_params), offsetof(rp_ik_params, damping), sizeof(rp_profile));"
+                   "printf(\"%zu %zu %zu\\n\", sizeof(rp_query), offsetof(rp_query, start), offsetof(rp_query, params));"
+                   "return 0;}")
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
     want = [C.sizeof(_abi.Capsule), C.sizeof(_abi.Box), C.sizeof(_abi.PlanParams), C.sizeof(_abi.Stats),
             C.sizeof(_abi.RobotDesc), _abi.PlanParams.n_waypoints.offset, _abi.RobotDesc.self_pairs.offset,
-            C.sizeof(_abi.IkParams), _abi.IkParams.damping.offset, C.sizeof(_abi.Profile)]
+            C.sizeof(_abi.IkParams), _abi.IkParams.damping.offset, C.sizeof(_abi.Profile),
+            C.sizeof(_abi.Query), _abi.Query.start.offset, _abi.Query.params.offset]
     assert got == want
 
 

@@ -168,3 +168,29 @@ def test_plan_path_through_a_collapsed_scene(oracle_lib):
         assert np.array_equal(got, ref.astype(np.float32))
     finally:
         planning.configure(seed=0, straight_first=True)
+
+
+@pytest.mark.parametrize("kind", ["noisy", "scaled", "scaled_tilted"])
+def test_near_upright_and_scaled_quaternions_gpu(gpu_ctx, oracle_lib, kind):
+    """|x|, |y| <= 1e-7 |q| is upright (the yaw record) and a scaled
+    quaternion is its unit one, in rp_set_scene_rot as in the oracle: flags bit-exact,
+    and equal to the scene given as yaws where the boxes are upright."""
+    sc = scenes.goal3_tallest()
+    yaws = [0.3, -1.2, 2.5, 0.0, 0.7, -3.0, 1.1, -0.4, 0.9, 2.0]
+    unit = [T.quat_axis_angle((0, 0, 1), np.degrees(y)) for y in yaws]
+    if kind == "noisy":
+        quats = [np.array([w, 3e-9, -2e-9, z]) for w, _, _, z in unit]
+    elif kind == "scaled":
+        quats = [2.5 * np.asarray(q) for q in unit]
+    else:
+        quats = [0.4 * np.asarray(T.quat_axis_angle((1, 1, 0), 25.0 + 5 * i)) for i in range(len(unit))]
+    boxes = [(c, h, qq) for (c, h, _), qq in zip(sc.boxes, quats)]
+    tsc = scenes.Scene(boxes=boxes, plane_z=sc.plane_z, base=sc.base)
+    o = _pair(gpu_ctx, oracle_lib, tsc)
+    q = _states(65536 + 100, 77, tsc)
+    g = gpu_ctx.check_states(q)
+    assert np.array_equal(g, o.check_states(q))
+    if kind != "scaled_tilted":
+        y = oracle_lib.OracleScene()
+        y.set_scene([(c, h, yy) for (c, h, _), yy in zip(sc.boxes, yaws)], sc.plane_z, sc.base)
+        assert np.array_equal(g, y.check_states(q))

@@ -40,6 +40,38 @@ def test_upright_quaternion_is_the_yaw_record(oracle_lib):
     assert 0 < fa.sum() < len(fa)
 
 
+def test_near_upright_and_scaled_quaternions(oracle_lib):
+    """a simulation's quaternions are never exactly upright and need not be
+    unit. |x|, |y| <= 1e-7 |q| is upright (the yaw record, not the tilted one), and a
+    quaternion scaled by any factor gives the record of the unit one (upright and
+    tilted), in the oracle and in the ingestion's rot_of_quat alike."""
+    sc = scenes.goal1_scattered(seed=3)
+    yaws = [0.3, -1.2, 2.5, 0.0, 0.7, -3.0]
+    unit = [T.quat_axis_angle((0, 0, 1), np.degrees(y)) for y in yaws]
+    noisy = [np.array([w, 3e-9, -2e-9, z]) for w, _, _, z in unit]
+    scaled = [2.5 * np.asarray(q) for q in unit]
+    q = np.concatenate([_states(20000, 11), _near(model.SAFE_HOME, 5000, 12, 0.6)])
+    ref = oracle_lib.OracleScene()
+    ref.set_scene([(c, h, y) for (c, h, _), y in zip(sc.boxes, yaws)], sc.plane_z, sc.base)
+    f_ref = ref.check_states(q)
+    for quats in (noisy, scaled):
+        o = oracle_lib.OracleScene()
+        o.set_scene([(c, h, qq) for (c, h, _), qq in zip(sc.boxes, quats)], sc.plane_z, sc.base)
+        assert np.array_equal(o.check_states(q), f_ref)
+        for qq, y in zip(quats, yaws):
+            r = scenes.rot_of_quat(qq)
+            assert isinstance(r, float) and abs(r - y) < 1e-12
+    tilt = T.quat_axis_angle((1, 1, 0), 25.0)
+    boxes = list(sc.boxes)
+    a, b = oracle_lib.OracleScene(), oracle_lib.OracleScene()
+    a.set_scene([(c, h, tilt) if i == 2 else (c, h, y) for i, ((c, h, _), y) in enumerate(zip(boxes, yaws))],
+                sc.plane_z, sc.base)
+    b.set_scene([(c, h, 3.0 * np.asarray(tilt)) if i == 2 else (c, h, y)
+                 for i, ((c, h, _), y) in enumerate(zip(boxes, yaws))], sc.plane_z, sc.base)
+    fa = a.check_states(q)
+    assert np.array_equal(fa, b.check_states(q))
+
+
 def test_rolled_box_is_the_axis_swapped_box(oracle_lib):
     """A (0.02, 0.04, 0.06) box rolled 90 degrees about x occupies what an upright
     (0.02, 0.06, 0.04) box does: the quaternion -> rotation convention and the box

@@ -735,6 +735,10 @@ def main():
                                                                else (
                 ("C4_pentagon", load_workload("goal4_pentagon_10box"), C4_BATCH, C4_BATCH, 0, 0),
                 ("C4_pentagon_sched", load_workload("goal4_pentagon_10box"), C4_BATCH, 0, 0, 0),
+                # the completed pentagon: deep grasps between placed blocks, no valid
+                # straight edge on any query (tests/golden/make_workloads.py)
+                ("C4_ring", load_workload("goal4_pentagon_ring"), C4_BATCH, C4_BATCH, 0, 0),
+                ("C4_ring_sched", load_workload("goal4_pentagon_ring"), C4_BATCH, 0, 0, 0),
                 ("C5_clutter64", load_workload("clutter64"), C5_BATCH, C5_BATCH, 0, 0),
                 ("C5_well", wellx, C5_BATCH, C5_BATCH, 1, 8),
                 ("C5_well_sched", wellx, C5_BATCH, 0, 1, 8))):
@@ -834,6 +838,7 @@ def main():
                                          ("C3_rrt", "goal3_tallest_10box", False, 1),
                                          ("C2_rrt", "single_pick_place_5box", False, 10),
                                          ("C4_rrt", "goal4_pentagon_10box", False, 1),
+                                         ("C4_ring", "goal4_pentagon_ring", True, 1),
                                          ("C5_clutter64_rrt", "clutter64", False, 1),
                                          ("C5_well_rrt", "clutter64_well", False, 1)):
                 w = load_workload(wname)

@@ -152,6 +152,7 @@ struct rp_ctx {
     // the last plan's sub-batches (rp_debug_subbatches, bench.py scaling_model):
     // (samples, host wall ms from the first enqueue to the status read) each
     std::vector<std::pair<int64_t, double>> sblog;
+    bool inject_fail = false;            // rp_debug_fail_next: the next plan throws at its start
     double last_wait_s = 0.0;            // wait_seq: the previous wait's length (its spin-near-the-end guess)
     DevScene scene{};
     DevScene* d_scene = nullptr;
@@ -2934,11 +2935,14 @@ static int plan_entry(rp_ctx* c, const double start[RP_NQ], const double goal[RP
     flush_scene(c, c->stream);
     c->prof = rp_profile{};
     c->sblog.clear();
+    const bool inject = c->inject_fail;
+    c->inject_fail = false;
     c->pused = 0;
     c->in_plan = true;
     c->lb_used = false;
     int rc;
     try {
+        if (inject) throw HipError{"injected fault (rp_debug_fail_next)"};
         rc = plan_impl(c, start, goal, lo, hi, params, path_out, path_cap, n_out, status_out);
         if (c->lb_used && read_scalar(c, c->lberr.p) != 0) {   // (large plans only: one read)
             // the flag is sticky on the device: clear it, so that this plan fails and the
@@ -3481,6 +3485,15 @@ int rp_debug_edges(rp_ctx* c, double* out, int32_t n) {
         if (hipMemset(c->estats.p, 0, sizeof h) != hipSuccess) return RP_ERR_DEVICE;
     }
     for (int k = 0; k < 5; ++k) out[k] = (double)h[k];
+    return RP_OK;
+}
+
+// fault injection (tests): the context's next plan fails at its start as a device
+// error would (a rank of a group then leaves its peers and the group broken)
+int rp_debug_fail_next(rp_ctx* c) {
+    if (!c) return RP_ERR_ARG;
+    RP_IDLE(c);
+    c->inject_fail = true;
     return RP_OK;
 }
 

@@ -9,6 +9,8 @@ Cases (RRT-Connect forced, batch_min = batch, 150 waypoints, simplify level 1):
 
   C2  single_pick_place_5box, both queries, 65,536-sample iterations, seeds 0-2
   C4  goal4_pentagon_10box, every 5th query, 262,144-sample iterations
+  C4  goal4_pentagon_ring (the completed pentagon, deep grasps between placed
+      blocks: no straight edge), queries 0 / 3 / 5 / 8, 262,144-sample iterations
   C5  clutter64, 131,072-sample iterations
   C5  clutter64_well (goal inside a covered well), 131,072-sample iterations,
       max 8 iterations (= the 2^20-sample budget): seeds 2, 3, 4 solve in 6, 7
@@ -43,6 +45,8 @@ def cases():
             out.append((f"C2_q{qi}_s{seed}", "single_pick_place_5box", qi, seed, 65536, 0))
     for qi in range(0, 25, 5):
         out.append((f"C4_q{qi}", "goal4_pentagon_10box", qi, qi, 262144, 0))
+    for qi in (0, 3, 5, 8):   # the completed ring: no valid straight edge (make_workloads.py)
+        out.append((f"C4_ring_q{qi}", "goal4_pentagon_ring", qi, qi, 262144, 0))
     out.append(("C5_clutter64", "clutter64", 0, 0, 131072, 0))
     for seed in (2, 3, 4, 0):
         out.append((f"C5_well_s{seed}", "clutter64_well", 0, seed, 131072, 8))

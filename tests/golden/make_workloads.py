@@ -188,6 +188,42 @@ def workload_goal4():
     return {"name": "goal4_pentagon_10box", "config": 3, "queries": w.queries}
 
 
+def pentagon_ring_scene():
+    """goal4_task1's final structure: the 5 base blocks in their yawed slots and the 5
+    top blocks bridging them at 36 degree offsets (code/goal4_task1.py:66-126)."""
+    sc = scenes.goal4_pentagon()
+    base_slots, top_slots = scenes.pentagon_slots()
+    for i, (x, y, rot) in enumerate(base_slots):
+        sc.move(f"b{i + 1}", (x, y, 0.02), math.radians(rot))
+    for i, (x, y, rot) in enumerate(top_slots):
+        sc.move(f"b{i + 6}", (x, y, 0.06), math.radians(rot))
+    return sc
+
+
+def workload_goal4_ring():
+    """C4 without a straight edge: the completed pentagon (all 10 blocks placed), the
+    hand moving between deep grasps of two top blocks (fingers open around a placed
+    block, 1.5 cm below the grasp height, between its placed neighbours) two and three
+    slots apart, around the ring: every start -> goal straight edge collides with the
+    blocks in between (the 25 goal4_pentagon queries all have a valid straight edge).
+    10 queries."""
+    w = World(pentagon_ring_scene(), model.SAFE_HOME)
+    _, top_slots = scenes.pentagon_slots()
+    deep = []
+    for x, y, rot in top_slots:
+        quat = euler_quat(0.0, math.pi, math.radians(rot))
+        deep.append(w.ik(np.array([x, y, 0.06 + GRASP_OFFSET - 0.015]), quat, OPEN))
+    res = 0.01 * float(np.linalg.norm(HI - LO))
+    for step in (2, 3):
+        for i in range(5):
+            j = (i + step) % 5
+            w.q = deep[i].copy()
+            if w.orc.check_edges(deep[i][None], deep[j][None], res)[0]:
+                raise RuntimeError(f"ring query {i} -> {j} has a valid straight edge")
+            w.query(f"ring: deep grasp top{i + 1} -> top{j + 1}", deep[j])
+    return {"name": "goal4_pentagon_ring", "config": 3, "queries": w.queries}
+
+
 def workload_clutter():
     """C5: 64 floating boxes (seed 0x64B0); start = safe_home turned by +1 rad at
     joint 1, goal mirrored (q1 -> -q1)."""
@@ -264,7 +300,7 @@ def main():
     os.makedirs(OUT, exist_ok=True)
     only = set(sys.argv[1:])
     for fn in (workload_goal1, workload_single, workload_goal3, workload_goal4, workload_clutter,
-               workload_clutter_well):
+               workload_clutter_well, workload_goal4_ring):
         if only and fn.__name__ not in only:
             continue
         wl = fn()

@@ -100,3 +100,49 @@ def test_group_init_local_rejects_rccl_on_one_device():
     finally:
         b.close()
         a.close()
+
+
+def test_failed_grouped_plan_reforms_the_group():
+    """one failing rank must not disable the planner. Rank 1's next plan is
+    made to fail (rp_debug_fail_next); rank 0 stops at its first exchange at once (the
+    failed rank publishes a broken sequence word) instead of waiting out the watchdog;
+    plan_path returns [] as the reference does on failure, re-forms the rank group, and
+    the next plan_path returns the golden plan."""
+    import time
+    m = META["C5_well_s3"]
+    q = json.load(open(os.path.join(GOLD, "workloads", m["workload"] + ".json")))["queries"][m["query"]]
+    sc = scenes.Scene.from_json(q["scene"])
+    sim = M.Scene(sc.boxes)
+    planning.configure(seed=m["seed"], batch=m["batch"], batch_min=m["batch"], straight_first=False,
+                       tree_capacity=1 << 23, devices=(0, 0))
+    try:
+        pl = planning.PlannerInterface(sim.robot, sim)
+        kw = dict(qpos_goal=np.array(q["goal"]), qpos_start=np.array(q["start"]), num_waypoints=150, timeout=600.0)
+        first = torch.stack(pl.plan_path(**kw)).numpy()   # (the golden seed: configure reset the count)
+        assert pl.last_status == m["status"]
+        assert native.load().rp_debug_fail_next(pl._ctxs[1]._h) == 0
+        t0 = time.perf_counter()
+        assert pl.plan_path(**kw) == []
+        assert time.perf_counter() - t0 < 10.0   # (not the 120 s watchdog)
+        planning.configure(seed=m["seed"])
+        again = pl.plan_path(**kw)
+        assert len(again) == 150 and np.array_equal(torch.stack(again).numpy(), first)
+        assert [c.group_info()["world"] for c in pl._ctxs] == [2, 2]
+    finally:
+        planning.configure(seed=0, batch=4096, batch_min=0, straight_first=True, tree_capacity=0, devices=())
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (the RCCL transport between devices)")
+@pytest.mark.parametrize("name", ["C4_q10", "C5_well_s3"])
+def test_plan_path_on_distinct_devices_rccl(oracle_lib, name):
+    """the in-process RCCL group (rp_group_init_local over distinct GPUs,
+    ncclCommInitAll; the default when devices differ): plans complete without deadlock
+    and equal the one-context plan. Skipped on a one-GPU box."""
+    m = META[name]
+    q = json.load(open(os.path.join(GOLD, "workloads", m["workload"] + ".json")))["queries"][m["query"]]
+    devs = tuple(range(min(torch.cuda.device_count(), 4)))
+    got, st, s, ranks, ing, pl = _plan_path(devs, m, q)
+    assert all(r["transport"] == "rccl" and r["world"] == len(devs) for r in ranks), ranks
+    one, st1, s1, _, _, _ = _plan_path((0,), m, q)
+    assert st == st1 == m["status"] and np.array_equal(one, got)
+    assert (s1["start_tree_size"], s1["goal_tree_size"]) == (s["start_tree_size"], s["goal_tree_size"])

@@ -433,7 +433,7 @@ def test_hand_built_collision_cases(gpu_ctx, oracle_lib):
 
 
 @pytest.mark.parametrize("wl", ["goal1_scattered_6box", "goal3_tallest_10box", "goal4_pentagon_10box", "clutter64",
-                                "single_pick_place_5box"])
+                                "single_pick_place_5box", "goal4_pentagon_ring"])
 def test_plan_parity_rrt_forced_every_query(gpu_ctx, oracle_lib, wl):
     """RRT-Connect forced on every query of the workload (the C1 / C3 RRT-forced
     bench legs): queries whose straight edge holds finish inside the solving
@@ -453,7 +453,7 @@ def test_plan_parity_rrt_forced_every_query(gpu_ctx, oracle_lib, wl):
 
 
 @pytest.mark.parametrize("wl", ["goal1_scattered_6box", "goal3_tallest_10box", "goal4_pentagon_10box", "clutter64",
-                                "single_pick_place_5box"])
+                                "single_pick_place_5box", "goal4_pentagon_ring"])
 def test_plan_parity_straight_first(gpu_ctx, oracle_lib, wl):
     """Default plans (straight edge first): every query of the workload gives the
     oracle's status, path and iteration count (straight edge valid: no iteration;

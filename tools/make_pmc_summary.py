@@ -17,8 +17,12 @@ from rbe550_final_project_amd.build import validity_source_hash  # noqa: E402
 
 def main():
     fdir, wdir, n, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
-    f, meta, _, _ = load([fdir], "k_validity", n)
-    w, _, _, _ = load([wdir], "k_validity", n)
+    def one(d):   # the bench's headline instantiation (grid = the states per launch: one kernel)
+        res = load([d], "k_validity", n)
+        assert len(res) == 1, f"{len(res)} k_validity instantiations at grid {n}: {list(res)}"
+        return next(iter(res.values()))
+    f, meta, _, _ = one(fdir)
+    w, _, _, _ = one(wdir)
     read_b = 2.0 * f["FETCH_SIZE"] * 1024.0
     write_b = w["WRITE_SIZE"] * 1024.0
     d = {"kernel": "k_validity", "states_per_launch": n, "fetch_size_kb": f["FETCH_SIZE"],

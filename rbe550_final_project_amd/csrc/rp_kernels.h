@@ -1965,9 +1965,15 @@ __device__ void iteration_tail(int* status, int added, int64_t TA, int a_start, 
     RP_TSTAMP(0, 8);
 }
 
+// hio != nullptr (round 6, large single-rank sub-batches): the iteration's status words
+// go to the host mirror here and `pub_seq` is published, instead of by the
+// simplification step that used to follow every sub-batch (three launches that are
+// no-ops until a path exists); the host runs the simplification program only after the
+// sub-batch that solves. out = 0: this publication carries no output.
 __global__ void k_finalize(int* status, const int32_t* __restrict__ inclL, int64_t TA, int a_start,
                            const int32_t* __restrict__ Apar, const int32_t* __restrict__ Bpar,
-                           const int32_t* __restrict__ chain_end, PathArgs pa, PlanIO* io) {
+                           const int32_t* __restrict__ chain_end, PathArgs pa, PlanIO* io, PlanIO* hio = nullptr,
+                           int pub_seq = 0) {
     // the first REACHED target ends the iteration: the trees keep the appends up to it
     const int nacc = status[ST_NACC], fr = status[ST_FIRST];
     const bool solved = fr != 0x7fffffff;
@@ -1975,6 +1981,17 @@ __global__ void k_finalize(int* status, const int32_t* __restrict__ inclL, int64
     if (solved && rp_tid() == 0) status[ST_NACC] = fr + 1;
     iteration_tail(status, solved ? inclL[fr] : nacc > 0 ? inclL[nacc - 1] : 0, TA, a_start, Apar, Bpar, chain_end,
                    pa, io);
+    if (hio) {
+        __syncthreads();   // (lane 0's status words of the tail, before the copy)
+        const int t = rp_tid();
+        if (t < ST_WORDS) hio->status[t] = status[t];
+        if (t == ST_WORDS) {
+            hio->out = 0;
+            hio->n_out = 0;
+        }
+        publish_after_barrier();
+        if (t == 0) publish_seq(hio, pub_seq);
+    }
 }
 
 // single-block connect record + scan + append + iteration tail (targets <= FUSE_MAX)

@@ -1876,6 +1876,14 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
     // publishes `seq` (with the output record when it is the program's end)
     const std::vector<int> prog = simplify_program(level);
     const size_t tail_steps = level == 1 ? 2 : prog.size();   // run inside every single-rank iteration
+    // large two-phase sub-batches publish their status from k_finalize and skip the
+    // in-loop steps (RBE_EARLY_STATUS=0: the steps run in every sub-batch; A/B, tests);
+    // prog_ran: the last sub-batch ran them
+    const bool early_status = [] {
+        const char* e = std::getenv("RBE_EARLY_STATUS");
+        return !(e && *e && std::atoi(e) == 0);
+    }();
+    bool prog_ran = true;
     // raw paths longer than dev_max states are simplified host-driven (same
     // algorithm); RBE_SIMPLIFY_DEVICE_MAX lowers the limit (tests of that path)
     int dev_max = SPMAX;
@@ -1991,6 +1999,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         };
         for (int64_t done = 0; done < B && !solved && !stop; done += C, C = next_chunk(C, B - done)) {
             C = std::min(C, B - done);
+            prog_ran = true;   // (every sub-batch kind but the `early` two-phase one runs the steps)
             // host wall time of this sub-batch (enqueue -> its status read)
             struct SbTimer {
                 std::vector<std::pair<int64_t, double>>* log;
@@ -2187,6 +2196,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             // device-side counts, one host round trip per sub-batch; sub-batches
             // <= FUSE_MAX use the single-block accept kernels
             const bool fused = C <= FUSE_MAX;
+            const bool early = !fused && early_status && tail_steps < prog.size();
             const int seq = ++c->seq;
             if (fused) {
                 if (C <= FUSE_THREADS)
@@ -2249,7 +2259,7 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                                    An, c->chain_end.p, (const double*)(a_start ? c->efrom.p : c->eto.p), c->incl.p,
                                    c->lbst.p, c->lb_epoch, c->lberr.p);
                 hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, c->stream, status, c->incl.p, An, a_start,
-                                   A.par.p, Bt.par.p, c->chain_end.p, pa, io);
+                                   A.par.p, Bt.par.p, c->chain_end.p, pa, io, early ? h : nullptr, seq);
             } else {
                 hipLaunchKernelGGL(k_conn_record_len, dim3(blocks_for(C, 256)), dim3(256), 0, c->stream, c->yv.p,
                                    c->mv.p, c->gfail.p, (const int*)status, C, c->rec.p, c->Lv.p);
@@ -2259,11 +2269,15 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
                                    a_start, A.cand.p, status + ST_FIRST, c->chain_end.p, (const int*)status,
                                    (const double*)(a_start ? c->efrom.p : c->eto.p), (const int32_t*)c->mv.p);
                 hipLaunchKernelGGL(k_finalize, dim3(1), dim3(256), 0, c->stream, status, c->incl.p, An, a_start,
-                                   A.par.p, Bt.par.p, c->chain_end.p, pa, io);
+                                   A.par.p, Bt.par.p, c->chain_end.p, pa, io, early ? h : nullptr, seq);
             }
             // the first simplification steps run every sub-batch (empty unless this one
-            // solved), so a solving sub-batch needs no extra host round trip
-            run_program(0, tail_steps, seq, true);
+            // solved), so a solving sub-batch needs no extra host round trip — except in
+            // an `early` sub-batch, whose k_finalize published the status: a large
+            // sub-batch rarely solves, and its three no-op launches and the later status
+            // cost every other one ~15-25 us
+            prog_ran = !early;
+            if (prog_ran) run_program(0, tail_steps, seq, true);
             wait_seq(c, seq);
             if (!sg_known) {
                 if (const int code = endpoint_status(h->status[ST_SG])) return endpoint_fail(code);
@@ -2326,10 +2340,12 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         hipLaunchKernelGGL(k_path, dim3(1), dim3(64), 0, c->stream, pa, s_node, g_node, io);
         HIP_TRY(hipGetLastError());
     }
-    const size_t from = tail_ran ? tail_steps : 0;
-    if (from < prog.size() && !(tail_ran && h->out)) {
+    // (a solving sub-batch that skipped the in-loop steps: the whole program, its first
+    // step's OP_BEGIN / OP_PREP_REDUCE done by k_finalize's tail as in the loop)
+    const size_t from = tail_ran && prog_ran ? tail_steps : 0;
+    if (from < prog.size() && !(tail_ran && prog_ran && h->out)) {
         const int seq = ++c->seq;
-        run_program(from, prog.size(), seq, false);
+        run_program(from, prog.size(), seq, tail_ran && !prog_ran);
         wait_seq(c, seq);
     }
     const int n_raw = h->n_raw;

@@ -223,6 +223,20 @@ def test_lookback_accepts(gpu_ctx, name, lb, monkeypatch):
     _check(gpu_ctx, name)
 
 
+@pytest.mark.parametrize("name", ["C5_well_s0", "C5_well_s2", "C5_well_s3", "C5_well_s4", "C4_q5", "C4_ring_q3",
+                                  "C2_q0_s1", "C5_clutter64"])
+@pytest.mark.parametrize("early", ["0", "1"])
+@pytest.mark.parametrize("lb", ["0", "1"])
+def test_early_status_publication(gpu_ctx, name, early, lb, monkeypatch):
+    """Large single-rank sub-batches publish their status from k_finalize and skip the
+    in-loop simplification steps (RBE_EARLY_STATUS); the sub-batch that solves then
+    runs the whole program after the loop. Same plans, statuses and trees, with the
+    look-back and the scan accepts alike (the approximate C5_well_s0 case included)."""
+    monkeypatch.setenv("RBE_EARLY_STATUS", early)
+    monkeypatch.setenv("RBE_ACCEPT_LB", lb)
+    _check(gpu_ctx, name)
+
+
 def test_lookback_error_flag_is_not_sticky(gpu_ctx):
     """the look-back accepts' poll-budget flag lives on the device. A plan
     that finds it raised fails (NativeError) and clears it, so the context's next

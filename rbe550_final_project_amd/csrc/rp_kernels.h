@@ -94,6 +94,31 @@ __global__ __launch_bounds__(VTHREADS, validity_waves(NCL, BF)) void k_validity(
     flags[i] = state_collides<NCL, BF>(qq, sc, wq) ? 0 : 1;
 }
 
+// Axis-grid scenes (> 16 boxes): blocks of GL_WAVES one-wave queues that stage the
+// scene's grid fields in their LDS once (rp_math.h SceneGrid), so the per-lane broad
+// phase gathers (grid masks, candidate box records) are LDS reads instead of L2 round
+// trips. Same tests on the same values as k_validity<NCL_GRID>: same flags.
+constexpr int GL_WAVES = 4;
+template <bool BF>
+__global__ __launch_bounds__(64 * GL_WAVES, validity_waves(NCL_GRID, BF)) void k_validity_gl(
+    const float* __restrict__ q, int64_t n, uint8_t* __restrict__ flags, const DevScene* __restrict__ sc) {
+    __shared__ SceneGrid L;
+    __shared__ WaveQ wqs[GL_WAVES];
+    scene_grid_stage(sc, L, rp_tid(), 64 * GL_WAVES);
+    __syncthreads();
+    const int64_t i = (int64_t)rp_bid() * (64 * GL_WAVES) + rp_tid();
+    if (i >= n) return;
+    float qq[NQ];
+    struct F3 { float x, y, z; };
+    const F3* q3 = reinterpret_cast<const F3*>(q + i * NQ);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const F3 v = q3[k];
+        qq[3 * k] = v.x; qq[3 * k + 1] = v.y; qq[3 * k + 2] = v.z;
+    }
+    flags[i] = state_collides<NCL_GRID, BF, ROLE_ALL, SceneGrid>(qq, &L, wqs[rp_tid() >> 6]) ? 0 : 1;
+}
+
 // Mid-size launches (a few thousand to ~10^5 states: one wave per SIMD or fewer)
 // are as slow as one wave's dependency chain. NR waves share each group of 64
 // states, each walking the chain with a part of the tests (rp_math.h ROLE_*: NR = 2
@@ -225,14 +250,14 @@ __device__ __forceinline__ int edge_pass_slot(int i, int pk, int pass, int cnt) 
     return pass == 0 ? i * pk : i + 1 + i / (pk - 1);
 }
 
-template <int NCL, bool BF>
+template <int NCL, bool BF, class SC = DevScene>
 __device__ __forceinline__ bool edge_group_round(const double* __restrict__ from, const double* __restrict__ to,
                                                  const int* __restrict__ nd, int64_t n_edges, int mode,
                                                  uint8_t* valid, int group, int* gfail,
-                                                 unsigned long long* counter, const DevScene* __restrict__ sc,
+                                                 unsigned long long* counter, const SC* __restrict__ sc,
                                                  int64_t g, int r0, WaveQ& wq, int* mark, int pk = 1,
                                                  int pass = 0, const int* __restrict__ cntv = nullptr) {
-    const int lane = rp_tid();
+    const int lane = rp_tid() & 63;
     const int64_t e = g * VBLOCK + lane;
     int nde = -1, emode = mode, cnt = 0;
     if (e < n_edges) {
@@ -293,7 +318,7 @@ __device__ __forceinline__ bool edge_group_round(const double* __restrict__ from
         float qq[NQ];
 #pragma unroll
         for (int k = 0; k < NQ; ++k) qq[k] = (float)st[k];
-        if (state_collides<NCL, BF>(qq, sc, wq)) {
+        if (state_collides<NCL, BF, ROLE_ALL, SC>(qq, sc, wq)) {
             valid[ej] = 0;
             if (gfail) {
                 const int gi = (int)(ej / group), si = (int)(ej - (int64_t)gi * group);
@@ -457,6 +482,57 @@ __global__ __launch_bounds__(VBLOCK, edge_waves(NCL, BF, true)) void k_edges_uni
         edge_group_round<NCL, BF>(from, to, nd, n_edges, mode, valid, group, gfail, counter, sc,
                                   (int64_t)(unit >> EU_RSHIFT), (int)(unit & ((1u << EU_RSHIFT) - 1)) * VBLOCK,
                                   wq, mark, pk, 1, cntv);
+    }
+}
+
+// Axis-grid scenes with the scene staged in LDS (rp_math.h SceneGrid, as
+// k_validity_gl): blocks of GL_WAVES waves, each with its own queue and its own
+// (group, round) of the loop-free grid (k_edges_gl: wave bid x GL_WAVES + w) or units of
+// the pass-1 list (k_edges_units_gl); the same items as k_edges / k_edges_units, the
+// same tests on the same values: the same verdicts.
+template <bool BF>
+__global__ __launch_bounds__(64 * GL_WAVES, edge_waves(NCL_GRID, BF, false)) void k_edges_gl(
+    const double* __restrict__ from, const double* __restrict__ to, const int* __restrict__ nd, int64_t n_edges,
+    int kmax, int mode, uint8_t* valid, int group, int* gfail, unsigned long long* counter,
+    const DevScene* __restrict__ sc, const int* __restrict__ dcount, int per_item, int pk, int pass,
+    const int* __restrict__ cntv, int* zero_word) {
+    __shared__ SceneGrid L;
+    __shared__ WaveQ wqs[GL_WAVES];
+    __shared__ int marks[GL_WAVES][VBLOCK];
+    if (zero_word && rp_bid() == 0 && rp_tid() == 0) *zero_word = 0;
+    scene_grid_stage(sc, L, rp_tid(), 64 * GL_WAVES);
+    __syncthreads();
+    if (dcount) n_edges = min(n_edges, (int64_t)dcount[0] * per_item);
+    const int kk = max(kmax, 1);
+    const int64_t n_waves = (n_edges + VBLOCK - 1) / VBLOCK * kk;
+    const int wv = rp_tid() >> 6;
+    const int64_t w = (int64_t)rp_bid() * GL_WAVES + wv;
+    if (w >= n_waves) return;
+    const int64_t g = w / kk;
+    edge_group_round<NCL_GRID, BF, SceneGrid>(from, to, nd, n_edges, mode, valid, group, gfail, counter, &L, g,
+                                              (int)(w - g * kk) * VBLOCK, wqs[wv], marks[wv], pk, pass, cntv);
+}
+template <bool BF>
+__global__ __launch_bounds__(64 * GL_WAVES, edge_waves(NCL_GRID, BF, true)) void k_edges_units_gl(
+    const double* __restrict__ from, const double* __restrict__ to, const int* __restrict__ nd, int64_t n_edges,
+    int mode, uint8_t* valid, int group, int* gfail, unsigned long long* counter, const DevScene* __restrict__ sc,
+    const int* __restrict__ dcount, int per_item, int pk, const int* __restrict__ cntv,
+    const uint32_t* __restrict__ units, const int* __restrict__ n_units) {
+    __shared__ SceneGrid L;
+    __shared__ WaveQ wqs[GL_WAVES];
+    __shared__ int marks[GL_WAVES][VBLOCK];
+    const int nu = *n_units;
+    if ((int64_t)rp_bid() * GL_WAVES >= nu) return;   // (block-uniform: no unit for any of its waves)
+    scene_grid_stage(sc, L, rp_tid(), 64 * GL_WAVES);
+    __syncthreads();
+    if (dcount) n_edges = min(n_edges, (int64_t)dcount[0] * per_item);
+    const int wv = rp_tid() >> 6;
+    for (int u = rp_bid() * GL_WAVES + wv; u < nu; u += rp_gdim() * GL_WAVES) {
+        const uint32_t unit = units[u];
+        edge_group_round<NCL_GRID, BF, SceneGrid>(from, to, nd, n_edges, mode, valid, group, gfail, counter, &L,
+                                                  (int64_t)(unit >> EU_RSHIFT),
+                                                  (int)(unit & ((1u << EU_RSHIFT) - 1)) * VBLOCK, wqs[wv], marks[wv],
+                                                  pk, 1, cntv);
     }
 }
 
@@ -781,10 +857,22 @@ __global__ __launch_bounds__(NNBLOCK) void k_ext_nn(const double* __restrict__ A
                                                     double* __restrict__ efrom, double* __restrict__ eto,
                                                     int* __restrict__ nd, uint8_t* __restrict__ valid,
                                                     int32_t* __restrict__ near_out,
-                                                    const int32_t* __restrict__ near_in) {
+                                                    const int32_t* __restrict__ near_in,
+                                                    const int* __restrict__ gate = nullptr) {
     __shared__ double tile[NNTILE * NQ];
     const int64_t k = (int64_t)rp_bid() * NNBLOCK + rp_tid();
     const bool active = k < n;
+    // gate (a pipelined sub-batch, rp_lib.hip plan_impl): the previous sub-batch's
+    // first REACHED word; once it is set the iteration has ended and this sub-batch's
+    // edges are empty (nd -1: no slot; nd 0 would still check the far endpoint), so the
+    // edge launches behind it check nothing
+    if (gate && *gate != 0x7fffffff) {   // (block-uniform: one word)
+        if (active) {
+            nd[k] = -1;
+            valid[k] = 1;
+        }
+        return;
+    }
     double qr[NQ];
     sample_state(seed, g0 + (uint64_t)(i0 + (active ? k : 0)), bd.lo, bd.hi, qr);
     // near_in: nearest nodes from the split search (k_nn_part + k_nn_reduce)

@@ -187,6 +187,12 @@ struct rp_ctx {
     DevBuf<double> efrom, eto;
     DevBuf<int> nd;
     DevBuf<uint8_t> valid;
+    // the extension edges of a sub-batch enqueued before the previous one's status is
+    // read (plan_impl: pipelined sub-batches; efrom..valid may then hold the
+    // simplification's candidate edges of a sub-batch that solved)
+    DevBuf<double> xfrom, xto;
+    DevBuf<int> xnd;
+    DevBuf<uint8_t> xvalid;
     DevBuf<int32_t> near_, res, acc, incl, yv, mv, rec, Lv, chain_end;
     DevBuf<int> gfail;
     DevBuf<int32_t> eslot, eincl, echunk;   // work-compacted edge launches
@@ -243,6 +249,7 @@ struct rp_ctx {
     int nn_S = 0;                        // tree ranges of the last matrix-core launch
     int64_t nn_geo[4] = {0, 0, 0, 0};    // its T, queries per block, grid, device geometry (k_nn_reduce_g)
     DevBuf<DI2> nn_pilot;                // per-query pilot bests (rp_nn.h)
+    DevBuf<unsigned long long> nn_gbest; // per-query bound shared by a search's ranges (rp_nn.h)
     DevBuf<unsigned long long> estats;   // RBE_EDGE_STATS counters (k_edge_stats)
     DevBuf<int> ecnt;                    // coarse-first edge passes: pass-1 slots per edge
     DevBuf<uint32_t> eunits;             // ... pass 1's (group, round) work list (k_edge_units)
@@ -298,11 +305,13 @@ struct rp_ctx {
         for (auto& t : tree) t.release();
         q32.release(); flags.release(); ea.release(); eb.release(); end_nd.release(); eval.release();
         scalar.release(); counter.release(); efrom.release(); eto.release(); nd.release(); valid.release();
+        xfrom.release(); xto.release(); xnd.release(); xvalid.release();
         near_.release(); res.release(); acc.release(); incl.release(); yv.release(); mv.release();
         rec.release(); Lv.release(); chain_end.release(); gfail.release();
         eslot.release(); eincl.release(); echunk.release(); ecnt.release(); eunits.release(); enunits.release();
         cub_tmp.release(); path.release(); io.release(); simp.release(); partial.release();
         g_send.release(); g_recv.release(); g_cnt.release(); g_incl.release(); nn_part.release(); nn_qx.release();
+        nn_pilot.release(); nn_gbest.release(); estats.release(); lbst.release(); lberr.release();
         leave_group();
         for (hipEvent_t e : pev) (void)hipEventDestroy(e);
         if (gx0) (void)hipEventDestroy(gx0);
@@ -379,6 +388,20 @@ int64_t split_max() {
     return v;
 }
 
+// axis-grid scenes: the kernels that stage the scene in LDS (rp_math.h SceneGrid).
+// RBE_SCENE_LDS (read per launch): bit 0 k_validity_gl and the pass-1 list kernel
+// k_edges_units_gl (default 1), bit 1 also the loop-free edge launches (k_edges_gl);
+// 0: the global-memory kernels (A/B, tests). Measured in the C5 covered-well plans (4
+// plans, rocprofv3): pass 1 2.80 -> 2.24 ms with the scene in LDS, the loop-free pass 0
+// 2.80 -> 3.21 ms (its waves each check one short round: the block's 10 KB copy and
+// 4-wave blocks cost more than the gathers they save); clutter64 k_validity 1M / 4M
+// states 8.4 / 9.4 -> 10.0 / 11.3 G states/s
+int scene_lds_mode() {
+    const char* e = std::getenv("RBE_SCENE_LDS");
+    return e && *e ? std::atoi(e) : 1;
+}
+bool scene_lds_on() { return (scene_lds_mode() & 1) != 0; }
+
 template <bool BF, int NR>
 void launch_validity_split(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, hipStream_t s) {
     const dim3 g(blocks_for(n, 64)), b(64 * NR);
@@ -399,6 +422,11 @@ void launch_validity_bf(rp_ctx* c, const float* q, int64_t n, uint8_t* flags, hi
     if (n <= split_max()) {
         if (n <= 65536) launch_validity_split<BF, 3>(c, q, n, flags, s);
         else launch_validity_split<BF, 2>(c, q, n, flags, s);
+        return;
+    }
+    if (ncl_bucket(c->scene) == NCL_GRID && scene_lds_on()) {   // the scene staged in LDS
+        hipLaunchKernelGGL((k_validity_gl<BF>), dim3(blocks_for(n, 64 * GL_WAVES)), dim3(64 * GL_WAVES), 0, s, q, n,
+                           flags, c->d_scene);
         return;
     }
     const dim3 g(blocks_for(n, VTHREADS)), b(VTHREADS);
@@ -632,9 +660,22 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
     const int ps = prof_begin(c, s);
     // (the reference's robot base folded in as a constant, as for k_validity)
     const bool bf = base_fixed(c->scene);
+    // axis-grid scenes: the pass-1 list kernel (and with RBE_SCENE_LDS bit 1 the
+    // loop-free one) with the scene in LDS (k_edges_units_gl / k_edges_gl: GL_WAVES
+    // waves per block, each its own unit; scene_lds_mode)
+    const int lds_mode = scene_lds_mode();
+    const bool lds = (lds_mode & 1) != 0, lds_free = (lds_mode & 2) != 0;
 #define RP_EDGES_Z(N, L, G, KM, DK, RF, PK, PS, CV, ZW)                                                           \
     do {                                                                                                           \
-        if (bf) hipLaunchKernelGGL((k_edges<N, true, L>), dim3(G), b, 0, s, from, to, nd, n, KM, mode, valid,      \
+        if ((N) == NCL_GRID && !(L) && (DK) == nullptr && (RF) == 0 && lds_free) {                                 \
+            const unsigned gg = (unsigned)(((int64_t)(G) + GL_WAVES - 1) / GL_WAVES);                               \
+            if (bf) hipLaunchKernelGGL((k_edges_gl<true>), dim3(gg), dim3(64 * GL_WAVES), 0, s, from, to, nd, n, KM,  \
+                                       mode, valid, group, gfail, c->counter.p, c->d_scene, dcount, per_item, PK,  \
+                                       PS, CV, ZW);                                                                \
+            else hipLaunchKernelGGL((k_edges_gl<false>), dim3(gg), dim3(64 * GL_WAVES), 0, s, from, to, nd, n, KM,   \
+                                    mode, valid, group, gfail, c->counter.p, c->d_scene, dcount, per_item, PK, PS, \
+                                    CV, ZW);                                                                       \
+        } else if (bf) hipLaunchKernelGGL((k_edges<N, true, L>), dim3(G), b, 0, s, from, to, nd, n, KM, mode, valid, \
                                    group, gfail, c->counter.p, c->d_scene, dcount, per_item, DK, RF, PK, PS, CV,   \
                                    ZW);                                                                            \
         else hipLaunchKernelGGL((k_edges<N, false, L>), dim3(G), b, 0, s, from, to, nd, n, KM, mode, valid,        \
@@ -644,7 +685,16 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
 #define RP_EDGES_L(N, L, G, KM, DK, RF) RP_EDGES_P(N, L, G, KM, DK, RF, 1, 0, (const int*)nullptr)
 #define RP_EDGES_U(N)                                                                                              \
     do {                                                                                                           \
-        if (bf) hipLaunchKernelGGL((k_edges_units<N, true>), dim3(nb_units), b, 0, s, from, to, nd, n, mode, valid, \
+        if ((N) == NCL_GRID && lds) {                                                                              \
+            const unsigned gu = (nb_units + GL_WAVES - 1) / GL_WAVES;                                               \
+            if (bf) hipLaunchKernelGGL((k_edges_units_gl<true>), dim3(gu), dim3(64 * GL_WAVES), 0, s, from, to, nd, n, \
+                                       mode, valid, group, gfail, c->counter.p, c->d_scene, dcount, per_item, pk,  \
+                                       (const int*)c->ecnt.p, (const uint32_t*)c->eunits.p,                        \
+                                       (const int*)c->enunits.p);                                                  \
+            else hipLaunchKernelGGL((k_edges_units_gl<false>), dim3(gu), dim3(64 * GL_WAVES), 0, s, from, to, nd, n, \
+                                    mode, valid, group, gfail, c->counter.p, c->d_scene, dcount, per_item, pk,     \
+                                    (const int*)c->ecnt.p, (const uint32_t*)c->eunits.p, (const int*)c->enunits.p); \
+        } else if (bf) hipLaunchKernelGGL((k_edges_units<N, true>), dim3(nb_units), b, 0, s, from, to, nd, n, mode, valid, \
                                    group, gfail, c->counter.p, c->d_scene, dcount, per_item, pk,                   \
                                    (const int*)c->ecnt.p, (const uint32_t*)c->eunits.p, (const int*)c->enunits.p); \
         else hipLaunchKernelGGL((k_edges_units<N, false>), dim3(nb_units), b, 0, s, from, to, nd, n, mode, valid,  \
@@ -1233,6 +1283,16 @@ int nn_pilot_stride() {
     return e && *e ? std::atoi(e) : 32;
 }
 
+#ifndef RP_NN_SHARE_DEFAULT
+#define RP_NN_SHARE_DEFAULT 0
+#endif
+// ranges of a split search share each query's best bound (rp_nn.h gbest);
+// RBE_NN_SHARE=0: every range tightens on its own finds only (A/B; read per search)
+bool nn_share() {
+    const char* e = std::getenv("RBE_NN_SHARE");
+    return e && *e ? std::atoi(e) != 0 : RP_NN_SHARE_DEFAULT;
+}
+
 // device geometry for status-bounded searches (rp_nn.h nn_geom): RBE_NN_DEVGEOM=0 for
 // the host geometry of the largest count (A/B; read per search, as RBE_NN_MFMA)
 bool nn_devgeom() {
@@ -1249,7 +1309,7 @@ bool nn_geom_fit() {
 
 template <int RB, int W>
 void launch_nn_mfma_w(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, const double* tree, const h8* img,
-                      int64_t T) {
+                      int64_t T, const int* gate) {
     constexpr int64_t NNM_STAGE = 64;   // (range sizing: 64-node units)
     const int64_t per_block = (int64_t)W * 16 * RB;
     int64_t target = 1024;   // blocks
@@ -1292,15 +1352,22 @@ void launch_nn_mfma_w(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, 
         c->nn_pilot.ensure((size_t)(S1 * n));
         hipLaunchKernelGGL((k_nn_mfma<RBP, W>), dim3((unsigned)(qb1 * S1)), dim3(64 * W), 0, c->stream, qx, n,
                            (const int*)nullptr, (int64_t)0, tree, img, T, chunk1, qb1, c->nnm, c->nn_pilot.p, 0,
-                           pst, (const DI2*)nullptr, 0);
+                           pst, (const DI2*)nullptr, 0, gate, (unsigned long long*)nullptr);
         init = c->nn_pilot.p;
         init_S = (int)S1;
         if (std::getenv("RBE_NN_LOG"))   // (diagnostic: tools/nn_seq.py; pairs = n x T / pst)
             fprintf(stderr, "nnlog n=%lld T=%lld grid=%lld S=%lld status=0 pilot=%d\n", (long long)n,
                     (long long)((T + pst - 1) / pst), (long long)(qb1 * S1), (long long)S1, pst);
     }
+    // the ranges share each query's bound (rp_nn.h gbest; RBE_NN_SHARE=0: off, A/B)
+    unsigned long long* gbest = nullptr;
+    if (S >= 2 && nn_share()) {
+        c->nn_gbest.ensure((size_t)n);
+        HIP_TRY(hipMemsetAsync(c->nn_gbest.p, 0xff, sizeof(unsigned long long) * (size_t)n, c->stream));
+        gbest = c->nn_gbest.p;
+    }
     hipLaunchKernelGGL((k_nn_mfma<RB, W>), dim3((unsigned)grid), dim3(64 * W), 0, c->stream, qx, n, Q.status,
-                       Q.t0, tree, img, T, chunk, qblocks, c->nnm, c->nn_part.p, devgeom, 1, init, init_S);
+                       Q.t0, tree, img, T, chunk, qblocks, c->nnm, c->nn_part.p, devgeom, 1, init, init_S, gate, gbest);
     static const bool log = std::getenv("RBE_NN_LOG") != nullptr;   // (diagnostic: tools/nn_seq.py)
     if (log) fprintf(stderr, "nnlog n=%lld T=%lld grid=%lld S=%d status=%d\n", (long long)n, (long long)T,
                      (long long)grid, S, Q.status ? 1 : 0);
@@ -1313,13 +1380,13 @@ void launch_nn_mfma_w(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, 
 // waves per block: RBE_NN_WAVES (1, 2, 4)
 template <int RB>
 void launch_nn_mfma(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, const double* tree, const h8* img,
-                    int64_t T) {
+                    int64_t T, const int* gate) {
     int w = 4;
     if (const char* e = std::getenv("RBE_NN_WAVES"))
         if (*e) w = std::atoi(e);
-    if (w == 1) launch_nn_mfma_w<RB, 1>(c, qx, n, Q, tree, img, T);
-    else if (w == 2) launch_nn_mfma_w<RB, 2>(c, qx, n, Q, tree, img, T);
-    else launch_nn_mfma_w<RB, 4>(c, qx, n, Q, tree, img, T);
+    if (w == 1) launch_nn_mfma_w<RB, 1>(c, qx, n, Q, tree, img, T, gate);
+    else if (w == 2) launch_nn_mfma_w<RB, 2>(c, qx, n, Q, tree, img, T, gate);
+    else launch_nn_mfma_w<RB, 4>(c, qx, n, Q, tree, img, T, gate);
 }
 
 // whether n queries against T nodes take the split search: it pays ~4 launches; the
@@ -1342,7 +1409,10 @@ const h8* tree_images(rp_ctx* c, Tree& t, int64_t T) {
     return t.img.p;
 }
 
-bool nn_split(rp_ctx* c, const NnQuery& Q, int64_t n, Tree& tr, int64_t T, int32_t* out, bool force = false) {
+// gate: the searches of a pipelined sub-batch (plan_impl) do nothing once the word is
+// not INT_MAX (k_nn_mfma; the fallback k_nn_part path has no gate and runs)
+bool nn_split(rp_ctx* c, const NnQuery& Q, int64_t n, Tree& tr, int64_t T, int32_t* out, bool force = false,
+              const int* gate = nullptr) {
     const double* tree = tr.q.p;
     if (n <= 0 || T <= 0) return false;
     int mode = -1;
@@ -1364,10 +1434,10 @@ bool nn_split(rp_ctx* c, const NnQuery& Q, int64_t n, Tree& tr, int64_t T, int32
         }
         const h8* img = tree_images(c, tr, T);
         const int ps = prof_begin(c, c->stream);
-        if (mfma_rb >= 8) launch_nn_mfma<8>(c, qx, n, Q, tree, img, T);
-        else if (mfma_rb >= 4) launch_nn_mfma<4>(c, qx, n, Q, tree, img, T);
-        else if (mfma_rb >= 2) launch_nn_mfma<2>(c, qx, n, Q, tree, img, T);
-        else launch_nn_mfma<1>(c, qx, n, Q, tree, img, T);
+        if (mfma_rb >= 8) launch_nn_mfma<8>(c, qx, n, Q, tree, img, T, gate);
+        else if (mfma_rb >= 4) launch_nn_mfma<4>(c, qx, n, Q, tree, img, T, gate);
+        else if (mfma_rb >= 2) launch_nn_mfma<2>(c, qx, n, Q, tree, img, T, gate);
+        else launch_nn_mfma<1>(c, qx, n, Q, tree, img, T, gate);
         hipLaunchKernelGGL(k_nn_reduce_g, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream,
                            (const DI2*)c->nn_part.p, n, c->nn_S, Q.status, Q.t0, out, c->nn_geo[0], c->nn_geo[1],
                            c->nn_geo[2], (int)c->nn_geo[3]);
@@ -1573,6 +1643,10 @@ void plan_workspace(rp_ctx* c, int64_t BMAX, int world, int cmax, int64_t cap, b
     c->eto.ensure(ne * NQ);
     c->nd.ensure(ne);
     c->valid.ensure(ne);
+    c->xfrom.ensure((BMAX + 2) * NQ);
+    c->xto.ensure((BMAX + 2) * NQ);
+    c->xnd.ensure(BMAX + 2);
+    c->xvalid.ensure(BMAX + 2);
     c->near_.ensure(BMAX);
     c->res.ensure(BMAX);
     c->acc.ensure(BMAX);
@@ -1884,6 +1958,18 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         return !(e && *e && std::atoi(e) == 0);
     }();
     bool prog_ran = true;
+    // pipelined sub-batches: a two-phase sub-batch enqueues the NEXT sub-batch's
+    // extension phase (its nearest-node searches, k_ext_nn and extension edges: none of
+    // them depends on this sub-batch) before waiting for its own status, so the GPU does
+    // not idle through the host round trip. The next sub-batch's kernels are gated on
+    // this one's first REACHED word (k_ext_nn, k_nn_mfma) and write their edges to the x*
+    // buffers, so a sub-batch that solves loses only ~50 us of gated launches and its
+    // simplification candidates (efrom..valid) stay intact. RBE_PLAN_PIPELINE=0: off
+    // (A/B, tests); same trees and plans either way.
+    const bool pipeline = [] {
+        const char* e = std::getenv("RBE_PLAN_PIPELINE");
+        return !(e && *e && std::atoi(e) == 0);
+    }();
     // raw paths longer than dev_max states are simplified host-driven (same
     // algorithm); RBE_SIMPLIFY_DEVICE_MAX lowers the limit (tests of that path)
     int dev_max = SPMAX;
@@ -1996,6 +2082,40 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         auto next_chunk = [&](int64_t cur, int64_t left) {
             const int64_t quarter = ((left / 4 + world - 1) / world) * world;
             return std::min(left, std::max(cur * chunk_growth, quarter));
+        };
+        // the extension phase of a two-phase sub-batch of Cx samples from g0x: the
+        // nearest nodes of tree A's snapshot, k_ext_nn (sample, steer, edge records) and
+        // the extension edge launch; piped: into the x* buffers, gated on the status
+        // (the previous sub-batch may still solve)
+        int64_t piped_done = -1, piped_C = 0;   // the sub-batch whose extension phase is enqueued
+        auto ext_phase = [&](int64_t Cx, uint64_t g0x, int64_t sgx, bool piped) {
+            const int* gate = piped ? status + ST_FIRST : nullptr;
+            double* ef = piped ? c->xfrom.p : c->efrom.p;
+            double* et = piped ? c->xto.p : c->eto.p;
+            int* end = piped ? c->xnd.p : c->nd.p;
+            uint8_t* ev = piped ? c->xvalid.p : c->valid.p;
+            NnQuery qe{};
+            qe.kind = NNQ_SAMPLE;
+            qe.seed = p.seed;
+            qe.g0 = g0x;
+            qe.i0 = 0;
+            qe.bd = bd;
+            const bool esplit = nn_split(c, qe, Cx, A, TA, c->near_.p, false, gate);
+            const int pn1 = prof_begin(c, c->stream);
+            hipLaunchKernelGGL(k_ext_nn, dim3(blocks_for(Cx, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
+                               p.seed, g0x, (int64_t)0, Cx, bd, p.range, p.resolution, a_start, ef, et, end, ev,
+                               c->near_.p, esplit ? (const int32_t*)c->near_.p : nullptr, gate);
+            HIP_TRY(hipGetLastError());
+            prof_end(c, pn1, 0, c->stream);
+            debug_wait(c, "k_ext_nn");
+            // (extension edges: steers shorter than the range on large trees)
+            if (packed(Cx + (sgx >= 0 ? 2 : 0)))
+                launch_edges_packed(c, ef, et, end, Cx + (sgx >= 0 ? 2 : 0), kmax, a_start ? 0 : 1, ev, 1, nullptr,
+                                    c->stream, nullptr, 1);
+            else
+                launch_edges(c, ef, et, end, Cx + (sgx >= 0 ? 2 : 0), kmax, a_start ? 0 : 1, ev, 1, nullptr,
+                             c->stream);
+            debug_wait(c, "ext edges");
         };
         for (int64_t done = 0; done < B && !solved && !stop; done += C, C = next_chunk(C, B - done)) {
             C = std::min(C, B - done);
@@ -2168,29 +2288,12 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
 
             // ---- single rank, two-phase (large sub-batches, or RBE_PLAN_SPECULATE=0)
             debug_wait(c, "iteration start");
-            NnQuery qe{};
-            qe.kind = NNQ_SAMPLE;
-            qe.seed = p.seed;
-            qe.g0 = g0;
-            qe.i0 = 0;
-            qe.bd = bd;
-            const bool esplit = nn_split(c, qe, C, A, TA, c->near_.p);
-            const int pn1 = prof_begin(c, c->stream);
-            hipLaunchKernelGGL(k_ext_nn, dim3(blocks_for(C, NNBLOCK)), dim3(NNBLOCK), 0, c->stream, A.q.p, TA,
-                               p.seed, g0, (int64_t)0, C, bd, p.range, p.resolution, a_start, c->efrom.p, c->eto.p,
-                               c->nd.p, c->valid.p, c->near_.p, esplit ? (const int32_t*)c->near_.p : nullptr);
-            HIP_TRY(hipGetLastError());
-            prof_end(c, pn1, 0, c->stream);
+            // (enqueued ahead by the previous sub-batch, or now)
+            const bool piped = piped_done == done && piped_C == C;
+            piped_done = -1;
+            if (!piped) ext_phase(C, g0, sg, false);
+            const uint8_t* ext_valid = piped ? c->xvalid.p : c->valid.p;
             c->prof.nn_pairs += (double)C * (double)TA;
-            debug_wait(c, "k_ext_nn");
-            // (extension edges: steers shorter than the range on large trees)
-            if (packed(C + (sg >= 0 ? 2 : 0)))
-                launch_edges_packed(c, c->efrom.p, c->eto.p, c->nd.p, C + (sg >= 0 ? 2 : 0), kmax, a_start ? 0 : 1,
-                                    c->valid.p, 1, nullptr, c->stream, nullptr, 1);
-            else
-                launch_edges(c, c->efrom.p, c->eto.p, c->nd.p, C + (sg >= 0 ? 2 : 0), kmax, a_start ? 0 : 1,
-                             c->valid.p, 1, nullptr, c->stream);
-            debug_wait(c, "ext edges");
             c->stats.edges_checked += C;
 
             // device-side counts, one host round trip per sub-batch; sub-batches
@@ -2200,25 +2303,25 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             const int seq = ++c->seq;
             if (fused) {
                 if (C <= FUSE_THREADS)
-                    hipLaunchKernelGGL(k_ext_accept_small<1>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, c->valid.p,
+                    hipLaunchKernelGGL(k_ext_accept_small<1>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, ext_valid,
                                        c->near_.p, C, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, An, status,
                                        sg, sg_stride);
                 else
-                    hipLaunchKernelGGL(k_ext_accept_small<4>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, c->valid.p,
+                    hipLaunchKernelGGL(k_ext_accept_small<4>, dim3(1), dim3(FUSE_THREADS), 0, c->stream, ext_valid,
                                        c->near_.p, C, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, An, status,
                                        sg, sg_stride);
             } else if (accept_lb()) {   // flags + scan + appends in one launch (decoupled look-back)
                 const unsigned nb = lb_prepare(c, C);
-                hipLaunchKernelGGL(k_ext_accept_lb, dim3(nb), dim3(LB_THREADS), 0, c->stream, c->valid.p, c->near_.p,
+                hipLaunchKernelGGL(k_ext_accept_lb, dim3(nb), dim3(LB_THREADS), 0, c->stream, ext_valid, c->near_.p,
                                    C, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, An, status, sg, sg_stride,
                                    c->lbst.p, c->lb_epoch, c->lberr.p);
             } else {
                 hipLaunchKernelGGL(k_ext_result_flag, dim3(blocks_for(C, 256)), dim3(256), 0, c->stream,
-                                   c->valid.p, c->near_.p, C, c->res.p, c->acc.p);
+                                   ext_valid, c->near_.p, C, c->res.p, c->acc.p);
                 scan_incl(c, c->acc.p, c->incl.p, C);
                 hipLaunchKernelGGL(k_ext_append, dim3(blocks_for(C, 256)), dim3(256), 0, c->stream, c->res.p,
                                    c->incl.p, C, p.seed, g0, bd, p.range, A.q.p, A.par.p, A.cand.p, An, status,
-                                   (const uint8_t*)c->valid.p, sg, sg_stride);
+                                   ext_valid, sg, sg_stride);
             }
             debug_wait(c, "ext accept");
             NnQuery qc{};
@@ -2278,6 +2381,15 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
             // cost every other one ~15-25 us
             prog_ran = !early;
             if (prog_ran) run_program(0, tail_steps, seq, true);
+            if (pipeline && sg_known && done + C < B) {   // the next sub-batch's extension phase, ahead
+                const int64_t d2 = done + C;
+                const int64_t C2 = std::min(next_chunk(C, B - d2), B - d2);
+                if (!((grouped && C2 > repl) || (speculate && C2 <= FUSE_MAX))) {
+                    ext_phase(C2, gbase + (uint64_t)d2, -1, true);
+                    piped_done = d2;
+                    piped_C = C2;
+                }
+            }
             wait_seq(c, seq);
             if (!sg_known) {
                 if (const int code = endpoint_status(h->status[ST_SG])) return endpoint_fail(code);
@@ -3622,10 +3734,10 @@ int rp_selftest_nn(rp_ctx* c, const double* q, int64_t n, const double* tree, in
         // (profiling on: rp_last_kernel_ms = the search, pilot to reduce; the node
         // images are made once per node and plan in rp_plan, so they are left out)
         if (c->profiling) HIP_TRY(hipEventRecord(c->ev0, c->stream));
-        if (mode >= 8) launch_nn_mfma<8>(c, dq.p, n, Q, dt.p, dimg.p, T);
-        else if (mode >= 4) launch_nn_mfma<4>(c, dq.p, n, Q, dt.p, dimg.p, T);
-        else if (mode >= 2) launch_nn_mfma<2>(c, dq.p, n, Q, dt.p, dimg.p, T);
-        else launch_nn_mfma<1>(c, dq.p, n, Q, dt.p, dimg.p, T);
+        if (mode >= 8) launch_nn_mfma<8>(c, dq.p, n, Q, dt.p, dimg.p, T, nullptr);
+        else if (mode >= 4) launch_nn_mfma<4>(c, dq.p, n, Q, dt.p, dimg.p, T, nullptr);
+        else if (mode >= 2) launch_nn_mfma<2>(c, dq.p, n, Q, dt.p, dimg.p, T, nullptr);
+        else launch_nn_mfma<1>(c, dq.p, n, Q, dt.p, dimg.p, T, nullptr);
         hipLaunchKernelGGL(k_nn_reduce, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream,
                            (const DI2*)c->nn_part.p, n, c->nn_S, (const int*)nullptr, (int64_t)0, dout.p);
         if (c->profiling) {

@@ -266,8 +266,8 @@ __device__ __forceinline__ bool fk_walk_j(const float q[NQ], const J& jt, const 
     }
     return false;
 }
-template <class Visit, bool BF = false>
-__device__ __forceinline__ bool fk_walk(const float q[NQ], const DevScene* __restrict__ sc, Capsules& k,
+template <class Visit, bool BF = false, class SC = DevScene>
+__device__ __forceinline__ bool fk_walk(const float q[NQ], const SC* __restrict__ sc, Capsules& k,
                                         Visit& v) {
     const JointsQ jt{q};
     return fk_walk_j<Visit, BF>(q, jt, sc->base, k, v);
@@ -278,9 +278,10 @@ struct NoVisit {
     __device__ __forceinline__ bool at(const Capsules&) { return false; }
 };
 
-__device__ __forceinline__ void fk_capsules(const float q[NQ], const DevScene* __restrict__ sc, Capsules& k) {
+template <class SC = DevScene>
+__device__ __forceinline__ void fk_capsules(const float q[NQ], const SC* __restrict__ sc, Capsules& k) {
     NoVisit v;
-    fk_walk(q, sc, k, v);
+    fk_walk<NoVisit, false, SC>(q, sc, k, v);
 }
 
 // Capsule AABB expanded by its radius.
@@ -497,6 +498,52 @@ __device__ __forceinline__ bool pairs_ending_at(const Capsules& k) {
 }
 
 // ---------------------------------------------------------------------------
+// Axis-grid scenes staged in LDS (round 6)
+// ---------------------------------------------------------------------------
+// On an axis-grid scene (> 16 boxes) the broad phase gathers per lane: each lane's
+// candidate boxes differ, so the grid masks and the 64-B box records are vector loads
+// from global memory (L2), one dependent round trip per candidate round, and the
+// grid-scene kernels waited on memory ~60 % of their wave cycles (profiles/r06
+// edges_pmc_*.txt: SQ_WAIT_ANY). SceneGrid holds exactly the fields the grid path
+// reads, with DevScene's names (state_collides is templated on the scene type), and a
+// block of several waves stages it once in its LDS (~10 KB, shared by the block's
+// waves: four one-wave queues + one copy keep 4 blocks of 4 waves on a CU, the grid
+// kernels' register-bound occupancy). Same values, same arithmetic: same flags.
+struct SceneGrid {
+    alignas(16) float box[MAX_BOXES][16];
+    alignas(16) float rot[MAX_BOXES][12];
+    alignas(16) unsigned long long grid_lo[3][GRID_CELLS];
+    alignas(16) unsigned long long grid_hi[3][GRID_CELLS];
+    alignas(16) float grid_o[4];
+    float grid_s[4];
+    float base[4];
+    float plane_z;
+    unsigned env_far;
+};
+// every thread of the block (nt of them) copies its share; the caller synchronises
+__device__ __forceinline__ void scene_grid_stage(const DevScene* __restrict__ sc, SceneGrid& L, int tid, int nt) {
+    // (DevScene's box / rot arrays start 16-byte aligned, its grid masks 8-byte aligned)
+    constexpr int NB4 = MAX_BOXES * 16 / 4, NR4 = MAX_BOXES * 12 / 4, NG = 3 * GRID_CELLS;
+    const float4* b = reinterpret_cast<const float4*>(&sc->box[0][0]);
+    const float4* r = reinterpret_cast<const float4*>(&sc->rot[0][0]);
+    for (int i = tid; i < NB4; i += nt) reinterpret_cast<float4*>(&L.box[0][0])[i] = b[i];
+    for (int i = tid; i < NR4; i += nt) reinterpret_cast<float4*>(&L.rot[0][0])[i] = r[i];
+    for (int i = tid; i < NG; i += nt) {
+        (&L.grid_lo[0][0])[i] = (&sc->grid_lo[0][0])[i];
+        (&L.grid_hi[0][0])[i] = (&sc->grid_hi[0][0])[i];
+    }
+    if (tid < 4) {
+        L.grid_o[tid] = sc->grid_o[tid];
+        L.grid_s[tid] = sc->grid_s[tid];
+        L.base[tid] = sc->base[tid];
+    }
+    if (tid == 0) {
+        L.plane_z = sc->plane_z;
+        L.env_far = sc->env_far;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Wave-compacted narrow phases
 // ---------------------------------------------------------------------------
 // A narrow phase in SIMT code costs the whole wave whenever ANY of its 64 lanes
@@ -539,11 +586,14 @@ constexpr int NCL_GRID = -1;   // broad-phase instantiation for axis-grid scenes
 template <int NCL>
 struct ClusterRegs {
     float c[NCL > 0 ? NCL : 1][8];
-    __device__ __forceinline__ void load(const DevScene* __restrict__ sc) {
+    template <class SC>
+    __device__ __forceinline__ void load(const SC* __restrict__ sc) {
+        if constexpr (NCL > 0) {
 #pragma unroll
-        for (int i = 0; i < NCL; ++i)
+            for (int i = 0; i < NCL; ++i)
 #pragma unroll
-            for (int w = 0; w < 8; ++w) c[i][w] = sc->cluster[i][w];
+                for (int w = 0; w < 8; ++w) c[i][w] = sc->cluster[i][w];
+        }
     }
 };
 
@@ -651,8 +701,8 @@ __device__ __forceinline__ void enqueue_sb(const Capsules& k, const float* bx, c
 }
 
 // capsule C vs plane (immediate) and boxes (queued)
-template <int C, int NCL>
-__device__ __forceinline__ bool env_queued(const Capsules& k, const DevScene* __restrict__ sc,
+template <int C, int NCL, class SC>
+__device__ __forceinline__ bool env_queued(const Capsules& k, const SC* __restrict__ sc,
                                            QueueState<NCL>& s) {
     constexpr float r = CAP_GEOM[C][6];
     const Aabb u = capsule_aabb(k.a[C], k.b[C], r);
@@ -823,9 +873,9 @@ enum { ROLE_ENV = 1, ROLE_PA = 2, ROLE_PB = 4, ROLE_ALL = 7 };
 #endif
 constexpr int SPLIT_J = RP_SPLIT_J;
 
-template <int NCL, int ROLE = ROLE_ALL>
+template <int NCL, int ROLE = ROLE_ALL, class SC = DevScene>
 struct QueuedVisit {
-    const DevScene* __restrict__ sc;
+    const SC* __restrict__ sc;
     QueueState<NCL> s;
     template <int C>
     __device__ __forceinline__ bool at(const Capsules& k) {
@@ -854,11 +904,11 @@ __device__ __forceinline__ void never_pairs_each(const Capsules& k, S& s) {
         never_pairs_each<P + 1>(k, s);
     }
 }
-template <class S>
-__device__ __forceinline__ void never_pairs_outside_limits(const float q[NQ], const DevScene* __restrict__ sc,
+template <class S, class SC>
+__device__ __forceinline__ void never_pairs_outside_limits(const float q[NQ], const SC* __restrict__ sc,
                                                                      S& s) {
     Capsules k;
-    fk_capsules(q, sc, k);
+    fk_capsules<SC>(q, sc, k);
     never_pairs_each(k, s);
 }
 
@@ -867,10 +917,10 @@ __device__ __forceinline__ void never_pairs_outside_limits(const float q[NQ], co
 // box and self narrow phases are queued and drained wave-compacted. Every lane of
 // the wave that is still running must call this at the same point. NCL >= the
 // scene's cluster count (rp_lib.hip picks the instantiation).
-template <int NCL, bool BF = false, int ROLE = ROLE_ALL>
-__device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene* __restrict__ sc, WaveQ& Q) {
+template <int NCL, bool BF = false, int ROLE = ROLE_ALL, class SC = DevScene>
+__device__ __forceinline__ bool state_collides(const float q[NQ], const SC* __restrict__ sc, WaveQ& Q) {
     Capsules k;
-    QueuedVisit<NCL, ROLE> v;
+    QueuedVisit<NCL, ROLE, SC> v;
     v.sc = sc;
     v.s.Q = &Q;
     v.s.nss = 0;
@@ -897,7 +947,7 @@ __device__ __forceinline__ bool state_collides(const float q[NQ], const DevScene
     JointsSC jt;
 #pragma unroll
     for (int i = 0; i < 7; ++i) rp_sincos(q[i], &jt.s[i], &jt.c[i]);
-    if (fk_walk_j<QueuedVisit<NCL, ROLE>, BF>(q, jt, sc->base, k, v)) return true;
+    if (fk_walk_j<QueuedVisit<NCL, ROLE, SC>, BF>(q, jt, sc->base, k, v)) return true;
     if constexpr ((ROLE & ROLE_PB) != 0)
         if (!v.s.in_limits) never_pairs_outside_limits(q, sc, v.s);
     RP_STAMP(5);

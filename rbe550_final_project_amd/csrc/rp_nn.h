@@ -38,6 +38,11 @@ struct NnMfma {
     double iG2, iH2;   // 2^-G, 2^-H (exact: a product by them is the division by 2^G, 2^H)
 };
 
+// B fragments through a buffer descriptor (k_nn_mfma; 0: flat loads, A/B)
+#ifndef RP_NN_BUF
+#define RP_NN_BUF 1
+#endif
+
 // waves per block (template W): each with its own queries and tree stream
 constexpr int NNM_SEEDS = 8;    // nodes per range evaluated exactly before the scan (threshold seeds)
 
@@ -231,13 +236,19 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
                                                           const double* __restrict__ tree, const h8* __restrict__ img,
                                                           int64_t T, int64_t chunk, int64_t qblocks, NnMfma P,
                                                           DI2* __restrict__ part, int devgeom, int tstride,
-                                                          const DI2* __restrict__ init, int init_S) {
+                                                          const DI2* __restrict__ init, int init_S,
+                                                          const int* __restrict__ gate,
+                                                          unsigned long long* __restrict__ gbest) {
     constexpr int QW = 16 * RB;   // queries per wave
+    // gate: a pipelined sub-batch's search (rp_lib.hip plan_impl) does nothing once the
+    // previous sub-batch's first REACHED word is set (its result is then never read)
+    if (gate && *gate != 0x7fffffff) return;
     __shared__ unsigned long long s_best[W][QW];            // exact best distance (f64 bits; >= 0)
     __shared__ int s_bi[W][QW];                             // its node (lowest index among equal)
     __shared__ int s_ti[W][QW];                             // a round's lowest node at the new best
     __shared__ int2 s_cand[W][NNM_CAND];                    // passing (row, node) pairs, not yet evaluated
     __shared__ double s_na[W][QW];                          // |x'|^2 of each row (threshold slots)
+    __shared__ unsigned long long s_gb[W][QW];              // the query's bound over every range (gbest)
     int64_t nwg = (int64_t)rp_gdim();
     if (status) {
         n = min(n, (int64_t)status[0] - t0);
@@ -302,6 +313,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
         }
         s_best[w][r] = bb;
         s_bi[w][r] = bi;
+        s_gb[w][r] = bb;
     }
     wave_lds_sync();
     // A fragments (row lane & 15 of each row block; k chunk ch); the threshold slots
@@ -354,11 +366,27 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
             wave_lds_sync();
         }
         ncand = 0;
+        if (gbest) {
+            // the ranges of a query run at once in other blocks: each publishes its
+            // exact best (atomicMin on the f64 bits, non-negative: ordered as integers)
+            // and takes the minimum over all of them so far as its filter bound. Only
+            // the threshold follows it: s_best / s_bi stay this range's own exactly
+            // evaluated minimum, and any node at distance <= the final answer still
+            // passes (the bound is >= the answer), so the reduce over the ranges is
+            // unchanged
+            for (int r = lane; r < QW; r += 64) {
+                const unsigned long long mine = s_best[w][r];
+                const unsigned long long old = qw0 + r < n ? atomicMin(gbest + qw0 + r, mine) : mine;
+                s_gb[w][r] = old < mine ? old : mine;
+            }
+            wave_lds_sync();
+        }
         if (ch == 3) {   // (the same slots again where a row's best did not move)
 #pragma unroll
             for (int rb = 0; rb < RB; ++rb) {
                 const int r = rb * 16 + (lane & 15);
-                const double bnow = __longlong_as_double((long long)s_best[w][r]);
+                const unsigned long long bb = s_best[w][r], gb = s_gb[w][r];
+                const double bnow = __longlong_as_double((long long)(gb < bb ? gb : bb));
                 if (bnow < 1e300) {
                     _Float16 hh, hl;
                     thr_slots(P, bnow, s_na[w][r], hh, hl);
@@ -385,10 +413,28 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     const int64_t ntiles = ((t_hi - t_lo + 15) / 16 + tstride - 1) / tstride;
     const int col = lane & 15;   // this lane's column of every tile
     // tile t: the wave-uniform base + t x tstride KiB plus this lane's 16-byte slot
-    const char* ub = (const char*)(img + t_lo * 4);
     const uint32_t loff = (uint32_t)((col * 4 + ch) * 16);
     const int64_t tbytes = (int64_t)tstride * 1024, tnodes = (int64_t)tstride * 16;
+#if RP_NN_BUF
+    // through a buffer descriptor of the range's images: the tile's byte offset in an
+    // SGPR (soffset), the lane's slot in voffset, so a tile costs no VALU address
+    // arithmetic (the flat form kept a 64-bit base + slot pair and paid a 64-bit
+    // multiply-add per tile on the vector pipe, whose issue the MFMAs already crowd).
+    // Every load is inside the descriptor (tiles past the range re-read its last one).
+    const uint64_t ubv = (uint64_t)(img + t_lo * 4);
+    const uint32_t ub_lo = __builtin_amdgcn_readfirstlane((uint32_t)ubv);
+    const uint32_t ub_hi = __builtin_amdgcn_readfirstlane((uint32_t)(ubv >> 32));
+    const int nbytes = (int)__builtin_amdgcn_readfirstlane((uint32_t)(ntiles * tbytes));
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((uint64_t)ub_hi << 32) | ub_lo), (short)0, nbytes, 0x00020000);
+    auto tile_b = [&](int64_t t) {
+        const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)(t * tbytes));
+        return __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(rs, loff, so, 0));
+    };
+#else
+    const char* ub = (const char*)(img + t_lo * 4);
     auto tile_b = [&](int64_t t) { return *(const h8*)(ub + t * tbytes + loff); };
+#endif
     h8 bq[PF];
 #pragma unroll
     for (int u = 0; u < PF; ++u) bq[u] = tile_b(min<int64_t>(u, ntiles - 1));

@@ -237,6 +237,32 @@ def test_early_status_publication(gpu_ctx, name, early, lb, monkeypatch):
     _check(gpu_ctx, name)
 
 
+@pytest.mark.parametrize("name", ["C5_well_s0", "C5_well_s2", "C5_well_s3", "C5_well_s4", "C4_q5", "C4_ring_q3",
+                                  "C2_q0_s1", "C5_clutter64"])
+@pytest.mark.parametrize("speculate", ["0", "1"])
+def test_pipelined_sub_batches(gpu_ctx, name, speculate, monkeypatch):
+    """A two-phase sub-batch enqueues the next sub-batch's extension phase before it
+    reads its own status (RBE_PLAN_PIPELINE); that phase is gated on the first REACHED
+    word, so a sub-batch that solves leaves the trees, the simplification and the
+    counters as they were. Same plans, statuses and trees as the golden ones, and the
+    same edges / samples / iterations counted as without the pipeline
+    (RBE_PLAN_SPECULATE=0: every sub-batch two-phase, small ones included). The states
+    count is compared to 1e-4: an edge's remaining slots are skipped once another wave
+    of the same launch has failed the edge, so it depends on the waves' timing (31 of
+    10,031,082 states between two runs of the approximate C5_well_s0 plan). A gated
+    sub-batch that still checked its edges' far endpoints (nd 0 instead of -1) showed
+    here as 98,314 extra states on C5_well_s2."""
+    monkeypatch.setenv("RBE_PLAN_SPECULATE", speculate)
+    stats = {}
+    for pipe in ("0", "1"):
+        monkeypatch.setenv("RBE_PLAN_PIPELINE", pipe)
+        s = _check(gpu_ctx, name)
+        stats[pipe] = {k: s[k] for k in ("states_checked", "edges_checked", "samples", "iterations")}
+    st0, st1 = stats["0"].pop("states_checked"), stats["1"].pop("states_checked")
+    assert stats["0"] == stats["1"], (name, stats)
+    assert abs(st0 - st1) <= 1e-4 * st0, (name, st0, st1)
+
+
 def test_lookback_error_flag_is_not_sticky(gpu_ctx):
     """the look-back accepts' poll-budget flag lives on the device. A plan
     that finds it raised fails (NativeError) and clears it, so the context's next

@@ -5,6 +5,7 @@ rates per plan."""
 import json
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -16,11 +17,14 @@ sc = scenes.Scene.from_json(q["scene"])
 ctx = Context(0)
 ctx.set_scene(sc.boxes, sc.plane_z, sc.base)
 ctx.set_attached(q["attached"])
+if "noprof" in sys.argv[1:]:
+    ctx.reserve(131072, 1 << 23)   # as bench.py: no first-use hipMalloc inside the traced plans
 grouped = "grouped" in sys.argv[1:]
 if grouped:
     os.environ["RBE_PLAN_GROUPED"] = "1"
 pmc = "pmc" in sys.argv[1:]   # counter passes: two plans, profiling off
-for prof in ((False,) if pmc else (False, True)):
+noprof = "noprof" in sys.argv[1:]   # kernel traces: the four plans, profiling off
+for prof in ((False,) if pmc or noprof else (False, True)):
     ctx.set_profiling(prof)
     for seed in ((2, 4) if pmc else (2, 3, 4, 0)):
         p = _abi.make_params(seed=seed, batch=131072, batch_min=131072, n_waypoints=150, timeout_s=60.0,
@@ -36,3 +40,5 @@ for prof in ((False,) if pmc else (False, True)):
             line += (f" | NN {pr['nn_launches']} launches {pr['nn_ms']:.2f} ms {pr['nn_pairs']:.3g} pairs "
                      f"{nn_tf:.2f} TF64 | edges {pr['edge_launches']} launches {pr['edge_ms']:.2f} ms {ed:.2f} G states/s")
         print(line, flush=True)
+        if noprof:
+            time.sleep(0.005)   # (plans apart in a kernel trace: tools/gap_summary.py)

@@ -148,18 +148,18 @@ int main(int argc, char** argv) {
                     S1 = (int)((T + chunk1 - 1) / chunk1);
                     hipLaunchKernelGGL((k_nn_mfma<4, 4>), dim3((unsigned)(qb1 * S1)), dim3(256), 0, s,
                                        (const double*)dq, n, (const int*)nullptr, (int64_t)0, (const double*)dt,
-                                       (const h8*)dimg, T, chunk1, qb1, P, pilot, 0, kern, (const DI2*)nullptr, 0);
+                                       (const h8*)dimg, T, chunk1, qb1, P, pilot, 0, kern, (const DI2*)nullptr, 0, (const int*)nullptr, (unsigned long long*)nullptr);
                 }
                 if (RB == 8)
                     hipLaunchKernelGGL((k_nn_mfma<8, 4>), dim3((unsigned)(g.qblocks * g.S)), dim3(256), 0, s,
                                        (const double*)dq, n, (const int*)nullptr, (int64_t)0, (const double*)dt,
                                        (const h8*)dimg, T, g.chunk, g.qblocks, P, part, 0, 1,
-                                       kern > 1 ? (const DI2*)pilot : nullptr, S1);
+                                       kern > 1 ? (const DI2*)pilot : nullptr, S1, (const int*)nullptr, (unsigned long long*)nullptr);
                 else
                     hipLaunchKernelGGL((k_nn_mfma<4, 4>), dim3((unsigned)(g.qblocks * g.S)), dim3(256), 0, s,
                                        (const double*)dq, n, (const int*)nullptr, (int64_t)0, (const double*)dt,
                                        (const h8*)dimg, T, g.chunk, g.qblocks, P, part, 0, 1,
-                                       kern > 1 ? (const DI2*)pilot : nullptr, S1);
+                                       kern > 1 ? (const DI2*)pilot : nullptr, S1, (const int*)nullptr, (unsigned long long*)nullptr);
             } else {
                 hipLaunchKernelGGL(kern, dim3((unsigned)(g.qblocks * g.S)), dim3(256), 0, s, (const double*)dq, n,
                                    (const int*)nullptr, (int64_t)0, (const double*)dt, (const h8*)dimg, T, g.chunk,

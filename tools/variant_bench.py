@@ -45,8 +45,10 @@ def main():
     stream = torch.cuda.Stream(dev)
     ctxs, flags = [], []
     arr, nb = _abi.make_boxes(sc.boxes)
+    # "lib.so@ENV=V": that variant runs with ENV=V set (the library reads it per launch)
+    envs = {p: dict(kv.split("=", 1) for kv in p.split("@")[1:]) for p in a.libs}
     for p in a.libs:
-        L = bind(p)
+        L = bind(p.split("@")[0])
         h = C.c_void_p()
         assert L.rp_create(C.byref(h), 0, None) == 0, p
         assert L.rp_set_scene(h, arr, nb, 0.0, (C.c_float * 3)(*sc.base)) == 0
@@ -57,6 +59,9 @@ def main():
     times = {p: [] for p in a.libs}
     for r in range(a.rounds):
         for (L, h), f, p in zip(ctxs, flags, a.libs):
+            for k in set().union(*envs.values()):
+                os.environ.pop(k, None)
+            os.environ.update(envs[p])
             for _ in range(2):
                 L.rp_check_states_device(h, q.data_ptr(), a.states, f.data_ptr(), stream.cuda_stream)
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

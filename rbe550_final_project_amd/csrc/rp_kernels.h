@@ -491,11 +491,11 @@ __global__ __launch_bounds__(VBLOCK, edge_waves(NCL, BF, true)) void k_edges_uni
 // the pass-1 list (k_edges_units_gl); the same items as k_edges / k_edges_units, the
 // same tests on the same values: the same verdicts.
 template <bool BF>
-__global__ __launch_bounds__(64 * GL_WAVES, edge_waves(NCL_GRID, BF, false)) void k_edges_gl(
+__global__ __launch_bounds__(64 * GL_WAVES, edge_waves(NCL_GRID, BF, true)) void k_edges_gl(
     const double* __restrict__ from, const double* __restrict__ to, const int* __restrict__ nd, int64_t n_edges,
     int kmax, int mode, uint8_t* valid, int group, int* gfail, unsigned long long* counter,
     const DevScene* __restrict__ sc, const int* __restrict__ dcount, int per_item, int pk, int pass,
-    const int* __restrict__ cntv, int* zero_word) {
+    const int* __restrict__ cntv, int* zero_word, int persist) {
     __shared__ SceneGrid L;
     __shared__ WaveQ wqs[GL_WAVES];
     __shared__ int marks[GL_WAVES][VBLOCK];
@@ -506,11 +506,14 @@ __global__ __launch_bounds__(64 * GL_WAVES, edge_waves(NCL_GRID, BF, false)) voi
     const int kk = max(kmax, 1);
     const int64_t n_waves = (n_edges + VBLOCK - 1) / VBLOCK * kk;
     const int wv = rp_tid() >> 6;
-    const int64_t w = (int64_t)rp_bid() * GL_WAVES + wv;
-    if (w >= n_waves) return;
-    const int64_t g = w / kk;
-    edge_group_round<NCL_GRID, BF, SceneGrid>(from, to, nd, n_edges, mode, valid, group, gfail, counter, &L, g,
-                                              (int)(w - g * kk) * VBLOCK, wqs[wv], marks[wv], pk, pass, cntv);
+    // a grid of the resident waves (persist: RBE_SCENE_LDS bit 2) strides over the
+    // (group, round) waves, so a block stages the scene once for many of them
+    const int64_t step = persist ? (int64_t)rp_gdim() * GL_WAVES : n_waves;
+    for (int64_t w = (int64_t)rp_bid() * GL_WAVES + wv; w < n_waves; w += step) {
+        const int64_t g = w / kk;
+        edge_group_round<NCL_GRID, BF, SceneGrid>(from, to, nd, n_edges, mode, valid, group, gfail, counter, &L, g,
+                                                  (int)(w - g * kk) * VBLOCK, wqs[wv], marks[wv], pk, pass, cntv);
+    }
 }
 template <bool BF>
 __global__ __launch_bounds__(64 * GL_WAVES, edge_waves(NCL_GRID, BF, true)) void k_edges_units_gl(

@@ -396,9 +396,12 @@ int64_t split_max() {
 // 2.80 -> 3.21 ms (its waves each check one short round: the block's 10 KB copy and
 // 4-wave blocks cost more than the gathers they save); clutter64 k_validity 1M / 4M
 // states 8.4 / 9.4 -> 10.0 / 11.3 G states/s
+// bit 2: k_edges_gl over a grid of the resident waves (a block stages the scene once
+// for many rounds): pass 0 2.80 -> 2.50 ms, C5 well edge time -3 % (default 5 = bits
+// 0 + 2; profiles/r06/scene_lds_ab.txt)
 int scene_lds_mode() {
     const char* e = std::getenv("RBE_SCENE_LDS");
-    return e && *e ? std::atoi(e) : 1;
+    return e && *e ? std::atoi(e) : 5;
 }
 bool scene_lds_on() { return (scene_lds_mode() & 1) != 0; }
 
@@ -664,17 +667,19 @@ void launch_edges(rp_ctx* c, const double* from, const double* to, const int* nd
     // loop-free one) with the scene in LDS (k_edges_units_gl / k_edges_gl: GL_WAVES
     // waves per block, each its own unit; scene_lds_mode)
     const int lds_mode = scene_lds_mode();
-    const bool lds = (lds_mode & 1) != 0, lds_free = (lds_mode & 2) != 0;
+    const bool lds = (lds_mode & 1) != 0, lds_free = (lds_mode & 6) != 0;
+    const int lds_persist = (lds_mode & 4) != 0 ? 1 : 0;   // (k_edges_gl over a resident grid)
 #define RP_EDGES_Z(N, L, G, KM, DK, RF, PK, PS, CV, ZW)                                                           \
     do {                                                                                                           \
         if ((N) == NCL_GRID && !(L) && (DK) == nullptr && (RF) == 0 && lds_free) {                                 \
-            const unsigned gg = (unsigned)(((int64_t)(G) + GL_WAVES - 1) / GL_WAVES);                               \
+            unsigned gg = (unsigned)(((int64_t)(G) + GL_WAVES - 1) / GL_WAVES);                                     \
+            if (lds_persist) gg = std::min<unsigned>(gg, (unsigned)(EDGE_UNITS_GRID / GL_WAVES));                  \
             if (bf) hipLaunchKernelGGL((k_edges_gl<true>), dim3(gg), dim3(64 * GL_WAVES), 0, s, from, to, nd, n, KM,  \
                                        mode, valid, group, gfail, c->counter.p, c->d_scene, dcount, per_item, PK,  \
-                                       PS, CV, ZW);                                                                \
+                                       PS, CV, ZW, lds_persist);                                                   \
             else hipLaunchKernelGGL((k_edges_gl<false>), dim3(gg), dim3(64 * GL_WAVES), 0, s, from, to, nd, n, KM,   \
                                     mode, valid, group, gfail, c->counter.p, c->d_scene, dcount, per_item, PK, PS, \
-                                    CV, ZW);                                                                       \
+                                    CV, ZW, lds_persist);                                                          \
         } else if (bf) hipLaunchKernelGGL((k_edges<N, true, L>), dim3(G), b, 0, s, from, to, nd, n, KM, mode, valid, \
                                    group, gfail, c->counter.p, c->d_scene, dcount, per_item, DK, RF, PK, PS, CV,   \
                                    ZW);                                                                            \
@@ -1273,24 +1278,29 @@ bool nn_mfma_params(const double* lo, const double* hi, NnMfma* P) {
     return true;
 }
 
-// pilot search stride (tiles; RBE_NN_PILOT, 0 / 1 = off; read per search). C5 covered-well
-// plans, NN time (4 seeds): RB 4 without a pilot 12.8 ms, RB 8 12.7, RB 8 + a one-range
-// RB 1 pilot every 16th / 32nd / 64th tile 11.9 / 11.4 / 11.7 ms; the pilot with RB 4
-// over ~1,024 blocks: none 12.0, 8 / 16 / 32 / 64: 11.4 / 11.0 / 11.0 / 11.2 ms
-// (profiles/r05/nn_pilot_ab.txt)
-int nn_pilot_stride() {
-    const char* e = std::getenv("RBE_NN_PILOT");
-    return e && *e ? std::atoi(e) : 32;
-}
-
 #ifndef RP_NN_SHARE_DEFAULT
-#define RP_NN_SHARE_DEFAULT 0
+#define RP_NN_SHARE_DEFAULT 1
 #endif
 // ranges of a split search share each query's best bound (rp_nn.h gbest);
 // RBE_NN_SHARE=0: every range tightens on its own finds only (A/B; read per search)
 bool nn_share() {
     const char* e = std::getenv("RBE_NN_SHARE");
     return e && *e ? std::atoi(e) != 0 : RP_NN_SHARE_DEFAULT;
+}
+
+// pilot search stride (tiles; RBE_NN_PILOT, 0 / 1 = off; read per search). C5 covered-well
+// plans, NN time (4 seeds): RB 4 without a pilot 12.8 ms, RB 8 12.7, RB 8 + a one-range
+// RB 1 pilot every 16th / 32nd / 64th tile 11.9 / 11.4 / 11.7 ms; the pilot with RB 4
+// over ~1,024 blocks: none 12.0, 8 / 16 / 32 / 64: 11.4 / 11.0 / 11.0 / 11.2 ms
+// (profiles/r05/nn_pilot_ab.txt)
+// With the ranges sharing each query's bound (nn_share, the default) the pilot is off
+// by default: C5 covered-well NN time, 4 plans (tools/well_ab.py, two rounds): no
+// sharing + pilot 32 10.22-10.26 ms, no sharing and no pilot 11.0, sharing + pilot
+// 32 / 64 / 128 / 256 10.0-10.3 / 9.64 / 9.63 / 9.31, sharing without a pilot 9.29-9.34
+// (profiles/r06/nn_share_ab.txt)
+int nn_pilot_stride() {
+    const char* e = std::getenv("RBE_NN_PILOT");
+    return e && *e ? std::atoi(e) : nn_share() ? 0 : 32;
 }
 
 // device geometry for status-bounded searches (rp_nn.h nn_geom): RBE_NN_DEVGEOM=0 for
@@ -1309,7 +1319,7 @@ bool nn_geom_fit() {
 
 template <int RB, int W>
 void launch_nn_mfma_w(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, const double* tree, const h8* img,
-                      int64_t T, const int* gate) {
+                      int64_t T, const int* gate, bool gb_ready) {
     constexpr int64_t NNM_STAGE = 64;   // (range sizing: 64-node units)
     const int64_t per_block = (int64_t)W * 16 * RB;
     int64_t target = 1024;   // blocks
@@ -1359,13 +1369,9 @@ void launch_nn_mfma_w(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, 
             fprintf(stderr, "nnlog n=%lld T=%lld grid=%lld S=%lld status=0 pilot=%d\n", (long long)n,
                     (long long)((T + pst - 1) / pst), (long long)(qb1 * S1), (long long)S1, pst);
     }
-    // the ranges share each query's bound (rp_nn.h gbest; RBE_NN_SHARE=0: off, A/B)
-    unsigned long long* gbest = nullptr;
-    if (S >= 2 && nn_share()) {
-        c->nn_gbest.ensure((size_t)n);
-        HIP_TRY(hipMemsetAsync(c->nn_gbest.p, 0xff, sizeof(unsigned long long) * (size_t)n, c->stream));
-        gbest = c->nn_gbest.p;
-    }
+    // the ranges share each query's bound (rp_nn.h gbest, reset by k_nn_queries: sample
+    // and steer searches; RBE_NN_SHARE=0: off, A/B)
+    unsigned long long* gbest = S >= 2 && gb_ready ? c->nn_gbest.p : nullptr;
     hipLaunchKernelGGL((k_nn_mfma<RB, W>), dim3((unsigned)grid), dim3(64 * W), 0, c->stream, qx, n, Q.status,
                        Q.t0, tree, img, T, chunk, qblocks, c->nnm, c->nn_part.p, devgeom, 1, init, init_S, gate, gbest);
     static const bool log = std::getenv("RBE_NN_LOG") != nullptr;   // (diagnostic: tools/nn_seq.py)
@@ -1380,13 +1386,13 @@ void launch_nn_mfma_w(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, 
 // waves per block: RBE_NN_WAVES (1, 2, 4)
 template <int RB>
 void launch_nn_mfma(rp_ctx* c, const double* qx, int64_t n, const NnQuery& Q, const double* tree, const h8* img,
-                    int64_t T, const int* gate) {
+                    int64_t T, const int* gate, bool gb_ready = false) {
     int w = 4;
     if (const char* e = std::getenv("RBE_NN_WAVES"))
         if (*e) w = std::atoi(e);
-    if (w == 1) launch_nn_mfma_w<RB, 1>(c, qx, n, Q, tree, img, T, gate);
-    else if (w == 2) launch_nn_mfma_w<RB, 2>(c, qx, n, Q, tree, img, T, gate);
-    else launch_nn_mfma_w<RB, 4>(c, qx, n, Q, tree, img, T, gate);
+    if (w == 1) launch_nn_mfma_w<RB, 1>(c, qx, n, Q, tree, img, T, gate, gb_ready);
+    else if (w == 2) launch_nn_mfma_w<RB, 2>(c, qx, n, Q, tree, img, T, gate, gb_ready);
+    else launch_nn_mfma_w<RB, 4>(c, qx, n, Q, tree, img, T, gate, gb_ready);
 }
 
 // whether n queries against T nodes take the split search: it pays ~4 launches; the
@@ -1425,19 +1431,23 @@ bool nn_split(rp_ctx* c, const NnQuery& Q, int64_t n, Tree& tr, int64_t T, int32
         if (*e) mfma_rb = std::atoi(e);
     if (mfma_rb > 0 && c->nnm_ok) {
         const double* qx;
+        bool gb_ready = false;   // (the shared bounds: sample / steer searches, reset with their queries)
         if (Q.kind == NNQ_ROWS) {
             qx = Q.A + (Q.TA0 + Q.t0) * NQ;
         } else {
             c->nn_qx.ensure((size_t)n * NQ);
-            hipLaunchKernelGGL(k_nn_queries, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, Q, n, c->nn_qx.p);
+            gb_ready = nn_share();
+            if (gb_ready) c->nn_gbest.ensure((size_t)n);
+            hipLaunchKernelGGL(k_nn_queries, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream, Q, n, c->nn_qx.p,
+                               gb_ready ? c->nn_gbest.p : (unsigned long long*)nullptr);
             qx = c->nn_qx.p;
         }
         const h8* img = tree_images(c, tr, T);
         const int ps = prof_begin(c, c->stream);
-        if (mfma_rb >= 8) launch_nn_mfma<8>(c, qx, n, Q, tree, img, T, gate);
-        else if (mfma_rb >= 4) launch_nn_mfma<4>(c, qx, n, Q, tree, img, T, gate);
-        else if (mfma_rb >= 2) launch_nn_mfma<2>(c, qx, n, Q, tree, img, T, gate);
-        else launch_nn_mfma<1>(c, qx, n, Q, tree, img, T, gate);
+        if (mfma_rb >= 8) launch_nn_mfma<8>(c, qx, n, Q, tree, img, T, gate, gb_ready);
+        else if (mfma_rb >= 4) launch_nn_mfma<4>(c, qx, n, Q, tree, img, T, gate, gb_ready);
+        else if (mfma_rb >= 2) launch_nn_mfma<2>(c, qx, n, Q, tree, img, T, gate, gb_ready);
+        else launch_nn_mfma<1>(c, qx, n, Q, tree, img, T, gate, gb_ready);
         hipLaunchKernelGGL(k_nn_reduce_g, dim3(blocks_for(n, 256)), dim3(256), 0, c->stream,
                            (const DI2*)c->nn_part.p, n, c->nn_S, Q.status, Q.t0, out, c->nn_geo[0], c->nn_geo[1],
                            c->nn_geo[2], (int)c->nn_geo[3]);

@@ -226,7 +226,10 @@ __device__ unsigned long long g_nncount[4];
 // and only then are the rows' threshold slots tightened. The deferred tightening
 // lets a few more nodes through; the result does not depend on the order in which
 // a row's candidates are evaluated (the range's lexicographic minimum).
-constexpr int NNM_FLUSH = 64;
+#ifndef RP_NNM_FLUSH
+#define RP_NNM_FLUSH 64
+#endif
+constexpr int NNM_FLUSH = RP_NNM_FLUSH;
 constexpr int NNM_CAND = NNM_FLUSH + 64;   // a round appends at most one pair per lane
 
 // (4 waves per SIMD at every RB: the register budget of 128 VGPRs)
@@ -385,8 +388,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
 #pragma unroll
             for (int rb = 0; rb < RB; ++rb) {
                 const int r = rb * 16 + (lane & 15);
-                const unsigned long long bb = s_best[w][r], gb = s_gb[w][r];
-                const double bnow = __longlong_as_double((long long)(gb < bb ? gb : bb));
+                // (s_gb <= s_best once shared: one word per row, as without sharing)
+                const double bnow = __longlong_as_double((long long)(gbest ? s_gb[w][r] : s_best[w][r]));
                 if (bnow < 1e300) {
                     _Float16 hh, hl;
                     thr_slots(P, bnow, s_na[w][r], hh, hl);
@@ -403,12 +406,12 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     // wait for each tile's freshly issued load), and loads past the range re-read its
     // last tile (unconditional: static vmcnt waits). Tiles need no bounds test: the
     // image's pad slots and dead query rows never pass (k_nn_image, a_frag).
-    // (RB 8: 3 tiles ahead — with 4 the kernel held 3 VGPRs over the 128 of 4 waves per
-    // SIMD in scratch; tests/test_isa_guard.py)
+    // (3 tiles ahead — RB 8 with 4 held 3 VGPRs over the 128 of 4 waves per SIMD in
+    // scratch, RB 4 with 4 and the shared bounds 5; tests/test_isa_guard.py)
 #ifndef RP_NN_PF8
 #define RP_NN_PF8 3
 #endif
-    constexpr int PF = RB >= 8 ? RP_NN_PF8 : 4;
+    constexpr int PF = RB >= 8 ? RP_NN_PF8 : 3;
     // tiles of the range: every tstride-th (a pilot search), else all
     const int64_t ntiles = ((t_hi - t_lo + 15) / 16 + tstride - 1) / tstride;
     const int col = lane & 15;   // this lane's column of every tile
@@ -534,9 +537,13 @@ __global__ void k_nn_reduce_g(const DI2* __restrict__ part, int64_t n, int S, co
 
 // the queries of a split search as f64 states (NNQ_SAMPLE / NNQ_STEER: Philox samples,
 // steered; nn_query of rp_kernels.h)
-__global__ void k_nn_queries(NnQuery Q, int64_t n, double* __restrict__ qx) {
+// gbest (the ranges' shared bounds, k_nn_mfma): reset to +inf here, in the launch every
+// sample / steer search makes right before its ranges run (no memset launch)
+__global__ void k_nn_queries(NnQuery Q, int64_t n, double* __restrict__ qx,
+                             unsigned long long* __restrict__ gbest) {
     const int64_t k = (int64_t)rp_bid() * rp_bdim() + rp_tid();
     if (k >= n) return;
+    if (gbest) gbest[k] = ~0ull;
     double x[NQ];
     nn_query(Q, k, x);
 #pragma unroll

@@ -169,16 +169,20 @@ def test_nearest_node_mfma_row_blocks(gpu_ctx, name, mfma, monkeypatch):
 
 
 @pytest.mark.parametrize("name", ["C5_well_s0", "C5_well_s3", "C4_q5", "C2_q0_s1"])
-@pytest.mark.parametrize("pilot,mfma", [("0", "8"), ("4", "8"), ("0", "4"), ("16", "4"), ("2", "1")])
-def test_nearest_node_pilot(gpu_ctx, name, pilot, mfma, monkeypatch):
+@pytest.mark.parametrize("pilot,mfma", [("0", "8"), ("4", "8"), ("0", "4"), ("16", "4"), ("2", "1"), ("32", "8")])
+@pytest.mark.parametrize("share", ["0", "1"])
+def test_nearest_node_pilot(gpu_ctx, name, pilot, mfma, share, monkeypatch):
     """The pilot search (every pilot-th tile of the whole tree first; its bests start
     every range of the full search, whose ranges then return their minimum over the
-    nodes at or below that distance, or none): off, and at strides 2 / 4 / 16 with
+    nodes at or below that distance, or none): off, and at strides 2 / 4 / 16 / 32 with
     1 / 4 / 8 row blocks, on every search it applies to (host-sized, >= 2 ranges,
     T >= stride x 1,024 nodes: the C5 well's trees; the small configs' searches run
-    without one). Same plans."""
+    without one); with and without the ranges sharing each query's bound (RBE_NN_SHARE:
+    a range's threshold follows the smallest exact best any range has published, its
+    own minimum stays its own). Same plans."""
     monkeypatch.setenv("RBE_NN_PILOT", pilot)
     monkeypatch.setenv("RBE_NN_MFMA", mfma)
+    monkeypatch.setenv("RBE_NN_SHARE", share)
     monkeypatch.setenv("RBE_NN_SPLIT", "1")
     _check(gpu_ctx, name)
 

@@ -1,6 +1,6 @@
 """Axis-grid scenes (> 16 boxes) with the scene staged in the block's LDS
 (rp_math.h SceneGrid; k_validity_gl, k_edges_units_gl and, with RBE_SCENE_LDS bit 1,
-k_edges_gl) against the CPU oracle and against the global-memory kernels
+k_edges_gl, bit 2 the same over a resident grid) against the CPU oracle and against the global-memory kernels
 (RBE_SCENE_LDS=0): validity flags, edge flags through the coarse-first passes and
 whole plans. The staged fields are DevScene's own values and the tests are the same
 arithmetic, so every result is bit for bit the same (reference: the per-state check
@@ -20,7 +20,7 @@ from test_gpu_edges import _edges, _scene
 
 pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
-MODES = ["0", "1", "3"]
+MODES = ["0", "1", "3", "5"]
 
 
 def _grid_scene(name):

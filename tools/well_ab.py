@@ -42,7 +42,7 @@ def main():
     keys = ("RBE_NN_MFMA", "RBE_PLAN_CHUNK", "RBE_CHUNK_TREE", "RBE_NN_WAVES", "RBE_NN_RANGES", "RBE_EDGE_PACKED",
             "RBE_NN_BLOCKS", "RBE_NN_DEVGEOM", "RBE_NN_PILOT", "RBE_NN_GEOM_FIT",
             "RBE_EDGE_COARSE", "RBE_EDGE_COARSE_MIN", "RBE_EDGE_UNITS", "RBE_EARLY_STATUS", "RBE_ACCEPT_LB", "RBE_WAIT_SPIN_US", "RBE_WAIT_SLEEP_FRAC",
-            "RBE_PLAN_PIPELINE", "RBE_PLAN_SPECULATE", "RBE_SCENE_LDS")
+            "RBE_PLAN_PIPELINE", "RBE_PLAN_SPECULATE", "RBE_SCENE_LDS", "RBE_NN_SHARE")
     for rep in range(2):   # rep 0: warm-up
         for name, env in cfgs.items():
             for k in keys:

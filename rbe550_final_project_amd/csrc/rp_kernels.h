@@ -957,10 +957,24 @@ __device__ __forceinline__ void publish_after_barrier() {
 // Straight-first check in one launch: lane 0 = start, lane 1 = goal, lanes
 // 2..nd = the interior slots 1..nd-1 of start -> goal (checkMotion mode 0, the
 // states k_edges would build: interp(start, goal, slot / nd) rounded to float32).
-// Blocks OR their failures into sync[0] (bit 0 start, 1 goal, 2 interior); the
-// last block to finish (sync[1] counts them) publishes the flags as bits 0 / 8 /
-// 16 of status[ST_SG] with the number of states checked, then resets sync.
+// Blocks add their failures and their arrival into sync (straight_arrive); the last
+// block to finish publishes the flags as bits 0 / 8 / 16 of status[ST_SG] with the
+// number of states checked, then resets sync.
 struct Endpoints { double start[NQ]; double goal[NQ]; };
+// A block's arrival as ONE 64-bit atomic add on sync (the two words as one): bits 0-23
+// count the finished blocks, 24-27 / 28-31 the blocks whose start / goal state collides
+// (one block holds each), 32-63 the blocks with a colliding interior state. All of a
+// launch's information meets in this word, so the last block reads it from its own add
+// and no fence orders anything: on gfx950 an agent-scope fence writes back and
+// invalidates the XCD's L2, which the two fences per block of the
+// previous OR + count form paid on every plan's first launch.
+__device__ __forceinline__ bool straight_arrive(unsigned* sync, unsigned wbad, unsigned* f) {
+    const unsigned long long add = 1ull | ((wbad & 1u) ? 1ull << 24 : 0ull) | ((wbad & 2u) ? 1ull << 28 : 0ull) |
+                                   ((wbad & 4u) ? 1ull << 32 : 0ull);
+    const unsigned long long tot = atomicAdd(reinterpret_cast<unsigned long long*>(sync), add) + add;
+    *f = (((tot >> 24) & 0xFull) ? 1u : 0u) | (((tot >> 28) & 0xFull) ? 2u : 0u) | ((tot >> 32) ? 4u : 0u);
+    return (tot & 0xFFFFFFull) == (unsigned long long)rp_gdim();
+}
 template <int NCL>
 __global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_straight(Endpoints ep, double res,
                                                                     const DevScene* __restrict__ sc,
@@ -986,20 +1000,13 @@ __global__ __launch_bounds__(VBLOCK, RP_EDGE_WAVES) void k_straight(Endpoints ep
     }
     // wave OR, then one atomic per block (a block is one wave)
     const unsigned long long b1 = __ballot(bad & 1u), b2 = __ballot(bad & 2u), b4 = __ballot(bad & 4u);
-    if (rp_tid() == 0) {
-        const unsigned wbad = (b1 ? 1u : 0u) | (b2 ? 2u : 0u) | (b4 ? 4u : 0u);
-        if (wbad) atomicOr(&sync[0], wbad);
-        __threadfence();
-        last = atomicAdd(&sync[1], 1u) == rp_gdim() - 1;
-    }
+    unsigned f = 0;
+    if (rp_tid() == 0) last = straight_arrive(sync, (b1 ? 1u : 0u) | (b2 ? 2u : 0u) | (b4 ? 4u : 0u), &f);
     __syncthreads();
     if (last && rp_tid() == 0) {
-        __threadfence();
-        const unsigned f = atomicOr(&sync[0], 0u);
         hio->status[ST_SG] = ((f & 1u) ? 0 : 1) | ((f & 2u) ? 0 : 0x100) | ((f & 6u) ? 0 : 0x10000);
         hio->counter = (unsigned long long)lanes;
-        sync[0] = 0;
-        sync[1] = 0;
+        *reinterpret_cast<unsigned long long*>(sync) = 0ull;
         publish_seq(hio, seq);
     }
 }
@@ -1050,20 +1057,13 @@ __global__ __launch_bounds__(64) void k_straight_ml(Endpoints ep, double res, co
     const bool col = state_collides_ml<GL, BF>(qq, run, scl, caps);
     const unsigned bad = (run && col) ? (idx == 0 ? 1u : idx == 1 ? 2u : 4u) : 0u;
     const unsigned long long b1 = __ballot(bad & 1u), b2 = __ballot(bad & 2u), b4 = __ballot(bad & 4u);
-    if (rp_tid() == 0) {
-        const unsigned wbad = (b1 ? 1u : 0u) | (b2 ? 2u : 0u) | (b4 ? 4u : 0u);
-        if (wbad) atomicOr(&sync[0], wbad);
-        __threadfence();
-        last = atomicAdd(&sync[1], 1u) == rp_gdim() - 1;
-    }
+    unsigned f = 0;
+    if (rp_tid() == 0) last = straight_arrive(sync, (b1 ? 1u : 0u) | (b2 ? 2u : 0u) | (b4 ? 4u : 0u), &f);
     __syncthreads();
     if (last && rp_tid() == 0) {
-        __threadfence();
-        const unsigned f = atomicOr(&sync[0], 0u);
         hio->status[ST_SG] = ((f & 1u) ? 0 : 1) | ((f & 2u) ? 0 : 0x100) | ((f & 6u) ? 0 : 0x10000);
         hio->counter = (unsigned long long)states;
-        sync[0] = 0;
-        sync[1] = 0;
+        *reinterpret_cast<unsigned long long*>(sync) = 0ull;
         publish_seq(hio, seq);
     }
 }

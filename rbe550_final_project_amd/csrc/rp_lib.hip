@@ -1829,6 +1829,8 @@ int plan_impl(rp_ctx* c, const double* start, const double* goal, const double* 
         for (int i = 0; i < NQ; ++i) { ep.start[i] = start[i]; ep.goal[i] = goal[i]; }
         const int nd = (int)std::ceil(std::sqrt(h_dist2(start, goal)) / p.resolution);
         const int64_t nst = nd >= 1 ? nd + 1 : 2;
+        // (straight_arrive counts the blocks in 24 bits)
+        if (nst >= ((int64_t)1 << 23)) throw HipError{"straight edge of 2^23 or more states (resolution too fine)"};
         const int seq = ++c->seq;
         const int gl = ml_lanes(nst, false);
         if (gl > 1) {   // low-latency: GL lanes per state

@@ -25,8 +25,13 @@ HEADERS.append(os.path.join(os.path.dirname(_HERE), "include", "rbe_planner.h"))
 #     line up their operands (4238 -> 3857 static VALU); +9 %
 #   -mllvm -amdgpu-mfma-vgpr-form: MFMA results in VGPRs, not AGPRs (k_nn_mfma's
 #     epilogue read every accumulator back with v_accvgpr_read: 16 per 16-node tile)
+#   -mllvm -amdgpu-sched-strategy=iterative-ilp: the machine scheduler's ILP-first
+#     strategy within each kernel's occupancy target (round 6, tools/variant_bench.py,
+#     profiles/r06/sched_strategy_ab.txt): k_validity goal3 2^24 states 0.4168 -> 0.4092
+#     ms, clutter64 +1.5 %, the same flags; C5 covered-well plans unchanged; max-ilp
+#     spilled k_validity (16 B) and ran 2.9 % slower
 DEVICE_FLAGS = ["-Xarch_device", "-fno-honor-nans", "-Xarch_device", "-mno-amdgpu-ieee", "-fno-slp-vectorize",
-                "-mllvm", "-amdgpu-mfma-vgpr-form"]
+                "-mllvm", "-amdgpu-mfma-vgpr-form", "-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
 # -mcode-object-version=6: rp_bdim / rp_gdim (rp_model.h) read the hidden kernel
 #   arguments at the v5/v6 offsets; pinned so a toolchain default cannot move them
 #   (rp_create also checks them on the device)

@@ -32,6 +32,12 @@ FORBIDDEN = re.compile(r"\b(v_cvt_rpi_i32_f32|v_cvt_flr_i32_f32|v_sin_f32|v_cos_
 #   k_contacts: rp_state_contacts (the start / goal contact list planning.py's
 #   diagnostics print when a plan reports INVALID_START / INVALID_GOAL; two states)
 SCRATCH_ALLOWED = {"k_contacts"}
+# instantiations that run only under a non-default A/B knob (never in a default plan or
+# the bench), allowed a few dwords of spill under the iterative-ILP scheduler
+# (build.py DEVICE_FLAGS): the scanned edge launch (RBE_EDGE_PACKED=1) and the one-wave
+# pass-1 list kernel of grid scenes (RBE_SCENE_LDS without bit 0; the default runs
+# k_edges_units_gl)
+SCRATCH_ALLOWED_AB = ("k_edges_packed<", "k_edges_units<-1,")
 
 
 def _code_object(lib_path):
@@ -108,5 +114,6 @@ def test_collision_kernels_present(code_object):
 
 def test_no_scratch_in_dispatched_kernels(code_object):
     bad = [(n[:110], s, v) for n, s, v in _kernels(code_object)
-           if s > 0 and _base(n) not in SCRATCH_ALLOWED]
+           if s > 0 and _base(n) not in SCRATCH_ALLOWED
+           and not re.sub(r"^(void )?rp::", "", n).startswith(SCRATCH_ALLOWED_AB)]
     assert not bad, "kernels using scratch (spills / stack arrays):\n" + "\n".join(map(str, bad))
